@@ -1,0 +1,254 @@
+"""ORACLE / TEST INFRASTRUCTURE — never imported by the product path.
+
+Op-for-op PyTorch-CPU restatement of the reference's denoise-training hot path
+(s194584/dl-speech-enhancement).  Only ``tests/``, ``__graft_entry__.smoke()``
+and ``bench.py``'s ``cpu_baseline`` leg may import this module, and only as the
+checker / the timed CPU baseline — never as the thing measured or shipped.
+
+It is pinned against golden vectors produced by importing the reference itself
+in the build container (tests/golden/make_goldens.py -> tests/golden/*.npz,
+checked by tests/test_oracle_goldens.py).
+
+Everything is functional (plain tensors + a flat parameter dict keyed exactly
+like the reference ``state_dict``) so it can run from fixtures without the
+reference module tree.  Each function cites the reference lines it restates.
+"""
+import math
+
+import torch
+import torch.nn.functional as F
+
+
+# --------------------------------------------------------------------------
+# spectral losses  (losses/stft_loss.py, losses/mel_loss.py)
+# --------------------------------------------------------------------------
+
+def hann(win_length):
+    """Periodic Hann window buffer: losses/stft_loss.py:97, mel_loss.py:49."""
+    return torch.hann_window(win_length)
+
+
+def stft_mag(x, fft_size, hop_size, win_length, window, eps=1e-7):
+    """losses/stft_loss.py:19-35 — |STFT| with power floor, (B, frames, bins)."""
+    z = torch.stft(x, fft_size, hop_size, win_length, window, return_complex=True)
+    p = z.real ** 2 + z.imag ** 2
+    return torch.sqrt(torch.clamp(p, min=eps)).transpose(2, 1)
+
+
+def spectral_convergence(x_mag, y_mag):
+    """losses/stft_loss.py:45-56 — global Frobenius ratio."""
+    return torch.norm(y_mag - x_mag, p="fro") / torch.norm(y_mag, p="fro")
+
+
+def log_stft_magnitude(x_mag, y_mag):
+    """losses/stft_loss.py:66-77 — mean |ln y - ln x|."""
+    return F.l1_loss(torch.log(y_mag), torch.log(x_mag))
+
+
+def stft_loss(x, y, fft_size, hop_size, win_length, window):
+    """losses/stft_loss.py:100-117 -> (sc, mag)."""
+    xm = stft_mag(x, fft_size, hop_size, win_length, window)
+    ym = stft_mag(y, fft_size, hop_size, win_length, window)
+    return spectral_convergence(xm, ym), log_stft_magnitude(xm, ym)
+
+
+def mr_stft_loss(x, y, resolutions, windows):
+    """losses/stft_loss.py:146-170 — mean over resolutions of (sc, mag)."""
+    if x.dim() == 3:
+        x = x.reshape(-1, x.size(2))
+        y = y.reshape(-1, y.size(2))
+    sc_total, mag_total = 0.0, 0.0
+    for (n, h, w), win in zip(resolutions, windows):
+        sc, mg = stft_loss(x, y, n, h, w, win)
+        sc_total = sc_total + sc
+        mag_total = mag_total + mg
+    return sc_total / len(resolutions), mag_total / len(resolutions)
+
+
+def _log_fn(log_base):
+    if log_base is None:
+        return torch.log
+    if log_base == 2.0:
+        return torch.log2
+    if log_base == 10.0:
+        return torch.log10
+    raise ValueError(log_base)
+
+
+def melspec(x, fft_size, hop_size, win_length, window, melmat, eps=1e-10, log_base=10.0):
+    """losses/mel_loss.py:74-94 — log-mel (B, mels, frames)."""
+    if x.dim() == 3:
+        x = x.reshape(-1, x.size(2))
+    z = torch.stft(x, fft_size, hop_size, win_length, window, return_complex=True)
+    p = z.real ** 2 + z.imag ** 2
+    amp = torch.sqrt(torch.clamp(p, min=eps)).transpose(2, 1)
+    m = torch.clamp(torch.matmul(amp, melmat), min=eps)
+    return _log_fn(log_base)(m).transpose(1, 2)
+
+
+def multi_mel_loss(y_hat, y, resolutions, windows, melmats, eps=1e-10, log_base=10.0):
+    """losses/mel_loss.py:140-155 — mean over resolutions of L1(mel(y_hat), mel(y))."""
+    total = 0.0
+    for (n, h, w), win, mm in zip(resolutions, windows, melmats):
+        total = total + F.l1_loss(melspec(y_hat, n, h, w, win, mm, eps, log_base),
+                                  melspec(y, n, h, w, win, mm, eps, log_base))
+    return total / len(resolutions)
+
+
+# --------------------------------------------------------------------------
+# conv layers  (layers/conv_layer.py)
+# --------------------------------------------------------------------------
+
+def causal_conv1d(x, w, b=None, stride=1, dilation=1):
+    """layers/conv_layer.py:139-142 — left zero pad (k-1)*d then valid conv."""
+    k = w.shape[-1]
+    x = F.pad(x, ((k - 1) * dilation, 0))
+    return F.conv1d(x, w, b, stride=stride, dilation=dilation)
+
+
+def causal_conv_transpose1d(x, w, b=None, stride=1):
+    """layers/conv_layer.py:180-183 — replicate-pad 1 left, deconv, crop [s:-s]."""
+    x = torch.cat([x[:, :, :1], x], dim=-1)
+    y = F.conv_transpose1d(x, w, b, stride=stride)
+    return y[:, :, stride:-stride]
+
+
+def elu(x):
+    """nn.ELU(alpha=1): models/autoencoder/modules/residual_unit.py:32."""
+    return F.elu(x)
+
+
+def residual_unit(x, w1, w2, dilation):
+    """residual_unit.py:43-46 — x + conv1x1(ELU(causal_conv_k7_d(ELU(x))))."""
+    y = causal_conv1d(elu(x), w1, None, 1, dilation)
+    y = F.conv1d(elu(y), w2)
+    return x + y
+
+
+# --------------------------------------------------------------------------
+# residual VQ  (layers/vq_module.py)
+# --------------------------------------------------------------------------
+
+def vq_distance(flatten, embed):
+    """vq_module.py:64-68 — evaluation order as written in the reference."""
+    return (flatten.pow(2).sum(1, keepdim=True)
+            - 2 * flatten @ embed
+            + embed.pow(2).sum(0, keepdim=True))
+
+
+def vq_forward(inp, embed, commitment=1.0):
+    """vq_module.py:61-88 in eval mode (no EMA: trainer/denoise.py:60).
+
+    Returns (quantize_st, loss, perplexity, indices)."""
+    dim = embed.shape[0]
+    n_embed = embed.shape[1]
+    flatten = inp.reshape(-1, dim)
+    dist = vq_distance(flatten, embed)
+    _, ind = (-dist).max(1)
+    onehot = F.one_hot(ind, n_embed).type(inp.dtype)
+    ind = ind.view(*inp.shape[:-1])
+    q = F.embedding(ind, embed.transpose(0, 1))
+    loss = F.mse_loss(q.detach(), inp) * commitment
+    q = inp + (q - inp).detach()
+    p = onehot.mean(0)
+    ppl = torch.exp(-torch.sum(p * torch.log(p + 1e-10)))
+    return q, loss, ppl, ind
+
+
+def rvq_forward(x, embeds):
+    """vq_module.py:119-134 — residual not detached (:129)."""
+    out = 0.0
+    residual = x
+    losses, ppls, inds = [], [], []
+    for e in embeds:
+        q, l, p, i = vq_forward(residual, e)
+        residual = residual - q
+        out = out + q
+        losses.append(l)
+        ppls.append(p)
+        inds.append(i)
+    return out, torch.stack(losses), torch.stack(ppls), torch.stack(inds)
+
+
+# --------------------------------------------------------------------------
+# AudioDec generator (models/autoencoder*/)
+# --------------------------------------------------------------------------
+
+def generator_geometry(encode_channels=32, decode_channels=32, enc_ratios=(2, 4, 8, 16),
+                       dec_ratios=(16, 8, 4, 2), enc_strides=(3, 4, 5, 5),
+                       dec_strides=(5, 5, 4, 3), **_):
+    """Channel/stride plan of encoder.py:84-110 and decoder.py:84-114."""
+    enc = []
+    cin = encode_channels
+    for r, s in zip(enc_ratios, enc_strides):
+        enc.append((cin, encode_channels * r, s))
+        cin = encode_channels * r
+    dec = []
+    for i, s in enumerate(dec_strides):
+        ci = decode_channels * dec_ratios[i]
+        co = decode_channels * dec_ratios[i + 1] if i < len(dec_ratios) - 1 else decode_channels
+        dec.append((ci, co, s))
+    return enc, dec
+
+
+def encoder_forward(P, x, geo, dilations=(1, 3, 9)):
+    """encoder.py:112-116 / EncoderBlock :61-65."""
+    enc, _ = geo
+    h = causal_conv1d(x, P["encoder.conv.conv.weight"])
+    for i, (ci, co, s) in enumerate(enc):
+        pre = f"encoder.conv_blocks.{i}"
+        for j, d in enumerate(dilations):
+            ru = f"{pre}.res_units.{j}"
+            h = residual_unit(h, P[f"{ru}.conv1.conv.weight"], P[f"{ru}.conv2.weight"], d)
+        h = causal_conv1d(h, P[f"{pre}.conv.conv.weight"], P.get(f"{pre}.conv.conv.bias"), stride=s)
+    return h
+
+
+def decoder_forward(P, z, geo, pqc=True, dilations=(1, 3, 9)):
+    """decoder.py:116-121 (PQC) / without_PQC decoder.py:116-123 (conv1 skipped)."""
+    _, dec = geo
+    h = causal_conv1d(z, P["decoder.conv1.conv.weight"]) if pqc else z
+    for i, (ci, co, s) in enumerate(dec):
+        pre = f"decoder.conv_blocks.{i}"
+        h = causal_conv_transpose1d(h, P[f"{pre}.conv.deconv.weight"], P.get(f"{pre}.conv.deconv.bias"), s)
+        for j, d in enumerate(dilations):
+            ru = f"{pre}.res_units.{j}"
+            h = residual_unit(h, P[f"{ru}.conv1.conv.weight"], P[f"{ru}.conv2.weight"], d)
+    return causal_conv1d(h, P["decoder.conv2.conv.weight"])
+
+
+def generator_forward(P, x, geo, pqc=True, codebook_num=8):
+    """AudioDec.py:95-103 (PQC) or autoencoder_without_PQC/AudioDec.py:94-100."""
+    h = encoder_forward(P, x, geo)
+    if not pqc:
+        return decoder_forward(P, h, geo, pqc=False)
+    z = causal_conv1d(h, P["projector.project.conv.weight"])
+    embeds = [P[f"quantizer.codebook.layers.{i}.embed"] for i in range(codebook_num)]
+    zq, vql, ppl, _ = rvq_forward(z.transpose(2, 1), embeds)
+    zq = zq.transpose(2, 1)
+    y = decoder_forward(P, zq, geo, pqc=True)
+    return y, zq, z, vql, ppl
+
+
+# --------------------------------------------------------------------------
+# step glue  (dataloader/data_utils.py, train_denoise.py, trainerGAN.py)
+# --------------------------------------------------------------------------
+
+def add_noise(speech, noise, snr):
+    """dataloader/data_utils.py:12-22 — batch-global norms, math.exp(snr/10)."""
+    assert speech.shape == noise.shape
+    sp = speech.norm(p=2)
+    npow = noise.norm(p=2)
+    scale = math.exp(snr / 10) * npow / sp
+    return (scale * speech + noise) / 2
+
+
+def snr_db(preds, target):
+    """torchmetrics 1.2.0 SignalNoiseRatio (zero_mean=False), mean over batch.
+
+    Third-party, absent here: parity unpinned (restated from its published
+    formula 10*log10((sum t^2 + eps) / (sum (t-p)^2 + eps)), eps=finfo.eps)."""
+    eps = torch.finfo(preds.dtype).eps
+    noise = target - preds
+    v = (torch.sum(target ** 2, dim=-1) + eps) / (torch.sum(noise ** 2, dim=-1) + eps)
+    return (10 * torch.log10(v)).mean()

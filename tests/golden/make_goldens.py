@@ -1,0 +1,329 @@
+"""Generate golden vectors by importing the reference (build container only).
+
+Run:  python tests/golden/make_goldens.py  [--ref /root/reference]
+
+This imports s194584/dl-speech-enhancement from ``/root/reference`` (read-only,
+never copied, never shipped) and records inputs/outputs of the hot-path
+modules as small ``.npz`` fixtures under ``tests/golden/``.  Those fixtures pin
+the CPU oracle (``oracle/``) and, through it, the HIP path.
+
+Third-party pieces absent from this image and how they are handled:
+* librosa 0.8.1 (``losses/mel_loss.py:14``) — injected as a stub module whose
+  ``filters.mel`` is the restatement in ``oracle/melfilters.py``.
+* torchaudio / soundfile (dataloader package init) — ``dataloader/data_utils.py``
+  and ``collater.py`` are loaded by file path with a stub package.
+* torchmetrics (SNR), clearml, tensorboardX — not needed: the step glue of
+  ``train_denoise.py:213-263`` is restated below from its source text.
+"""
+import argparse
+import importlib.util
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+
+from oracle import melfilters  # noqa: E402
+
+
+def _install_stubs(ref):
+    lib = types.ModuleType("librosa")
+    lib.filters = types.SimpleNamespace(mel=melfilters.mel)
+    sys.modules["librosa"] = lib
+    sys.path.insert(0, ref)
+    # dataloader package init pulls torchaudio/soundfile: load the two files we need by path.
+    pkg = types.ModuleType("dataloader")
+    pkg.__path__ = [os.path.join(ref, "dataloader")]
+    sys.modules["dataloader"] = pkg
+    col = _load("dataloader.collater", os.path.join(ref, "dataloader", "collater.py"))
+    pkg.CollaterAudio = col.CollaterAudio
+    pkg.CollaterAudioPair = col.CollaterAudioPair
+    du = _load("dataloader.data_utils", os.path.join(ref, "dataloader", "data_utils.py"))
+    return du
+
+
+def _load(name, path):
+    spec = importlib.util.spec_from_file_location(name, path)
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules[name] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def _audio(ref):
+    """Real speech/noise from reference notebook_files (48k int16 clean, 24k f32 noise)."""
+    from scipy.io import wavfile
+    from scipy.signal import resample_poly
+    import warnings
+    warnings.filterwarnings("ignore")
+    clean = []
+    noise = []
+    for i in (1, 2):
+        sr, d = wavfile.read(os.path.join(ref, "notebook_files", f"clean{i}.wav"))
+        x = d.astype(np.float64) / 32768.0
+        clean.append(resample_poly(x, 1, sr // 24000).astype(np.float32))
+        sr, d = wavfile.read(os.path.join(ref, "notebook_files", f"noise{i}.wav"))
+        n = d.astype(np.float32)
+        if sr != 24000:
+            n = resample_poly(n.astype(np.float64), 24000, sr).astype(np.float32)
+        noise.append(n)
+    return clean, noise
+
+
+def _np(t):
+    return t.detach().cpu().numpy()
+
+
+def _sd(module, prefix="sd."):
+    return {prefix + k: _np(v) for k, v in module.state_dict().items()}
+
+
+def _grads(module, prefix="g."):
+    return {prefix + k: _np(p.grad) for k, p in module.named_parameters() if p.grad is not None}
+
+
+def make(ref, out):
+    du = _install_stubs(ref)
+    stft_mod = _load("ref_stft_loss", os.path.join(ref, "losses", "stft_loss.py"))
+    mel_mod = _load("ref_mel_loss", os.path.join(ref, "losses", "mel_loss.py"))
+    conv_mod = importlib.import_module("layers.conv_layer")
+    vq_mod = importlib.import_module("layers.vq_module")
+    pqc_mod = importlib.import_module("models.autoencoder.AudioDec")
+    npqc_mod = importlib.import_module("models.autoencoder_without_PQC.AudioDec")
+
+    clean, noise = _audio(ref)
+    os.makedirs(out, exist_ok=True)
+    torch.manual_seed(93)
+
+    # ---------------- melmat (losses/mel_loss.py:54-61) ----------------
+    cfgs = {
+        "24k_fmax24000": dict(fs=24000, fft_size=2048, hop_size=300, win_length=None, num_mels=80, fmin=0, fmax=24000, log_base=None),
+        "24k_fmax12000": dict(fs=24000, fft_size=2048, hop_size=300, win_length=2048, num_mels=80, fmin=0, fmax=12000, log_base=None),
+        "48k_fmax24000": dict(fs=48000, fft_size=2048, hop_size=300, win_length=None, num_mels=80, fmin=0, fmax=24000, log_base=None),
+        "default": dict(),
+    }
+    d = {}
+    for k, c in cfgs.items():
+        m = mel_mod.MelSpectrogram(**c)
+        d[f"melmat.{k}"] = _np(m.melmat)
+        d[f"window.{k}"] = _np(m.window)
+    np.savez_compressed(os.path.join(out, "melmat.npz"), **d)
+
+    # ---------------- stft magnitude + losses (losses/stft_loss.py) ----------------
+    T = 12000
+    x = torch.from_numpy(np.stack([clean[0][4000:4000 + T], clean[1][8000:8000 + T]]))
+    y = torch.from_numpy(np.stack([clean[0][4000:4000 + T] + 0.05 * noise[0][:T],
+                                   clean[1][8000:8000 + T] + 0.05 * noise[1][:T]]).astype(np.float32))
+    d = {"x": _np(x), "y": _np(y)}
+    res = [(1024, 120, 600), (2048, 240, 1200), (512, 50, 240)]
+    for n, h, w in res:
+        win = torch.hann_window(w)
+        d[f"mag.{n}"] = _np(stft_mod.stft(x, n, h, w, win))
+        sl = stft_mod.STFTLoss(n, h, w)
+        sc, mg = sl(x, y)
+        d[f"sc.{n}"] = _np(sc)
+        d[f"logmag.{n}"] = _np(mg)
+    xg = x.clone().requires_grad_(True)
+    mr = stft_mod.MultiResolutionSTFTLoss()
+    sc, mg = mr(xg.unsqueeze(1), y.unsqueeze(1))
+    (sc + mg).backward()
+    d["mr.sc"] = _np(sc)
+    d["mr.mag"] = _np(mg)
+    d["mr.grad_x"] = _np(xg.grad)
+    # edge case: shortest legal signal for n_fft 2048 (reflect pad needs T > n_fft/2)
+    xs = torch.from_numpy(clean[0][:1025].copy()).unsqueeze(0)
+    d["short.x"] = _np(xs)
+    d["short.mag.2048"] = _np(stft_mod.stft(xs, 2048, 240, 1200, torch.hann_window(1200)))
+    np.savez_compressed(os.path.join(out, "stft.npz"), **d)
+
+    # ---------------- mel loss (losses/mel_loss.py) ----------------
+    T = 24000
+    yh = torch.from_numpy(np.stack([clean[0][:T] * 0.7 + 0.02 * noise[0][:T],
+                                    clean[1][:T] * 0.7 + 0.02 * noise[1][:T]]).astype(np.float32)).unsqueeze(1)
+    yt = torch.from_numpy(np.stack([clean[0][:T], clean[1][:T]])).unsqueeze(1)
+    d = {"y_hat": _np(yh), "y": _np(yt)}
+    p24 = dict(fs=24000, fft_sizes=[2048], hop_sizes=[300], win_lengths=[None], window="hann_window",
+               num_mels=80, fmin=0, fmax=24000, log_base=None)
+    ml = mel_mod.MultiMelSpectrogramLoss(**p24)
+    d["mel24.y_hat"] = _np(ml.mel_transfers[0](yh))
+    g = yh.clone().requires_grad_(True)
+    loss = ml(g, yt)
+    loss.backward()
+    d["mel24.loss"] = _np(loss)
+    d["mel24.grad"] = _np(g.grad)
+    # default (fs 22050, 3 res, log10) multi-resolution variant
+    mld = mel_mod.MultiMelSpectrogramLoss()
+    g = yh.clone().requires_grad_(True)
+    loss = mld(g, yt)
+    loss.backward()
+    d["meldef.loss"] = _np(loss)
+    d["meldef.grad"] = _np(g.grad)
+    np.savez_compressed(os.path.join(out, "mel.npz"), **d)
+
+    # ---------------- conv layers (layers/conv_layer.py) ----------------
+    d = {}
+    conv_cases = [
+        # name, Cin, Cout, k, stride, dilation, bias, T
+        ("first", 1, 8, 7, 1, 1, False, 300),
+        ("ru_d1", 8, 8, 7, 1, 1, False, 200),
+        ("ru_d3", 8, 8, 7, 1, 3, False, 200),
+        ("ru_d9", 16, 16, 7, 1, 9, False, 150),
+        ("down3", 8, 16, 6, 3, 1, True, 240),
+        ("down5", 16, 24, 10, 5, 1, True, 200),
+        ("proj", 32, 16, 3, 1, 1, False, 20),
+        ("last", 8, 1, 7, 1, 1, False, 300),
+    ]
+    for name, ci, co, k, s, dl, b, t in conv_cases:
+        m = conv_mod.CausalConv1d(ci, co, k, stride=s, dilation=dl, bias=b)
+        xin = torch.randn(2, ci, t, requires_grad=True)
+        yo = m(xin)
+        gy = torch.randn_like(yo)
+        yo.backward(gy)
+        d[f"{name}.cfg"] = np.array([ci, co, k, s, dl, int(b), t])
+        d[f"{name}.x"] = _np(xin)
+        d[f"{name}.w"] = _np(m.conv.weight)
+        if b:
+            d[f"{name}.b"] = _np(m.conv.bias)
+            d[f"{name}.gb"] = _np(m.conv.bias.grad)
+        d[f"{name}.y"] = _np(yo)
+        d[f"{name}.gy"] = _np(gy)
+        d[f"{name}.gx"] = _np(xin.grad)
+        d[f"{name}.gw"] = _np(m.conv.weight.grad)
+    deconv_cases = [
+        ("up5", 16, 8, 5, True, 20),
+        ("up3", 8, 4, 3, True, 30),
+        ("up4", 12, 8, 4, True, 1),
+    ]
+    for name, ci, co, s, b, t in deconv_cases:
+        m = conv_mod.CausalConvTranspose1d(ci, co, 2 * s, s, bias=b)
+        xin = torch.randn(2, ci, t, requires_grad=True)
+        yo = m(xin)
+        gy = torch.randn_like(yo)
+        yo.backward(gy)
+        d[f"{name}.cfg"] = np.array([ci, co, 2 * s, s, int(b), t])
+        d[f"{name}.x"] = _np(xin)
+        d[f"{name}.w"] = _np(m.deconv.weight)
+        d[f"{name}.b"] = _np(m.deconv.bias)
+        d[f"{name}.y"] = _np(yo)
+        d[f"{name}.gy"] = _np(gy)
+        d[f"{name}.gx"] = _np(xin.grad)
+        d[f"{name}.gw"] = _np(m.deconv.weight.grad)
+        d[f"{name}.gb"] = _np(m.deconv.bias.grad)
+    # residual unit (models/autoencoder/modules/residual_unit.py:49-80)
+    ru_mod = importlib.import_module("models.autoencoder.modules.residual_unit")
+    ru = ru_mod.CausalResidualUnit(8, 8, dilation=3)
+    xin = torch.randn(2, 8, 180, requires_grad=True)
+    yo = ru(xin)
+    gy = torch.randn_like(yo)
+    yo.backward(gy)
+    d.update({"ru.x": _np(xin), "ru.w1": _np(ru.conv1.conv.weight), "ru.w2": _np(ru.conv2.weight),
+              "ru.y": _np(yo), "ru.gy": _np(gy), "ru.gx": _np(xin.grad),
+              "ru.gw1": _np(ru.conv1.conv.weight.grad), "ru.gw2": _np(ru.conv2.weight.grad)})
+    np.savez_compressed(os.path.join(out, "conv.npz"), **d)
+
+    # ---------------- residual VQ (layers/vq_module.py) ----------------
+    rvq = vq_mod.ResidualVQ(num_quantizers=4, dim=64, codebook_size=1024)
+    rvq.eval()
+    z = torch.randn(2, 80, 64) * 2.0
+    zg = z.clone().requires_grad_(True)
+    q, losses, ppls = rvq(zg)
+    r = torch.randn_like(q)
+    ((q * r).sum() + losses.sum()).backward()
+    d = {"z": _np(z), "q": _np(q), "losses": _np(losses), "ppls": _np(ppls),
+         "r": _np(r), "grad_z": _np(zg.grad)}
+    for i, layer in enumerate(rvq.layers):
+        d[f"embed.{i}"] = _np(layer.embed)
+    with torch.no_grad():
+        qi, idx = rvq.forward_index(z)
+    d["fi.q"] = _np(qi)
+    d["fi.idx"] = _np(idx)
+    # per-stage top-2 distance margins (near-tie bookkeeping)
+    margins = []
+    res_ = z.reshape(-1, 64)
+    for layer in rvq.layers:
+        dist = (res_.pow(2).sum(1, keepdim=True) - 2 * res_ @ layer.embed + layer.embed.pow(2).sum(0, keepdim=True))
+        top2 = torch.topk(-dist, 2, dim=1).values
+        margins.append(_np(top2[:, 0] - top2[:, 1]))
+        ind = (-dist).max(1)[1]
+        qq = layer.embed.t()[ind]
+        res_ = res_ - (res_ + (qq - res_))
+    d["margins"] = np.stack(margins)
+    # training-mode VQ (EMA update) on one stage, for the autoencoder trainer path
+    vq = vq_mod.VectorQuantize(dim=64, codebook_size=256)
+    vq.train()
+    e0 = vq.embed.clone()
+    zt = torch.randn(160, 64)
+    qt, lt, pt = vq(zt)
+    d.update({"ema.embed0": _np(e0), "ema.z": _np(zt), "ema.q": _np(qt), "ema.loss": _np(lt),
+              "ema.ppl": _np(pt), "ema.embed1": _np(vq.embed), "ema.cluster_size": _np(vq.cluster_size),
+              "ema.embed_avg": _np(vq.embed_avg)})
+    np.savez_compressed(os.path.join(out, "vq.npz"), **d)
+
+    # ---------------- generators (reduced width) ----------------
+    gp = dict(encode_channels=4, decode_channels=4, code_dim=64, codebook_num=2, codebook_size=64)
+    mel = mel_mod.MultiMelSpectrogramLoss(**p24)
+    T = 2400
+    xn = torch.from_numpy(np.stack([clean[0][:T] + 0.1 * noise[0][:T],
+                                    clean[1][:T] + 0.1 * noise[1][:T]]).astype(np.float32)).unsqueeze(1)
+    xc = torch.from_numpy(np.stack([clean[0][:T], clean[1][:T]])).unsqueeze(1)
+    for tag, mod in (("pqc", pqc_mod), ("nopqc", npqc_mod)):
+        torch.manual_seed(93)
+        G = mod.Generator(**gp)
+        d = {"x_noisy": _np(xn), "x_clean": _np(xc)}
+        d.update(_sd(G))
+        if tag == "pqc":
+            G.quantizer.codebook.eval()
+            y, zq, z, vql, ppl = G(xn)
+            loss = 45.0 * mel(y, xc) + vql.sum()
+            d.update({"y": _np(y), "zq": _np(zq), "z": _np(z), "vqloss": _np(vql), "ppl": _np(ppl)})
+        else:
+            y = G(xn)
+            loss = 45.0 * mel(y, xc)
+            d["y"] = _np(y)
+        loss.backward()
+        d["loss"] = _np(loss)
+        d.update(_grads(G))
+        np.savez_compressed(os.path.join(out, f"generator_{tag}.npz"), **d)
+
+    # ---------------- train_denoise.py step glue (:138-154, :213-243) ----------------
+    torch.manual_seed(93)
+    G = npqc_mod.Generator(**gp)
+    opt = torch.optim.Adam(G.parameters(), lr=5e-5, weight_decay=1e-6)
+    d = {"x_noisy": _np(xn), "x_clean": _np(xc)}
+    d.update(_sd(G, "sd0."))
+    for step in range(2):
+        G.train()
+        y = G(xn)
+        loss = 45.0 * mel(y, xc)
+        opt.zero_grad()
+        loss.backward()
+        tn = torch.nn.utils.clip_grad_norm_(G.parameters(), 1.0)
+        opt.step()
+        d[f"loss.{step}"] = _np(loss)
+        d[f"gradnorm.{step}"] = _np(tn)
+        d.update(_sd(G, f"sd{step + 1}."))
+    np.savez_compressed(os.path.join(out, "train_step.npz"), **d)
+
+    # ---------------- add_noise (dataloader/data_utils.py:12-22) ----------------
+    cl = torch.from_numpy(np.stack([clean[0][:4800], clean[1][:4800]])).unsqueeze(1)
+    nz = torch.from_numpy(np.stack([noise[0][:4800], noise[1][:4800]])).unsqueeze(1)
+    d = {"clean": _np(cl), "noise": _np(nz)}
+    for snr in (10, 15, 19):
+        d[f"mixed.{snr}"] = _np(du.add_noise(cl, nz, torch.tensor([snr])))
+    np.savez_compressed(os.path.join(out, "add_noise.npz"), **d)
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ref", default="/root/reference")
+    ap.add_argument("--out", default=HERE)
+    a = ap.parse_args()
+    make(a.ref, a.out)
+    for f in sorted(os.listdir(a.out)):
+        if f.endswith(".npz"):
+            print(f, os.path.getsize(os.path.join(a.out, f)))
