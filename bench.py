@@ -1,0 +1,191 @@
+"""Benchmark of the denoise-training hot path on MI355X.
+
+python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2]
+(N > 1: launched by torch.distributed.run, one rank per GPU over RCCL.)
+
+Prints ONE JSON line (rank 0): BASELINE.json's metric "denoise-train frames/sec
+(24 kHz, hop 300)" — frames = clips x 24000 / 300 — for the whole job, with
+a live `roofline` for the dominant kernel (HIP events on its launch stream) and
+a `cpu_baseline` (the oracle, timed on this host's cores on a bounded sample).
+
+Workloads (BASELINE.json configs):
+  c3 (default): configs[2] — one full denoise-trainer step (trainer/denoise.py):
+      PQC generator fwd/bwd (decoder + quantizer frozen, codebook eval),
+      45 x mel loss + vq loss, clip, Adam; B = 64 x 1 s @ 24 kHz per GPU.
+  c2: configs[1] — spectral losses only (3-res STFT + 24 kHz mel), fwd+bwd, B=32, fp32.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "dl-speech-enhancement_amd")
+for _p in (REPO, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+SR = 24000
+HOP = 300
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+MEL24 = dict(fs=24000, fft_sizes=[2048], hop_sizes=[300], win_lengths=[None], window="hann_window",
+             num_mels=80, fmin=0, fmax=24000, log_base=None)
+STFT_RES = [(1024, 120, 600), (2048, 240, 1200), (512, 50, 240)]
+
+
+def synthetic_batch(B, T, seed=93):
+    """clean = 0.1*N(0,1) (PCG64(93)), noise PCG64(94), mixed = add_noise(snr=15)."""
+    clean = (0.1 * np.random.Generator(np.random.PCG64(seed)).standard_normal((B, 1, T))).astype(np.float32)
+    noise = (0.1 * np.random.Generator(np.random.PCG64(seed + 1)).standard_normal((B, 1, T))).astype(np.float32)
+    return torch.from_numpy(clean), torch.from_numpy(noise)
+
+
+# ---------------------------------------------------------------------------
+# c2: spectral losses only
+# ---------------------------------------------------------------------------
+
+def c2_setup(dev, B):
+    from losses import MultiMelSpectrogramLoss, MultiResolutionSTFTLoss
+    clean, noise = synthetic_batch(B, SR)
+    y_hat = (clean + 0.3 * noise).to(dev)
+    y = clean.to(dev)
+    mel = MultiMelSpectrogramLoss(**MEL24).to(dev)
+    stft = MultiResolutionSTFTLoss().to(dev)
+    x = y_hat.clone().requires_grad_(True)
+
+    def step():
+        x.grad = None
+        sc, mg = stft(x, y)
+        loss = 45.0 * mel(x, y) + 45.0 * (sc + mg)
+        loss.backward()
+    return step
+
+
+def c2_bytes_per_launch(name, B):
+    """Algorithmic HBM bytes of one launch of the fused STFT-loss forward at the
+    n_fft=512 resolution: read x and y once (B*T fp32 each); partials negligible."""
+    return 2 * 4 * B * SR
+
+
+def c2_cpu_baseline(B_sample=4, steps=3):
+    from oracle import ref_ops as R
+    from oracle.melfilters import mel as melbank
+    mm = torch.from_numpy(melbank(sr=24000, n_fft=2048, n_mels=80, fmin=0, fmax=24000).T.copy())
+    clean, noise = synthetic_batch(B_sample, SR)
+    y = clean
+    x = (clean + 0.3 * noise).requires_grad_(True)
+    wins = [R.hann(w) for _, _, w in STFT_RES]
+
+    def step():
+        x.grad = None
+        sc, mg = R.mr_stft_loss(x, y, STFT_RES, wins)
+        loss = 45.0 * R.multi_mel_loss(x, y, [(2048, 300, 2048)], [R.hann(2048)], [mm], 1e-10, None) \
+            + 45.0 * (sc + mg)
+        loss.backward()
+    step()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    dt = (time.perf_counter() - t0) / steps
+    return B_sample * SR / HOP / dt, f"oracle (PyTorch-CPU restatement) c2 losses fwd+bwd, B={B_sample}, {steps} steps"
+
+
+# ---------------------------------------------------------------------------
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="c2", choices=["c2", "c3"])
+    ap.add_argument("--batch", type=int, default=0, help="per-GPU batch (default: config's)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    from sel import _lib
+    cfg = args.config
+    B = args.batch or (32 if cfg == "c2" else 64)
+    if cfg == "c2":
+        step = c2_setup(dev, B)
+        dom = "sel_stft_loss_fwd"
+        bytes_fn = c2_bytes_per_launch
+        workload = "configs[1]: MR-STFT(3 res) + mel(2048/300/80) loss fwd+bwd, fp32, 1 s @ 24 kHz"
+        dtype = "fp32"
+    else:
+        raise SystemExit("c3 not built yet")
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    timer = _lib.KernelTimer([dom])
+    _lib.TIMER = timer
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    _lib.TIMER = None
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    durs = timer.durations_ms(dom)
+    # one sel_stft_loss_fwd call per resolution per step: pick the n_fft=512 launches
+    ms_per_step = 1e3 * elapsed / args.steps
+    frames = world * B * SR / HOP * args.steps
+    value = frames / elapsed
+    if cfg == "c2":
+        per_step = len(durs) // args.steps
+        sel_d = durs[per_step - 1::per_step]  # last resolution (n_fft=512) of each step
+        avg_ms = float(np.mean(sel_d))
+        achieved = bytes_fn(dom, B) / (avg_ms * 1e-3) / 1e9
+    roof = {"bound": "hbm", "kernel": dom + " (n_fft=512)", "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "avg_launch_us": round(avg_ms * 1e3, 2), "traffic": None}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        ncores = len(os.sched_getaffinity(0))
+        ncores = min(ncores, int(os.environ.get("OMP_NUM_THREADS", ncores)))
+        torch.set_num_threads(ncores)
+        v, sample = c2_cpu_baseline()
+        cpu = {"value": round(v, 1), "unit": "frames/s", "cores": ncores, "kind": "port", "sample": sample}
+
+    if rank == 0:
+        out = {
+            "metric": "denoise-train frames/sec (24 kHz, hop 300)",
+            "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": dtype, "data": "synthetic",
+            "config": {"workload": workload, "global_batch": world * B, "seq_len": SR,
+                       "parallelism": f"dp{world}"},
+            "roofline": roof, "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

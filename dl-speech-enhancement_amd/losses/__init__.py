@@ -1,0 +1,2 @@
+from .mel_loss import *  # NOQA
+from .stft_loss import *  # NOQA

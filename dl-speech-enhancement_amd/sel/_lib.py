@@ -1,0 +1,146 @@
+"""ctypes binding of libsel.so (include/sel.h).
+
+The product path has no CPU fallback: every op requires ROCm device tensors and
+the built library; anything else raises.  PyTorch is used only for device
+memory (caching allocator), streams and autograd plumbing.
+"""
+import ctypes
+import os
+import threading
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("SEL_LIB", os.path.join(_HERE, "libsel.so"))
+
+P = ctypes.c_void_p
+I64 = ctypes.c_int64
+I32 = ctypes.c_int
+F32 = ctypes.c_float
+SZ = ctypes.c_size_t
+
+# name -> (restype, argtypes); must cover every function declared in include/sel.h
+SIGNATURES = {
+    "sel_init": (I32, []),
+    "sel_last_error": (ctypes.c_char_p, []),
+    "sel_version": (I32, []),
+    "sel_stft_mag_fwd": (I32, [P, I64, I64, I32, I32, I32, P, F32, P, P]),
+    "sel_stft_bwd_workspace": (SZ, [I64, I64, I32, I32, I32]),
+    "sel_stft_mag_bwd": (I32, [P, I64, I64, I32, I32, I32, P, F32, P, P, P, SZ, P]),
+    "sel_mag_pair_workspace": (SZ, [I64]),
+    "sel_mag_pair_sums": (I32, [P, P, I64, P, P, SZ, P]),
+    "sel_mag_pair_bwd": (I32, [P, P, I64, P, P, P, P]),
+    "sel_stft_loss_workspace": (SZ, [I64, I64, I32, I32, I32]),
+    "sel_stft_loss_fwd": (I32, [P, P, I64, I64, I32, I32, I32, P, P, P, SZ, P]),
+    "sel_stft_loss_bwd": (I32, [P, P, I64, I64, I32, I32, I32, P, P, P, P, SZ, P]),
+    "sel_stft_loss_finish": (I32, [P, I64, P, P]),
+    "sel_stft_loss_coef": (I32, [P, I64, P, P, P, P]),
+    "sel_logmel_fwd": (I32, [P, I64, I64, I32, I32, I32, P, P, P, I32, F32, I32, P, P]),
+    "sel_l1_workspace": (SZ, [I64]),
+    "sel_l1_mean": (I32, [P, P, I64, P, P, SZ, P]),
+    "sel_logmel_bwd_workspace": (SZ, [I64, I64, I32, I32, I32]),
+    "sel_logmel_bwd": (I32, [P, I64, I64, I32, I32, I32, P, P, P, P, I32, F32, I32,
+                             P, P, P, F32, P, P, SZ, P]),
+}
+
+_lock = threading.Lock()
+_lib = None
+_initialized = False
+
+
+class SelError(RuntimeError):
+    pass
+
+
+def load():
+    """dlopen libsel.so (no GPU needed) and declare every C signature."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise SelError(f"libsel.so not found at {LIB_PATH}: build it with "
+                               f"`make -C dl-speech-enhancement_amd/csrc` (hipcc, gfx950)")
+            lib = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = lib
+    return _lib
+
+
+def lib():
+    """Loaded + initialised library (uploads FFT tables; needs the GPU)."""
+    global _initialized
+    L = load()
+    if not _initialized:
+        with _lock:
+            if not _initialized:
+                if not torch.cuda.is_available():
+                    raise SelError("sel: no ROCm GPU visible; the MI355X path has no CPU fallback")
+                torch.cuda.init()
+                rc = L.sel_init()
+                if rc != 0:
+                    raise SelError(f"sel_init failed ({rc}): {L.sel_last_error().decode()}")
+                _initialized = True
+    return L
+
+
+class KernelTimer:
+    """Brackets selected C-ABI calls with HIP events on the launching stream
+    (torch.cuda.current_stream()) — used by bench.py for the live roofline."""
+
+    def __init__(self, names):
+        self.names = set(names)
+        self.events = {n: [] for n in self.names}
+
+    def durations_ms(self, name):
+        torch.cuda.synchronize()
+        return [a.elapsed_time(b) for a, b in self.events[name]]
+
+
+TIMER = None
+
+
+def call(name, *args):
+    """Invoke a C entry point, raise SelError on failure, optionally timed."""
+    fn = getattr(lib(), name)
+    t = TIMER
+    if t is not None and name in t.names:
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record()
+        rc = fn(*args)
+        b.record()
+        t.events[name].append((a, b))
+    else:
+        rc = fn(*args)
+    check(rc, name)
+
+
+def check(rc, what):
+    if rc != 0:
+        raise SelError(f"{what} failed ({rc}): {load().sel_last_error().decode()}")
+
+
+def stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def need_device(*tensors):
+    for t in tensors:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise SelError("sel: the MI355X path needs ROCm device tensors (got a CPU tensor); "
+                           "there is no CPU fallback")
+
+
+def workspace(nbytes, device):
+    return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
