@@ -1,0 +1,20 @@
+"""Projector — drop-in for models/autoencoder/modules/projector.py (:20-56)."""
+import torch
+
+from layers.conv_layer import CausalConv1d, NonCausalConv1d
+
+
+class Projector(torch.nn.Module):
+    def __init__(self, input_channels, code_dim, kernel_size=3, stride=1, bias=False, mode="causal",
+                 model="conv1d"):
+        super().__init__()
+        self.mode = mode
+        Conv = {"causal": CausalConv1d, "noncausal": NonCausalConv1d}.get(mode)
+        if Conv is None:
+            raise NotImplementedError(f"Mode ({mode}) is not supported!")
+        if model != "conv1d":
+            raise NotImplementedError(f"Model ({model}) is not supported!")
+        self.project = Conv(input_channels, code_dim, kernel_size=kernel_size, stride=stride, bias=bias)
+
+    def forward(self, x):
+        return self.project(x)

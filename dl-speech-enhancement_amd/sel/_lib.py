@@ -41,6 +41,18 @@ SIGNATURES = {
     "sel_logmel_bwd_workspace": (SZ, [I64, I64, I32, I32, I32]),
     "sel_logmel_bwd": (I32, [P, I64, I64, I32, I32, I32, P, P, P, P, I32, F32, I32,
                              P, P, P, F32, P, P, SZ, P]),
+    "sel_conv_fwd": (I32, [P, I32, I32, P, P, P, P, P, P, P]),
+    "sel_conv_wgrad_workspace": (SZ, [P]),
+    "sel_conv_wgrad": (I32, [P, I32, P, P, P, P, P, SZ, P]),
+    "sel_pack_weight": (I32, [I32, P, I32, I32, I32, I32, I32, P, P]),
+    "sel_pack_dgrad": (I32, [P, I32, I32, I32, I32, P, P]),
+    "sel_unpack_wgrad": (I32, [I32, P, I32, I32, I32, I32, P, P]),
+    "sel_conv_replicate_fix": (I32, [P, I32, P, P, P, P]),
+    "sel_cast": (I32, [P, I32, P, I32, I64, P]),
+    "sel_rvq_workspace": (SZ, [I64, I32, I32]),
+    "sel_rvq_fwd": (I32, [P, I64, I32, P, I32, I32, P, P, P, P, P, SZ, P]),
+    "sel_rvq_finish": (I32, [P, P, I64, I32, I32, I32, F32, P, P, P]),
+    "sel_rvq_bwd": (I32, [P, I64, I32, P, I32, P, P, P, F32, P, P]),
 }
 
 _lock = threading.Lock()

@@ -1,0 +1,271 @@
+"""Autograd ops over the conv-stack kernels of libsel.so.
+
+Activations live channels-last in HBM: a (B, C, T) tensor handed between the
+drop-in modules is a transposed *view* of a contiguous (B, T, C) buffer, so the
+reference's (B, C, T) module API is kept with zero layout copies.
+
+Reference semantics (file:line under the reference root):
+* CausalConv1d            layers/conv_layer.py:109-150 (left zero pad (k-1)*d)
+* CausalConvTranspose1d   layers/conv_layer.py:153-191 (replicate pad 1, crop [s:-s])
+* Conv1d1x1               layers/conv_layer.py:19-23
+* CausalResidualUnit      models/autoencoder/modules/residual_unit.py:43-80
+"""
+import ctypes
+import threading
+from contextlib import contextmanager
+
+import torch
+
+from . import _lib as L
+
+F32, BF16 = 0, 1
+PAD_ZERO, PAD_REPLICATE = 0, 1
+PACK_FWD, PACK_FWD_STRIDED, PACK_CONVT = 0, 1, 2
+
+
+class ConvDesc(ctypes.Structure):
+    _fields_ = [("rows", ctypes.c_int64), ("T", ctypes.c_int32), ("C", ctypes.c_int32),
+                ("N", ctypes.c_int32), ("K", ctypes.c_int32), ("dil", ctypes.c_int32),
+                ("pad", ctypes.c_int32), ("pad_mode", ctypes.c_int32), ("in_elu", ctypes.c_int32),
+                ("bias_period", ctypes.c_int32)]
+
+    def adjoint(self):
+        """dgrad of this primitive: same primitive on gout with Wd[C][K][N]."""
+        return ConvDesc(self.rows, self.T, self.N, self.C, self.K, self.dil,
+                        (self.K - 1) * self.dil - self.pad, PAD_ZERO, 0, 0)
+
+    def with_(self, **kw):
+        d = ConvDesc(*[getattr(self, f) for f, _ in self._fields_])
+        for k, v in kw.items():
+            setattr(d, k, v)
+        return d
+
+
+_state = threading.local()
+
+
+def compute_dtype():
+    return getattr(_state, "dtype", torch.float32)
+
+
+@contextmanager
+def precision(dtype):
+    """Run the conv stack in `dtype` (torch.float32 = parity path, torch.bfloat16 =
+    bf16 MFMA with fp32 accumulation).  Parameters and their grads stay fp32."""
+    prev = compute_dtype()
+    _state.dtype = dtype
+    try:
+        yield
+    finally:
+        _state.dtype = prev
+
+
+def _code(dtype):
+    if dtype == torch.float32:
+        return F32
+    if dtype == torch.bfloat16:
+        return BF16
+    raise TypeError(f"unsupported activation dtype {dtype}")
+
+
+def to_cl(x):
+    """(B, C, T) tensor -> contiguous (B, T, C) storage (a view when possible)."""
+    y = x.transpose(1, 2)
+    return y if y.is_contiguous() else y.contiguous()
+
+
+def _cast_raw(x, dtype):
+    out = torch.empty(x.shape, dtype=dtype, device=x.device)
+    xc = x.contiguous()
+    L.call("sel_cast", L.ptr(xc), _code(xc.dtype), L.ptr(out), _code(dtype), xc.numel(), L.stream())
+    return out
+
+
+class _CastFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, dtype):
+        ctx.src = x.dtype
+        return _cast_raw(x, dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        return _cast_raw(g, ctx.src), None
+
+
+def cast(x, dtype):
+    """dtype cast on device (sel_cast), differentiable."""
+    if x.dtype == dtype:
+        return x
+    L.need_device(x)
+    if torch.is_grad_enabled() and x.requires_grad:
+        return _CastFn.apply(x, dtype)
+    return _cast_raw(x, dtype)
+
+
+def pack(kind, w, stride, dtype):
+    """fp32 torch weight -> packed (dtype) Wp[N][K][C] on device."""
+    if kind == PACK_CONVT:
+        cin, cout, k = w.shape
+        shape = (stride * cout, 2, cin)
+    else:
+        cout, cin, k = w.shape
+        shape = (cout, k, cin) if kind == PACK_FWD else (cout, 3, stride * cin)
+    wc = w.detach().contiguous().float()
+    out = torch.empty(shape, dtype=dtype, device=w.device)
+    L.call("sel_pack_weight", kind, L.ptr(wc), cout, cin, k, stride, _code(dtype), L.ptr(out), L.stream())
+    return out
+
+
+def pack_dgrad(wp):
+    N, K, C = wp.shape
+    out = torch.empty((C, K, N), dtype=wp.dtype, device=wp.device)
+    L.call("sel_pack_dgrad", L.ptr(wp), N, K, C, _code(wp.dtype), L.ptr(out), L.stream())
+    return out
+
+
+def prim(desc, x, wp, bias=None, aux=None, res=None, out_dtype=None):
+    """The conv primitive; x is (rows, C) channels-last (any leading shape)."""
+    out_dtype = out_dtype or x.dtype
+    out = torch.empty((desc.rows, desc.N), dtype=out_dtype, device=x.device)
+    for t in (aux, res):
+        if t is not None:
+            assert t.dtype == out_dtype and t.is_contiguous() and t.numel() == out.numel()
+    assert x.is_contiguous() and x.numel() == desc.rows * desc.C and wp.dtype == x.dtype
+    L.call("sel_conv_fwd", ctypes.byref(desc), _code(x.dtype), _code(out_dtype), L.ptr(x), L.ptr(wp),
+           L.ptr(bias), L.ptr(aux), L.ptr(res), L.ptr(out), L.stream())
+    return out
+
+
+def wgrad(desc, gout, x, want_bias):
+    lib = L.lib()
+    ws = L.workspace(lib.sel_conv_wgrad_workspace(ctypes.byref(desc)), x.device)
+    gwp = torch.empty((desc.N, desc.K, desc.C), dtype=torch.float32, device=x.device)
+    gb = torch.empty(desc.bias_period, dtype=torch.float32, device=x.device) if want_bias else None
+    L.call("sel_conv_wgrad", ctypes.byref(desc), _code(x.dtype), L.ptr(gout), L.ptr(x), L.ptr(gwp),
+           L.ptr(gb), L.ptr(ws), ws.numel(), L.stream())
+    return gwp, gb
+
+
+def unpack(kind, gwp, w_shape, stride):
+    gw = torch.empty(w_shape, dtype=torch.float32, device=gwp.device)
+    if kind == PACK_CONVT:
+        cin, cout, k = w_shape
+    else:
+        cout, cin, k = w_shape
+    L.call("sel_unpack_wgrad", kind, L.ptr(gwp), cout, cin, k, stride, L.ptr(gw), L.stream())
+    return gw
+
+
+def _layer_desc(kind, B, T_in, cin, cout, k, stride, dil, has_bias):
+    """Descriptor + output length for a reference layer in primitive form."""
+    if kind == PACK_FWD:
+        if stride != 1:
+            raise NotImplementedError("stride > 1 conv is lowered through PACK_FWD_STRIDED")
+        d = ConvDesc(B * T_in, T_in, cin, cout, k, dil, (k - 1) * dil, PAD_ZERO, 0, cout if has_bias else 0)
+        return d, T_in, cout
+    if kind == PACK_FWD_STRIDED:
+        if T_in % stride:
+            raise L.SelError(f"sel: strided conv needs T ({T_in}) divisible by the stride ({stride})")
+        To = T_in // stride
+        d = ConvDesc(B * To, To, stride * cin, cout, 3, 1, 2, PAD_ZERO, 0, cout if has_bias else 0)
+        return d, To, cout
+    # transposed: (B, L, Cin) -> (B, L*s, Cout) as (B, L, s*Cout)
+    d = ConvDesc(B * T_in, T_in, cin, stride * cout, 2, 1, 1, PAD_REPLICATE, 0, cout if has_bias else 0)
+    return d, T_in * stride, cout
+
+
+class ConvLayerFn(torch.autograd.Function):
+    """One reference conv layer (causal / strided / transposed), channels-last."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, kind, stride, dil):
+        # x: (B, T, Cin) contiguous in compute dtype
+        L.need_device(x, w)
+        B, T_in, cin = x.shape
+        if kind == PACK_CONVT:
+            cout, k = w.shape[1], w.shape[2]
+        else:
+            cout, k = w.shape[0], w.shape[2]
+        if kind == PACK_FWD and stride > 1:
+            kind = PACK_FWD_STRIDED
+            if k != 2 * stride:
+                raise L.SelError(f"sel: strided CausalConv1d needs kernel_size == 2*stride (got {k}, {stride})")
+        desc, T_out, c_out = _layer_desc(kind, B, T_in, cin, cout, k, stride, dil, b is not None)
+        wp = pack(kind, w, stride, x.dtype)
+        bias = b.detach().contiguous().float() if b is not None else None
+        y = prim(desc, x, wp, bias=bias)
+        ctx.save_for_backward(x, wp)
+        ctx.meta = (desc, kind, stride, tuple(w.shape), b is not None)
+        return y.view(B, T_out, c_out)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, wp = ctx.saved_tensors
+        desc, kind, stride, w_shape, has_bias = ctx.meta
+        gy = gy.contiguous()
+        if gy.dtype != x.dtype:
+            gy = cast(gy, x.dtype)
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = prim(desc.adjoint(), gy, pack_dgrad(wp))
+            if desc.pad_mode == PAD_REPLICATE:
+                L.call("sel_conv_replicate_fix", ctypes.byref(desc), _code(gy.dtype), L.ptr(gy), L.ptr(wp),
+                       L.ptr(gx), L.stream())
+            gx = gx.view(x.shape)
+        if ctx.needs_input_grad[1] or (has_bias and ctx.needs_input_grad[2]):
+            gwp, gbv = wgrad(desc, gy, x, has_bias and ctx.needs_input_grad[2])
+            if ctx.needs_input_grad[1]:
+                gw = unpack(kind, gwp, w_shape, stride)
+            gb = gbv
+        return gx, gw, gb, None, None, None
+
+
+class ResidualUnitFn(torch.autograd.Function):
+    """x + conv1x1(ELU(causal_conv_k(ELU(x)))) fused into two primitive calls
+    forward and four backward (residual_unit.py:43-46)."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, dil):
+        L.need_device(x, w1, w2)
+        B, T, C = x.shape
+        k = w1.shape[2]
+        cm = w1.shape[0]
+        d1 = ConvDesc(B * T, T, C, cm, k, dil, (k - 1) * dil, PAD_ZERO, 1, cm if b1 is not None else 0)
+        d2 = ConvDesc(B * T, T, cm, w2.shape[0], 1, 1, 0, PAD_ZERO, 1, w2.shape[0] if b2 is not None else 0)
+        if w2.shape[0] != C:
+            raise L.SelError("residual unit needs out_channels == in_channels")
+        wp1 = pack(PACK_FWD, w1, 1, x.dtype)
+        wp2 = pack(PACK_FWD, w2, 1, x.dtype)
+        bb1 = b1.detach().float().contiguous() if b1 is not None else None
+        bb2 = b2.detach().float().contiguous() if b2 is not None else None
+        xf = x.view(B * T, C)
+        h = prim(d1, xf, wp1, bias=bb1)
+        out = prim(d2, h, wp2, bias=bb2, res=xf)
+        ctx.save_for_backward(x, h, wp1, wp2)
+        ctx.meta = (d1, d2, tuple(w1.shape), tuple(w2.shape))
+        return out.view(B, T, C)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, h, wp1, wp2 = ctx.saved_tensors
+        d1, d2, s1, s2 = ctx.meta
+        B, T, C = x.shape
+        g = g.contiguous()
+        if g.dtype != x.dtype:
+            g = cast(g, x.dtype)
+        gf = g.view(B * T, C)
+        xf = x.view(B * T, C)
+        # dL/dh = (W2^T g) * ELU'(h)
+        gh = prim(d2.adjoint(), gf, pack_dgrad(wp2), aux=h)
+        gw1 = gb1 = gw2 = gb2 = None
+        if ctx.needs_input_grad[3] or ctx.needs_input_grad[4]:
+            gwp2, gb2 = wgrad(d2, gf, h, d2.bias_period > 0 and ctx.needs_input_grad[4])
+            gw2 = unpack(PACK_FWD, gwp2, s2, 1) if ctx.needs_input_grad[3] else None
+        gx = None
+        if ctx.needs_input_grad[0]:
+            # dL/dx = g + (conv_adjoint(gh)) * ELU'(x)
+            gx = prim(d1.adjoint(), gh, pack_dgrad(wp1), aux=xf, res=gf).view(B, T, C)
+        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+            gwp1, gb1 = wgrad(d1, gh, xf, d1.bias_period > 0 and ctx.needs_input_grad[2])
+            gw1 = unpack(PACK_FWD, gwp1, s1, 1) if ctx.needs_input_grad[1] else None
+        return gx, gw1, gb1, gw2, gb2, None

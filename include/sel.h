@@ -111,6 +111,82 @@ int sel_logmel_bwd(const float* x, int64_t B, int64_t T, int n_fft, int hop,
                    const float* g_out, const float* ref, const float* g_scale, float g_mul,
                    float* g_x, void* ws, size_t ws_bytes, sel_stream_t stream);
 
+/* ---- AudioDec conv stack: layers/conv_layer.py, residual_unit.py -------
+ * Every conv of the generator is lowered to ONE primitive over channels-last
+ * activations (rows = B*T flat, row pitch = channels):
+ *   out[m, n] = epi( sum_{k<K} sum_{c<C} Wp[n][k][c] * act(in[row(m,k), c]) )
+ *   row(m,k) = b*T + t + k*dil - pad  (t = m % T, b = m / T); rows outside the
+ *   sample read 0 (SEL_PAD_ZERO) or clamp to the sample (SEL_PAD_REPLICATE);
+ *   act = ELU (alpha 1) when in_elu, else identity;
+ *   epi(v) = (v + bias[n % bias_period]) * (aux ? ELU'(aux[m,n]) : 1) + (res ? res[m,n] : 0).
+ * Strided convs (encoder down-sampling, conv_layer.py:109-150 with stride s) run
+ * as a 3-tap conv on the phase-expanded input (B, T/s, s*Cin); transposed convs
+ * (conv_layer.py:153-191) as a 2-tap replicate-padded conv producing
+ * (B, T, s*Cout) = (B, T*s, Cout).  Weights are repacked on device each step
+ * (sel_pack_weight) and weight gradients unpacked (sel_unpack_wgrad). */
+enum { SEL_F32 = 0, SEL_BF16 = 1 };
+enum { SEL_PAD_ZERO = 0, SEL_PAD_REPLICATE = 1 };
+enum {
+  SEL_PACK_FWD = 0,          /* Conv1d W[Cout][Cin][K]          -> Wp[Cout][K][Cin] */
+  SEL_PACK_FWD_STRIDED = 1,  /* Conv1d W[Cout][Cin][2s], stride s -> Wp[Cout][3][s*Cin] */
+  SEL_PACK_CONVT = 2         /* ConvTranspose1d W[Cin][Cout][2s]  -> Wp[s*Cout][2][Cin] */
+};
+
+typedef struct sel_conv_desc {
+  int64_t rows;       /* B*T */
+  int32_t T;          /* rows per sample */
+  int32_t C, N;       /* in / out channels */
+  int32_t K, dil, pad;
+  int32_t pad_mode;   /* SEL_PAD_* */
+  int32_t in_elu;
+  int32_t bias_period;/* 0: no bias */
+} sel_conv_desc;
+
+int sel_conv_fwd(const sel_conv_desc* d, int in_dtype, int out_dtype, const void* in,
+                 const void* wpack, const float* bias, const void* aux, const void* res,
+                 void* out, sel_stream_t stream);
+/* weight/bias gradient of the same primitive: gwpack[N][K][C] (fp32) and, when
+ * gbias != NULL, gbias[bias_period] = sum over rows and phases of gout. */
+size_t sel_conv_wgrad_workspace(const sel_conv_desc* d);
+int sel_conv_wgrad(const sel_conv_desc* d, int dtype, const void* gout, const void* in,
+                   float* gwpack, float* gbias, void* ws, size_t ws_bytes, sel_stream_t stream);
+/* Repack fp32 torch weights (kind SEL_PACK_*) into Wp (dtype), and the dgrad
+ * form of a packed Wp[N][K][C] -> Wd[C][K][N] with taps reversed (the adjoint is
+ * the same primitive with pad' = (K-1)*dil - pad). */
+int sel_pack_weight(int kind, const float* w, int cout, int cin, int k, int stride,
+                    int dtype, void* wpack, sel_stream_t stream);
+int sel_pack_dgrad(const void* wpack, int N, int K, int C, int dtype, void* wd,
+                   sel_stream_t stream);
+/* gwpack (packed fp32) -> torch layout gw (kind as in sel_pack_weight). */
+int sel_unpack_wgrad(int kind, const float* gwpack, int cout, int cin, int k, int stride,
+                     float* gw, sel_stream_t stream);
+/* adjoint of SEL_PAD_REPLICATE (pad 1, K 2): gin[b*T + 0, c] += sum_n gout[b*T + 0, n] * Wp[n][0][c] */
+int sel_conv_replicate_fix(const sel_conv_desc* d, int dtype, const void* gout,
+                           const void* wpack, void* gin, sel_stream_t stream);
+/* dtype casts (activations in/out of the bf16 path) */
+int sel_cast(const void* src, int src_dtype, void* dst, int dst_dtype, int64_t n,
+             sel_stream_t stream);
+
+/* ---- residual VQ: layers/vq_module.py:61-88 (eval), :119-134 -------------
+ * All stages of one row block in one launch (rows are independent):
+ *   dist_k = (|r|^2 - (2r).e_k) + |e_k|^2, idx = argmin (lowest index on ties),
+ *   q = e_idx, qst = r + (q - r), r <- r - qst, out += qst.
+ * x (N, D) fp32; embeds (S, D, K) fp32 (the `embed` buffers stacked);
+ * out (N, D); idx (S, N) int64; counts (S, K) int32 (zeroed by the call);
+ * sqerr (S) fp64: sum (q - r)^2 per stage. */
+size_t sel_rvq_workspace(int64_t N, int S, int K);
+int sel_rvq_fwd(const float* x, int64_t N, int D, const float* embeds, int S, int K,
+                float* out, int64_t* idx, int32_t* counts, double* sqerr,
+                void* ws, size_t ws_bytes, sel_stream_t stream);
+/* per-stage loss = sqerr/(N*D)*commitment and perplexity from counts -> loss[S], ppl[S] */
+int sel_rvq_finish(const int32_t* counts, const double* sqerr, int64_t N, int D, int S, int K,
+                   float commitment, float* loss, float* ppl, sel_stream_t stream);
+/* g_x = g_out + g_loss[0]*commitment*2*(x - e0[idx0])/(N*D)  (only stage 0's
+ * commitment term reaches x: later residuals have zero Jacobian w.r.t. x, vq_module.py:83,129) */
+int sel_rvq_bwd(const float* x, int64_t N, int D, const float* embed0, int K, const int64_t* idx0,
+                const float* g_out, const float* g_loss, float commitment, float* g_x,
+                sel_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,159 @@
+"""GPU parity of the conv-stack kernels (layers/conv_layer.py drop-ins, residual unit).
+
+fp32 path (v_mfma_f32_16x16x4_f32, exact fp32 products, different summation
+order than MKL-DNN): relative error <= 1e-5 on outputs, 1e-4 on gradients
+(norm-wise), plus elementwise |a-b| <= 1e-4|b| + 1e-5 max|b|.
+bf16 path (bf16 operands, fp32 accumulation): <= 2e-2 norm-wise relative.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+
+def _np(t):
+    return t.detach().float().cpu().numpy() if torch.is_tensor(t) else np.asarray(t)
+
+
+def close(a, b, rtol=1e-4, floor=1e-5):
+    a, b = _np(a).astype(np.float64), _np(b).astype(np.float64)
+    assert a.shape == b.shape, (a.shape, b.shape)
+    nb = np.linalg.norm(b) + 1e-30
+    assert np.linalg.norm(a - b) <= rtol * nb, np.linalg.norm(a - b) / nb
+    bad = np.abs(a - b) > rtol * np.abs(b) + floor * np.abs(b).max()
+    assert not bad.any(), f"{bad.sum()} bad, worst {np.abs(a - b)[bad].max()}"
+
+
+def nclose(a, b, rtol):
+    a, b = _np(a).astype(np.float64), _np(b).astype(np.float64)
+    assert a.shape == b.shape
+    e = np.linalg.norm(a - b) / (np.linalg.norm(b) + 1e-30)
+    assert e <= rtol, e
+
+
+def _layer(name, cfg, g, dev):
+    from layers.conv_layer import CausalConv1d, CausalConvTranspose1d
+    if len(cfg) == 7:
+        ci, co, k, s, d, hb, t = (int(v) for v in cfg)
+        m = CausalConv1d(ci, co, k, stride=s, dilation=d, bias=bool(hb))
+        p = m.conv
+    else:
+        ci, co, k, s, hb, t = (int(v) for v in cfg)
+        m = CausalConvTranspose1d(ci, co, k, s, bias=bool(hb))
+        p = m.deconv
+    with torch.no_grad():
+        p.weight.copy_(torch.from_numpy(g[f"{name}.w"]))
+        if p.bias is not None:
+            p.bias.copy_(torch.from_numpy(g[f"{name}.b"]))
+    return m.to(dev), p
+
+
+@pytest.mark.parametrize("name", ["first", "ru_d1", "ru_d3", "ru_d9", "down3", "down5", "proj", "last",
+                                  "up5", "up3", "up4"])
+def test_conv_layer_matches_reference_golden(gpu, name):
+    g = golden("conv")
+    m, p = _layer(name, g[f"{name}.cfg"], g, gpu)
+    x = torch.from_numpy(g[f"{name}.x"]).to(gpu).requires_grad_(True)
+    y = m(x)
+    close(y, g[f"{name}.y"], 1e-5)
+    y.backward(torch.from_numpy(g[f"{name}.gy"]).to(gpu))
+    close(x.grad, g[f"{name}.gx"])
+    close(p.weight.grad, g[f"{name}.gw"])
+    if p.bias is not None:
+        close(p.bias.grad, g[f"{name}.gb"])
+
+
+def test_residual_unit_matches_reference_golden(gpu):
+    from models.autoencoder.modules.residual_unit import CausalResidualUnit
+    g = golden("conv")
+    ru = CausalResidualUnit(8, 8, dilation=3)
+    with torch.no_grad():
+        ru.conv1.conv.weight.copy_(torch.from_numpy(g["ru.w1"]))
+        ru.conv2.weight.copy_(torch.from_numpy(g["ru.w2"]))
+    ru = ru.to(gpu)
+    x = torch.from_numpy(g["ru.x"]).to(gpu).requires_grad_(True)
+    y = ru(x)
+    close(y, g["ru.y"], 1e-5)
+    y.backward(torch.from_numpy(g["ru.gy"]).to(gpu))
+    close(x.grad, g["ru.gx"])
+    close(ru.conv1.conv.weight.grad, g["ru.gw1"])
+    close(ru.conv2.weight.grad, g["ru.gw2"])
+
+
+SHAPES = [
+    # (kind, Cin, Cout, k, stride, dil, bias, B, T)   full-width AudioDec layers, short T
+    ("conv", 32, 32, 7, 1, 9, False, 2, 600),
+    ("conv", 64, 64, 7, 1, 3, False, 2, 320),
+    ("conv", 256, 256, 7, 1, 9, False, 2, 80),
+    ("conv", 512, 512, 7, 1, 1, False, 2, 20),
+    ("conv", 512, 64, 3, 1, 1, False, 3, 20),
+    ("conv", 32, 1, 7, 1, 1, False, 2, 300),
+    ("conv", 1, 32, 7, 1, 1, False, 2, 300),
+    ("conv", 32, 64, 6, 3, 1, True, 2, 600),
+    ("conv", 256, 512, 10, 5, 1, True, 2, 100),
+    ("convT", 512, 256, 10, 5, 1, True, 2, 16),
+    ("convT", 64, 32, 6, 3, 1, True, 3, 100),
+]
+
+
+def _ref_and_dev(kind, ci, co, k, s, d, hb, B, T, dev, seed):
+    from layers.conv_layer import CausalConv1d, CausalConvTranspose1d
+    from oracle import ref_ops as R
+    torch.manual_seed(seed)
+    if kind == "conv":
+        m = CausalConv1d(ci, co, k, stride=s, dilation=d, bias=hb)
+        p = m.conv
+        ref = lambda x, w, b: R.causal_conv1d(x, w, b, s, d)
+    else:
+        m = CausalConvTranspose1d(ci, co, k, s, bias=hb)
+        p = m.deconv
+        ref = lambda x, w, b: R.causal_conv_transpose1d(x, w, b, s)
+    x = torch.randn(B, ci, T)
+    w = p.weight.detach().clone().requires_grad_(True)
+    b = p.bias.detach().clone().requires_grad_(True) if hb else None
+    xr = x.clone().requires_grad_(True)
+    yr = ref(xr, w, b)
+    gy = torch.randn_like(yr)
+    yr.backward(gy)
+    return m.to(dev), p, x, gy, (yr, xr.grad, w.grad, b.grad if hb else None)
+
+
+@pytest.mark.parametrize("shape", SHAPES, ids=[f"{s[0]}{s[1]}-{s[2]}k{s[3]}s{s[4]}d{s[5]}" for s in SHAPES])
+def test_conv_layer_fp32_vs_oracle(gpu, shape):
+    m, p, x, gy, (yr, gxr, gwr, gbr) = _ref_and_dev(*shape, gpu, seed=hash(shape) % 1000)
+    xd = x.to(gpu).requires_grad_(True)
+    y = m(xd)
+    close(y, yr, 1e-5)
+    y.backward(gy.to(gpu))
+    close(xd.grad, gxr)
+    close(p.weight.grad, gwr)
+    if gbr is not None:
+        close(p.bias.grad, gbr)
+
+
+@pytest.mark.parametrize("shape", SHAPES[:4] + SHAPES[7:], ids=lambda s: f"{s[0]}{s[1]}-{s[2]}")
+def test_conv_layer_bf16_vs_oracle(gpu, shape):
+    from sel import convops as CO
+    m, p, x, gy, (yr, gxr, gwr, gbr) = _ref_and_dev(*shape, gpu, seed=7)
+    xd = x.to(gpu).requires_grad_(True)
+    with CO.precision(torch.bfloat16):
+        y = m(xd)
+        assert y.dtype == torch.bfloat16
+        nclose(y, yr, 2e-2)
+        y.float().backward(gy.to(gpu))
+    nclose(xd.grad, gxr, 2e-2)
+    nclose(p.weight.grad, gwr, 2e-2)
+
+
+def test_channels_last_views_flow_without_copies(gpu):
+    from layers.conv_layer import CausalConv1d
+    a = CausalConv1d(32, 32, 7, dilation=3).to(gpu)
+    b = CausalConv1d(32, 64, 6, stride=3).to(gpu)
+    x = torch.randn(2, 32, 600, device=gpu)
+    y = a(x)
+    assert y.shape == (2, 32, 600) and y.stride(1) == 1  # (B,C,T) view of (B,T,C)
+    z = b(y)
+    assert z.shape == (2, 64, 200) and z.stride(1) == 1
