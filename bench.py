@@ -96,13 +96,92 @@ def c2_cpu_baseline(B_sample=4, steps=3):
 
 
 # ---------------------------------------------------------------------------
+# c3: full denoise-trainer step
+# ---------------------------------------------------------------------------
+
+C3_CONFIG = "symAD_libritts_24000_hop300"
+
+
+def c3_setup(dev, B, world, local):
+    from sel import configs
+    from sel.convops import precision
+    from models.autoencoder.AudioDec import Generator
+    from losses import MultiMelSpectrogramLoss
+    from trainer.denoise import Trainer
+    from dataloader.data_utils import add_noise
+
+    cfg = configs.get(C3_CONFIG)
+    cfg["outdir"] = None
+    cfg["train_max_steps"] = 1 << 40
+    torch.manual_seed(93)
+    G = Generator(**cfg["generator_params"]).to(dev)
+    model = {"generator": G, "discriminator": None}
+    if world > 1:
+        from torch.nn.parallel import DistributedDataParallel as DDP
+        # freeze first so DDP only buckets the trainable (encoder + projector) grads
+        for p in list(G.quantizer.parameters()) + list(G.decoder.parameters()):
+            p.requires_grad = False
+        model["generator"] = DDP(G, device_ids=[local], broadcast_buffers=False, bucket_cap_mb=16)
+    mel = MultiMelSpectrogramLoss(**cfg["mel_loss_params"]).to(dev)
+    opt = torch.optim.Adam(G.parameters(), **cfg["generator_optimizer_params"])
+    sched = torch.optim.lr_scheduler.StepLR(opt, **cfg["generator_scheduler_params"])
+    tr = Trainer(steps=0, epochs=0, data_loader={}, model=model, criterion={"mel": mel},
+                 optimizer={"generator": opt}, scheduler={"generator": sched}, config=cfg, device=dev)
+    clean, noise = synthetic_batch(B, SR, seed=93 + 2 * int(os.environ.get("RANK", "0")))
+    clean, noise = clean.to(dev), noise.to(dev)
+    mixed = add_noise(clean, noise, 15)
+
+    def step():
+        with precision(torch.bfloat16):
+            tr._train_step((mixed, clean))
+    return step
+
+
+def c3_cpu_baseline(B_sample=2, steps=2):
+    """Oracle (op-for-op PyTorch-CPU restatement) of the same denoise-trainer step."""
+    from oracle import ref_ops as R
+    from oracle.melfilters import mel as melbank
+    from sel import configs
+    cfg = configs.get(C3_CONFIG)
+    mp = cfg["mel_loss_params"]
+    mm = torch.from_numpy(melbank(sr=mp["fs"], n_fft=2048, n_mels=80, fmin=mp["fmin"], fmax=mp["fmax"]).T.copy())
+    torch.manual_seed(93)
+    from models.autoencoder.AudioDec import Generator
+    P = {k: v.clone() for k, v in Generator(**cfg["generator_params"]).state_dict().items()}
+    train = [k for k in P if (k.startswith("encoder.") or k.startswith("projector.")) and
+             (k.endswith("weight") or k.endswith("bias"))]
+    for k in train:
+        P[k].requires_grad_(True)
+    opt = torch.optim.Adam([P[k] for k in train], **cfg["generator_optimizer_params"])
+    geo = R.generator_geometry()
+    clean, noise = synthetic_batch(B_sample, SR)
+    mixed = R.add_noise(clean, noise, 15)
+    win = R.hann(2048)
+
+    def step():
+        y, zq, z, vql, ppl = R.generator_forward(P, mixed, geo, pqc=True)
+        loss = vql.sum() * cfg["lambda_vq_loss"] + cfg["lambda_mel_loss"] * R.multi_mel_loss(
+            y, clean, [(2048, 300, 2048)], [win], [mm], 1e-10, None)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+    step()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    dt = (time.perf_counter() - t0) / steps
+    return B_sample * SR / HOP / dt, (f"oracle (PyTorch-CPU op-for-op restatement) denoise-trainer step, "
+                                      f"PQC generator fp32, B={B_sample} x 1 s, {steps} timed steps")
+
+
+# ---------------------------------------------------------------------------
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default="c2", choices=["c2", "c3"])
+    ap.add_argument("--config", default="c3", choices=["c2", "c3"])
     ap.add_argument("--batch", type=int, default=0, help="per-GPU batch (default: config's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -125,7 +204,12 @@ def main():
         workload = "configs[1]: MR-STFT(3 res) + mel(2048/300/80) loss fwd+bwd, fp32, 1 s @ 24 kHz"
         dtype = "fp32"
     else:
-        raise SystemExit("c3 not built yet")
+        step = c3_setup(dev, B, world, local)
+        dom = "sel_conv_fwd"
+        bytes_fn = None
+        workload = (f"configs[2]/[3]: denoise-trainer step (trainer/denoise.py) on the PQC AudioDec generator, "
+                    f"{C3_CONFIG} (derived), bf16 convs / fp32 losses, {B} x 1 s @ 24 kHz per GPU")
+        dtype = "bf16"
 
     for _ in range(args.warmup):
         step()
@@ -155,6 +239,7 @@ def main():
     ms_per_step = 1e3 * elapsed / args.steps
     frames = world * B * SR / HOP * args.steps
     value = frames / elapsed
+    avg_ms, achieved = 0.0, 0.0
     if cfg == "c2":
         per_step = len(durs) // args.steps
         sel_d = durs[per_step - 1::per_step]  # last resolution (n_fft=512) of each step
@@ -169,7 +254,7 @@ def main():
         ncores = len(os.sched_getaffinity(0))
         ncores = min(ncores, int(os.environ.get("OMP_NUM_THREADS", ncores)))
         torch.set_num_threads(ncores)
-        v, sample = c2_cpu_baseline()
+        v, sample = c2_cpu_baseline() if cfg == "c2" else c3_cpu_baseline()
         cpu = {"value": round(v, 1), "unit": "frames/s", "cores": ncores, "kind": "port", "sample": sample}
 
     if rank == 0:

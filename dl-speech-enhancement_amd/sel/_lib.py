@@ -53,6 +53,8 @@ SIGNATURES = {
     "sel_rvq_fwd": (I32, [P, I64, I32, P, I32, I32, P, P, P, P, P, SZ, P]),
     "sel_rvq_finish": (I32, [P, P, I64, I32, I32, I32, F32, P, P, P]),
     "sel_rvq_bwd": (I32, [P, I64, I32, P, I32, P, P, P, F32, P, P]),
+    "sel_add_noise_workspace": (SZ, [I64]),
+    "sel_add_noise": (I32, [P, P, I64, F32, P, P, SZ, P]),
 }
 
 _lock = threading.Lock()

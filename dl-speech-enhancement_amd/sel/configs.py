@@ -1,0 +1,59 @@
+"""Hot-path hyper-parameters of the reference configs (no reference YAML is
+shipped; these are the keys the training step reads).
+
+* SYMAD_24MEL — config/denoise/symAD_24Mel.yaml (train_denoise.py's config).
+* SYMAD_LIBRITTS_24K_DENOISE — BASELINE config C4 names
+  config/denoise/symAD_libritts_24000_hop300, which does not exist in the
+  reference.  Derived from config/autoencoder/symAD_libritts_24000_hop300.yaml
+  exactly as the shipped 48 kHz pair differs: train_mode denoise,
+  mel win_lengths [null] (== n_fft 2048), batch_length 24000 (1 s).
+"""
+import copy
+
+GENERATOR = dict(input_channels=1, output_channels=1, encode_channels=32, decode_channels=32, code_dim=64,
+                 codebook_num=8, codebook_size=1024, bias=True, enc_ratios=[2, 4, 8, 16],
+                 dec_ratios=[16, 8, 4, 2], enc_strides=[3, 4, 5, 5], dec_strides=[5, 5, 4, 3], mode="causal",
+                 codec="audiodec", projector="conv1d", quantier="residual_vq")
+
+STFT = dict(fft_sizes=[1024, 2048, 512], hop_sizes=[120, 240, 50], win_lengths=[600, 1200, 240],
+            window="hann_window")
+
+SYMAD_LIBRITTS_24K_DENOISE = dict(
+    sampling_rate=24000, train_mode="denoise", initial="",
+    generator_params=GENERATOR,
+    use_mel_loss=True,
+    mel_loss_params=dict(fs=24000, fft_sizes=[2048], hop_sizes=[300], win_lengths=[None], window="hann_window",
+                         num_mels=80, fmin=0, fmax=12000, log_base=None),
+    use_stft_loss=False, stft_loss_params=STFT, use_shape_loss=False,
+    lambda_adv=1.0, lambda_feat_match=2.0, lambda_vq_loss=1.0, lambda_mel_loss=45.0, lambda_stft_loss=45.0,
+    lambda_shape_loss=45.0,
+    batch_size=16, batch_length=24000,
+    generator_optimizer_type="Adam", generator_optimizer_params=dict(lr=1.0e-4, betas=[0.5, 0.9], weight_decay=0.0),
+    generator_scheduler_type="StepLR", generator_scheduler_params=dict(step_size=200000, gamma=1.0),
+    generator_grad_norm=-1,
+    train_max_steps=200000, save_interval_steps=100000, eval_interval_steps=1000, log_interval_steps=100,
+)
+
+SYMAD_24MEL = dict(
+    sample_rate=24000, initial_model="", step=0, experiment_name="24Mel", epochs=500,
+    epoch_to_enable_discriminator=100, noise_dropout_rate=0.0, noise_dropout_rate_decay=0.05,
+    epoch_to_enable_noise_dropout_decay=1000, seed=93, lambda_snr_loss=0.0,
+    generator_params=GENERATOR,
+    use_mel_loss=True,
+    mel_loss_params=dict(fs=24000, fft_sizes=[2048], hop_sizes=[300], win_lengths=[None], window="hann_window",
+                         num_mels=80, fmin=0, fmax=24000, log_base=None),
+    use_stft_loss=False, stft_loss_params=STFT, use_shape_loss=False,
+    lambda_adv=1.0, lambda_feat_match=1000.0, lambda_vq_loss=1.0, lambda_mel_loss=45.0, lambda_stft_loss=45.0,
+    lambda_shape_loss=45.0,
+    batch_size=8, batch_length=96000,
+    generator_optimizer_type="Adam", generator_optimizer_params=dict(lr=5.0e-5, weight_decay=1.0e-6),
+    generator_scheduler_type="StepLR", generator_scheduler_params=dict(step_size=200000, gamma=1.0),
+    generator_grad_norm=1,
+    discriminator_optimizer_params=dict(lr=2.0e-4, weight_decay=1.0e-6), discriminator_grad_norm=1,
+)
+
+CONFIGS = {"symAD_libritts_24000_hop300": SYMAD_LIBRITTS_24K_DENOISE, "symAD_24Mel": SYMAD_24MEL}
+
+
+def get(name):
+    return copy.deepcopy(CONFIGS[name])

@@ -187,6 +187,13 @@ int sel_rvq_bwd(const float* x, int64_t N, int D, const float* embed0, int K, co
                 const float* g_out, const float* g_loss, float commitment, float* g_x,
                 sel_stream_t stream);
 
+/* ---- data glue: dataloader/data_utils.py:12-22 (add_noise) ---------------
+ * out = (exp(snr/10) * ||noise||_2 / ||speech||_2 * speech + noise) / 2 with
+ * BATCH-GLOBAL norms over all n elements (math.exp, not 10^x, as the reference). */
+size_t sel_add_noise_workspace(int64_t n);
+int sel_add_noise(const float* speech, const float* noise, int64_t n, float snr, float* out,
+                  void* ws, size_t ws_bytes, sel_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif
