@@ -135,6 +135,13 @@ __device__ __forceinline__ void mma_chunk(floatx4& acc, const __bf16* xs_row, co
   acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc, 0, 0, 0);
 }
 
+template <typename T> struct Vec16;
+template <> struct Vec16<float> { static constexpr int n = 4; };
+template <> struct Vec16<__bf16> { static constexpr int n = 8; };
+
+// Forward primitive.  Per 32-channel chunk: stage the input rows (with halo) and
+// the packed weights of ALL K taps once, one barrier pair, then K x TM x TN MFMAs
+// per wave.  Epilogue goes through LDS so every lane stores/loads 16 B vectors.
 template <typename TI, typename TO, int BM, int BN>
 __global__ __launch_bounds__(256) void k_conv_fwd(Args a, const TI* __restrict__ in,
                                                   const TI* __restrict__ wp,
@@ -143,11 +150,12 @@ __global__ __launch_bounds__(256) void k_conv_fwd(Args a, const TI* __restrict__
                                                   const TO* __restrict__ res, TO* __restrict__ out) {
   constexpr int P = Pitch<TI>::v;
   constexpr int TM = BM / 32, TN = BN / 32;  // 16x16 tiles per wave (2x2 waves)
+  constexpr int OP = BN + 4;                 // fp32 epilogue tile pitch
   extern __shared__ __align__(16) unsigned char smem[];
   const int halo = (a.K - 1) * a.dil;
   const int span = BM + halo;
   TI* xs = reinterpret_cast<TI*>(smem);
-  TI* ws = xs + span * P;
+  TI* ws = xs + span * P;  // [K][BN][P]
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -155,57 +163,101 @@ __global__ __launch_bounds__(256) void k_conv_fwd(Args a, const TI* __restrict__
   const int n0 = blockIdx.y * BN;
   const int64_t g0 = m0 - a.pad;
 
+  // per-lane output rows: local row and time index inside its sample
+  int lr[TM], tt[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    lr[i] = wm * (BM / 2) + i * 16 + (lane & 15);
+    const int64_t m = m0 + lr[i];
+    tt[i] = m < a.rows ? int(m % a.T) : -(1 << 30);
+  }
+
   floatx4 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  // per-lane A rows (one per 16-row tile): local row within the block tile
   for (int c0 = 0; c0 < a.C; c0 += CK) {
     __syncthreads();
     stage_rows<TI>(in, a, g0, span, c0, xs, a.in_elu != 0);
+    for (int k = 0; k < a.K; ++k) stage_w<TI, BN>(wp, a, n0, k, c0, ws + k * BN * P);
+    __syncthreads();
     for (int k = 0; k < a.K; ++k) {
-      if (k > 0) __syncthreads();
-      stage_w<TI, BN>(wp, a, n0, k, c0, ws);
-      __syncthreads();
+      const TI* wk = ws + k * BN * P;
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        const int lr = wm * (BM / 2) + i * 16 + (lane & 15);
-        const int64_t m = m0 + lr;
-        // row in xs for (m, k): in_row(m,k) - g0 ; validity from the sample bounds
-        int64_t g = m < a.rows ? in_row(a, m, k) : -1;
-        const bool valid = g >= 0;
-        const int xr = valid ? int(g - g0) : 0;
-        const TI* xrow = xs + xr * P;
+        int ti = tt[i] + k * a.dil - a.pad;
+        bool valid = ti >= 0 && ti < a.T;
+        int xr = lr[i] + k * a.dil;
+        if (!valid && a.pad_mode == SEL_PAD_REPLICATE && tt[i] >= 0) {
+          const int tc = ti < 0 ? 0 : a.T - 1;
+          xr = lr[i] + a.pad + tc - tt[i];
+          valid = true;
+        }
+        const TI* xrow = xs + (valid ? xr : 0) * P;
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           const int nc = wn * (BN / 2) + j * 16 + (lane & 15);
-          mma_chunk(acc[i][j], xrow, ws + nc * P, lane, valid);
+          mma_chunk(acc[i][j], xrow, wk + nc * P, lane, valid);
         }
       }
     }
   }
 
-  // epilogue: col = lane & 15, row = 4*(lane >> 4) + e
+  // epilogue: accumulators -> LDS (fp32) -> 16-B vectors with bias / ELU' / residual
+  __syncthreads();
+  float* ot = reinterpret_cast<float*>(smem);
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      const int n = n0 + wn * (BN / 2) + j * 16 + (lane & 15);
-      if (n >= a.N) continue;
-      const float bv = (bias && a.bias_period) ? bias[n % a.bias_period] : 0.f;
+      const int col = wn * (BN / 2) + j * 16 + (lane & 15);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int64_t m = m0 + wm * (BM / 2) + i * 16 + 4 * (lane >> 4) + e;
-        if (m >= a.rows) continue;
-        const int64_t o = m * a.N + n;
-        float v = acc[i][j][e] + bv;
-        if (aux) v *= elu_grad(to_f(aux[o]));
-        if (res) v += to_f(res[o]);
-        out[o] = from_f<TO>(v);
+      for (int e = 0; e < 4; ++e) ot[(wm * (BM / 2) + i * 16 + 4 * (lane >> 4) + e) * OP + col] = acc[i][j][e];
+    }
+  __syncthreads();
+  constexpr int V = Vec16<TO>::n;
+  const bool vec_ok = (a.N % V) == 0;
+  for (int idx = threadIdx.x; idx < BM * (BN / V); idx += blockDim.x) {
+    const int r = idx / (BN / V), cv = (idx % (BN / V)) * V;
+    const int64_t m = m0 + r;
+    const int n = n0 + cv;
+    if (m >= a.rows || n >= a.N) continue;
+    const int64_t o = m * a.N + n;
+    float v[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      const int ne = n + e;
+      const float bv = (bias && a.bias_period && ne < a.N) ? bias[ne % a.bias_period] : 0.f;
+      v[e] = ot[r * OP + cv + e] + bv;
+    }
+    if (vec_ok) {
+      if (aux) {
+        TO av[V];
+        *reinterpret_cast<uint4*>(av) = *reinterpret_cast<const uint4*>(aux + o);
+#pragma unroll
+        for (int e = 0; e < V; ++e) v[e] *= elu_grad(to_f(av[e]));
+      }
+      if (res) {
+        TO rv[V];
+        *reinterpret_cast<uint4*>(rv) = *reinterpret_cast<const uint4*>(res + o);
+#pragma unroll
+        for (int e = 0; e < V; ++e) v[e] += to_f(rv[e]);
+      }
+      TO ov[V];
+#pragma unroll
+      for (int e = 0; e < V; ++e) ov[e] = from_f<TO>(v[e]);
+      *reinterpret_cast<uint4*>(out + o) = *reinterpret_cast<uint4*>(ov);
+    } else {
+      for (int e = 0; e < V && n + e < a.N; ++e) {
+        float x = v[e];
+        if (aux) x *= elu_grad(to_f(aux[o + e]));
+        if (res) x += to_f(res[o + e]);
+        out[o + e] = from_f<TO>(x);
       }
     }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -314,25 +366,149 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(Args a, const TI* __restrict
     bpart[int64_t(split) * a.N + n0 + threadIdx.x] = bsum;
 }
 
-__global__ __launch_bounds__(256) void k_split_reduce(const float* __restrict__ part, int nsplit,
-                                                      int64_t n, float* __restrict__ out) {
-  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
-       i += int64_t(gridDim.x) * blockDim.x) {
-    float s = 0.f;
-    for (int p = 0; p < nsplit; ++p) s += part[int64_t(p) * n + i];
-    out[i] = s;
-  }
+// bf16 weight gradient.  One workgroup owns (n-tile BN, c-tile 32, all K taps) and
+// a contiguous range of 64-row m-tiles that never cross a sample boundary (so
+// the causal halo can be zero/replicate-filled while staging and no per-element
+// masks are needed).  Both MFMA operands reduce over m, i.e. over the ROW index
+// of the row-major LDS tiles: they are read with ds_read_b64_tr_b16 (gfx950
+// transposing LDS read, 4 rows x 16 columns per 16-lane group).  The MFMA k-index
+// kk = 8g + e maps to tile row 4g + e (e < 4) / 16 + 4g + e - 4 (e >= 4) so that
+// each 32-lane half reads 8 consecutive rows: with a row pitch of 8u dwords
+// (u odd) those reads are bank-conflict free.
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef short v8i16 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ v4i16 tr_read(const __bf16* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)(p));
+}
+__device__ __forceinline__ bf16x8 tr_frag(const __bf16* p, int pitch) {
+  const v4i16 lo = tr_read(p);
+  const v4i16 hi = tr_read(p + 16 * pitch);
+  const v8i16 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, v);
 }
 
-// bias grad: sum splits and phases: gb[j] = sum_{p, n % period == j} bpart[p][n]
-__global__ void k_bias_reduce(const float* __restrict__ bpart, int nsplit, int N, int period,
-                              float* __restrict__ gb) {
-  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < period; j += gridDim.x * blockDim.x) {
-    float s = 0.f;
-    for (int p = 0; p < nsplit; ++p)
-      for (int n = j; n < N; n += period) s += bpart[int64_t(p) * N + n];
-    gb[j] = s;
+constexpr int WB_BM = 64;
+constexpr int WB_BC = 32;
+constexpr int WB_MAXJ = 16;
+
+template <int BN>
+__global__ __launch_bounds__(256) void k_wgrad_bf16(Args a, const __bf16* __restrict__ gout,
+                                                    const __bf16* __restrict__ in, int tiles_per_sample,
+                                                    int64_t n_tiles, int tiles_per_split,
+                                                    float* __restrict__ part, float* __restrict__ bpart) {
+  constexpr int NT = BN / 16;
+  constexpr int WPN = 4 / NT;        // waves sharing one n-subtile
+  constexpr int PG = BN + 16;        // elements; (PG/2) dwords = 8 x odd
+  constexpr int PX = WB_BC + 16;     // 48 elements = 24 dwords
+  extern __shared__ __align__(16) unsigned char smem[];
+  __bf16* gs = reinterpret_cast<__bf16*>(smem);
+  __bf16* xs = gs + WB_BM * PG;
+  const int halo = (a.K - 1) * a.dil;
+  const int span = WB_BM + halo;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nt = wave % NT, wsub = wave / NT;
+  const int n0 = blockIdx.x * BN, c0 = blockIdx.y * WB_BC;
+  const int64_t tb = int64_t(blockIdx.z) * tiles_per_split;
+  const int64_t te = tb + tiles_per_split < n_tiles ? tb + tiles_per_split : n_tiles;
+  const int npairs = a.K * (WB_BC / 16);
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const bool vecG = (a.N % 8) == 0, vecX = (a.C % 8) == 0;
+
+  floatx4 acc[WB_MAXJ];
+#pragma unroll
+  for (int j = 0; j < WB_MAXJ; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  float bsum = 0.f;
+
+  for (int64_t tile = tb; tile < te; ++tile) {
+    const int64_t b = tile / tiles_per_sample;
+    const int t0 = int(tile % tiles_per_sample) * WB_BM;
+    const int64_t rb = b * a.T;
+    __syncthreads();
+    for (int idx = tid; idx < WB_BM * (BN / 8); idx += 256) {
+      const int r = idx / (BN / 8), v = (idx % (BN / 8)) * 8;
+      const int t = t0 + r, n = n0 + v;
+      __bf16 vals[8];
+      if (t < a.T && vecG && n + 8 <= a.N) {
+        *reinterpret_cast<uint4*>(vals) = *reinterpret_cast<const uint4*>(gout + (rb + t) * a.N + n);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          vals[e] = (t < a.T && n + e < a.N) ? gout[(rb + t) * a.N + n + e] : __bf16(0.f);
+      }
+      *reinterpret_cast<uint4*>(gs + r * PG + v) = *reinterpret_cast<uint4*>(vals);
+    }
+    for (int idx = tid; idx < span * (WB_BC / 8); idx += 256) {
+      const int r = idx / (WB_BC / 8), v = (idx % (WB_BC / 8)) * 8;
+      int ti = t0 - a.pad + r;
+      const int c = c0 + v;
+      bool ok = ti >= 0 && ti < a.T;
+      if (!ok && a.pad_mode == SEL_PAD_REPLICATE) {
+        ti = ti < 0 ? 0 : a.T - 1;
+        ok = true;
+      }
+      __bf16 vals[8];
+      if (ok && vecX && c + 8 <= a.C) {
+        *reinterpret_cast<uint4*>(vals) = *reinterpret_cast<const uint4*>(in + (rb + ti) * a.C + c);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) vals[e] = (ok && c + e < a.C) ? in[(rb + ti) * a.C + c + e] : __bf16(0.f);
+      }
+      if (a.in_elu) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) vals[e] = __bf16(elu(float(vals[e])));
+      }
+      *reinterpret_cast<uint4*>(xs + r * PX + v) = *reinterpret_cast<uint4*>(vals);
+    }
+    __syncthreads();
+    if (bpart && c0 == 0 && tid < BN) {
+      for (int r = 0; r < WB_BM; ++r) bsum += float(gs[r * PG + tid]);
+    }
+#pragma unroll
+    for (int grp = 0; grp < WB_BM / 32; ++grp) {
+      const bf16x8 A = tr_frag(gs + (grp * 32 + 4 * g + q) * PG + nt * 16 + 4 * p, PG);
+#pragma unroll
+      for (int j = 0; j < WB_MAXJ; ++j) {
+        const int pr = wsub + WPN * j;
+        if (pr >= npairs) break;
+        const int k = pr >> 1, ct = pr & 1;
+        const bf16x8 Bf = tr_frag(xs + (grp * 32 + 4 * g + q + k * a.dil) * PX + ct * 16 + 4 * p, PX);
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, Bf, acc[j], 0, 0, 0);
+      }
+    }
   }
+  float* pdst = part + int64_t(blockIdx.z) * a.N * a.K * a.C;
+#pragma unroll
+  for (int j = 0; j < WB_MAXJ; ++j) {
+    const int pr = wsub + WPN * j;
+    if (pr >= npairs) break;
+    const int k = pr >> 1, ct = pr & 1;
+    const int c = c0 + ct * 16 + (lane & 15);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int n = n0 + nt * 16 + 4 * (lane >> 4) + e;
+      if (n < a.N && c < a.C) pdst[(int64_t(n) * a.K + k) * a.C + c] = acc[j][e];
+    }
+  }
+  if (bpart && c0 == 0 && tid < BN && n0 + tid < a.N) bpart[int64_t(blockIdx.z) * a.N + n0 + tid] = bsum;
+}
+
+// Deterministic split reduction: out[j] = sum_s sum_{i % period == j} part[s*n + i]
+// (period == n: plain sum over splits).  64 outputs per block, 4 waves over splits.
+__global__ __launch_bounds__(256) void k_split_sum(const float* __restrict__ part, int nsplit, int64_t n,
+                                                   int period, float* __restrict__ out) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t j = int64_t(blockIdx.x) * 64 + lane;
+  float s = 0.f;
+  if (j < period) {
+    for (int sp = wave; sp < nsplit; sp += 4)
+      for (int64_t i = j; i < n; i += period) s += part[int64_t(sp) * n + i];
+  }
+  red[wave][lane] = s;
+  __syncthreads();
+  if (wave == 0 && j < period) out[j] = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
 }
 
 // ---------------------------------------------------------------------------
@@ -429,16 +605,24 @@ __global__ void k_unpack(int kind, const float* __restrict__ gp, int cout, int c
   }
 }
 
+// adjoint of the replicate pad: gin[b*T, c] += sum_n gout[b*T, n] * Wp[n][0][c]
+// block = (sample b, 64 channels); 16 waves split n, LDS reduce.
 template <typename T>
-__global__ void k_replicate_fix(Args a, const T* __restrict__ gout, const T* __restrict__ wp,
-                                T* __restrict__ gin) {
-  // one block per sample b, threads over c
-  const int64_t b = blockIdx.x;
-  const int64_t row = b * a.T;
-  for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
-    float s = 0.f;
-    for (int n = 0; n < a.N; ++n) s += to_f(gout[row * a.N + n]) * to_f(wp[(int64_t(n) * a.K + 0) * a.C + c]);
-    gin[row * a.C + c] = from_f<T>(to_f(gin[row * a.C + c]) + s);
+__global__ __launch_bounds__(1024) void k_replicate_fix(Args a, const T* __restrict__ gout, const T* __restrict__ wp,
+                                                        T* __restrict__ gin) {
+  __shared__ float red[16][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t row = int64_t(blockIdx.x) * a.T;
+  const int c = blockIdx.y * 64 + lane;
+  float s = 0.f;
+  if (c < a.C)
+    for (int n = wave; n < a.N; n += 16) s += to_f(gout[row * a.N + n]) * to_f(wp[(int64_t(n) * a.K + 0) * a.C + c]);
+  red[wave][lane] = s;
+  __syncthreads();
+  if (wave == 0 && c < a.C) {
+    float t = 0.f;
+    for (int w = 0; w < 16; ++w) t += red[w][lane];
+    gin[row * a.C + c] = from_f<T>(to_f(gin[row * a.C + c]) + t);
   }
 }
 
@@ -490,15 +674,22 @@ Args to_args(const sel_conv_desc* d) {
 }
 
 template <typename TI, typename TO, int BM, int BN>
+size_t fwd_lds(const Args& a) {
+  const size_t stage = (size_t(BM + (a.K - 1) * a.dil) + size_t(a.K) * BN) * Pitch<TI>::v * sizeof(TI);
+  const size_t epi = size_t(BM) * (BN + 4) * sizeof(float);
+  return stage > epi ? stage : epi;
+}
+
+template <typename TI, typename TO, int BM, int BN>
 int launch_fwd(const Args& a, const void* in, const void* wp, const float* bias, const void* aux,
                const void* res, void* out, hipStream_t s) {
-  const int span = BM + (a.K - 1) * a.dil;
-  const size_t lds = size_t(span + BN) * Pitch<TI>::v * sizeof(TI);
+  const size_t lds = fwd_lds<TI, TO, BM, BN>(a);
   SEL_REQUIRE(lds <= 160 * 1024, SEL_ERR_UNSUPPORTED, "conv tile needs %zu B of LDS", lds);
   dim3 grid(unsigned((a.rows + BM - 1) / BM), unsigned((a.N + BN - 1) / BN));
   if (grid.x == 0) return SEL_OK;
   auto kern = k_conv_fwd<TI, TO, BM, BN>;
-  if (lds > 64 * 1024) SEL_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
+  if (lds > 64 * 1024)
+    SEL_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
   hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, a, static_cast<const TI*>(in),
                      static_cast<const TI*>(wp), bias, static_cast<const TO*>(aux),
                      static_cast<const TO*>(res), static_cast<TO*>(out));
@@ -509,25 +700,44 @@ int launch_fwd(const Args& a, const void* in, const void* wp, const float* bias,
 template <typename TI, typename TO>
 int dispatch_fwd(const Args& a, const void* in, const void* wp, const float* bias, const void* aux,
                  const void* res, void* out, hipStream_t s) {
-  // tile choice: narrow outputs use BN=32; long thin GEMMs BM=128
+  // Tiles sized so the staged input+weights of one 32-channel chunk stay <= ~53 KB
+  // (3 workgroups per CU) for the common taps; narrow outputs use BN = 32.
+  if (sizeof(TI) == 4) {
+    if (a.N <= 32) return launch_fwd<TI, TO, 128, 32>(a, in, wp, bias, aux, res, out, s);
+    return launch_fwd<TI, TO, 64, 64>(a, in, wp, bias, aux, res, out, s);
+  }
   if (a.N <= 32) return launch_fwd<TI, TO, 128, 32>(a, in, wp, bias, aux, res, out, s);
-  if (a.N <= 64) return launch_fwd<TI, TO, 128, 64>(a, in, wp, bias, aux, res, out, s);
+  if (a.N <= 64 || a.K >= 5) return launch_fwd<TI, TO, 128, 64>(a, in, wp, bias, aux, res, out, s);
   if (a.rows >= 4096) return launch_fwd<TI, TO, 128, 128>(a, in, wp, bias, aux, res, out, s);
   return launch_fwd<TI, TO, 64, 64>(a, in, wp, bias, aux, res, out, s);
 }
 
 constexpr int kWgBN = 64;
 
-void wgrad_plan(const sel_conv_desc* d, int& nsplit, int64_t& rows_per_split) {
-  const int ntiles = ((d->N + kWgBN - 1) / kWgBN) * ((d->C + CK - 1) / CK);
-  int64_t chunks = (d->rows + WG_BM - 1) / WG_BM;
-  int want = std::max(1, 1024 / ntiles);
-  nsplit = int(std::min<int64_t>(chunks, want));
-  nsplit = std::max(nsplit, 1);
-  int64_t cps = (chunks + nsplit - 1) / nsplit;
-  rows_per_split = cps * WG_BM;
-  nsplit = int((d->rows + rows_per_split - 1) / rows_per_split);
-  nsplit = std::max(nsplit, 1);
+int wgrad_bn(int N) { return N <= 16 ? 16 : (N <= 32 ? 32 : 64); }
+
+// Split plan shared by both dtypes: 64-row m-tiles that never cross a sample,
+// enough splits for ~2 workgroups per CU, partial buffer capped at 64 MB.
+struct WgPlan {
+  int64_t tiles_per_sample, n_tiles;
+  int nsplit, tiles_per_split, bn;
+};
+
+WgPlan wgrad_plan(const sel_conv_desc* d) {
+  WgPlan p;
+  p.bn = wgrad_bn(d->N);
+  p.tiles_per_sample = (d->T + WB_BM - 1) / WB_BM;
+  p.n_tiles = (d->rows / d->T) * p.tiles_per_sample;
+  const int64_t blocks = int64_t((d->N + p.bn - 1) / p.bn) * ((d->C + WB_BC - 1) / WB_BC);
+  int64_t want = std::max<int64_t>(1, (512 + blocks - 1) / blocks);
+  const int64_t per_split = (int64_t(d->N) * d->K * d->C + d->N) * 4;
+  want = std::min<int64_t>(want, std::max<int64_t>(1, (int64_t(64) << 20) / per_split));
+  want = std::min<int64_t>(want, std::max<int64_t>(1, p.n_tiles));
+  p.tiles_per_split = int((p.n_tiles + want - 1) / want);
+  if (p.tiles_per_split < 1) p.tiles_per_split = 1;
+  p.nsplit = int((p.n_tiles + p.tiles_per_split - 1) / p.tiles_per_split);
+  if (p.nsplit < 1) p.nsplit = 1;
+  return p;
 }
 
 }  // namespace
@@ -550,53 +760,74 @@ int sel_conv_fwd(const sel_conv_desc* d, int in_dtype, int out_dtype, const void
 }
 
 size_t sel_conv_wgrad_workspace(const sel_conv_desc* d) {
-  if (!d || d->rows <= 0) return 16;
-  int nsplit;
-  int64_t rps;
-  wgrad_plan(d, nsplit, rps);
-  return size_t(nsplit) * (size_t(d->N) * d->K * d->C + d->N) * sizeof(float);
+  if (!d || d->rows <= 0 || d->T <= 0) return 16;
+  const WgPlan p = wgrad_plan(d);
+  return size_t(p.nsplit) * (size_t(d->N) * d->K * d->C + d->N) * sizeof(float);
 }
 
 int sel_conv_wgrad(const sel_conv_desc* d, int dtype, const void* gout, const void* in, float* gwpack,
                    float* gbias, void* ws, size_t ws_bytes, sel_stream_t stream) {
   if (int rc = check_desc(d)) return rc;
-  SEL_REQUIRE(d->K * (kWgBN / 16) * 2 <= 4 * WG_MAXT, SEL_ERR_UNSUPPORTED, "wgrad: K=%d too large", d->K);
+  SEL_REQUIRE(d->K * 2 <= WB_MAXJ * 1 || dtype == SEL_F32, SEL_ERR_UNSUPPORTED, "wgrad: K=%d too large", d->K);
+  SEL_REQUIRE(dtype == SEL_BF16 || d->K * (kWgBN / 16) * 2 <= 4 * WG_MAXT, SEL_ERR_UNSUPPORTED,
+              "wgrad: K=%d too large", d->K);
   SEL_REQUIRE(ws_bytes >= sel_conv_wgrad_workspace(d), SEL_ERR_WORKSPACE, "workspace too small");
   const Args a = to_args(d);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  int nsplit;
-  int64_t rps;
-  wgrad_plan(d, nsplit, rps);
+  const WgPlan p = wgrad_plan(d);
   float* part = static_cast<float*>(ws);
-  float* bpart = gbias ? part + size_t(nsplit) * d->N * d->K * d->C : nullptr;
-  const int span = WG_BM + (d->K - 1) * d->dil;
-  const size_t lds = (size_t(WG_BM) * (kWgBN + WG_GP) + size_t(span) * (CK + WG_GP)) * sizeof(float);
-  SEL_REQUIRE(lds <= 160 * 1024, SEL_ERR_UNSUPPORTED, "wgrad tile needs %zu B of LDS", lds);
-  dim3 grid(unsigned((d->N + kWgBN - 1) / kWgBN), unsigned((d->C + CK - 1) / CK), unsigned(nsplit));
-  if (d->rows > 0) {
-    if (dtype == SEL_F32) {
-      auto kern = k_conv_wgrad<float, kWgBN>;
-      if (lds > 64 * 1024) SEL_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
-      hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, a, static_cast<const float*>(gout),
-                         static_cast<const float*>(in), rps, part, bpart);
-    } else if (dtype == SEL_BF16) {
-      auto kern = k_conv_wgrad<__bf16, kWgBN>;
-      if (lds > 64 * 1024) SEL_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
-      hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, a, static_cast<const __bf16*>(gout),
-                         static_cast<const __bf16*>(in), rps, part, bpart);
-    } else {
-      set_error("bad dtype %d", dtype);
-      return SEL_ERR_ARG;
-    }
+  float* bpart = gbias ? part + size_t(p.nsplit) * d->N * d->K * d->C : nullptr;
+  if (d->rows > 0 && dtype == SEL_BF16) {
+    const int span = WB_BM + (d->K - 1) * d->dil;
+    const size_t lds = (size_t(WB_BM) * (p.bn + 16) + size_t(span) * (WB_BC + 16)) * sizeof(__bf16);
+    SEL_REQUIRE(lds <= 160 * 1024, SEL_ERR_UNSUPPORTED, "wgrad tile needs %zu B of LDS", lds);
+    dim3 grid(unsigned((d->N + p.bn - 1) / p.bn), unsigned((d->C + WB_BC - 1) / WB_BC), unsigned(p.nsplit));
+#define SEL_WG_LAUNCH(BNV)                                                                                     \
+  {                                                                                                            \
+    auto kern = k_wgrad_bf16<BNV>;                                                                             \
+    if (lds > 64 * 1024)                                                                                       \
+      SEL_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));   \
+    hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, a, static_cast<const __bf16*>(gout),                     \
+                       static_cast<const __bf16*>(in), int(p.tiles_per_sample), p.n_tiles, p.tiles_per_split,  \
+                       part, bpart);                                                                           \
+  }
+    if (p.bn == 16) SEL_WG_LAUNCH(16)
+    else if (p.bn == 32) SEL_WG_LAUNCH(32)
+    else SEL_WG_LAUNCH(64)
+#undef SEL_WG_LAUNCH
     SEL_LAUNCH_CHECK();
+  } else if (d->rows > 0 && dtype == SEL_F32) {
+    // fp32 parity path: flat row ranges, same number of splits as the plan
+    const int64_t rps = ((d->rows + p.nsplit - 1) / p.nsplit + WG_BM - 1) / WG_BM * WG_BM;
+    const int nsplit = int((d->rows + rps - 1) / rps);
+    SEL_REQUIRE(nsplit <= p.nsplit, SEL_ERR_STATE, "internal split plan mismatch");
+    const int span = WG_BM + (d->K - 1) * d->dil;
+    const size_t lds = (size_t(WG_BM) * (kWgBN + WG_GP) + size_t(span) * (CK + WG_GP)) * sizeof(float);
+    SEL_REQUIRE(lds <= 160 * 1024, SEL_ERR_UNSUPPORTED, "wgrad tile needs %zu B of LDS", lds);
+    // unused tail splits must contribute zeros
+    if (nsplit < p.nsplit)
+      SEL_HIP(hipMemsetAsync(part + size_t(nsplit) * d->N * d->K * d->C, 0,
+                             size_t(p.nsplit - nsplit) * d->N * d->K * d->C * sizeof(float), s));
+    if (bpart && nsplit < p.nsplit)
+      SEL_HIP(hipMemsetAsync(bpart + size_t(nsplit) * d->N, 0, size_t(p.nsplit - nsplit) * d->N * sizeof(float), s));
+    dim3 grid(unsigned((d->N + kWgBN - 1) / kWgBN), unsigned((d->C + CK - 1) / CK), unsigned(nsplit));
+    auto kern = k_conv_wgrad<float, kWgBN>;
+    if (lds > 64 * 1024)
+      SEL_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
+    hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, a, static_cast<const float*>(gout),
+                       static_cast<const float*>(in), rps, part, bpart);
+    SEL_LAUNCH_CHECK();
+  } else if (d->rows > 0) {
+    set_error("bad dtype %d", dtype);
+    return SEL_ERR_ARG;
   }
   const int64_t nw = int64_t(d->N) * d->K * d->C;
-  hipLaunchKernelGGL(k_split_reduce, dim3(unsigned(std::min<int64_t>(1024, (nw + 255) / 256))), dim3(256), 0, s,
-                     part, nsplit, nw, gwpack);
+  hipLaunchKernelGGL(k_split_sum, dim3(unsigned((nw + 63) / 64)), dim3(256), 0, s, part, p.nsplit, nw, int(nw),
+                     gwpack);
   SEL_LAUNCH_CHECK();
   if (gbias) {
-    hipLaunchKernelGGL(k_bias_reduce, dim3(unsigned((d->bias_period + 255) / 256)), dim3(256), 0, s, bpart,
-                       nsplit, d->N, d->bias_period, gbias);
+    hipLaunchKernelGGL(k_split_sum, dim3(unsigned((d->bias_period + 63) / 64)), dim3(256), 0, s, bpart,
+                       p.nsplit, int64_t(d->N), d->bias_period, gbias);
     SEL_LAUNCH_CHECK();
   }
   return SEL_OK;
@@ -653,11 +884,12 @@ int sel_conv_replicate_fix(const sel_conv_desc* d, int dtype, const void* gout, 
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const unsigned nb = unsigned(d->rows / d->T);
   if (nb == 0) return SEL_OK;
+  const dim3 grid(nb, unsigned((d->C + 63) / 64));
   if (dtype == SEL_F32)
-    hipLaunchKernelGGL(k_replicate_fix<float>, dim3(nb), dim3(256), 0, s, a, static_cast<const float*>(gout),
+    hipLaunchKernelGGL(k_replicate_fix<float>, grid, dim3(1024), 0, s, a, static_cast<const float*>(gout),
                        static_cast<const float*>(wpack), static_cast<float*>(gin));
   else
-    hipLaunchKernelGGL(k_replicate_fix<__bf16>, dim3(nb), dim3(256), 0, s, a, static_cast<const __bf16*>(gout),
+    hipLaunchKernelGGL(k_replicate_fix<__bf16>, grid, dim3(1024), 0, s, a, static_cast<const __bf16*>(gout),
                        static_cast<const __bf16*>(wpack), static_cast<__bf16*>(gin));
   SEL_LAUNCH_CHECK();
   return SEL_OK;

@@ -1,0 +1,15 @@
+#!/bin/bash
+# One GPU session: parity tests, bench, rocprof kernel stats.  Usage: tools/gpu_round.sh <tag> [tests...]
+set -o pipefail
+TAG=${1:-run}; shift
+TESTS=${@:-tests}
+OUT=$GRAFT_REPO_ROOT/gpurun_out
+mkdir -p $OUT
+timeout -k 10 600 python -m pytest $TESTS -q -m gpu -x > $OUT/${TAG}_tests.log 2>&1
+echo "tests rc=$?"; tail -3 $OUT/${TAG}_tests.log
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $OUT/${TAG}_bench.log 2>&1 || exit 1
+tail -1 $OUT/${TAG}_bench.log
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/${TAG}_prof -o run -- \
+  python $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 2 --no-cpu-baseline > $OUT/${TAG}_prof.log 2>&1
+echo "prof rc=$?"
