@@ -261,6 +261,203 @@ __global__ __launch_bounds__(256) void k_conv_fwd(Args a, const TI* __restrict__
 }
 
 // ---------------------------------------------------------------------------
+// bf16 forward primitive (the hot one).  Per 32-channel chunk the input rows
+// [m0 - pad, m0 + BM + (K-1)*dil - pad) are staged ONCE (ELU applied once per
+// element) together with the packed weights of all K taps; the K taps then
+// re-read the staged rows at shifted offsets (implicit GEMM).  The next
+// chunk's rows/weights are fetched into registers while the current chunk's
+// MFMAs run (T14 issue-early / write-late), and all global loads are branch-free
+// (clamped address + select; requires C % 32 == 0) so hipcc emits no per-element
+// fallback waits.  MFMA: v_mfma_f32_32x32x16_bf16; staged rows are 80 B apart,
+// which makes its 16-B fragment reads bank-conflict free.
+// ---------------------------------------------------------------------------
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+constexpr int F4_HALOMAX = 64;
+constexpr int F4_P = 40;  // staged row pitch (bf16 elements) = 80 B
+
+template <int BM, int BN, int WAVES_M, int KMAX, typename TO>
+__global__ __launch_bounds__(256) void k_conv_fwd_bf16(Args a, const __bf16* __restrict__ in,
+                                                       const __bf16* __restrict__ wp,
+                                                       const float* __restrict__ bias,
+                                                       const TO* __restrict__ aux, const TO* __restrict__ res,
+                                                       TO* __restrict__ out) {
+  constexpr int P = F4_P;
+  constexpr int WAVES_N = 4 / WAVES_M;
+  constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
+  constexpr int TM = WTM / 32, TN = WTN / 32;
+  constexpr int XV = ((BM + F4_HALOMAX) * 4 + 255) / 256;
+  constexpr int WV = (KMAX * BN * 4 + 255) / 256;
+  constexpr int OP = BN + 4;
+  extern __shared__ __align__(16) unsigned char smem[];
+  __bf16* const xs = reinterpret_cast<__bf16*>(smem);
+  const int halo = (a.K - 1) * a.dil;
+  const int span = BM + halo;
+  __bf16* const ws = xs + span * P;  // [k][BN][P]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+  const int64_t m0 = int64_t(blockIdx.x) * BM;
+  const int n0 = blockIdx.y * BN;
+  const int64_t g0 = m0 - a.pad;
+  const int nchunk = a.C / CK;
+
+  // staging rows of this thread: flat row g = g0 + (v >> 2); clamp into [0, rows)
+  int64_t xrow[XV];
+  bool xok[XV];
+#pragma unroll
+  for (int u = 0; u < XV; ++u) {
+    const int r = (tid + u * 256) >> 2;
+    const int64_t g = g0 + r;
+    xok[u] = r < span && g >= 0 && g < a.rows;
+    xrow[u] = xok[u] ? g : 0;
+  }
+  uint4 xr[XV], wr[WV];
+  auto load = [&](int c0) {
+#pragma unroll
+    for (int u = 0; u < XV; ++u) {
+      const int c = c0 + ((tid + u * 256) & 3) * 8;
+      uint4 v = *reinterpret_cast<const uint4*>(in + xrow[u] * a.C + c);
+      if (!xok[u]) v = make_uint4(0, 0, 0, 0);
+      xr[u] = v;
+    }
+#pragma unroll
+    for (int u = 0; u < WV; ++u) {
+      const int v = tid + u * 256;
+      const int k = v / (BN * 4), n = (v >> 2) % BN, c = c0 + (v & 3) * 8;
+      const bool ok = k < a.K && n0 + n < a.N;
+      uint4 val = *reinterpret_cast<const uint4*>(wp + (int64_t(ok ? n0 + n : 0) * a.K + (ok ? k : 0)) * a.C + c);
+      if (!ok) val = make_uint4(0, 0, 0, 0);
+      wr[u] = val;
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int u = 0; u < XV; ++u) {
+      const int v = tid + u * 256;
+      if ((v >> 2) >= span) continue;
+      uint4 val = xr[u];
+      if (a.in_elu) {
+        __bf16* t = reinterpret_cast<__bf16*>(&val);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) t[e] = __bf16(elu(float(t[e])));
+      }
+      *reinterpret_cast<uint4*>(xs + (v >> 2) * P + (v & 3) * 8) = val;
+    }
+#pragma unroll
+    for (int u = 0; u < WV; ++u) {
+      const int v = tid + u * 256;
+      const int k = v / (BN * 4), n = (v >> 2) % BN;
+      if (k < a.K) *reinterpret_cast<uint4*>(ws + (k * BN + n) * P + (v & 3) * 8) = wr[u];
+    }
+  };
+
+  // per-lane output row (one per 32-row tile) -> time index within its sample
+  int lr[TM], tt[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    lr[i] = wm * WTM + i * 32 + (lane & 31);
+    const int64_t m = m0 + lr[i];
+    tt[i] = m < a.rows ? int(m % a.T) : -(1 << 30);
+  }
+
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  load(0);
+  for (int ch = 0; ch < nchunk; ++ch) {
+    if (ch) __syncthreads();
+    store();
+    __syncthreads();
+    if (ch + 1 < nchunk) load((ch + 1) * CK);
+    for (int k = 0; k < a.K; ++k) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {  // two K=16 halves of the 32-channel chunk
+        const int co = 16 * h + 8 * (lane >> 5);
+        bf16x8 bf[TN];
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          bf[j] = *reinterpret_cast<const bf16x8*>(ws + (k * BN + wn * WTN + j * 32 + (lane & 31)) * P + co);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int ti = tt[i] + k * a.dil - a.pad;
+          bool valid = ti >= 0 && ti < a.T;
+          int xrw = lr[i] + k * a.dil;
+          if (!valid && a.pad_mode == SEL_PAD_REPLICATE && tt[i] >= 0) {
+            xrw = lr[i] + a.pad + (ti < 0 ? 0 : a.T - 1) - tt[i];
+            valid = true;
+          }
+          bf16x8 af = *reinterpret_cast<const bf16x8*>(xs + (valid ? xrw : 0) * P + co);
+          if (!valid) af = bf16x8{};
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf[j], acc[i][j], 0, 0, 0);
+        }
+      }
+    }
+  }
+
+  // epilogue: C/D of 32x32x16: col = lane & 31, row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)
+  __syncthreads();
+  float* ot = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = wn * WTN + j * 32 + (lane & 31);
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        ot[(wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * OP + col] = acc[i][j][r];
+    }
+  __syncthreads();
+  constexpr int V = Vec16<TO>::n;
+  const bool vec_ok = (a.N % V) == 0;
+  for (int idx = tid; idx < BM * (BN / V); idx += 256) {
+    const int r = idx / (BN / V), cv = (idx % (BN / V)) * V;
+    const int64_t m = m0 + r;
+    const int n = n0 + cv;
+    if (m >= a.rows || n >= a.N) continue;
+    const int64_t o = m * a.N + n;
+    float v[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      const int ne = n + e;
+      const float bv = (bias && a.bias_period && ne < a.N) ? bias[ne % a.bias_period] : 0.f;
+      v[e] = ot[r * OP + cv + e] + bv;
+    }
+    if (vec_ok) {
+      if (aux) {
+        TO av[V];
+        *reinterpret_cast<uint4*>(av) = *reinterpret_cast<const uint4*>(aux + o);
+#pragma unroll
+        for (int e = 0; e < V; ++e) v[e] *= elu_grad(to_f(av[e]));
+      }
+      if (res) {
+        TO rv[V];
+        *reinterpret_cast<uint4*>(rv) = *reinterpret_cast<const uint4*>(res + o);
+#pragma unroll
+        for (int e = 0; e < V; ++e) v[e] += to_f(rv[e]);
+      }
+      TO ov[V];
+#pragma unroll
+      for (int e = 0; e < V; ++e) ov[e] = from_f<TO>(v[e]);
+      *reinterpret_cast<uint4*>(out + o) = *reinterpret_cast<uint4*>(ov);
+    } else {
+      for (int e = 0; e < V && n + e < a.N; ++e) {
+        float x = v[e];
+        if (aux) x *= elu_grad(to_f(aux[o + e]));
+        if (res) x += to_f(res[o + e]);
+        out[o + e] = from_f<TO>(x);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // weight gradient: gWp[n][k][c] = sum_m gout[m][n] * act(in[row(m,k)][c])
 // block = (n-tile BN, c-chunk CK, m-split); all K taps per block.
 // ---------------------------------------------------------------------------
@@ -697,11 +894,67 @@ int launch_fwd(const Args& a, const void* in, const void* wp, const float* bias,
   return SEL_OK;
 }
 
+template <int BM, int BN, int WAVES_M, int KMAX, typename TO>
+int launch_fwd4(const Args& a, const void* in, const void* wp, const float* bias, const void* aux,
+                const void* res, void* out, hipStream_t s) {
+  const int span = BM + (a.K - 1) * a.dil;
+  const size_t stage = (size_t(span) + size_t(a.K) * BN) * F4_P * 2;
+  const size_t epi = size_t(BM) * (BN + 4) * 4;
+  const size_t lds = stage > epi ? stage : epi;
+  dim3 grid(unsigned((a.rows + BM - 1) / BM), unsigned((a.N + BN - 1) / BN));
+  if (grid.x == 0) return SEL_OK;
+  auto kern = k_conv_fwd_bf16<BM, BN, WAVES_M, KMAX, TO>;
+  if (lds > 64 * 1024)
+    SEL_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
+  hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, a, static_cast<const __bf16*>(in),
+                     static_cast<const __bf16*>(wp), bias, static_cast<const TO*>(aux), static_cast<const TO*>(res),
+                     static_cast<TO*>(out));
+  SEL_LAUNCH_CHECK();
+  return SEL_OK;
+}
+
+template <int KMAX, typename TO>
+int fwd4_variant(int v, const Args& a, const void* in, const void* wp, const float* bias, const void* aux,
+                 const void* res, void* out, hipStream_t s) {
+  switch (v) {
+    case 21: return launch_fwd4<256, 32, 4, KMAX, TO>(a, in, wp, bias, aux, res, out, s);
+    case 22: return launch_fwd4<128, 32, 4, KMAX, TO>(a, in, wp, bias, aux, res, out, s);
+    case 23: return launch_fwd4<128, 64, 2, KMAX, TO>(a, in, wp, bias, aux, res, out, s);
+    case 24: return launch_fwd4<256, 64, 4, KMAX, TO>(a, in, wp, bias, aux, res, out, s);
+    case 25: return launch_fwd4<128, 128, 2, KMAX, TO>(a, in, wp, bias, aux, res, out, s);
+    case 26: return launch_fwd4<64, 128, 1, KMAX, TO>(a, in, wp, bias, aux, res, out, s);
+    default: break;
+  }
+  // heuristic from tools/conv_bench.py on the C3 layer shapes (profiles/r1_conv_bench.md):
+  // narrow / non-64-multiple outputs and short row counts favour 128x32 tiles
+  // (more workgroups in flight); wide layers 128x64 or 256x64.
+  if (a.N <= 32 || (a.N % 64) != 0 || a.rows < 8192)
+    return launch_fwd4<128, 32, 4, KMAX, TO>(a, in, wp, bias, aux, res, out, s);
+  if (a.N <= 64 || a.rows < 65536) return launch_fwd4<128, 64, 2, KMAX, TO>(a, in, wp, bias, aux, res, out, s);
+  return launch_fwd4<256, 64, 4, KMAX, TO>(a, in, wp, bias, aux, res, out, s);
+}
+
 template <typename TI, typename TO>
 int dispatch_fwd(const Args& a, const void* in, const void* wp, const float* bias, const void* aux,
                  const void* res, void* out, hipStream_t s) {
-  // Tiles sized so the staged input+weights of one 32-channel chunk stay <= ~53 KB
-  // (3 workgroups per CU) for the common taps; narrow outputs use BN = 32.
+  if constexpr (sizeof(TI) == 2) {
+    const int v = tune(0);
+    const bool fast = (a.C % CK) == 0 && (a.K - 1) * a.dil <= F4_HALOMAX && a.K <= 8 && (v == 0 || v > 20);
+    if (fast) {
+      if (a.K == 1) return fwd4_variant<1, TO>(v, a, in, wp, bias, aux, res, out, s);
+      if (a.K <= 3) return fwd4_variant<3, TO>(v, a, in, wp, bias, aux, res, out, s);
+      return fwd4_variant<8, TO>(v, a, in, wp, bias, aux, res, out, s);
+    }
+    switch (v) {
+      case 1: return launch_fwd<TI, TO, 128, 32>(a, in, wp, bias, aux, res, out, s);
+      case 2: return launch_fwd<TI, TO, 128, 64>(a, in, wp, bias, aux, res, out, s);
+      case 3: return launch_fwd<TI, TO, 128, 128>(a, in, wp, bias, aux, res, out, s);
+      case 4: return launch_fwd<TI, TO, 64, 64>(a, in, wp, bias, aux, res, out, s);
+      case 5: return launch_fwd<TI, TO, 256, 32>(a, in, wp, bias, aux, res, out, s);
+      case 6: return launch_fwd<TI, TO, 256, 64>(a, in, wp, bias, aux, res, out, s);
+      default: break;
+    }
+  }
   if (sizeof(TI) == 4) {
     if (a.N <= 32) return launch_fwd<TI, TO, 128, 32>(a, in, wp, bias, aux, res, out, s);
     return launch_fwd<TI, TO, 64, 64>(a, in, wp, bias, aux, res, out, s);

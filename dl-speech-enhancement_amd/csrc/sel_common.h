@@ -12,6 +12,7 @@ namespace sel {
 
 void set_error(const char* fmt, ...);
 bool initialized();
+int tune(int key);
 
 constexpr int kWave = 64;
 

@@ -41,6 +41,9 @@ enum { SEL_LOG_E = 0, SEL_LOG_2 = 1, SEL_LOG_10 = 2 };
 int sel_init(void);                 /* uploads FFT twiddle tables; idempotent */
 const char* sel_last_error(void);   /* thread-local, never NULL */
 int sel_version(void);
+/* tuning knobs for A/B runs inside one process (key 0: conv fwd kernel variant,
+ * 0 = built-in heuristic); returns the previous value. */
+int sel_tune(int key, int value);
 
 /* ---- STFT magnitude: losses/stft_loss.py:19-35 (stft) ------------------
  * x (B,T) -> mag (B, F, K), F = 1 + T/hop, K = n_fft/2 + 1.

@@ -1,0 +1,90 @@
+"""Microbenchmark of the conv primitive on the C3 layer shapes (bf16), A/B over
+kernel variants inside ONE process (sel_tune key 0).
+
+usage: python tools/conv_bench.py [variants...]    (GPU)
+"""
+import ctypes
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "dl-speech-enhancement_amd"))
+
+import torch  # noqa: E402
+
+from sel import _lib as L  # noqa: E402
+from sel import convops as CO  # noqa: E402
+
+Z, R = CO.PAD_ZERO, CO.PAD_REPLICATE
+# name, rows, T, C, N, K, dil, pad, mode, in_elu, aux, res, bias
+SHAPES = [
+    ("first 1->32 k7", 1536000, 24000, 1, 32, 7, 1, 6, Z, 0, 0, 0, 0),
+    ("RU32 k7d9 fwd", 1536000, 24000, 32, 32, 7, 9, 54, Z, 1, 0, 0, 0),
+    ("RU32 1x1 fwd", 1536000, 24000, 32, 32, 1, 1, 0, Z, 1, 0, 1, 0),
+    ("RU32 k7d9 dgrad", 1536000, 24000, 32, 32, 7, 9, 0, Z, 0, 1, 1, 0),
+    ("RU32 1x1 dgrad", 1536000, 24000, 32, 32, 1, 1, 0, Z, 0, 1, 0, 0),
+    ("down0 96->64 k3", 512000, 8000, 96, 64, 3, 1, 2, Z, 0, 0, 0, 1),
+    ("RU64 k7d3 fwd", 512000, 8000, 64, 64, 7, 3, 18, Z, 1, 0, 0, 0),
+    ("RU64 1x1 fwd", 512000, 8000, 64, 64, 1, 1, 0, Z, 1, 0, 1, 0),
+    ("up3 64->96 k2 rep", 512000, 8000, 64, 96, 2, 1, 1, R, 0, 0, 0, 1),
+    ("RU128 k7d9 fwd", 128000, 2000, 128, 128, 7, 9, 54, Z, 1, 0, 0, 0),
+    ("down1 256->128 k3", 128000, 2000, 256, 128, 3, 1, 2, Z, 0, 0, 0, 1),
+    ("RU256 k7d1 fwd", 25600, 400, 256, 256, 7, 1, 6, Z, 1, 0, 0, 0),
+    ("RU256 k7 dgrad", 25600, 400, 256, 256, 7, 1, 0, Z, 0, 1, 1, 0),
+    ("down2 640->256 k3", 25600, 400, 640, 256, 3, 1, 2, Z, 0, 0, 0, 1),
+    ("down3 1280->512 k3", 5120, 80, 1280, 512, 3, 1, 2, Z, 0, 0, 0, 1),
+    ("dec conv1 64->512", 5120, 80, 64, 512, 7, 1, 6, Z, 0, 0, 0, 0),
+    ("up0 512->1280 k2", 5120, 80, 512, 1280, 2, 1, 1, R, 0, 0, 0, 1),
+]
+
+
+def run(shape, variant, iters=20):
+    name, rows, T, C, N, K, dil, pad, mode, elu, aux, res, bias = shape
+    dev = torch.device("cuda")
+    d = CO.ConvDesc(rows, T, C, N, K, dil, pad, mode, elu, N if bias else 0)
+    x = (0.5 * torch.randn(rows, C, device=dev)).to(torch.bfloat16)
+    wp = (0.05 * torch.randn(N, K, C, device=dev)).to(torch.bfloat16)
+    b = torch.randn(N, device=dev) if bias else None
+    a_ = torch.randn(rows, N, device=dev).to(torch.bfloat16) if aux else None
+    r_ = torch.randn(rows, N, device=dev).to(torch.bfloat16) if res else None
+    L.lib().sel_tune(0, variant)
+    try:
+        for _ in range(3):
+            y = CO.prim(d, x, wp, bias=b, aux=a_, res=r_)
+    except L.SelError as e:
+        return None, str(e)[:40]
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        y = CO.prim(d, x, wp, bias=b, aux=a_, res=r_)
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / iters
+    del y
+    return us, None
+
+
+def main():
+    variants = [int(v) for v in sys.argv[1:]] or [0, 1, 5, 6, 21, 22, 23, 24, 25, 26]
+    L.lib()
+    print("| shape | " + " | ".join(f"v{v}" for v in variants) + " | best | GB/s | TF/s |")
+    print("|---" * (len(variants) + 4) + "|")
+    for sh in SHAPES:
+        name, rows, T, C, N, K, dil, pad, mode, elu, aux, res, bias = sh
+        times = []
+        for v in variants:
+            us, err = run(sh, v)
+            times.append(us)
+        ok = [(t, v) for t, v in zip(times, variants) if t is not None]
+        best_t, best_v = min(ok)
+        nbytes = 2 * (rows * C + rows * N * (1 + aux + res) + N * K * C)
+        flops = 2.0 * rows * N * K * C
+        cells = " | ".join("-" if t is None else f"{t:.1f}" for t in times)
+        print(f"| {name} | {cells} | v{best_v} | {nbytes / best_t / 1e3:.0f} | {flops / best_t / 1e6:.0f} |",
+              flush=True)
+    L.lib().sel_tune(0, 0)
+
+
+if __name__ == "__main__":
+    main()
