@@ -176,6 +176,39 @@ def c3_cpu_baseline(B_sample=2, steps=2):
 
 # ---------------------------------------------------------------------------
 
+MFMA_BF16_PEAK_TFS = 2500.0  # MI355X dense bf16 (MI355X_MICROARCH.md)
+
+
+def roofline(cfg, timer, dom, B, steps):
+    """Dominant timed kernel instance -> achieved vs peak (HIP events, same stream)."""
+    summ = timer.summary()
+    if cfg == "c2":
+        # one fused STFT-loss forward per resolution per step; n_fft=512 is the last one
+        durs = timer.durations_ms(dom)
+        per_step = len(durs) // steps
+        sel_d = durs[per_step - 1::per_step]
+        avg_ms = float(np.mean(sel_d))
+        achieved = c2_bytes_per_launch(dom, B) / (avg_ms * 1e-3) / 1e9
+        return {"bound": "hbm", "kernel": dom + " (n_fft=512)", "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "avg_launch_us": round(avg_ms * 1e3, 2), "traffic": None}
+    tag, (n, ms, nbytes, flops) = max(summ.items(), key=lambda kv: kv[1][1])
+    intensity = flops / max(nbytes, 1)
+    ridge = MFMA_BF16_PEAK_TFS * 1e12 / (HBM_PEAK_GBS * 1e9)
+    if intensity > ridge:
+        ach = flops / (ms * 1e-3) / 1e12
+        r = {"bound": "mfma", "achieved": round(ach, 1), "peak": MFMA_BF16_PEAK_TFS, "unit": "TFLOP/s",
+             "frac": round(ach / MFMA_BF16_PEAK_TFS, 4)}
+    else:
+        ach = nbytes / (ms * 1e-3) / 1e9
+        r = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+             "frac": round(ach / HBM_PEAK_GBS, 4)}
+    r.update({"kernel": tag, "launches": n, "avg_launch_us": round(1e3 * ms / n, 2),
+              "bytes_per_launch": int(nbytes / n), "flops_per_launch": int(flops / n),
+              "share_of_timed_conv_ms": round(ms / sum(v[1] for v in summ.values()), 3), "traffic": None})
+    return r
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -234,21 +267,10 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    durs = timer.durations_ms(dom)
-    # one sel_stft_loss_fwd call per resolution per step: pick the n_fft=512 launches
     ms_per_step = 1e3 * elapsed / args.steps
     frames = world * B * SR / HOP * args.steps
     value = frames / elapsed
-    avg_ms, achieved = 0.0, 0.0
-    if cfg == "c2":
-        per_step = len(durs) // args.steps
-        sel_d = durs[per_step - 1::per_step]  # last resolution (n_fft=512) of each step
-        avg_ms = float(np.mean(sel_d))
-        achieved = bytes_fn(dom, B) / (avg_ms * 1e-3) / 1e9
-    roof = {"bound": "hbm", "kernel": dom + " (n_fft=512)", "achieved": round(achieved, 1),
-            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "avg_launch_us": round(avg_ms * 1e3, 2), "traffic": None}
-
+    roof = roofline(cfg, timer, dom, B, args.steps)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         ncores = len(os.sched_getaffinity(0))

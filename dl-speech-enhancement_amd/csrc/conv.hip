@@ -913,6 +913,17 @@ int launch_fwd4(const Args& a, const void* in, const void* wp, const float* bias
   return SEL_OK;
 }
 
+// Variant the dispatcher picks for a bf16 forward launch (see fwd4_variant);
+// -1 when the generic (non-pipelined) kernel is used.
+int fwd4_choice(const Args& a) {
+  const int v = tune(0);
+  if (!((a.C % CK) == 0 && (a.K - 1) * a.dil <= F4_HALOMAX && a.K <= 8 && (v == 0 || v > 20))) return -1;
+  if (v > 20) return v;
+  if (a.N <= 32 || (a.N % 64) != 0 || a.rows < 8192) return 22;
+  if (a.N <= 64 || a.rows < 65536) return 23;
+  return 24;
+}
+
 template <int KMAX, typename TO>
 int fwd4_variant(int v, const Args& a, const void* in, const void* wp, const float* bias, const void* aux,
                  const void* res, void* out, hipStream_t s) {
@@ -996,6 +1007,18 @@ WgPlan wgrad_plan(const sel_conv_desc* d) {
 }  // namespace
 
 extern "C" {
+
+int sel_conv_fwd_kernel_id(const sel_conv_desc* d, int in_dtype, int out_dtype) {
+  if (!d || in_dtype != SEL_BF16) return -1;
+  (void)out_dtype;
+  const Args a = to_args(d);
+  const int v = fwd4_choice(a);
+  if (v < 0) return -1;
+  const int kmax = a.K == 1 ? 1 : (a.K <= 3 ? 3 : 8);
+  static const int bm[] = {256, 128, 128, 256, 128, 64}, bn[] = {32, 32, 64, 64, 128, 128}, wm[] = {4, 4, 2, 4, 2, 1};
+  const int i = v - 21;
+  return ((bm[i] * 1000 + bn[i]) * 10 + wm[i]) * 10 + kmax;  // BM,BN,WAVES_M,KMAX packed
+}
 
 int sel_conv_fwd(const sel_conv_desc* d, int in_dtype, int out_dtype, const void* in, const void* wpack,
                  const float* bias, const void* aux, const void* res, void* out, sel_stream_t stream) {

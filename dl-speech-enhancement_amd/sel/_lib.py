@@ -42,6 +42,7 @@ SIGNATURES = {
     "sel_logmel_bwd_workspace": (SZ, [I64, I64, I32, I32, I32]),
     "sel_logmel_bwd": (I32, [P, I64, I64, I32, I32, I32, P, P, P, P, I32, F32, I32,
                              P, P, P, F32, P, P, SZ, P]),
+    "sel_conv_fwd_kernel_id": (I32, [P, I32, I32]),
     "sel_conv_fwd": (I32, [P, I32, I32, P, P, P, P, P, P, P]),
     "sel_conv_wgrad_workspace": (SZ, [P]),
     "sel_conv_wgrad": (I32, [P, I32, P, P, P, P, P, SZ, P]),
@@ -105,22 +106,38 @@ def lib():
 
 class KernelTimer:
     """Brackets selected C-ABI calls with HIP events on the launching stream
-    (torch.cuda.current_stream()) — used by bench.py for the live roofline."""
+    (torch.cuda.current_stream(), the stream every sel call enqueues on) — used
+    by bench.py for the live roofline.  Each record carries the caller's tag
+    (kernel instance) and algorithmic bytes / flops of that launch."""
 
     def __init__(self, names):
         self.names = set(names)
-        self.events = {n: [] for n in self.names}
+        self.records = []  # (name, tag, bytes, flops, ev0, ev1)
+
+    def add(self, name, meta, ev0, ev1):
+        tag, nbytes, flops = meta if meta else (name, 0, 0)
+        self.records.append((name, tag, nbytes, flops, ev0, ev1))
+
+    def summary(self):
+        """{tag: (launches, total_ms, bytes, flops)}"""
+        torch.cuda.synchronize()
+        out = {}
+        for name, tag, nb, fl, a, b in self.records:
+            n, ms, B, F = out.get(tag, (0, 0.0, 0, 0))
+            out[tag] = (n + 1, ms + a.elapsed_time(b), B + nb, F + fl)
+        return out
 
     def durations_ms(self, name):
         torch.cuda.synchronize()
-        return [a.elapsed_time(b) for a, b in self.events[name]]
+        return [a.elapsed_time(b) for n, _, _, _, a, b in self.records if n == name]
 
 
 TIMER = None
 
 
-def call(name, *args):
-    """Invoke a C entry point, raise SelError on failure, optionally timed."""
+def call(name, *args, meta=None):
+    """Invoke a C entry point, raise SelError on failure, optionally timed.
+    meta = (tag, algorithmic bytes, flops) for the KernelTimer."""
     fn = getattr(lib(), name)
     t = TIMER
     if t is not None and name in t.names:
@@ -129,7 +146,7 @@ def call(name, *args):
         a.record()
         rc = fn(*args)
         b.record()
-        t.events[name].append((a, b))
+        t.add(name, meta() if callable(meta) else meta, a, b)
     else:
         rc = fn(*args)
     check(rc, name)

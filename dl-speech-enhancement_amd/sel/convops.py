@@ -132,8 +132,33 @@ def prim(desc, x, wp, bias=None, aux=None, res=None, out_dtype=None):
             assert t.dtype == out_dtype and t.is_contiguous() and t.numel() == out.numel()
     assert x.is_contiguous() and x.numel() == desc.rows * desc.C and wp.dtype == x.dtype
     L.call("sel_conv_fwd", ctypes.byref(desc), _code(x.dtype), _code(out_dtype), L.ptr(x), L.ptr(wp),
-           L.ptr(bias), L.ptr(aux), L.ptr(res), L.ptr(out), L.stream())
+           L.ptr(bias), L.ptr(aux), L.ptr(res), L.ptr(out), L.stream(),
+           meta=lambda: _fwd_meta(desc, x, out, wp, aux, res))
     return out
+
+
+def fwd_kernel_name(desc, in_dtype, out_dtype):
+    """rocprof name fragment of the kernel instance a launch uses."""
+    kid = L.lib().sel_conv_fwd_kernel_id(ctypes.byref(desc), _code(in_dtype), _code(out_dtype))
+    if kid < 0:
+        return f"k_conv_fwd<{in_dtype}>"
+    kmax, kid = kid % 10, kid // 10
+    wm, kid = kid % 10, kid // 10
+    bm, bn = kid // 1000, kid % 1000
+    to = "bf16" if out_dtype == torch.bfloat16 else "float"
+    return f"k_conv_fwd_bf16<{bm}, {bn}, {wm}, {kmax}, {to}>"
+
+
+def _fwd_meta(desc, x, out, wp, aux, res):
+    """(kernel tag, algorithmic HBM bytes, flops) of one primitive launch:
+    read the input rows once, the packed weights once, aux/res once, write out once."""
+    es = x.element_size()
+    nbytes = desc.rows * desc.C * es + out.numel() * out.element_size() + wp.numel() * es
+    for t in (aux, res):
+        if t is not None:
+            nbytes += t.numel() * t.element_size()
+    flops = 2.0 * desc.rows * desc.N * desc.K * desc.C
+    return fwd_kernel_name(desc, x.dtype, out.dtype), nbytes, flops
 
 
 def wgrad(desc, gout, x, want_bias):
