@@ -691,21 +691,193 @@ __global__ __launch_bounds__(256) void k_wgrad_bf16(Args a, const __bf16* __rest
   if (bpart && c0 == 0 && tid < BN && n0 + tid < a.N) bpart[int64_t(blockIdx.z) * a.N + n0 + tid] = bsum;
 }
 
-// Deterministic split reduction: out[j] = sum_s sum_{i % period == j} part[s*n + i]
-// (period == n: plain sum over splits).  64 outputs per block, 4 waves over splits.
-__global__ __launch_bounds__(256) void k_split_sum(const float* __restrict__ part, int nsplit, int64_t n,
-                                                   int period, float* __restrict__ out) {
-  __shared__ float red[4][64];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t j = int64_t(blockIdx.x) * 64 + lane;
-  float s = 0.f;
-  if (j < period) {
-    for (int sp = wave; sp < nsplit; sp += 4)
-      for (int64_t i = j; i < n; i += period) s += part[int64_t(sp) * n + i];
+// bf16 weight gradient, fast path (C % 32 == 0, N % 32 == 0, halo <= 64, K <= 8):
+// block = (32 output channels n, 32 input channels c, m-split).  m-tiles are 128
+// rows of one sample; each of the 4 waves owns 32 rows of the tile and
+// accumulates ALL K taps as 32x32 tiles (v_mfma_f32_32x32x16_bf16), reading
+// both operands with ds_read_b64_tr_b16 from 64-B LDS rows (rows 4h..4h+3 per
+// 32-lane half: conflict free).  The next tile's rows are prefetched into
+// registers during the MFMAs (branch-free clamped loads); the 4 waves' partial
+// tiles are summed through LDS once per split.
+constexpr int W2_BM = 128;
+constexpr int W2_HALO = 64;
+
+template <int TW>  // waves split taps into TW groups and rows into 4/TW groups
+__global__ __launch_bounds__(256) void k_wgrad2_bf16(Args a, const __bf16* __restrict__ gout,
+                                                     const __bf16* __restrict__ in, int tiles_per_sample,
+                                                     int64_t n_tiles, int tiles_per_split,
+                                                     float* __restrict__ part, float* __restrict__ bpart) {
+  constexpr int GV = W2_BM * 32 / 8 / 256;                  // 2
+  constexpr int XV = ((W2_BM + W2_HALO) * 4 + 255) / 256;   // 3
+  constexpr int GS = W2_BM * 32, XS = (W2_BM + W2_HALO) * 32;  // elements per buffer
+  constexpr int RG = 4 / TW;                                // row groups
+  constexpr int RROWS = W2_BM / RG;                         // rows per wave per tile
+  constexpr int KPW = TW == 1 ? 1 : 2;                      // taps per wave: K=1 | K<=4 (TW=2) | K<=8 (TW=4)
+  extern __shared__ __align__(16) unsigned char smem[];
+  __bf16* const base = reinterpret_cast<__bf16*>(smem);  // [buf]{G[128][32], X[192][32]}
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tg = wave % TW, rg = wave / TW;
+  const int n0 = blockIdx.x * 32, c0 = blockIdx.y * 32;
+  const int64_t tb = int64_t(blockIdx.z) * tiles_per_split;
+  const int64_t te = tb + tiles_per_split < n_tiles ? tb + tiles_per_split : n_tiles;
+  const int halo = (a.K - 1) * a.dil;
+  const int span = W2_BM + halo;
+
+  uint4 gr[GV], xr[XV];
+  auto load = [&](int64_t tile) {
+    const int64_t b = tile / tiles_per_sample;
+    const int t0 = int(tile % tiles_per_sample) * W2_BM;
+    const int64_t rb = b * a.T;
+#pragma unroll
+    for (int u = 0; u < GV; ++u) {
+      const int v = tid + u * 256;
+      const int t = t0 + (v >> 2);
+      const bool ok = t < a.T;
+      uint4 val = *reinterpret_cast<const uint4*>(gout + (rb + (ok ? t : 0)) * a.N + n0 + (v & 3) * 8);
+      if (!ok) val = make_uint4(0, 0, 0, 0);
+      gr[u] = val;
+    }
+#pragma unroll
+    for (int u = 0; u < XV; ++u) {
+      const int v = tid + u * 256;
+      const int r = v >> 2;
+      int ti = t0 - a.pad + r;
+      const bool inside = ti >= 0 && ti < a.T;
+      const bool ok = r < span && (inside || a.pad_mode == SEL_PAD_REPLICATE);
+      ti = ti < 0 ? 0 : (ti >= a.T ? a.T - 1 : ti);
+      uint4 val = *reinterpret_cast<const uint4*>(in + (rb + ti) * a.C + c0 + (v & 3) * 8);
+      if (!ok) val = make_uint4(0, 0, 0, 0);
+      xr[u] = val;
+    }
+  };
+  auto store = [&](int buf) {
+    __bf16* g = base + buf * (GS + XS);
+    __bf16* x = g + GS;
+#pragma unroll
+    for (int u = 0; u < GV; ++u) {
+      const int v = tid + u * 256;
+      *reinterpret_cast<uint4*>(g + (v >> 2) * 32 + (v & 3) * 8) = gr[u];
+    }
+#pragma unroll
+    for (int u = 0; u < XV; ++u) {
+      const int v = tid + u * 256;
+      if ((v >> 2) >= W2_BM + W2_HALO) continue;
+      uint4 val = xr[u];
+      if (a.in_elu) {
+        __bf16* t = reinterpret_cast<__bf16*>(&val);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) t[e] = __bf16(elu(float(t[e])));
+      }
+      *reinterpret_cast<uint4*>(x + (v >> 2) * 32 + (v & 3) * 8) = val;
+    }
+  };
+
+  floatx16 acc[KPW];
+#pragma unroll
+  for (int j = 0; j < KPW; ++j)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
+  float bsum = 0.f;
+
+  const int h = lane >> 5;
+  const int col = ((lane >> 4) & 1) * 16 + 4 * (lane & 3);
+  const int q = (lane & 15) >> 2;
+
+  if (tb < te) load(tb);
+  int buf = 0;
+  for (int64_t tile = tb; tile < te; ++tile, buf ^= 1) {
+    store(buf);
+    __syncthreads();
+    if (tile + 1 < te) load(tile + 1);
+    const __bf16* g = base + buf * (GS + XS);
+    const __bf16* x = g + GS;
+#pragma unroll
+    for (int kh = 0; kh < RROWS / 16; ++kh) {
+      const int R = rg * RROWS + kh * 16;
+      const v4i16 a0 = tr_read(g + (R + 4 * h + q) * 32 + col);
+      const v4i16 a1 = tr_read(g + (R + 8 + 4 * h + q) * 32 + col);
+      const bf16x8 A = __builtin_bit_cast(bf16x8, __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7));
+      if (bpart && tg == 0) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bsum += float(A[e]);
+      }
+#pragma unroll
+      for (int j = 0; j < KPW; ++j) {
+        const int k = tg + j * TW;
+        if (k >= a.K) break;
+        const int Rx = R + k * a.dil;
+        const v4i16 b0 = tr_read(x + (Rx + 4 * h + q) * 32 + col);
+        const v4i16 b1 = tr_read(x + (Rx + 8 + 4 * h + q) * 32 + col);
+        const bf16x8 Bf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7));
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, Bf, acc[j], 0, 0, 0);
+      }
+    }
   }
-  red[wave][lane] = s;
+
+  // sum the RG row-group partials of every tap, write the split partial
   __syncthreads();
-  if (wave == 0 && j < period) out[j] = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+  float* red = reinterpret_cast<float*>(smem);  // [wave][KPW][32*32]
+#pragma unroll
+  for (int j = 0; j < KPW; ++j) {
+    if (tg + j * TW >= a.K) break;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      red[(wave * KPW + j) * 1024 + row * 32 + (lane & 31)] = acc[j][r];
+    }
+  }
+  if (bpart) {
+    bsum += __shfl_xor(bsum, 32, 64);
+  }
+  __syncthreads();
+  float* pdst = part + int64_t(blockIdx.z) * a.N * a.K * a.C;
+  for (int i = tid; i < a.K * 1024; i += 256) {
+    const int k = i >> 10, e = i & 1023;
+    const int t = k % TW, j = k / TW;
+    float v = 0.f;
+#pragma unroll
+    for (int r = 0; r < RG; ++r) v += red[((r * TW + t) * KPW + j) * 1024 + e];
+    const int n = n0 + (e >> 5), c = c0 + (e & 31);
+    pdst[(int64_t(n) * a.K + k) * a.C + c] = v;
+  }
+  if (bpart && c0 == 0) {
+    __syncthreads();
+    if (tg == 0 && lane < 32) red[rg * 32 + lane] = bsum;
+    __syncthreads();
+    if (tid < 32) {
+      float v = 0.f;
+#pragma unroll
+      for (int r = 0; r < RG; ++r) v += red[r * 32 + tid];
+      bpart[int64_t(blockIdx.z) * a.N + n0 + tid] = v;
+    }
+  }
+}
+
+// Deterministic split reduction in two parallel passes:
+//   pass 1: part2[g][i] = sum_{s in group g (32 splits)} part[s][i]   (grid: i-blocks x groups)
+//   pass 2: out[j] = sum_g sum_{i % period == j} part2[g][i]
+constexpr int SPLIT_GROUP = 32;
+
+__global__ __launch_bounds__(256) void k_split_sum1(const float* __restrict__ part, int nsplit, int64_t n,
+                                                    float* __restrict__ part2) {
+  const int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int s0 = blockIdx.y * SPLIT_GROUP;
+  const int s1 = s0 + SPLIT_GROUP < nsplit ? s0 + SPLIT_GROUP : nsplit;
+  float acc = 0.f;
+  for (int sp = s0; sp < s1; ++sp) acc += part[int64_t(sp) * n + i];
+  part2[int64_t(blockIdx.y) * n + i] = acc;
+}
+
+__global__ __launch_bounds__(256) void k_split_sum2(const float* __restrict__ part2, int ngroups, int64_t n,
+                                                    int period, float* __restrict__ out) {
+  const int64_t j = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (j >= period) return;
+  float acc = 0.f;
+  for (int g = 0; g < ngroups; ++g)
+    for (int64_t i = j; i < n; i += period) acc += part2[int64_t(g) * n + i];
+  out[j] = acc;
 }
 
 // ---------------------------------------------------------------------------
@@ -985,15 +1157,25 @@ int wgrad_bn(int N) { return N <= 16 ? 16 : (N <= 32 ? 32 : 64); }
 struct WgPlan {
   int64_t tiles_per_sample, n_tiles;
   int nsplit, tiles_per_split, bn;
+  bool fast;
 };
 
-WgPlan wgrad_plan(const sel_conv_desc* d) {
+bool wgrad_fast(const sel_conv_desc* d) {
+  if (!(d->C % 32 == 0 && d->N % 32 == 0 && (d->K - 1) * d->dil <= W2_HALO && d->K <= 8)) return false;
+  // measured (profiles/r1_wgrad_bench.md): the tr-read kernel wins for K <= 3 and the 32-channel stage
+  return d->K <= 3 || d->C == 32;
+}
+
+WgPlan wgrad_plan(const sel_conv_desc* d, bool fast) {
   WgPlan p;
-  p.bn = wgrad_bn(d->N);
-  p.tiles_per_sample = (d->T + WB_BM - 1) / WB_BM;
+  p.fast = fast;
+  const int bm = fast ? W2_BM : WB_BM;
+  p.bn = fast ? 32 : wgrad_bn(d->N);
+  const int bc = fast ? 32 : WB_BC;
+  p.tiles_per_sample = (d->T + bm - 1) / bm;
   p.n_tiles = (d->rows / d->T) * p.tiles_per_sample;
-  const int64_t blocks = int64_t((d->N + p.bn - 1) / p.bn) * ((d->C + WB_BC - 1) / WB_BC);
-  int64_t want = std::max<int64_t>(1, (512 + blocks - 1) / blocks);
+  const int64_t blocks = int64_t((d->N + p.bn - 1) / p.bn) * ((d->C + bc - 1) / bc);
+  int64_t want = std::max<int64_t>(1, (768 + blocks - 1) / blocks);
   const int64_t per_split = (int64_t(d->N) * d->K * d->C + d->N) * 4;
   want = std::min<int64_t>(want, std::max<int64_t>(1, (int64_t(64) << 20) / per_split));
   want = std::min<int64_t>(want, std::max<int64_t>(1, p.n_tiles));
@@ -1037,8 +1219,10 @@ int sel_conv_fwd(const sel_conv_desc* d, int in_dtype, int out_dtype, const void
 
 size_t sel_conv_wgrad_workspace(const sel_conv_desc* d) {
   if (!d || d->rows <= 0 || d->T <= 0) return 16;
-  const WgPlan p = wgrad_plan(d);
-  return size_t(p.nsplit) * (size_t(d->N) * d->K * d->C + d->N) * sizeof(float);
+  const WgPlan p0 = wgrad_plan(d, false), p1 = wgrad_plan(d, true);
+  const int ns = std::max(p0.nsplit, wgrad_fast(d) ? p1.nsplit : 0);
+  const int ng = (ns + SPLIT_GROUP - 1) / SPLIT_GROUP;
+  return size_t(ns + ng) * (size_t(d->N) * d->K * d->C + d->N) * sizeof(float);
 }
 
 int sel_conv_wgrad(const sel_conv_desc* d, int dtype, const void* gout, const void* in, float* gwpack,
@@ -1050,10 +1234,24 @@ int sel_conv_wgrad(const sel_conv_desc* d, int dtype, const void* gout, const vo
   SEL_REQUIRE(ws_bytes >= sel_conv_wgrad_workspace(d), SEL_ERR_WORKSPACE, "workspace too small");
   const Args a = to_args(d);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const WgPlan p = wgrad_plan(d);
+  const WgPlan p = wgrad_plan(d, dtype == SEL_BF16 && wgrad_fast(d) && tune(1) == 0);
   float* part = static_cast<float*>(ws);
   float* bpart = gbias ? part + size_t(p.nsplit) * d->N * d->K * d->C : nullptr;
-  if (d->rows > 0 && dtype == SEL_BF16) {
+  if (d->rows > 0 && dtype == SEL_BF16 && p.fast) {
+    // staging double buffer (40 KB) also hosts the [wave][taps][32x32] fp32 reduction
+    const size_t lds = std::max<size_t>(size_t(2) * (W2_BM * 32 + (W2_BM + W2_HALO) * 32) * sizeof(__bf16),
+                                        size_t(4) * 8 * 1024 * sizeof(float) / 4 * 1);
+    dim3 grid(unsigned(d->N / 32), unsigned(d->C / 32), unsigned(p.nsplit));
+#define SEL_WG2_LAUNCH(KM)                                                                                    \
+  hipLaunchKernelGGL(k_wgrad2_bf16<KM>, grid, dim3(256), lds, s, a, static_cast<const __bf16*>(gout),          \
+                     static_cast<const __bf16*>(in), int(p.tiles_per_sample), p.n_tiles, p.tiles_per_split, part, \
+                     bpart)
+    if (d->K == 1) SEL_WG2_LAUNCH(1);
+    else if (d->K <= 4) SEL_WG2_LAUNCH(2);
+    else SEL_WG2_LAUNCH(4);
+#undef SEL_WG2_LAUNCH
+    SEL_LAUNCH_CHECK();
+  } else if (d->rows > 0 && dtype == SEL_BF16) {
     const int span = WB_BM + (d->K - 1) * d->dil;
     const size_t lds = (size_t(WB_BM) * (p.bn + 16) + size_t(span) * (WB_BC + 16)) * sizeof(__bf16);
     SEL_REQUIRE(lds <= 160 * 1024, SEL_ERR_UNSUPPORTED, "wgrad tile needs %zu B of LDS", lds);
@@ -1097,13 +1295,23 @@ int sel_conv_wgrad(const sel_conv_desc* d, int dtype, const void* gout, const vo
     set_error("bad dtype %d", dtype);
     return SEL_ERR_ARG;
   }
+  // two-pass split reduction; the second-level partials live after the first-level ones
   const int64_t nw = int64_t(d->N) * d->K * d->C;
-  hipLaunchKernelGGL(k_split_sum, dim3(unsigned((nw + 63) / 64)), dim3(256), 0, s, part, p.nsplit, nw, int(nw),
+  const int ng = (p.nsplit + SPLIT_GROUP - 1) / SPLIT_GROUP;
+  float* part2 = part + size_t(p.nsplit) * (size_t(d->N) * d->K * d->C + d->N);
+  hipLaunchKernelGGL(k_split_sum1, dim3(unsigned((nw + 255) / 256), unsigned(ng)), dim3(256), 0, s, part, p.nsplit,
+                     nw, part2);
+  SEL_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_split_sum2, dim3(unsigned((nw + 255) / 256)), dim3(256), 0, s, part2, ng, nw, int(nw),
                      gwpack);
   SEL_LAUNCH_CHECK();
   if (gbias) {
-    hipLaunchKernelGGL(k_split_sum, dim3(unsigned((d->bias_period + 63) / 64)), dim3(256), 0, s, bpart,
-                       p.nsplit, int64_t(d->N), d->bias_period, gbias);
+    float* bpart2 = part2 + size_t(ng) * nw;
+    hipLaunchKernelGGL(k_split_sum1, dim3(unsigned((d->N + 255) / 256), unsigned(ng)), dim3(256), 0, s, bpart,
+                       p.nsplit, int64_t(d->N), bpart2);
+    SEL_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_split_sum2, dim3(unsigned((d->bias_period + 255) / 256)), dim3(256), 0, s, bpart2, ng,
+                       int64_t(d->N), d->bias_period, gbias);
     SEL_LAUNCH_CHECK();
   }
   return SEL_OK;

@@ -86,5 +86,45 @@ def main():
     L.lib().sel_tune(0, 0)
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and os.environ.get("WGRAD", "0") != "1":
     main()
+
+
+WG_SHAPES = [s for s in SHAPES if "dgrad" not in s[0]]
+
+
+def run_wgrad(shape, variant, iters=10):
+    name, rows, T, C, N, K, dil, pad, mode, elu, aux, res, bias = shape
+    dev = torch.device("cuda")
+    d = CO.ConvDesc(rows, T, C, N, K, dil, pad, mode, elu, N if bias else 0)
+    x = (0.5 * torch.randn(rows, C, device=dev)).to(torch.bfloat16)
+    g = (0.5 * torch.randn(rows, N, device=dev)).to(torch.bfloat16)
+    L.lib().sel_tune(1, variant)
+    try:
+        for _ in range(2):
+            CO.wgrad(d, g, x, bool(bias))
+    except L.SelError as e:
+        return None
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        CO.wgrad(d, g, x, bool(bias))
+    e1.record()
+    torch.cuda.synchronize()
+    L.lib().sel_tune(1, 0)
+    return e0.elapsed_time(e1) * 1e3 / iters
+
+
+def main_wgrad():
+    print("\n| wgrad shape | fast (us) | generic (us) | GB/s | TF/s |\n|---|---|---|---|---|")
+    for sh in WG_SHAPES:
+        name, rows, T, C, N, K, dil, pad, mode, elu, aux, res, bias = sh
+        t0, t1 = run_wgrad(sh, 0), run_wgrad(sh, 1)
+        nbytes = 2 * (rows * C + rows * N)
+        flops = 2.0 * rows * N * K * C
+        print(f"| {name} | {t0:.1f} | {t1:.1f} | {nbytes / t0 / 1e3:.0f} | {flops / t0 / 1e6:.0f} |", flush=True)
+
+
+if __name__ == "__main__" and os.environ.get("WGRAD", "0") == "1":
+    main_wgrad()
