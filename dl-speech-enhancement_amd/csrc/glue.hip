@@ -49,6 +49,71 @@ __global__ __launch_bounds__(256) void k_mix(const float* __restrict__ a, const 
     out[i] = (s * a[i] + b[i]) / 2.f;
 }
 
+__global__ __launch_bounds__(256) void k_finish2(const double* __restrict__ part, int np, double* __restrict__ sums2) {
+  __shared__ double red[16];
+  double sa = 0.0, sb = 0.0;
+  for (int i = threadIdx.x; i < np; i += blockDim.x) {
+    sa += part[2 * i];
+    sb += part[2 * i + 1];
+  }
+  sa = block_sum<double>(sa, red);
+  sb = block_sum<double>(sb, red);
+  if (threadIdx.x == 0) {
+    sums2[0] = sa;
+    sums2[1] = sb;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_mix2(const float* __restrict__ a, const float* __restrict__ b, int64_t n,
+                                              const double* __restrict__ sums2, float snr, float* __restrict__ out) {
+  const float sp = sqrtf(float(sums2[0])), npw = sqrtf(float(sums2[1]));
+  const float s = float(std::exp(double(snr) / 10.0)) * npw / sp;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+    out[i] = (s * a[i] + b[i]) / 2.f;
+}
+
+// SNR (torchmetrics SignalNoiseRatio, zero_mean=False): one block per sample.
+__global__ __launch_bounds__(256) void k_snr_sums(const float* __restrict__ p, const float* __restrict__ t, int64_t T,
+                                                  double* __restrict__ sums) {
+  __shared__ double red[16];
+  const int64_t b = blockIdx.x;
+  double st = 0.0, sd = 0.0;
+  for (int64_t i = threadIdx.x; i < T; i += blockDim.x) {
+    const float tv = t[b * T + i], d = tv - p[b * T + i];
+    st += double(tv) * tv;
+    sd += double(d) * d;
+  }
+  st = block_sum<double>(st, red);
+  sd = block_sum<double>(sd, red);
+  if (threadIdx.x == 0) {
+    sums[2 * b] = st;
+    sums[2 * b + 1] = sd;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_snr_finish(const double* __restrict__ sums, int64_t B, float* __restrict__ out) {
+  __shared__ float red[16];
+  const float eps = 1.1920928955078125e-07f;  // torch.finfo(float32).eps
+  float v = 0.f;
+  for (int64_t b = threadIdx.x; b < B; b += blockDim.x)
+    v += 10.f * log10f((float(sums[2 * b]) + eps) / (float(sums[2 * b + 1]) + eps));
+  v = block_sum<float>(v, red);
+  if (threadIdx.x == 0) out[0] = v / float(B);
+}
+
+__global__ __launch_bounds__(256) void k_snr_bwd(const float* __restrict__ p, const float* __restrict__ t, int64_t B,
+                                                 int64_t T, const double* __restrict__ sums,
+                                                 const float* __restrict__ g, float* __restrict__ gp) {
+  const float eps = 1.1920928955078125e-07f;
+  const float gv = g[0] * (20.f / 2.302585092994046f) / float(B);
+  const int64_t n = B * T;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t b = i / T;
+    const float den = float(sums[2 * b + 1]) + eps;
+    gp[i] = gv * (t[i] - p[i]) / den;
+  }
+}
+
 }  // namespace glue
 }  // namespace sel
 
@@ -72,6 +137,51 @@ int sel_add_noise(const float* speech, const float* noise, int64_t n, float snr,
   hipLaunchKernelGGL(k_sumsq2, dim3(nb), dim3(256), 0, s, speech, noise, n, part);
   SEL_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_mix, dim3(nb), dim3(256), 0, s, speech, noise, n, part, nb, snr, out);
+  SEL_LAUNCH_CHECK();
+  return SEL_OK;
+}
+
+int sel_sumsq2(const float* speech, const float* noise, int64_t n, double* sums2, void* ws, size_t ws_bytes,
+               sel_stream_t stream) {
+  SEL_REQUIRE(n > 0, SEL_ERR_ARG, "empty batch");
+  SEL_REQUIRE(ws_bytes >= sel_add_noise_workspace(n), SEL_ERR_WORKSPACE, "workspace too small");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int nb = int(std::min<int64_t>(kBlocks, (n + 255) / 256));
+  double* part = static_cast<double*>(ws);
+  hipLaunchKernelGGL(k_sumsq2, dim3(nb), dim3(256), 0, s, speech, noise, n, part);
+  SEL_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_finish2, dim3(1), dim3(256), 0, s, part, nb, sums2);
+  SEL_LAUNCH_CHECK();
+  return SEL_OK;
+}
+
+int sel_mix_noise(const float* speech, const float* noise, int64_t n, const double* sums2, float snr, float* out,
+                  sel_stream_t stream) {
+  SEL_REQUIRE(n > 0, SEL_ERR_ARG, "empty batch");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int nb = int(std::min<int64_t>(4096, (n + 255) / 256));
+  hipLaunchKernelGGL(k_mix2, dim3(nb), dim3(256), 0, s, speech, noise, n, sums2, snr, out);
+  SEL_LAUNCH_CHECK();
+  return SEL_OK;
+}
+
+int sel_snr_fwd(const float* pred, const float* target, int64_t B, int64_t T, double* sums, float* out,
+                sel_stream_t stream) {
+  SEL_REQUIRE(B > 0 && T > 0, SEL_ERR_ARG, "empty SNR input");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(k_snr_sums, dim3(unsigned(B)), dim3(256), 0, s, pred, target, T, sums);
+  SEL_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_snr_finish, dim3(1), dim3(256), 0, s, sums, B, out);
+  SEL_LAUNCH_CHECK();
+  return SEL_OK;
+}
+
+int sel_snr_bwd(const float* pred, const float* target, int64_t B, int64_t T, const double* sums, const float* g_out,
+                float* g_pred, sel_stream_t stream) {
+  SEL_REQUIRE(B > 0 && T > 0, SEL_ERR_ARG, "empty SNR input");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int nb = int(std::min<int64_t>(4096, (B * T + 255) / 256));
+  hipLaunchKernelGGL(k_snr_bwd, dim3(nb), dim3(256), 0, s, pred, target, B, T, sums, g_out, g_pred);
   SEL_LAUNCH_CHECK();
   return SEL_OK;
 }

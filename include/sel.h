@@ -199,6 +199,20 @@ int sel_rvq_bwd(const float* x, int64_t N, int D, const float* embed0, int K, co
 size_t sel_add_noise_workspace(int64_t n);
 int sel_add_noise(const float* speech, const float* noise, int64_t n, float snr, float* out,
                   void* ws, size_t ws_bytes, sel_stream_t stream);
+/* the same in two halves for data-parallel mixing: per-rank sums2 = {sum s^2, sum n^2}
+ * (device doubles, all-reduced by the caller across ranks), then the mix */
+int sel_sumsq2(const float* speech, const float* noise, int64_t n, double* sums2, void* ws,
+               size_t ws_bytes, sel_stream_t stream);
+int sel_mix_noise(const float* speech, const float* noise, int64_t n, const double* sums2, float snr,
+                  float* out, sel_stream_t stream);
+
+/* ---- SNR term of train_denoise.py:140 (torchmetrics 1.2.0 SignalNoiseRatio,
+ * zero_mean=False): snr_b = 10 log10((sum t^2 + eps) / (sum (t-p)^2 + eps)) over the
+ * last dim, out[0] = mean_b snr_b.  bwd: g_p = g * 20/ln10 * (t-p) / (D_b + eps) / B. */
+int sel_snr_fwd(const float* pred, const float* target, int64_t B, int64_t T, double* sums /*2B*/,
+                float* out, sel_stream_t stream);
+int sel_snr_bwd(const float* pred, const float* target, int64_t B, int64_t T, const double* sums,
+                const float* g_out, float* g_pred, sel_stream_t stream);
 
 #ifdef __cplusplus
 }

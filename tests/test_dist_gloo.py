@@ -1,0 +1,141 @@
+"""World-size-2 data-parallel tests on CPU (gloo, 127.0.0.1).
+
+Cover the host logic of sel/dist.py: equal sharding of the global batch, the
+batch-global add_noise exchange (per-rank sums -> all-reduce -> mix; the two
+device kernels are replaced by their oracle math so only the exchange is under
+test here — tests/test_gpu_glue.py checks the kernels themselves), and that the
+DDP wrapper's averaged gradients equal the single-process full-batch gradient
+for a mean loss (the property the denoise step relies on, sel/dist.py docstring).
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import ref_ops as R
+
+WORLD = 2
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, port, fn, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(WORLD), LOCAL_RANK=str(rank))
+    try:
+        from sel import dist as D
+        D.init_from_env(backend="gloo")
+        res = fn(rank)
+        # numpy, not tensors: torch's shared-memory handles die with the child
+        res = [t.numpy() for t in res] if isinstance(res, list) else res.numpy()
+        q.put((rank, res))
+    except Exception as e:  # pragma: no cover - surfaced by the parent
+        q.put((rank, e))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def _run(fn):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, port, fn, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    for r, v in out.items():
+        if isinstance(v, Exception):
+            raise v
+    conv = lambda v: [torch.from_numpy(a) for a in v] if isinstance(v, list) else torch.from_numpy(v)
+    return {r: conv(v) for r, v in out.items()}
+
+
+def _global_batch():
+    g = torch.Generator().manual_seed(7)
+    speech = torch.randn(4, 1, 4800, generator=g, dtype=torch.float64).float()
+    noise = 0.3 * torch.randn(4, 1, 4800, generator=g, dtype=torch.float64).float()
+    return speech, noise
+
+
+def _add_noise_case(rank):
+    from sel import dist as D
+
+    def local_sumsq(s, n):  # oracle math of sel_sumsq2
+        return torch.stack([(s.double() ** 2).sum(), (n.double() ** 2).sum()])
+
+    def mix(s, n, sums, snr):  # oracle math of sel_mix_noise
+        import math
+        scale = math.exp(snr / 10) * math.sqrt(float(sums[1])) / math.sqrt(float(sums[0]))
+        return ((scale * s.double() + n.double()) / 2).float()
+
+    D._local_sumsq, D._mix = local_sumsq, mix
+    speech, noise = _global_batch()
+    return D.add_noise_global(D.shard(speech), D.shard(noise), 5.0)
+
+
+def test_add_noise_global_matches_single_device():
+    out = _run(_add_noise_case)
+    speech, noise = _global_batch()
+    ref = R.add_noise(speech.double(), noise.double(), 5.0).float()
+    got = torch.cat([out[0], out[1]])
+    torch.testing.assert_close(got, ref, rtol=1e-6, atol=1e-6)
+    # rank-local norms would differ: the exchange is load-bearing
+    loc = torch.cat([R.add_noise(speech[:2], noise[:2], 5.0), R.add_noise(speech[2:], noise[2:], 5.0)])
+    assert (loc - ref).abs().max() > 1e-3
+
+
+def _tiny_model():
+    torch.manual_seed(3)
+    return torch.nn.Sequential(torch.nn.Conv1d(1, 8, 7, padding=3), torch.nn.ELU(), torch.nn.Conv1d(8, 1, 3, padding=1))
+
+
+def _batch():
+    g = torch.Generator().manual_seed(11)
+    return torch.randn(4, 1, 256, generator=g), torch.randn(4, 1, 256, generator=g)
+
+
+def _ddp_case(rank):
+    from sel import dist as D
+    m = D.wrap_ddp(_tiny_model())
+    x, y = _batch()
+    loss = torch.nn.functional.l1_loss(m(D.shard(x)), D.shard(y))
+    loss.backward()
+    return [p.grad.clone() for p in m.parameters()]
+
+
+def test_ddp_grad_equals_full_batch():
+    out = _run(_ddp_case)
+    m = _tiny_model()
+    x, y = _batch()
+    torch.nn.functional.l1_loss(m(x), y).backward()
+    for r in range(WORLD):
+        for g, p in zip(out[r], m.parameters()):
+            torch.testing.assert_close(g, p.grad, rtol=1e-5, atol=1e-6)
+
+
+def _shard_case(rank):
+    from sel import dist as D
+    t = torch.arange(8)
+    assert D.rank_world() == (rank, WORLD)
+    return D.shard(t)
+
+
+def test_shard_disjoint_cover():
+    out = _run(_shard_case)
+    assert torch.equal(torch.cat([out[0], out[1]]), torch.arange(8))
+
+
+def test_shard_rejects_ragged():
+    from sel import dist as D
+    with pytest.raises(ValueError):
+        D.shard(torch.arange(5), rank=0, world=2)
