@@ -52,7 +52,17 @@ SYMAD_24MEL = dict(
     discriminator_optimizer_params=dict(lr=2.0e-4, weight_decay=1.0e-6), discriminator_grad_norm=1,
 )
 
-CONFIGS = {"symAD_libritts_24000_hop300": SYMAD_LIBRITTS_24K_DENOISE, "symAD_24Mel": SYMAD_24MEL}
+# noise-dropout continuations of 24Mel (config/denoise/symAD_24MelNDO{,SNR}.yaml, symAD_custom.yaml)
+_NDO = dict(noise_dropout_rate=0.8, noise_dropout_rate_decay=0.1, epoch_to_enable_noise_dropout_decay=1,
+            experiment_name="24Mel-NDR08-NDRD01-Cont.")
+SYMAD_24MEL_NDO = dict(SYMAD_24MEL, **_NDO, initial_model="24kHz-NDR08-NDRD01-SISDRcheckpoint-30701.pkl", step=30701)
+SYMAD_24MEL_NDOSNR = dict(SYMAD_24MEL, **_NDO, initial_model="24kHz-NDR08-NDRD01-SNRcheckpoint-55830.pkl",
+                          step=55830, lambda_snr_loss=45.0)
+SYMAD_CUSTOM = dict(SYMAD_24MEL, **_NDO, sample_rate=48000, step=55830, batch_size=16)
+
+CONFIGS = {"symAD_libritts_24000_hop300": SYMAD_LIBRITTS_24K_DENOISE, "symAD_24Mel": SYMAD_24MEL,
+           "symAD_24MelNDO": SYMAD_24MEL_NDO, "symAD_24MelNDOSNR": SYMAD_24MEL_NDOSNR,
+           "symAD_custom": SYMAD_CUSTOM}
 
 
 def get(name):

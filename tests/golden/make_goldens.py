@@ -76,7 +76,7 @@ def _audio(ref):
 
 
 def _np(t):
-    return t.detach().cpu().numpy()
+    return t.detach().cpu().numpy().copy()  # never alias live parameters
 
 
 def _sd(module, prefix="sd."):

@@ -155,3 +155,30 @@ def test_add_noise():
     g = golden("add_noise")
     for snr in (10, 15, 19):
         close(R.add_noise(T(g["clean"]), T(g["noise"]), snr), g[f"mixed.{snr}"], rtol=1e-6, atol=1e-7)
+
+
+def test_train_step():
+    """train_denoise.py:213-243 for the without-PQC generator: 45*mel, backward,
+    clip_grad_norm_(1), Adam(lr 5e-5, wd 1e-6) — two steps vs the reference's run."""
+    g = golden("train_step")
+    gm = golden("melmat")
+    P = {k[4:]: T(v).clone() for k, v in g.items() if k.startswith("sd0.")}
+    train = [k for k in P if k.startswith(("encoder.", "decoder.conv_blocks", "decoder.conv2"))
+             and not k.endswith("pad_buffer")]
+    for k in train:
+        P[k].requires_grad_(True)
+    opt = torch.optim.Adam([P[k] for k in train], lr=5e-5, weight_decay=1e-6)
+    geo = R.generator_geometry(encode_channels=4, decode_channels=4)
+    mm = T(gm["melmat.24k_fmax24000"])
+    xn, xc = T(g["x_noisy"]), T(g["x_clean"])
+    for s in range(2):
+        y = R.generator_forward(P, xn, geo, pqc=False)
+        loss = 45.0 * R.multi_mel_loss(y, xc, [(2048, 300, 2048)], [R.hann(2048)], [mm], 1e-10, None)
+        opt.zero_grad()
+        loss.backward()
+        tn = torch.nn.utils.clip_grad_norm_([P[k] for k in train], 1.0)
+        opt.step()
+        close(loss, g[f"loss.{s}"], rtol=1e-5)
+        close(tn, g[f"gradnorm.{s}"], rtol=1e-4)
+        for k in train:
+            close(P[k], g[f"sd{s + 1}.{k}"], rtol=1e-5, atol=1e-7)

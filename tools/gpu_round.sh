@@ -6,7 +6,12 @@ TESTS=${@:-tests}
 OUT=$GRAFT_REPO_ROOT/gpurun_out
 mkdir -p $OUT
 timeout -k 10 600 python -m pytest $TESTS -q -m gpu -x > $OUT/${TAG}_tests.log 2>&1
-echo "tests rc=$?"; tail -3 $OUT/${TAG}_tests.log
+RC=$?; echo "tests rc=$RC"; tail -3 $OUT/${TAG}_tests.log
+# 0 pass / 1 test failure: go on; anything else (fault, abort, timeout): stop here
+[ $RC -le 1 ] || exit $RC
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/${TAG}_smoke.log 2>&1 || exit 1
+tail -1 $OUT/${TAG}_smoke.log
+[ -n "$NO_BENCH" ] && exit 0
 timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $OUT/${TAG}_bench.log 2>&1 || exit 1
 tail -1 $OUT/${TAG}_bench.log
 cd /tmp && export TMPDIR=/tmp

@@ -1,0 +1,70 @@
+"""Microbenchmark of the spectral kernels at SURVEY §8d's HBM-measurement size
+(B >= 512 signals x 1 s @ 24 kHz, beyond the 256 MB Infinity Cache).
+
+Per signal per resolution: STFT magnitude bytes = 4*(T + F*K)
+(read the waveform once, write the magnitudes once), flops = F*(2.5 n log2 n + n + 4K).
+usage: python tools/stft_bench.py [B]     (GPU)
+"""
+import math
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "dl-speech-enhancement_amd")]
+
+import torch  # noqa: E402
+
+from sel import _lib as L  # noqa: E402
+from sel import spectral as S  # noqa: E402
+
+RES = [(1024, 120, 600), (2048, 240, 1200), (512, 50, 240), (2048, 300, 2048)]
+
+
+def timed(fn, iters=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters * 1e-3
+
+
+def main():
+    B = int(sys.argv[1]) if len(sys.argv) > 1 else 512
+    T = 24000
+    dev = torch.device("cuda")
+    L.lib()
+    x = 0.1 * torch.randn(B, T, device=dev)
+    y = 0.1 * torch.randn(B, T, device=dev)
+    print(f"B={B} T={T}")
+    print("| kernel | n_fft/hop/win | us | alg. bytes | GB/s | % of 8 TB/s | GFLOP/s |")
+    print("|---|---|---|---|---|---|---|")
+    for n, h, w in RES:
+        win = torch.hann_window(w, device=dev)
+        F, K = 1 + T // h, n // 2 + 1
+        nbytes = 4 * B * (T + F * K)
+        flops = B * F * (2.5 * n * math.log2(n) + n + 4 * K)
+        mag = torch.empty(B, F, K, device=dev)
+        s = timed(lambda: L.call("sel_stft_mag_fwd", L.ptr(x), B, T, n, h, w, L.ptr(win), 1e-7, L.ptr(mag),
+                                 L.stream()))
+        print(f"| stft_mag_fwd | {n}/{h}/{w} | {s * 1e6:.1f} | {nbytes / 1e6:.1f} MB | {nbytes / s / 1e9:.0f} | "
+              f"{100 * nbytes / s / 8e12:.1f} | {flops / s / 1e9:.0f} |", flush=True)
+        # fused STFT loss forward: both signals, partial sums only (compute-bound)
+        xr = x.clone().requires_grad_(True)
+
+        def fused():
+            return S.StftLoss.apply(xr, y, n, h, w, win) if hasattr(S, "StftLoss") else None
+        try:
+            s2 = timed(lambda: fused())
+            print(f"| stft_loss_fwd (x,y) | {n}/{h}/{w} | {s2 * 1e6:.1f} | {2 * 4 * B * T / 1e6:.1f} MB in | "
+                  f"{2 * 4 * B * T / s2 / 1e9:.0f} | - | {2 * flops / s2 / 1e9:.0f} |", flush=True)
+        except Exception as e:  # noqa: BLE001
+            print(f"| stft_loss_fwd | {n}/{h}/{w} | n/a ({str(e)[:60]}) |")
+
+
+if __name__ == "__main__":
+    main()
