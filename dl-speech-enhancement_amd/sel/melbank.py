@@ -47,3 +47,22 @@ def slaney_mel(sr, n_fft, n_mels=128, fmin=0.0, fmax=None):
         w[i] = np.maximum(0, np.minimum(rise, fall))
     w *= (2.0 / (edges[2:int(n_mels) + 2] - edges[:int(n_mels)]))[:, None]
     return w
+
+
+def htk_fbanks(n_freqs, f_min, f_max, n_mels, sample_rate):
+    """torchaudio.functional.melscale_fbanks(..., norm=None, mel_scale="htk")
+    (torchaudio 2.1.1, the default of transforms.MelSpectrogram used by
+    mel_spectrogram.py:38; torchaudio is not installed here).  fp32 like
+    torchaudio: linspace bin freqs, HTK mel points, min(down, up) triangles.
+    Returns (n_freqs, n_mels) float32 — torchaudio's `fb` buffer layout."""
+    import torch
+    all_freqs = torch.linspace(0, sample_rate // 2, n_freqs)
+    m_min = 2595.0 * np.log10(1.0 + f_min / 700.0)
+    m_max = 2595.0 * np.log10(1.0 + f_max / 700.0)
+    m_pts = torch.linspace(float(m_min), float(m_max), n_mels + 2)
+    f_pts = 700.0 * (10.0 ** (m_pts / 2595.0) - 1.0)
+    f_diff = f_pts[1:] - f_pts[:-1]
+    slopes = f_pts.unsqueeze(0) - all_freqs.unsqueeze(1)
+    down = (-1.0 * slopes[:, :-2]) / f_diff[:-1]
+    up = slopes[:, 2:] / f_diff[1:]
+    return torch.max(torch.zeros(1), torch.min(down, up))

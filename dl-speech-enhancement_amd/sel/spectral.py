@@ -228,3 +228,20 @@ class MelL1(torch.autograd.Function):
                                    L.ptr(a), L.ptr(b), L.ptr(g), 1.0 / a.numel(), L.ptr(gx), L.ptr(ws),
                                    ws.numel(), L.stream())
         return gx, None, None, None, None, None, None, None, None, None, None
+
+
+def power_mel(x, n_fft, hop, win_length, window, fb, krange, power=2.0):
+    """|STFT|^power @ fb (torchaudio MelSpectrogram semantics, mel_spectrogram.py:38).
+    x (B, T) fp32 device -> (B, n_mels, 1 + T // hop).  Forward only: the reference
+    uses it as an eval metric (Mel_L1), so a grad-requiring input is refused
+    rather than silently detached."""
+    if torch.is_grad_enabled() and x.requires_grad:
+        raise NotImplementedError("sel power_mel is forward-only (eval metric); call under torch.no_grad()")
+    x = _signal_2d(x)
+    L.need_device(x, window, fb, krange)
+    B, T = x.shape
+    n_mels = fb.shape[1]
+    out = torch.empty(B, n_mels, _frames(T, hop), device=x.device, dtype=torch.float32)
+    L.call("sel_power_mel_fwd", L.ptr(x), B, T, int(n_fft), int(hop), int(win_length), L.ptr(window),
+           L.ptr(fb), L.ptr(krange), n_mels, float(power), L.ptr(out), L.stream())
+    return out

@@ -98,6 +98,14 @@ int sel_logmel_fwd(const float* x, int64_t B, int64_t T, int n_fft, int hop,
                    int win_length, const float* window, const float* melmat,
                    const int32_t* krange, int n_mels, float eps, int log_kind,
                    float* out, sel_stream_t stream);
+/* ---- power-mel: mel_spectrogram.py:38-44 (torchaudio MelSpectrogram(48000), eval Mel-L1) --
+ * x (B,T) -> out (B, n_mels, F), F = 1 + T/hop: |STFT|^power (center/reflect, periodic
+ * window of win_length centred in n_fft, onesided) @ fb (K, n_mels), K = n_fft/2 + 1.
+ * n_fft even, n_fft/2 <= 512 with prime factors in {2,3,5} (n_fft 400 -> 200 = 4*2*5*5).
+ * krange as for sel_logmel_fwd.  Forward only (an eval metric). */
+int sel_power_mel_fwd(const float* x, int64_t B, int64_t T, int n_fft, int hop, int win_length,
+                      const float* window, const float* fb, const int32_t* krange, int n_mels, float power,
+                      float* out, sel_stream_t stream);
 /* L1 between two (n) tensors: losses/mel_loss.py:153 F.l1_loss -> out (1 float, mean). */
 size_t sel_l1_workspace(int64_t n);
 int sel_l1_mean(const float* a, const float* b, int64_t n, float* out, void* ws,

@@ -35,6 +35,46 @@ def stft_mag(x, fft_size, hop_size, win_length, window, eps=1e-7):
     return torch.sqrt(torch.clamp(p, min=eps)).transpose(2, 1)
 
 
+def htk_melscale_fbanks(n_freqs, f_min, f_max, n_mels, sample_rate):
+    """torchaudio 2.1.1 functional.melscale_fbanks(norm=None, mel_scale="htk")
+    (third-party, absent here: restated from its published algorithm; parity of
+    mel_spectrogram.py:38 is therefore unpinned beyond this restatement).
+    fp32 throughout, as torchaudio: linspace freqs, HTK mel points, triangles."""
+    all_freqs = torch.linspace(0, sample_rate // 2, n_freqs)
+    m_min = 2595.0 * math.log10(1.0 + (f_min / 700.0))
+    m_max = 2595.0 * math.log10(1.0 + (f_max / 700.0))
+    m_pts = torch.linspace(m_min, m_max, n_mels + 2)
+    f_pts = 700.0 * (10.0 ** (m_pts / 2595.0) - 1.0)
+    f_diff = f_pts[1:] - f_pts[:-1]
+    slopes = f_pts.unsqueeze(0) - all_freqs.unsqueeze(1)
+    down = (-1.0 * slopes[:, :-2]) / f_diff[:-1]
+    up = slopes[:, 2:] / f_diff[1:]
+    return torch.max(torch.zeros(1), torch.min(down, up))  # (n_freqs, n_mels)
+
+
+def power_melspec(x, sample_rate=48000, n_fft=400, hop_length=None, win_length=None, n_mels=128, f_min=0.0,
+                  f_max=None, power=2.0):
+    """mel_spectrogram.py:38 — torchaudio transforms.MelSpectrogram(48000) with its
+    defaults: Spectrogram(center, reflect, periodic Hann, onesided, |X|^power)
+    then MelScale (HTK, no norm).  x (..., T) -> (..., n_mels, 1 + T // hop)."""
+    win_length = win_length or n_fft
+    hop_length = hop_length or win_length // 2
+    f_max = f_max if f_max is not None else float(sample_rate // 2)
+    shape = x.shape
+    x2 = x.reshape(-1, shape[-1])
+    z = torch.stft(x2, n_fft, hop_length, win_length, torch.hann_window(win_length), center=True,
+                   pad_mode="reflect", normalized=False, onesided=True, return_complex=True)
+    spec = z.abs().pow(power)  # (N, K, F)
+    fb = htk_melscale_fbanks(n_fft // 2 + 1, f_min, f_max, n_mels, sample_rate)
+    mel = torch.matmul(spec.transpose(-1, -2), fb).transpose(-1, -2)
+    return mel.reshape(shape[:-1] + mel.shape[-2:])
+
+
+def mel_l1(pred, target, **kw):
+    """mel_spectrogram.py:40-44 Mel_L1: nn.L1Loss()(mel(pred), mel(target))."""
+    return F.l1_loss(power_melspec(pred, **kw), power_melspec(target, **kw))
+
+
 def spectral_convergence(x_mag, y_mag):
     """losses/stft_loss.py:45-56 — global Frobenius ratio."""
     return torch.norm(y_mag - x_mag, p="fro") / torch.norm(y_mag, p="fro")

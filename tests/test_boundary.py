@@ -75,3 +75,11 @@ def test_mel_ranges_cover_nonzeros():
         nz = np.nonzero(mm[k])[0]
         if nz.size:
             assert mr[k, 0] <= nz.min() and mr[k, 1] > nz.max()
+
+
+def test_product_htk_filterbank_matches_oracle():
+    """The product's torchaudio-HTK filterbank restatement equals the oracle's."""
+    from oracle import ref_ops as R
+    from sel.melbank import htk_fbanks
+    for args in [(201, 0.0, 24000.0, 128, 48000), (121, 0.0, 12000.0, 40, 24000), (257, 20.0, 8000.0, 80, 16000)]:
+        assert torch.equal(htk_fbanks(*args), R.htk_melscale_fbanks(*args))
