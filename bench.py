@@ -179,6 +179,36 @@ def c3_cpu_baseline(B_sample=2, steps=2):
 MFMA_BF16_PEAK_TFS = 2500.0  # MI355X dense bf16 (MI355X_MICROARCH.md)
 
 
+PMC_FILE = os.path.join(REPO, "profiles", "r1_c3_pmc_traffic.json")
+
+
+def _mangled_fragment(tag):
+    """'k_conv_fwd_bf16<128, 64, 2, 8, bf16>' -> 'k_conv_fwd_bf16ILi128ELi64ELi2ELi8EDF16bE' (Itanium)."""
+    import re
+    m = re.match(r"(\w+)<(.*)>", tag)
+    if not m:
+        return tag
+    parts = []
+    for a in (x.strip() for x in m.group(2).split(",")):
+        parts.append({"bf16": "DF16b", "float": "f"}.get(a, f"Li{a}E"))
+    return m.group(1) + "I" + "".join(parts) + "E"
+
+
+def pmc_traffic(tag, B, steps_cfg="c3"):
+    """HBM bytes per launch of kernel `tag` from the committed rocprofv3 PMC passes
+    (tools/pmc_traffic.py over FETCH_SIZE / WRITE_SIZE runs of this same bench
+    command, gfx950 corrections applied there), or None if not measured."""
+    if steps_cfg != "c3" or B != 64 or not os.path.exists(PMC_FILE):
+        return None
+    frag = _mangled_fragment(tag)
+    with open(PMC_FILE) as f:
+        table = json.load(f)
+    hits = [v for k, v in table.items() if frag in k]
+    if len(hits) != 1:
+        return None
+    return hits[0]["traffic_bytes_per_launch"]
+
+
 def roofline(cfg, timer, dom, B, steps):
     """Dominant timed kernel instance -> achieved vs peak (HIP events, same stream)."""
     summ = timer.summary()
@@ -205,7 +235,8 @@ def roofline(cfg, timer, dom, B, steps):
              "frac": round(ach / HBM_PEAK_GBS, 4)}
     r.update({"kernel": tag, "launches": n, "avg_launch_us": round(1e3 * ms / n, 2),
               "bytes_per_launch": int(nbytes / n), "flops_per_launch": int(flops / n),
-              "share_of_timed_conv_ms": round(ms / sum(v[1] for v in summ.values()), 3), "traffic": None})
+              "share_of_timed_conv_ms": round(ms / sum(v[1] for v in summ.values()), 3),
+              "traffic": pmc_traffic(tag, B, cfg), "traffic_unit": "bytes/launch (rocprofv3 PMC, profiles/)"})
     return r
 
 
