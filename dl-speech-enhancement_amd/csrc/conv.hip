@@ -39,6 +39,10 @@ template <> __device__ __forceinline__ __bf16 from_f<__bf16>(float v) { return _
 
 __device__ __forceinline__ float elu(float v) { return v > 0.f ? v : expm1f(v); }
 __device__ __forceinline__ float elu_grad(float v) { return v > 0.f ? 1.f : expf(v); }
+// bf16 path: the result is rounded to bf16 (8-bit mantissa), so the hardware
+// exp (v_exp_f32, a few ulp of fp32) replaces the libm expm1/exp range reduction.
+__device__ __forceinline__ float elu_fast(float v) { return v > 0.f ? v : __expf(v) - 1.f; }
+__device__ __forceinline__ float elu_grad_fast(float v) { return v > 0.f ? 1.f : __expf(v); }
 
 struct Args {
   int64_t rows;
@@ -339,7 +343,7 @@ __global__ __launch_bounds__(256) void k_conv_fwd_bf16(Args a, const __bf16* __r
       if (a.in_elu) {
         __bf16* t = reinterpret_cast<__bf16*>(&val);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) t[e] = __bf16(elu(float(t[e])));
+        for (int e = 0; e < 8; ++e) t[e] = __bf16(elu_fast(float(t[e])));
       }
       *reinterpret_cast<uint4*>(xs + (v >> 2) * P + (v & 3) * 8) = val;
     }
@@ -416,6 +420,8 @@ __global__ __launch_bounds__(256) void k_conv_fwd_bf16(Args a, const __bf16* __r
   __syncthreads();
   constexpr int V = Vec16<TO>::n;
   const bool vec_ok = (a.N % V) == 0;
+  // bias index: one modulo per V-vector (period % V == 0 keeps a vector inside one period)
+  const bool bias_vec = bias && a.bias_period && (a.bias_period % V) == 0;
   for (int idx = tid; idx < BM * (BN / V); idx += 256) {
     const int r = idx / (BN / V), cv = (idx % (BN / V)) * V;
     const int64_t m = m0 + r;
@@ -423,18 +429,24 @@ __global__ __launch_bounds__(256) void k_conv_fwd_bf16(Args a, const __bf16* __r
     if (m >= a.rows || n >= a.N) continue;
     const int64_t o = m * a.N + n;
     float v[V];
+    if (bias_vec) {
+      const float* bp = bias + (n % a.bias_period);
 #pragma unroll
-    for (int e = 0; e < V; ++e) {
-      const int ne = n + e;
-      const float bv = (bias && a.bias_period && ne < a.N) ? bias[ne % a.bias_period] : 0.f;
-      v[e] = ot[r * OP + cv + e] + bv;
+      for (int e = 0; e < V; ++e) v[e] = ot[r * OP + cv + e] + bp[e];
+    } else {
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        const int ne = n + e;
+        const float bv = (bias && a.bias_period && ne < a.N) ? bias[ne % a.bias_period] : 0.f;
+        v[e] = ot[r * OP + cv + e] + bv;
+      }
     }
     if (vec_ok) {
       if (aux) {
         TO av[V];
         *reinterpret_cast<uint4*>(av) = *reinterpret_cast<const uint4*>(aux + o);
 #pragma unroll
-        for (int e = 0; e < V; ++e) v[e] *= elu_grad(to_f(av[e]));
+        for (int e = 0; e < V; ++e) v[e] *= elu_grad_fast(to_f(av[e]));
       }
       if (res) {
         TO rv[V];
@@ -449,7 +461,7 @@ __global__ __launch_bounds__(256) void k_conv_fwd_bf16(Args a, const __bf16* __r
     } else {
       for (int e = 0; e < V && n + e < a.N; ++e) {
         float x = v[e];
-        if (aux) x *= elu_grad(to_f(aux[o + e]));
+        if (aux) x *= elu_grad_fast(to_f(aux[o + e]));
         if (res) x += to_f(res[o + e]);
         out[o + e] = from_f<TO>(x);
       }
@@ -654,7 +666,7 @@ __global__ __launch_bounds__(256) void k_wgrad_bf16(Args a, const __bf16* __rest
       }
       if (a.in_elu) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) vals[e] = __bf16(elu(float(vals[e])));
+        for (int e = 0; e < 8; ++e) vals[e] = __bf16(elu_fast(float(vals[e])));
       }
       *reinterpret_cast<uint4*>(xs + r * PX + v) = *reinterpret_cast<uint4*>(vals);
     }
@@ -740,6 +752,10 @@ __global__ __launch_bounds__(256) void k_wgrad2_bf16(Args a, const __bf16* __res
     }
 #pragma unroll
     for (int u = 0; u < XV; ++u) {
+      if (u * 64 >= span) {  // block-uniform: no halo rows to fetch (K = 1 / short halo)
+        xr[u] = make_uint4(0, 0, 0, 0);
+        continue;
+      }
       const int v = tid + u * 256;
       const int r = v >> 2;
       int ti = t0 - a.pad + r;
@@ -767,7 +783,7 @@ __global__ __launch_bounds__(256) void k_wgrad2_bf16(Args a, const __bf16* __res
       if (a.in_elu) {
         __bf16* t = reinterpret_cast<__bf16*>(&val);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) t[e] = __bf16(elu(float(t[e])));
+        for (int e = 0; e < 8; ++e) t[e] = __bf16(elu_fast(float(t[e])));
       }
       *reinterpret_cast<uint4*>(x + (v >> 2) * 32 + (v & 3) * 8) = val;
     }
@@ -935,6 +951,55 @@ __global__ void k_pack_dgrad(const T* __restrict__ wp, int N, int K, int C, T* _
     const int j = int((i / N) % K);
     const int c = int(i / (int64_t(N) * K));
     wd[i] = wp[(int64_t(n) * K + (K - 1 - j)) * C + c];
+  }
+}
+
+// Multi-tensor pack: every job's fwd pack Wp and (optionally) its dgrad form Wd
+// in ONE launch (the per-layer launches of sel_pack_weight + sel_pack_dgrad were
+// ~120 x 4 us per training step).  Grid-stride over the concatenated packed
+// elements; a thread binary-searches its job in the device job table.
+template <typename TO>
+__global__ void k_pack_many(const sel_pack_job* __restrict__ jobs, int njobs, int64_t total) {
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+       i += int64_t(gridDim.x) * blockDim.x) {
+    int lo = 0, hi = njobs - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (jobs[mid].offset <= i) lo = mid;
+      else hi = mid - 1;
+    }
+    const sel_pack_job& J = jobs[lo];
+    const int64_t li = i - J.offset;
+    const int s = J.stride, cin = J.cin, cout = J.cout, K = J.k;
+    float v = 0.f;
+    int N, KP, CP, n, kp, cp;
+    if (J.kind == SEL_PACK_FWD) {
+      N = cout, KP = K, CP = cin;
+      cp = int(li % cin);
+      kp = int((li / cin) % K);
+      n = int(li / (int64_t(cin) * K));
+      v = J.w[(int64_t(n) * cin + cp) * K + kp];
+    } else if (J.kind == SEL_PACK_FWD_STRIDED) {
+      N = cout, KP = 3, CP = s * cin;
+      cp = int(li % CP);
+      kp = int((li / CP) % 3);
+      n = int(li / (int64_t(CP) * 3));
+      const int ph = cp / cin, ci = cp % cin;
+      const int k = strided_k(kp, ph, s);
+      v = k >= 0 ? J.w[(int64_t(n) * cin + ci) * (2 * s) + k] : 0.f;
+    } else {
+      N = s * cout, KP = 2, CP = cin;
+      cp = int(li % cin);
+      kp = int((li / cin) % 2);
+      n = int(li / (int64_t(cin) * 2));
+      const int ph = n / cout, co = n % cout;
+      const int k = kp == 0 ? ph + s : ph;
+      v = J.w[(int64_t(cp) * cout + co) * (2 * s) + k];
+    }
+    const TO tv = from_f<TO>(v);
+    static_cast<TO*>(J.wpack)[li] = tv;
+    // Wd[c][j][n] = Wp[n][KP-1-j][c]
+    if (J.wdgrad) static_cast<TO*>(J.wdgrad)[(int64_t(cp) * KP + (KP - 1 - kp)) * N + n] = tv;
   }
 }
 
@@ -1333,6 +1398,18 @@ int sel_pack_weight(int kind, const float* w, int cout, int cin, int k, int stri
   else
     hipLaunchKernelGGL(k_pack<__bf16>, grid, dim3(256), 0, s, kind, w, cout, cin, k, stride,
                        static_cast<__bf16*>(wpack));
+  SEL_LAUNCH_CHECK();
+  return SEL_OK;
+}
+
+int sel_pack_many(const sel_pack_job* jobs, int njobs, int64_t total, int dtype, sel_stream_t stream) {
+  SEL_REQUIRE(jobs && njobs > 0 && total > 0, SEL_ERR_ARG, "empty pack job table");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  dim3 grid(unsigned(std::min<int64_t>(8192, (total + 255) / 256)));
+  if (dtype == SEL_F32)
+    hipLaunchKernelGGL(k_pack_many<float>, grid, dim3(256), 0, s, jobs, njobs, total);
+  else
+    hipLaunchKernelGGL(k_pack_many<__bf16>, grid, dim3(256), 0, s, jobs, njobs, total);
   SEL_LAUNCH_CHECK();
   return SEL_OK;
 }

@@ -12,6 +12,7 @@ Reference semantics (file:line under the reference root):
 """
 import ctypes
 import threading
+import weakref
 from contextlib import contextmanager
 
 import torch
@@ -123,6 +124,97 @@ def pack_dgrad(wp):
     return out
 
 
+class _PackJob(ctypes.Structure):
+    """include/sel.h sel_pack_job"""
+    _fields_ = [("w", ctypes.c_void_p), ("wpack", ctypes.c_void_p), ("wdgrad", ctypes.c_void_p),
+                ("offset", ctypes.c_int64), ("kind", ctypes.c_int32), ("cout", ctypes.c_int32),
+                ("cin", ctypes.c_int32), ("k", ctypes.c_int32), ("stride", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
+
+
+def _packed_shape(kind, w, stride):
+    if kind == PACK_CONVT:
+        cin, cout, k = w.shape
+        return (stride * cout, 2, cin), cout, cin, k
+    cout, cin, k = w.shape
+    return ((cout, k, cin) if kind == PACK_FWD else (cout, 3, stride * cin)), cout, cin, k
+
+
+class _PackEntry:
+    __slots__ = ("wref", "kind", "stride", "dtype", "version", "wp", "wd")
+
+
+class PackCache:
+    """Packed bf16/fp32 forms (fwd Wp and dgrad Wd) of every conv weight, refreshed
+    in ONE sel_pack_many launch per weight update instead of two launches per
+    layer per step.
+
+    Validity is tracked with the parameter's version counter (bumped by every
+    in-place update through autograd-visible ops: optimizer steps, copy_,
+    load_state_dict).  A refresh repacks every stale entry into FRESH buffers,
+    so tensors saved by a graph that has not run backward yet are never
+    overwritten.  Code that mutates a weight through ``.data`` (which has its own
+    version counter) must call ``invalidate()``.
+    """
+
+    def __init__(self):
+        self._entries = {}
+        self._lock = threading.Lock()
+
+    def invalidate(self):
+        with self._lock:
+            self._entries.clear()
+
+    def get(self, kind, w, stride, dtype):
+        key = (w.data_ptr(), kind, stride, dtype, tuple(w.shape), w.device)
+        with self._lock:
+            e = self._entries.get(key)
+            if e is not None and e.wref() is w and e.version == w._version:
+                return e.wp, e.wd
+            if e is None or e.wref() is not w:
+                e = _PackEntry()
+                e.wref, e.kind, e.stride, e.dtype = weakref.ref(w), kind, stride, dtype
+                e.version, e.wp, e.wd = None, None, None
+                self._entries[key] = e
+            self._refresh(w.device, dtype)
+            return e.wp, e.wd
+
+    def _refresh(self, device, dtype):
+        stale = []
+        for key, e in list(self._entries.items()):
+            w = e.wref()
+            if w is None:
+                del self._entries[key]
+                continue
+            if e.dtype == dtype and w.device == device and e.version != w._version:
+                stale.append((e, w))
+        if not stale:
+            return
+        shapes = []
+        total = 0
+        for e, w in stale:
+            shp, cout, cin, k = _packed_shape(e.kind, w, e.stride)
+            n = shp[0] * shp[1] * shp[2]
+            shapes.append((shp, cout, cin, k, total, n))
+            total += n
+        flat = torch.empty(2 * total, dtype=dtype, device=device)
+        jobs = (_PackJob * len(stale))()
+        for j, ((e, w), (shp, cout, cin, k, off, n)) in enumerate(zip(stale, shapes)):
+            if not w.is_contiguous() or w.dtype != torch.float32:
+                raise L.SelError("sel: conv weights must be contiguous fp32 parameters")
+            e.wp = flat[off:off + n].view(shp)
+            e.wd = flat[total + off:total + off + n].view(shp[2], shp[1], shp[0])
+            e.version = w._version
+            jobs[j] = _PackJob(w.data_ptr(), e.wp.data_ptr(), e.wd.data_ptr(), off, e.kind, cout, cin, k,
+                               e.stride, 0)
+        host = torch.frombuffer(bytearray(jobs), dtype=torch.uint8).pin_memory()
+        dev = host.to(device, non_blocking=True)
+        L.call("sel_pack_many", L.ptr(dev), len(stale), total, _code(dtype), L.stream())
+
+
+PACKS = PackCache()
+
+
 def prim(desc, x, wp, bias=None, aux=None, res=None, out_dtype=None):
     """The conv primitive; x is (rows, C) channels-last (any leading shape)."""
     out_dtype = out_dtype or x.dtype
@@ -216,23 +308,23 @@ class ConvLayerFn(torch.autograd.Function):
             if k != 2 * stride:
                 raise L.SelError(f"sel: strided CausalConv1d needs kernel_size == 2*stride (got {k}, {stride})")
         desc, T_out, c_out = _layer_desc(kind, B, T_in, cin, cout, k, stride, dil, b is not None)
-        wp = pack(kind, w, stride, x.dtype)
+        wp, wd = PACKS.get(kind, w, stride, x.dtype)
         bias = b.detach().contiguous().float() if b is not None else None
         y = prim(desc, x, wp, bias=bias)
-        ctx.save_for_backward(x, wp)
+        ctx.save_for_backward(x, wp, wd)
         ctx.meta = (desc, kind, stride, tuple(w.shape), b is not None)
         return y.view(B, T_out, c_out)
 
     @staticmethod
     def backward(ctx, gy):
-        x, wp = ctx.saved_tensors
+        x, wp, wd = ctx.saved_tensors
         desc, kind, stride, w_shape, has_bias = ctx.meta
         gy = gy.contiguous()
         if gy.dtype != x.dtype:
             gy = cast(gy, x.dtype)
         gx = gw = gb = None
         if ctx.needs_input_grad[0]:
-            gx = prim(desc.adjoint(), gy, pack_dgrad(wp))
+            gx = prim(desc.adjoint(), gy, wd)
             if desc.pad_mode == PAD_REPLICATE:
                 L.call("sel_conv_replicate_fix", ctypes.byref(desc), _code(gy.dtype), L.ptr(gy), L.ptr(wp),
                        L.ptr(gx), L.stream())
@@ -259,20 +351,20 @@ class ResidualUnitFn(torch.autograd.Function):
         d2 = ConvDesc(B * T, T, cm, w2.shape[0], 1, 1, 0, PAD_ZERO, 1, w2.shape[0] if b2 is not None else 0)
         if w2.shape[0] != C:
             raise L.SelError("residual unit needs out_channels == in_channels")
-        wp1 = pack(PACK_FWD, w1, 1, x.dtype)
-        wp2 = pack(PACK_FWD, w2, 1, x.dtype)
+        wp1, wd1 = PACKS.get(PACK_FWD, w1, 1, x.dtype)
+        wp2, wd2 = PACKS.get(PACK_FWD, w2, 1, x.dtype)
         bb1 = b1.detach().float().contiguous() if b1 is not None else None
         bb2 = b2.detach().float().contiguous() if b2 is not None else None
         xf = x.view(B * T, C)
         h = prim(d1, xf, wp1, bias=bb1)
         out = prim(d2, h, wp2, bias=bb2, res=xf)
-        ctx.save_for_backward(x, h, wp1, wp2)
+        ctx.save_for_backward(x, h, wd1, wd2)
         ctx.meta = (d1, d2, tuple(w1.shape), tuple(w2.shape))
         return out.view(B, T, C)
 
     @staticmethod
     def backward(ctx, g):
-        x, h, wp1, wp2 = ctx.saved_tensors
+        x, h, wd1, wd2 = ctx.saved_tensors
         d1, d2, s1, s2 = ctx.meta
         B, T, C = x.shape
         g = g.contiguous()
@@ -281,7 +373,7 @@ class ResidualUnitFn(torch.autograd.Function):
         gf = g.view(B * T, C)
         xf = x.view(B * T, C)
         # dL/dh = (W2^T g) * ELU'(h)
-        gh = prim(d2.adjoint(), gf, pack_dgrad(wp2), aux=h)
+        gh = prim(d2.adjoint(), gf, wd2, aux=h)
         gw1 = gb1 = gw2 = gb2 = None
         if ctx.needs_input_grad[3] or ctx.needs_input_grad[4]:
             gwp2, gb2 = wgrad(d2, gf, h, d2.bias_period > 0 and ctx.needs_input_grad[4])
@@ -289,7 +381,7 @@ class ResidualUnitFn(torch.autograd.Function):
         gx = None
         if ctx.needs_input_grad[0]:
             # dL/dx = g + (conv_adjoint(gh)) * ELU'(x)
-            gx = prim(d1.adjoint(), gh, pack_dgrad(wp1), aux=xf, res=gf).view(B, T, C)
+            gx = prim(d1.adjoint(), gh, wd1, aux=xf, res=gf).view(B, T, C)
         if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
             gwp1, gb1 = wgrad(d1, gh, xf, d1.bias_period > 0 and ctx.needs_input_grad[2])
             gw1 = unpack(PACK_FWD, gwp1, s1, 1) if ctx.needs_input_grad[1] else None

@@ -171,6 +171,17 @@ int sel_pack_weight(int kind, const float* w, int cout, int cin, int k, int stri
                     int dtype, void* wpack, sel_stream_t stream);
 int sel_pack_dgrad(const void* wpack, int N, int K, int C, int dtype, void* wd,
                    sel_stream_t stream);
+/* Batched form of sel_pack_weight + sel_pack_dgrad for many layers in one launch.
+ * `jobs` is a DEVICE array of njobs entries sorted by `offset` (the prefix sum of
+ * each job's packed element count); total = sum of the counts.  wdgrad may be NULL. */
+typedef struct sel_pack_job {
+  const float* w;     /* torch-layout fp32 weight */
+  void* wpack;        /* Wp (dtype) */
+  void* wdgrad;       /* dgrad form of Wp (dtype) or NULL */
+  int64_t offset;
+  int32_t kind, cout, cin, k, stride, reserved;
+} sel_pack_job;
+int sel_pack_many(const sel_pack_job* jobs, int njobs, int64_t total, int dtype, sel_stream_t stream);
 /* gwpack (packed fp32) -> torch layout gw (kind as in sel_pack_weight). */
 int sel_unpack_wgrad(int kind, const float* gwpack, int cout, int cin, int k, int stride,
                      float* gw, sel_stream_t stream);
