@@ -320,18 +320,14 @@ __global__ __launch_bounds__(256) void k_conv_fwd_bf16(Args a, const __bf16* __r
 #pragma unroll
     for (int u = 0; u < XV; ++u) {
       const int c = c0 + ((tid + u * 256) & 3) * 8;
-      uint4 v = *reinterpret_cast<const uint4*>(in + xrow[u] * a.C + c);
-      if (!xok[u]) v = make_uint4(0, 0, 0, 0);
-      xr[u] = v;
+      xr[u] = *reinterpret_cast<const uint4*>(in + xrow[u] * a.C + c);  // masked in store()
     }
 #pragma unroll
     for (int u = 0; u < WV; ++u) {
       const int v = tid + u * 256;
       const int k = v / (BN * 4), n = (v >> 2) % BN, c = c0 + (v & 3) * 8;
       const bool ok = k < a.K && n0 + n < a.N;
-      uint4 val = *reinterpret_cast<const uint4*>(wp + (int64_t(ok ? n0 + n : 0) * a.K + (ok ? k : 0)) * a.C + c);
-      if (!ok) val = make_uint4(0, 0, 0, 0);
-      wr[u] = val;
+      wr[u] = *reinterpret_cast<const uint4*>(wp + (int64_t(ok ? n0 + n : 0) * a.K + (ok ? k : 0)) * a.C + c);
     }
   };
   auto store = [&]() {
@@ -339,7 +335,9 @@ __global__ __launch_bounds__(256) void k_conv_fwd_bf16(Args a, const __bf16* __r
     for (int u = 0; u < XV; ++u) {
       const int v = tid + u * 256;
       if ((v >> 2) >= span) continue;
-      uint4 val = xr[u];
+      // zero-fill AFTER the wait: masking right at the load would make hipcc wait
+      // on the load there (vmcnt(0)) and serialise the register prefetch
+      uint4 val = xok[u] ? xr[u] : make_uint4(0, 0, 0, 0);
       if (a.in_elu) {
         __bf16* t = reinterpret_cast<__bf16*>(&val);
 #pragma unroll
@@ -351,7 +349,8 @@ __global__ __launch_bounds__(256) void k_conv_fwd_bf16(Args a, const __bf16* __r
     for (int u = 0; u < WV; ++u) {
       const int v = tid + u * 256;
       const int k = v / (BN * 4), n = (v >> 2) % BN;
-      if (k < a.K) *reinterpret_cast<uint4*>(ws + (k * BN + n) * P + (v & 3) * 8) = wr[u];
+      const uint4 val = n0 + n < a.N ? wr[u] : make_uint4(0, 0, 0, 0);
+      if (k < a.K) *reinterpret_cast<uint4*>(ws + (k * BN + n) * P + (v & 3) * 8) = val;
     }
   };
 
@@ -870,6 +869,196 @@ __global__ __launch_bounds__(256) void k_wgrad2_bf16(Args a, const __bf16* __res
   }
 }
 
+// bf16 weight gradient, general tr-read path (C % 32 == 0, N % 32 == 0,
+// halo <= 64, K <= 8).  A block owns NB = 32*NT output channels x CB = 32*CT
+// input channels x ALL K taps over a contiguous range of 128-row tiles, so a
+// 64x64 layer streams gout and act(in) exactly once (the 32x32 kernel above
+// re-read both per (n, c) block).  The TT = NT*CT*K 32x32 accumulator tiles are
+// spread over the 4 waves (TPW each, contiguous so consecutive tiles share the
+// gout fragment); with TT < 4 the waves split the tile rows instead (RG row
+// groups) and meet in LDS.  Operands come from 64-B LDS rows through
+// ds_read_b64_tr_b16 (conflict free); the next tile is prefetched into
+// registers during the MFMAs.  Grid x = row split (fastest), so the blocks
+// sharing a row range are 8-aligned apart... i.e. on the same XCD when the
+// split count is a multiple of 8.
+template <int NT, int CT, int MAXT>
+__global__ __launch_bounds__(256) void k_wgrad3_bf16(Args a, const __bf16* __restrict__ gout,
+                                                     const __bf16* __restrict__ in, int tiles_per_sample,
+                                                     int64_t n_tiles, int tiles_per_split,
+                                                     float* __restrict__ part, float* __restrict__ bpart) {
+  constexpr int NB = 32 * NT, CB = 32 * CT;
+  constexpr int XROWS = W2_BM + W2_HALO;
+  constexpr int GV = W2_BM * NB / 8 / 256;   // 2*NT
+  constexpr int XV = XROWS * CB / 8 / 256;   // 3*CT
+  constexpr int GS = NT * W2_BM * 32, XS = CT * XROWS * 32;
+  constexpr int WPN = 4 / NT;                // waves per 32-wide n subtile
+  extern __shared__ __align__(16) unsigned char smem[];
+  __bf16* const base = reinterpret_cast<__bf16*>(smem);  // [buf]{G[NT][128][32], X[CT][192][32]}
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t split = blockIdx.x;
+  const int n0 = blockIdx.y * NB, c0 = blockIdx.z * CB;
+  const int64_t tb = split * tiles_per_split;
+  const int64_t te = tb + tiles_per_split < n_tiles ? tb + tiles_per_split : n_tiles;
+  const int halo = (a.K - 1) * a.dil;
+  const int span = W2_BM + halo;
+  // wave -> (n subtile, (ct, k) pairs); too few pairs -> the waves split the rows
+  const int P = CT * a.K;
+  const int RG = P >= WPN ? 1 : WPN / P;     // P in {1, 2} when RG > 1
+  const int WPP = WPN / RG;                  // waves sharing the pair list
+  const int nt = wave / WPN, wsub = wave % WPN;
+  const int rg = wsub / WPP, pw = wsub % WPP;
+  const int RROWS = W2_BM / RG;
+  const bool do_bias = bpart && blockIdx.z == 0;
+
+  uint4 gr[GV], xr[XV];
+  bool gok[GV], xok[XV];
+  auto load = [&](int64_t tile) {
+    const int64_t b = tile / tiles_per_sample;
+    const int t0 = int(tile % tiles_per_sample) * W2_BM;
+    const int64_t rb = b * a.T;
+#pragma unroll
+    for (int u = 0; u < GV; ++u) {
+      const int v = tid + u * 256;
+      const int t = t0 + v / (NB / 8);
+      gok[u] = t < a.T;
+      gr[u] = *reinterpret_cast<const uint4*>(gout + (rb + (gok[u] ? t : 0)) * a.N + n0 + (v % (NB / 8)) * 8);
+    }
+#pragma unroll
+    for (int u = 0; u < XV; ++u) {
+      const int v = tid + u * 256;
+      const int r = v / (CB / 8);
+      int ti = t0 - a.pad + r;
+      const bool inside = ti >= 0 && ti < a.T;
+      xok[u] = r < span && (inside || a.pad_mode == SEL_PAD_REPLICATE);
+      ti = ti < 0 ? 0 : (ti >= a.T ? a.T - 1 : ti);
+      if (u * 256 / (CB / 8) < span)  // block-uniform: rows past the halo are never fetched
+        xr[u] = *reinterpret_cast<const uint4*>(in + (rb + ti) * a.C + c0 + (v % (CB / 8)) * 8);
+    }
+  };
+  // zero-fill happens here, after the wait (see the v4 forward kernel's store())
+  auto store = [&](int buf) {
+    __bf16* g = base + buf * (GS + XS);
+    __bf16* x = g + GS;
+#pragma unroll
+    for (int u = 0; u < GV; ++u) {
+      const int v = tid + u * 256;
+      const int r = v / (NB / 8), c8 = v % (NB / 8);
+      *reinterpret_cast<uint4*>(g + (c8 >> 2) * (W2_BM * 32) + r * 32 + (c8 & 3) * 8) =
+          gok[u] ? gr[u] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < XV; ++u) {
+      if (u * 256 / (CB / 8) >= span) continue;
+      const int v = tid + u * 256;
+      const int r = v / (CB / 8), c8 = v % (CB / 8);
+      uint4 val = xok[u] ? xr[u] : make_uint4(0, 0, 0, 0);
+      if (a.in_elu) {
+        __bf16* t = reinterpret_cast<__bf16*>(&val);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) t[e] = __bf16(elu_fast(float(t[e])));
+      }
+      *reinterpret_cast<uint4*>(x + (c8 >> 2) * (XROWS * 32) + r * 32 + (c8 & 3) * 8) = val;
+    }
+  };
+
+  // pair j of this wave: p = pw + WPP*j -> (ct, k); slots past P compute into
+  // accumulators that are never stored (branch-free MFMA stream)
+  int xoff[MAXT];
+#pragma unroll
+  for (int j = 0; j < MAXT; ++j) {
+    int p = pw + WPP * j;
+    p = p < P ? p : P - 1;
+    xoff[j] = (p / a.K) * (XROWS * 32) + (p % a.K) * a.dil * 32;
+  }
+
+  floatx16 acc[MAXT];
+#pragma unroll
+  for (int j = 0; j < MAXT; ++j)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
+  float bsum = 0.f;
+  const int bcol = tid % NB, brow = tid / NB;
+
+  const int h = lane >> 5;
+  const int col = ((lane >> 4) & 1) * 16 + 4 * (lane & 3);
+  const int q = (lane & 15) >> 2;
+  const int lrow = (4 * h + q) * 32 + col;
+
+  if (tb < te) load(tb);
+  int buf = 0;
+  for (int64_t tile = tb; tile < te; ++tile, buf ^= 1) {
+    store(buf);
+    __syncthreads();
+    if (tile + 1 < te) load(tile + 1);
+    const __bf16* g = base + buf * (GS + XS) + nt * (W2_BM * 32);
+    const __bf16* x = base + buf * (GS + XS) + GS;
+    if (do_bias) {
+      const __bf16* gb = base + buf * (GS + XS) + (bcol >> 5) * (W2_BM * 32) + (bcol & 31);
+      for (int r = brow; r < W2_BM; r += 256 / NB) bsum += float(gb[r * 32]);
+    }
+    for (int kh = 0; kh < RROWS / 16; ++kh) {
+      const int R = (rg * RROWS + kh * 16) * 32 + lrow;
+      const v4i16 a0 = tr_read(g + R);
+      const v4i16 a1 = tr_read(g + R + 8 * 32);
+      const bf16x8 A = __builtin_bit_cast(bf16x8, __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+      for (int j = 0; j < MAXT; ++j) {
+        const v4i16 b0 = tr_read(x + xoff[j] + R);
+        const v4i16 b1 = tr_read(x + xoff[j] + R + 8 * 32);
+        const bf16x8 Bf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7));
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, Bf, acc[j], 0, 0, 0);
+      }
+    }
+  }
+
+  float* pdst = part + split * int64_t(a.N) * a.K * a.C;
+  if (RG == 1) {
+#pragma unroll
+    for (int j = 0; j < MAXT; ++j) {
+      const int p = pw + WPP * j;
+      if (p >= P) break;
+      const int ct = p / a.K, k = p % a.K;
+      const int c = c0 + ct * 32 + (lane & 31);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int n = n0 + nt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        pdst[(int64_t(n) * a.K + k) * a.C + c] = acc[j][r];
+      }
+    }
+  } else {
+    // RG > 1 only for P < WPN, i.e. MAXT slots hold at most one pair per wave
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);  // [wave][32*32]
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      red[wave * 1024 + row * 32 + (lane & 31)] = acc[0][r];
+    }
+    __syncthreads();
+    for (int i = tid; i < NT * P * 1024; i += 256) {
+      const int e = i & 1023, pi = (i >> 10) % P, ni = (i >> 10) / P;
+      float v = 0.f;
+      for (int r = 0; r < RG; ++r) v += red[(ni * WPN + r * WPP + pi) * 1024 + e];
+      const int ct = pi / a.K, k = pi % a.K;
+      const int n = n0 + ni * 32 + (e >> 5), c = c0 + ct * 32 + (e & 31);
+      pdst[(int64_t(n) * a.K + k) * a.C + c] = v;
+    }
+  }
+  if (do_bias) {
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);
+    red[tid] = bsum;
+    __syncthreads();
+    if (tid < NB) {
+      float v = 0.f;
+      for (int r = 0; r < 256 / NB; ++r) v += red[r * NB + tid];
+      bpart[split * a.N + n0 + tid] = v;
+    }
+  }
+}
+
 // Deterministic split reduction in two parallel passes:
 //   pass 1: part2[g][i] = sum_{s in group g (32 splits)} part[s][i]   (grid: i-blocks x groups)
 //   pass 2: out[j] = sum_g sum_{i % period == j} part2[g][i]
@@ -1222,33 +1411,87 @@ int wgrad_bn(int N) { return N <= 16 ? 16 : (N <= 32 ? 32 : 64); }
 struct WgPlan {
   int64_t tiles_per_sample, n_tiles;
   int nsplit, tiles_per_split, bn;
-  bool fast;
+  int mode;  // 0 generic (k_wgrad_bf16 / fp32), 2 k_wgrad2_bf16 (32x32), 3 k_wgrad3_bf16
+  int nt, ct, maxt;
 };
 
-bool wgrad_fast(const sel_conv_desc* d) {
-  if (!(d->C % 32 == 0 && d->N % 32 == 0 && (d->K - 1) * d->dil <= W2_HALO && d->K <= 8)) return false;
-  // measured (profiles/r1_wgrad_bench.md): the tr-read kernel wins for K <= 3 and the 32-channel stage
-  return d->K <= 3 || d->C == 32;
+bool wgrad_tr_ok(const sel_conv_desc* d) {
+  return d->C % 32 == 0 && d->N % 32 == 0 && (d->K - 1) * d->dil <= W2_HALO && d->K <= 8;
 }
 
-WgPlan wgrad_plan(const sel_conv_desc* d, bool fast) {
+// tune key 1: 0 = k_wgrad3 where legal, 1 = generic, 2 = k_wgrad2 (32x32 blocks)
+int wgrad_mode(const sel_conv_desc* d, int dtype) {
+  if (dtype != SEL_BF16) return 0;
+  const int t = tune(1);
+  if (t == 1 || !wgrad_tr_ok(d)) return 0;
+  return t == 2 ? 2 : 3;
+}
+
+WgPlan wgrad_plan(const sel_conv_desc* d, int mode) {
   WgPlan p;
-  p.fast = fast;
-  const int bm = fast ? W2_BM : WB_BM;
-  p.bn = fast ? 32 : wgrad_bn(d->N);
-  const int bc = fast ? 32 : WB_BC;
+  p.mode = mode;
+  p.nt = p.ct = p.maxt = 1;
+  const bool tr = mode >= 2;
+  const int bm = tr ? W2_BM : WB_BM;
+  int bn, bc;
+  if (mode == 3) {
+    // widest block whose per-wave tile count stays <= 4 (8 accumulators = 1 wave/SIMD,
+    // measured slower than re-reading a 32-wide operand from L2)
+    auto tiles_per_wave = [&](int nt, int ct) {
+      const int wpn = 4 / nt, pairs = ct * d->K;
+      const int wpp = pairs >= wpn ? wpn : pairs;  // waves sharing one pair list (kernel: WPN / RG)
+      return (pairs + wpp - 1) / wpp;
+    };
+    p.nt = d->N % 64 == 0 ? 2 : 1;
+    p.ct = d->C % 64 == 0 ? 2 : 1;
+    if (tiles_per_wave(p.nt, p.ct) > 4 && p.ct == 2) p.ct = 1;
+    if (tiles_per_wave(p.nt, p.ct) > 4 && p.nt == 2) p.nt = 1;
+    const int tpw = tiles_per_wave(p.nt, p.ct);
+    p.maxt = tpw <= 1 ? 1 : (tpw <= 2 ? 2 : (tpw <= 4 ? 4 : 8));
+    bn = 32 * p.nt;
+    bc = 32 * p.ct;
+  } else {
+    bn = tr ? 32 : wgrad_bn(d->N);
+    bc = tr ? 32 : WB_BC;
+  }
+  p.bn = bn;
   p.tiles_per_sample = (d->T + bm - 1) / bm;
   p.n_tiles = (d->rows / d->T) * p.tiles_per_sample;
-  const int64_t blocks = int64_t((d->N + p.bn - 1) / p.bn) * ((d->C + bc - 1) / bc);
-  int64_t want = std::max<int64_t>(1, (768 + blocks - 1) / blocks);
+  const int64_t blocks = int64_t((d->N + bn - 1) / bn) * ((d->C + bc - 1) / bc);
+  const int64_t target = mode == 3 ? 512 : 768;
+  int64_t want = std::max<int64_t>(1, (target + blocks - 1) / blocks);
+  if (mode == 3) want = (want + 7) / 8 * 8;  // splits on x: blocks of one row range share an XCD
   const int64_t per_split = (int64_t(d->N) * d->K * d->C + d->N) * 4;
-  want = std::min<int64_t>(want, std::max<int64_t>(1, (int64_t(64) << 20) / per_split));
+  want = std::min<int64_t>(want, std::max<int64_t>(1, (int64_t(mode == 3 ? 32 : 64) << 20) / per_split));
   want = std::min<int64_t>(want, std::max<int64_t>(1, p.n_tiles));
   p.tiles_per_split = int((p.n_tiles + want - 1) / want);
   if (p.tiles_per_split < 1) p.tiles_per_split = 1;
   p.nsplit = int((p.n_tiles + p.tiles_per_split - 1) / p.tiles_per_split);
   if (p.nsplit < 1) p.nsplit = 1;
   return p;
+}
+
+template <int NT, int CT>
+hipError_t launch_wgrad3(const WgPlan& p, const Args& a, const __bf16* gout, const __bf16* in, float* part,
+                         float* bpart, hipStream_t s) {
+  constexpr size_t lds = size_t(2) * (NT * W2_BM * 32 + CT * (W2_BM + W2_HALO) * 32) * sizeof(__bf16);
+  dim3 grid(unsigned(p.nsplit), unsigned(a.N / (32 * NT)), unsigned(a.C / (32 * CT)));
+#define SEL_WG3(MT)                                                                                            \
+  {                                                                                                            \
+    auto kern = k_wgrad3_bf16<NT, CT, MT>;                                                                     \
+    if (lds > 64 * 1024) {                                                                                     \
+      hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)); \
+      if (e != hipSuccess) return e;                                                                           \
+    }                                                                                                          \
+    hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, a, gout, in, int(p.tiles_per_sample), p.n_tiles,          \
+                       p.tiles_per_split, part, bpart);                                                        \
+  }
+  if (p.maxt == 1) SEL_WG3(1)
+  else if (p.maxt == 2) SEL_WG3(2)
+  else if (p.maxt == 4) SEL_WG3(4)
+  else SEL_WG3(8)
+#undef SEL_WG3
+  return hipGetLastError();
 }
 
 }  // namespace
@@ -1284,8 +1527,8 @@ int sel_conv_fwd(const sel_conv_desc* d, int in_dtype, int out_dtype, const void
 
 size_t sel_conv_wgrad_workspace(const sel_conv_desc* d) {
   if (!d || d->rows <= 0 || d->T <= 0) return 16;
-  const WgPlan p0 = wgrad_plan(d, false), p1 = wgrad_plan(d, true);
-  const int ns = std::max(p0.nsplit, wgrad_fast(d) ? p1.nsplit : 0);
+  int ns = wgrad_plan(d, 0).nsplit;
+  if (wgrad_tr_ok(d)) ns = std::max(ns, std::max(wgrad_plan(d, 2).nsplit, wgrad_plan(d, 3).nsplit));
   const int ng = (ns + SPLIT_GROUP - 1) / SPLIT_GROUP;
   return size_t(ns + ng) * (size_t(d->N) * d->K * d->C + d->N) * sizeof(float);
 }
@@ -1299,10 +1542,17 @@ int sel_conv_wgrad(const sel_conv_desc* d, int dtype, const void* gout, const vo
   SEL_REQUIRE(ws_bytes >= sel_conv_wgrad_workspace(d), SEL_ERR_WORKSPACE, "workspace too small");
   const Args a = to_args(d);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const WgPlan p = wgrad_plan(d, dtype == SEL_BF16 && wgrad_fast(d) && tune(1) == 0);
+  const WgPlan p = wgrad_plan(d, wgrad_mode(d, dtype));
   float* part = static_cast<float*>(ws);
   float* bpart = gbias ? part + size_t(p.nsplit) * d->N * d->K * d->C : nullptr;
-  if (d->rows > 0 && dtype == SEL_BF16 && p.fast) {
+  if (d->rows > 0 && p.mode == 3) {
+    const __bf16* g16 = static_cast<const __bf16*>(gout);
+    const __bf16* x16 = static_cast<const __bf16*>(in);
+    if (p.nt == 1 && p.ct == 1) SEL_HIP((launch_wgrad3<1, 1>(p, a, g16, x16, part, bpart, s)));
+    else if (p.nt == 2 && p.ct == 1) SEL_HIP((launch_wgrad3<2, 1>(p, a, g16, x16, part, bpart, s)));
+    else if (p.nt == 1 && p.ct == 2) SEL_HIP((launch_wgrad3<1, 2>(p, a, g16, x16, part, bpart, s)));
+    else SEL_HIP((launch_wgrad3<2, 2>(p, a, g16, x16, part, bpart, s)));
+  } else if (d->rows > 0 && p.mode == 2) {
     // staging double buffer (40 KB) also hosts the [wave][taps][32x32] fp32 reduction
     const size_t lds = std::max<size_t>(size_t(2) * (W2_BM * 32 + (W2_BM + W2_HALO) * 32) * sizeof(__bf16),
                                         size_t(4) * 8 * 1024 * sizeof(float) / 4 * 1);

@@ -157,3 +157,55 @@ def test_channels_last_views_flow_without_copies(gpu):
     assert y.shape == (2, 32, 600) and y.stride(1) == 1  # (B,C,T) view of (B,T,C)
     z = b(y)
     assert z.shape == (2, 64, 200) and z.stride(1) == 1
+
+
+# C3 layer shapes (primitive form): C, N, K, dil, pad_mode, in_elu, bias, T
+WGRAD_SHAPES = [(32, 32, 7, 9, 0, 1, 0, 2400), (32, 32, 1, 1, 0, 1, 0, 2400), (96, 64, 3, 1, 0, 0, 64, 800),
+                (64, 64, 7, 3, 0, 1, 0, 800), (64, 64, 1, 1, 0, 1, 0, 800), (64, 96, 2, 1, 1, 0, 32, 800),
+                (256, 128, 3, 1, 0, 0, 128, 200), (128, 128, 7, 9, 0, 1, 0, 200), (256, 256, 7, 1, 0, 1, 0, 40),
+                (640, 256, 3, 1, 0, 0, 256, 40), (512, 1280, 2, 1, 1, 0, 256, 8), (32, 64, 7, 1, 0, 0, 0, 300)]
+
+
+@pytest.mark.parametrize("shape", WGRAD_SHAPES)
+def test_wgrad_kernels_agree(gpu, shape):
+    """Every bf16 weight-gradient kernel (tune key 1: 0 = k_wgrad3, 1 = generic,
+    2 = k_wgrad2) must give the same fp32 sums as the fp32 oracle of the same
+    bf16 operands: 1e-5 norm-wise (fp32 accumulation, different orders)."""
+    import ctypes
+    from sel import _lib as L
+    from sel import convops as CO
+    C, N, K, dil, mode, elu, bias, T = shape
+    B = 4
+    pad = (K - 1) * dil if mode == 0 else 1
+    d = CO.ConvDesc(B * T, T, C, N, K, dil, pad, mode, elu, bias)
+    torch.manual_seed(C + N + K)
+    x = (0.5 * torch.randn(B * T, C, device=gpu)).to(torch.bfloat16)
+    g = (0.5 * torch.randn(B * T, N, device=gpu)).to(torch.bfloat16)
+    # fp64 reference of the same bf16 operands
+    xa = x.double().view(B, T, C)
+    if elu:
+        xa = torch.nn.functional.elu(xa.float()).to(torch.bfloat16).double()
+    ga = g.double().view(B, T, N)
+    ref = torch.zeros(N, K, C, dtype=torch.float64, device=gpu)
+    for k in range(K):
+        idx = torch.arange(T, device=gpu) + k * dil - pad
+        if mode == 0:
+            ok = (idx >= 0) & (idx < T)
+            xs = torch.zeros(B, T, C, dtype=torch.float64, device=gpu)
+            xs[:, ok] = xa[:, idx[ok]]
+        else:
+            xs = xa[:, idx.clamp(0, T - 1)]
+        ref[:, k, :] = torch.einsum("btn,btc->nc", ga, xs)
+    bref = ga.sum((0, 1)).view(-1, bias).sum(0) if bias else None
+    lib = L.lib()
+    for variant in (0, 1, 2):
+        prev = lib.sel_tune(1, variant)
+        try:
+            gw, gb = CO.wgrad(d, g, x, bool(bias))
+        finally:
+            lib.sel_tune(1, prev)
+        e = ((gw.double() - ref).norm() / ref.norm()).item()
+        assert e < 2e-3 if elu else e < 1e-5, (variant, e)
+        if bias:
+            eb = ((gb.double() - bref).norm() / bref.norm()).item()
+            assert eb < 1e-5, (variant, eb)

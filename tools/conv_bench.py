@@ -70,7 +70,7 @@ def main():
     L.lib()
     print("| shape | " + " | ".join(f"v{v}" for v in variants) + " | best | GB/s | TF/s |")
     print("|---" * (len(variants) + 4) + "|")
-    for sh in SHAPES:
+    for sh in [x for x in SHAPES if os.environ.get("SHAPE", "") in x[0]]:
         name, rows, T, C, N, K, dil, pad, mode, elu, aux, res, bias = sh
         times = []
         for v in variants:
@@ -90,7 +90,7 @@ if __name__ == "__main__" and os.environ.get("WGRAD", "0") != "1":
     main()
 
 
-WG_SHAPES = [s for s in SHAPES if "dgrad" not in s[0]]
+WG_SHAPES = [s for s in SHAPES if "dgrad" not in s[0] and os.environ.get("SHAPE", "") in s[0]]
 
 
 def run_wgrad(shape, variant, iters=10):
@@ -120,7 +120,7 @@ def main_wgrad():
     print("\n| wgrad shape | fast (us) | generic (us) | GB/s | TF/s |\n|---|---|---|---|---|")
     for sh in WG_SHAPES:
         name, rows, T, C, N, K, dil, pad, mode, elu, aux, res, bias = sh
-        t0, t1 = run_wgrad(sh, 0), run_wgrad(sh, 1)
+        t0, t1 = run_wgrad(sh, int(os.environ.get("WG_A", "0"))), run_wgrad(sh, int(os.environ.get("WG_B", "1")))
         nbytes = 2 * (rows * C + rows * N)
         flops = 2.0 * rows * N * K * C
         print(f"| {name} | {t0:.1f} | {t1:.1f} | {nbytes / t0 / 1e3:.0f} | {flops / t0 / 1e6:.0f} |", flush=True)
