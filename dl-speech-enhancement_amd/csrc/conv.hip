@@ -298,22 +298,30 @@ __global__ __launch_bounds__(256) void k_conv_fwd_bf16(Args a, const __bf16* __r
   const int span = BM + halo;
   __bf16* const ws = xs + span * P;  // [k][BN][P]
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WAVES_N, wn = wave % WAVES_N;
-  const int64_t m0 = int64_t(blockIdx.x) * BM;
+  // sample-aligned tiles: every output row of the block belongs to sample b, so
+  // the causal zero / replicate padding is resolved once while staging and the
+  // MFMA loop needs no per-tap row validity (blocks past T are clipped at store)
+  const int tps = (a.T + BM - 1) / BM;
+  const int64_t b = blockIdx.x / tps;
+  const int t0 = int(blockIdx.x % tps) * BM;
+  const int64_t m0 = b * a.T + t0;
+  const int mrows = a.T - t0 < BM ? a.T - t0 : BM;
   const int n0 = blockIdx.y * BN;
-  const int64_t g0 = m0 - a.pad;
   const int nchunk = a.C / CK;
 
-  // staging rows of this thread: flat row g = g0 + (v >> 2); clamp into [0, rows)
+  // staging row r <-> input time t0 - pad + r of sample b
   int64_t xrow[XV];
   bool xok[XV];
 #pragma unroll
   for (int u = 0; u < XV; ++u) {
     const int r = (tid + u * 256) >> 2;
-    const int64_t g = g0 + r;
-    xok[u] = r < span && g >= 0 && g < a.rows;
-    xrow[u] = xok[u] ? g : 0;
+    int ti = t0 - a.pad + r;
+    const bool inside = ti >= 0 && ti < a.T;
+    xok[u] = r < span && (inside || a.pad_mode == SEL_PAD_REPLICATE);
+    ti = ti < 0 ? 0 : (ti >= a.T ? a.T - 1 : ti);
+    xrow[u] = b * a.T + ti;
   }
   uint4 xr[XV], wr[WV];
   auto load = [&](int c0) {
@@ -354,14 +362,10 @@ __global__ __launch_bounds__(256) void k_conv_fwd_bf16(Args a, const __bf16* __r
     }
   };
 
-  // per-lane output row (one per 32-row tile) -> time index within its sample
-  int lr[TM], tt[TM];
+  // per-lane output row of each 32-row tile -> its staged-row offset
+  int lr[TM];
 #pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    lr[i] = wm * WTM + i * 32 + (lane & 31);
-    const int64_t m = m0 + lr[i];
-    tt[i] = m < a.rows ? int(m % a.T) : -(1 << 30);
-  }
+  for (int i = 0; i < TM; ++i) lr[i] = (wm * WTM + i * 32 + (lane & 31)) * P;
 
   floatx16 acc[TM][TN];
 #pragma unroll
@@ -385,17 +389,10 @@ __global__ __launch_bounds__(256) void k_conv_fwd_bf16(Args a, const __bf16* __r
 #pragma unroll
         for (int j = 0; j < TN; ++j)
           bf[j] = *reinterpret_cast<const bf16x8*>(ws + (k * BN + wn * WTN + j * 32 + (lane & 31)) * P + co);
+        const int kofs = k * a.dil * P + co;
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
-          const int ti = tt[i] + k * a.dil - a.pad;
-          bool valid = ti >= 0 && ti < a.T;
-          int xrw = lr[i] + k * a.dil;
-          if (!valid && a.pad_mode == SEL_PAD_REPLICATE && tt[i] >= 0) {
-            xrw = lr[i] + a.pad + (ti < 0 ? 0 : a.T - 1) - tt[i];
-            valid = true;
-          }
-          bf16x8 af = *reinterpret_cast<const bf16x8*>(xs + (valid ? xrw : 0) * P + co);
-          if (!valid) af = bf16x8{};
+          const bf16x8 af = *reinterpret_cast<const bf16x8*>(xs + lr[i] + kofs);
 #pragma unroll
           for (int j = 0; j < TN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf[j], acc[i][j], 0, 0, 0);
@@ -425,7 +422,7 @@ __global__ __launch_bounds__(256) void k_conv_fwd_bf16(Args a, const __bf16* __r
     const int r = idx / (BN / V), cv = (idx % (BN / V)) * V;
     const int64_t m = m0 + r;
     const int n = n0 + cv;
-    if (m >= a.rows || n >= a.N) continue;
+    if (r >= mrows || n >= a.N) continue;
     const int64_t o = m * a.N + n;
     float v[V];
     if (bias_vec) {
@@ -1327,7 +1324,8 @@ int launch_fwd4(const Args& a, const void* in, const void* wp, const float* bias
   const size_t stage = (size_t(span) + size_t(a.K) * BN) * F4_P * 2;
   const size_t epi = size_t(BM) * (BN + 4) * 4;
   const size_t lds = stage > epi ? stage : epi;
-  dim3 grid(unsigned((a.rows + BM - 1) / BM), unsigned((a.N + BN - 1) / BN));
+  const int64_t tiles = (a.rows / a.T) * ((a.T + BM - 1) / BM);  // sample-aligned tiles
+  dim3 grid(unsigned(tiles), unsigned((a.N + BN - 1) / BN));
   if (grid.x == 0) return SEL_OK;
   auto kern = k_conv_fwd_bf16<BM, BN, WAVES_M, KMAX, TO>;
   if (lds > 64 * 1024)
