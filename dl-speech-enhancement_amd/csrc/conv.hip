@@ -466,6 +466,159 @@ __global__ __launch_bounds__(256) void k_conv_fwd_bf16(Args a, const __bf16* __r
 }
 
 // ---------------------------------------------------------------------------
+// Single-input-channel layers (the encoder's first conv 1->32 k7, and the dgrad
+// of the decoder's last conv 32->1 k7): an implicit GEMM with a reduction of
+// only K taps would leave MFMA idle and stage a 1-wide tile, so this is a
+// streaming kernel instead: one output row per thread, K input samples, N x K
+// FMAs against LDS-broadcast weights, 16-B vector stores of the N outputs.
+// ---------------------------------------------------------------------------
+constexpr int C1_NMAX = 64;
+constexpr int C1_KMAX = 8;
+constexpr int C1_TR = 256;    // rows per sample-aligned tile
+constexpr int C1_HALO = 64;   // max (K-1)*dil
+
+// Stage act(x) for input times [t0 - pad, t0 - pad + C1_TR + halo) of sample b as
+// fp32 in LDS, causal zero / replicate padding resolved here.
+__device__ __forceinline__ void c1_stage(const Args& a, const __bf16* __restrict__ in, int64_t b, int t0,
+                                         float* xs) {
+  const int span = C1_TR + (a.K - 1) * a.dil;
+  for (int r = threadIdx.x; r < span; r += 256) {
+    int ti = t0 - a.pad + r;
+    const bool inside = ti >= 0 && ti < a.T;
+    const bool ok = inside || a.pad_mode == SEL_PAD_REPLICATE;
+    ti = ti < 0 ? 0 : (ti >= a.T ? a.T - 1 : ti);
+    const float v = float(in[b * a.T + ti]);
+    xs[r] = ok ? (a.in_elu ? elu_fast(v) : v) : 0.f;
+  }
+}
+
+// Thread = (8-wide output group g, row lane rl): its 8 x K weights live in
+// registers; per row it reads K staged samples and writes one 16-B vector, the
+// NG lanes of a row together writing the row's contiguous N outputs.
+template <typename TO>
+__global__ __launch_bounds__(256) void k_conv_c1_bf16(Args a, const __bf16* __restrict__ in,
+                                                      const __bf16* __restrict__ wp, const float* __restrict__ bias,
+                                                      const TO* __restrict__ aux, const TO* __restrict__ res,
+                                                      TO* __restrict__ out) {
+  __shared__ float xs[C1_TR + C1_HALO];
+  constexpr int V = Vec16<TO>::n;  // outputs per vector store (8 bf16 / 4 fp32)
+  const int NG = a.N / V;
+  const int tid = threadIdx.x, grp = tid % NG, rl = tid / NG, nrl = 256 / NG;
+  float w[V][C1_KMAX], bs[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) {
+    const int n = grp * V + e;
+    bs[e] = (bias && a.bias_period) ? bias[n % a.bias_period] : 0.f;
+#pragma unroll
+    for (int k = 0; k < C1_KMAX; ++k) w[e][k] = k < a.K ? float(wp[n * a.K + k]) : 0.f;
+  }
+  const int tps = (a.T + C1_TR - 1) / C1_TR;
+  const int64_t ntiles = (a.rows / a.T) * tps;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t b = tile / tps;
+    const int t0 = int(tile % tps) * C1_TR;
+    __syncthreads();
+    c1_stage(a, in, b, t0, xs);
+    __syncthreads();
+    const int rows = a.T - t0 < C1_TR ? a.T - t0 : C1_TR;
+    for (int r = rl; r < rows; r += nrl) {
+      float v[V];
+#pragma unroll
+      for (int e = 0; e < V; ++e) v[e] = bs[e];
+#pragma unroll
+      for (int k = 0; k < C1_KMAX; ++k) {
+        if (k >= a.K) break;
+        const float x = xs[r + k * a.dil];
+#pragma unroll
+        for (int e = 0; e < V; ++e) v[e] = fmaf(w[e][k], x, v[e]);
+      }
+      const int64_t o = (b * a.T + t0 + r) * a.N + grp * V;
+      if (aux) {
+        TO av[V];
+        *reinterpret_cast<uint4*>(av) = *reinterpret_cast<const uint4*>(aux + o);
+#pragma unroll
+        for (int e = 0; e < V; ++e) v[e] *= elu_grad_fast(to_f(av[e]));
+      }
+      if (res) {
+        TO rv[V];
+        *reinterpret_cast<uint4*>(rv) = *reinterpret_cast<const uint4*>(res + o);
+#pragma unroll
+        for (int e = 0; e < V; ++e) v[e] += to_f(rv[e]);
+      }
+      TO ov[V];
+#pragma unroll
+      for (int e = 0; e < V; ++e) ov[e] = from_f<TO>(v[e]);
+      *reinterpret_cast<uint4*>(out + o) = *reinterpret_cast<uint4*>(ov);
+    }
+  }
+}
+
+// Weight gradient of a single-input-channel layer: gWp[n][k] = sum_m g[m][n] *
+// act(x[row(m, k)]) and the bias sums.  Thread = (8-wide n group, row lane);
+// each block walks its contiguous range of sample-aligned 256-row tiles with the
+// samples staged in LDS, then reduces its lanes (shuffles, LDS over waves) into
+// one partial per block.
+__global__ __launch_bounds__(256) void k_wgrad_c1_bf16(Args a, const __bf16* __restrict__ gout,
+                                                       const __bf16* __restrict__ in, int64_t tiles_per_split,
+                                                       float* __restrict__ part, float* __restrict__ bpart) {
+  __shared__ float xs[C1_TR + C1_HALO];
+  __shared__ float red[4][C1_NMAX * (C1_KMAX + 1)];
+  const int NG = a.N / 8;  // 1, 2, 4 or 8 n-groups
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int grp = tid % NG, rl = tid / NG, nrl = 256 / NG;
+  const int tps = (a.T + C1_TR - 1) / C1_TR;
+  const int64_t ntiles = (a.rows / a.T) * tps;
+  const int64_t tb = int64_t(blockIdx.x) * tiles_per_split;
+  const int64_t te = tb + tiles_per_split < ntiles ? tb + tiles_per_split : ntiles;
+  float acc[8][C1_KMAX], bsum[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    bsum[e] = 0.f;
+#pragma unroll
+    for (int k = 0; k < C1_KMAX; ++k) acc[e][k] = 0.f;
+  }
+  for (int64_t tile = tb; tile < te; ++tile) {
+    const int64_t b = tile / tps;
+    const int t0 = int(tile % tps) * C1_TR;
+    __syncthreads();
+    c1_stage(a, in, b, t0, xs);
+    __syncthreads();
+    const int rows = a.T - t0 < C1_TR ? a.T - t0 : C1_TR;
+    for (int r = rl; r < rows; r += nrl) {
+      __bf16 gv[8];
+      *reinterpret_cast<uint4*>(gv) = *reinterpret_cast<const uint4*>(gout + (b * a.T + t0 + r) * a.N + grp * 8);
+      float xv[C1_KMAX];
+#pragma unroll
+      for (int k = 0; k < C1_KMAX; ++k) xv[k] = k < a.K ? xs[r + k * a.dil] : 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float g = float(gv[e]);
+        bsum[e] += g;
+#pragma unroll
+        for (int k = 0; k < C1_KMAX; ++k) acc[e][k] = fmaf(g, xv[k], acc[e][k]);
+      }
+    }
+  }
+  // lanes of one wave with the same n group differ in the bits >= log2(NG)
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+#pragma unroll
+    for (int k = 0; k <= C1_KMAX; ++k) {
+      float v = k < C1_KMAX ? acc[e][k] : bsum[e];
+      for (int o = 32; o >= NG; o >>= 1) v += __shfl_xor(v, o, 64);
+      if (lane < NG) red[wave][(grp * 8 + e) * (C1_KMAX + 1) + k] = v;
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < a.N * (C1_KMAX + 1); i += 256) {
+    const int n = i / (C1_KMAX + 1), k = i % (C1_KMAX + 1);
+    const float v = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+    if (k < a.K) part[int64_t(blockIdx.x) * a.N * a.K + n * a.K + k] = v;
+    else if (k == C1_KMAX && bpart) bpart[int64_t(blockIdx.x) * a.N + n] = v;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // weight gradient: gWp[n][k][c] = sum_m gout[m][n] * act(in[row(m,k)][c])
 // block = (n-tile BN, c-chunk CK, m-split); all K taps per block.
 // ---------------------------------------------------------------------------
@@ -1189,6 +1342,45 @@ __global__ void k_pack_many(const sel_pack_job* __restrict__ jobs, int njobs, in
   }
 }
 
+// Packed index of torch-layout weight element i (the gather map of k_unpack).
+__device__ __forceinline__ int64_t unpack_src(int kind, int64_t i, int cout, int cin, int K, int s) {
+  if (kind == SEL_PACK_FWD) {
+    const int k = int(i % K);
+    const int ci = int((i / K) % cin);
+    const int co = int(i / (int64_t(K) * cin));
+    return (int64_t(co) * K + k) * cin + ci;
+  }
+  const int KK = 2 * s;
+  const int k = int(i % KK);
+  if (kind == SEL_PACK_FWD_STRIDED) {
+    const int ci = int((i / KK) % cin);
+    const int co = int(i / (int64_t(KK) * cin));
+    int tap, ph;
+    if (k <= s - 2) { tap = 0; ph = k + 1; }
+    else if (k <= 2 * s - 2) { tap = 1; ph = k - s + 1; }
+    else { tap = 2; ph = 0; }
+    return (int64_t(co) * 3 + tap) * (int64_t(s) * cin) + ph * cin + ci;
+  }
+  const int co = int((i / KK) % cout);
+  const int ci = int(i / (int64_t(KK) * cout));
+  const int ph = k < s ? k : k - s;
+  const int tap = k < s ? 1 : 0;
+  return (int64_t(ph * cout + co) * 2 + tap) * cin + ci;
+}
+
+// Second reduction pass fused with the unpack: gw (torch layout) = sum over the
+// split groups of the packed partials (one launch instead of two per layer).
+__global__ __launch_bounds__(256) void k_split_sum2_unpack(const float* __restrict__ part2, int ngroups, int64_t n,
+                                                           int64_t n_torch, int kind, int cout, int cin, int K,
+                                                           int s, float* __restrict__ gw) {
+  const int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= n_torch) return;
+  const int64_t j = unpack_src(kind, i, cout, cin, K, s);
+  float acc = 0.f;
+  for (int g = 0; g < ngroups; ++g) acc += part2[int64_t(g) * n + j];
+  gw[i] = acc;
+}
+
 __global__ void k_unpack(int kind, const float* __restrict__ gp, int cout, int cin, int K, int s,
                          float* __restrict__ gw) {
   // iterate over torch-layout elements
@@ -1373,6 +1565,15 @@ template <typename TI, typename TO>
 int dispatch_fwd(const Args& a, const void* in, const void* wp, const float* bias, const void* aux,
                  const void* res, void* out, hipStream_t s) {
   if constexpr (sizeof(TI) == 2) {
+    if (a.C == 1 && a.N % 8 == 0 && a.N <= C1_NMAX && a.K <= C1_KMAX && (a.K - 1) * a.dil <= C1_HALO &&
+        tune(3) == 0) {
+      const int64_t blocks = std::min<int64_t>((a.rows / a.T) * ((a.T + C1_TR - 1) / C1_TR), 4096);
+      hipLaunchKernelGGL(k_conv_c1_bf16<TO>, dim3(unsigned(blocks)), dim3(256), 0, s, a,
+                         static_cast<const __bf16*>(in), static_cast<const __bf16*>(wp), bias,
+                         static_cast<const TO*>(aux), static_cast<const TO*>(res), static_cast<TO*>(out));
+      SEL_LAUNCH_CHECK();
+      return SEL_OK;
+    }
     const int v = tune(0);
     const bool fast = (a.C % CK) == 0 && (a.K - 1) * a.dil <= F4_HALOMAX && a.K <= 8 && (v == 0 || v > 20);
     if (fast) {
@@ -1418,9 +1619,14 @@ bool wgrad_tr_ok(const sel_conv_desc* d) {
 }
 
 // tune key 1: 0 = k_wgrad3 where legal, 1 = generic, 2 = k_wgrad2 (32x32 blocks)
+bool wgrad_c1_ok(const sel_conv_desc* d) {
+  return d->C == 1 && d->N % 8 == 0 && d->N <= C1_NMAX && d->K <= C1_KMAX && (d->K - 1) * d->dil <= C1_HALO;
+}
+
 int wgrad_mode(const sel_conv_desc* d, int dtype) {
   if (dtype != SEL_BF16) return 0;
   const int t = tune(1);
+  if (wgrad_c1_ok(d) && t != 1) return 4;
   if (t == 1 || !wgrad_tr_ok(d)) return 0;
   return t == 2 ? 2 : 3;
 }
@@ -1429,6 +1635,14 @@ WgPlan wgrad_plan(const sel_conv_desc* d, int mode) {
   WgPlan p;
   p.mode = mode;
   p.nt = p.ct = p.maxt = 1;
+  if (mode == 4) {  // k_wgrad_c1_bf16: contiguous ranges of sample-aligned 256-row tiles
+    p.bn = d->N;
+    p.tiles_per_sample = (d->T + C1_TR - 1) / C1_TR;
+    p.n_tiles = (d->rows / d->T) * p.tiles_per_sample;
+    p.tiles_per_split = int(std::max<int64_t>(1, (p.n_tiles + 511) / 512));
+    p.nsplit = int((p.n_tiles + p.tiles_per_split - 1) / p.tiles_per_split);
+    return p;
+  }
   const bool tr = mode >= 2;
   const int bm = tr ? W2_BM : WB_BM;
   int bn, bc;
@@ -1527,12 +1741,44 @@ size_t sel_conv_wgrad_workspace(const sel_conv_desc* d) {
   if (!d || d->rows <= 0 || d->T <= 0) return 16;
   int ns = wgrad_plan(d, 0).nsplit;
   if (wgrad_tr_ok(d)) ns = std::max(ns, std::max(wgrad_plan(d, 2).nsplit, wgrad_plan(d, 3).nsplit));
+  if (wgrad_c1_ok(d)) ns = std::max(ns, wgrad_plan(d, 4).nsplit);
   const int ng = (ns + SPLIT_GROUP - 1) / SPLIT_GROUP;
   return size_t(ns + ng) * (size_t(d->N) * d->K * d->C + d->N) * sizeof(float);
 }
 
+namespace sel {
+namespace conv {
+struct UnpackSpec {
+  int kind, cout, cin, k, stride;
+};
+int wgrad_impl(const sel_conv_desc* d, int dtype, const void* gout, const void* in, float* gwout,
+               const UnpackSpec* up, float* gbias, void* ws, size_t ws_bytes, sel_stream_t stream);
+}  // namespace conv
+}  // namespace sel
+
 int sel_conv_wgrad(const sel_conv_desc* d, int dtype, const void* gout, const void* in, float* gwpack,
                    float* gbias, void* ws, size_t ws_bytes, sel_stream_t stream) {
+  return sel::conv::wgrad_impl(d, dtype, gout, in, gwpack, nullptr, gbias, ws, ws_bytes, stream);
+}
+
+int sel_conv_wgrad_unpacked(const sel_conv_desc* d, int dtype, const void* gout, const void* in, int kind, int cout,
+                            int cin, int k, int stride, float* gw, float* gbias, void* ws, size_t ws_bytes,
+                            sel_stream_t stream) {
+  SEL_REQUIRE(kind >= SEL_PACK_FWD && kind <= SEL_PACK_CONVT, SEL_ERR_ARG, "bad pack kind");
+  const int64_t packed = kind == SEL_PACK_FWD ? int64_t(cout) * k * cin
+                         : kind == SEL_PACK_FWD_STRIDED ? int64_t(cout) * 3 * stride * cin
+                                                        : int64_t(stride) * cout * 2 * cin;
+  SEL_REQUIRE(d && packed == int64_t(d->N) * d->K * d->C, SEL_ERR_ARG, "weight shape does not match the descriptor");
+  const sel::conv::UnpackSpec up{kind, cout, cin, k, stride};
+  return sel::conv::wgrad_impl(d, dtype, gout, in, gw, &up, gbias, ws, ws_bytes, stream);
+}
+
+}  // extern "C"
+
+namespace sel {
+namespace conv {
+int wgrad_impl(const sel_conv_desc* d, int dtype, const void* gout, const void* in, float* gwpack,
+               const UnpackSpec* up, float* gbias, void* ws, size_t ws_bytes, sel_stream_t stream) {
   if (int rc = check_desc(d)) return rc;
   SEL_REQUIRE(d->K * 2 <= WB_MAXJ * 1 || dtype == SEL_F32, SEL_ERR_UNSUPPORTED, "wgrad: K=%d too large", d->K);
   SEL_REQUIRE(dtype == SEL_BF16 || d->K * (kWgBN / 16) * 2 <= 4 * WG_MAXT, SEL_ERR_UNSUPPORTED,
@@ -1543,7 +1789,12 @@ int sel_conv_wgrad(const sel_conv_desc* d, int dtype, const void* gout, const vo
   const WgPlan p = wgrad_plan(d, wgrad_mode(d, dtype));
   float* part = static_cast<float*>(ws);
   float* bpart = gbias ? part + size_t(p.nsplit) * d->N * d->K * d->C : nullptr;
-  if (d->rows > 0 && p.mode == 3) {
+  if (d->rows > 0 && p.mode == 4) {
+    hipLaunchKernelGGL(k_wgrad_c1_bf16, dim3(unsigned(p.nsplit)), dim3(256), 0, s, a,
+                       static_cast<const __bf16*>(gout), static_cast<const __bf16*>(in), int64_t(p.tiles_per_split),
+                       part, bpart);
+    SEL_LAUNCH_CHECK();
+  } else if (d->rows > 0 && p.mode == 3) {
     const __bf16* g16 = static_cast<const __bf16*>(gout);
     const __bf16* x16 = static_cast<const __bf16*>(in);
     if (p.nt == 1 && p.ct == 1) SEL_HIP((launch_wgrad3<1, 1>(p, a, g16, x16, part, bpart, s)));
@@ -1615,8 +1866,15 @@ int sel_conv_wgrad(const sel_conv_desc* d, int dtype, const void* gout, const vo
   hipLaunchKernelGGL(k_split_sum1, dim3(unsigned((nw + 255) / 256), unsigned(ng)), dim3(256), 0, s, part, p.nsplit,
                      nw, part2);
   SEL_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_split_sum2, dim3(unsigned((nw + 255) / 256)), dim3(256), 0, s, part2, ng, nw, int(nw),
-                     gwpack);
+  if (up) {
+    const int64_t nt = up->kind == SEL_PACK_CONVT ? int64_t(up->cin) * up->cout * 2 * up->stride
+                       : int64_t(up->cout) * up->cin * (up->kind == SEL_PACK_FWD ? up->k : 2 * up->stride);
+    hipLaunchKernelGGL(k_split_sum2_unpack, dim3(unsigned((nt + 255) / 256)), dim3(256), 0, s, part2, ng, nw, nt,
+                       up->kind, up->cout, up->cin, up->k, up->stride, gwpack);
+  } else {
+    hipLaunchKernelGGL(k_split_sum2, dim3(unsigned((nw + 255) / 256)), dim3(256), 0, s, part2, ng, nw, int(nw),
+                       gwpack);
+  }
   SEL_LAUNCH_CHECK();
   if (gbias) {
     float* bpart2 = part2 + size_t(ng) * nw;
@@ -1629,6 +1887,10 @@ int sel_conv_wgrad(const sel_conv_desc* d, int dtype, const void* gout, const vo
   }
   return SEL_OK;
 }
+}  // namespace conv
+}  // namespace sel
+
+extern "C" {
 
 int sel_pack_weight(int kind, const float* w, int cout, int cin, int k, int stride, int dtype, void* wpack,
                     sel_stream_t stream) {

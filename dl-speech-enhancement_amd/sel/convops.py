@@ -263,6 +263,22 @@ def wgrad(desc, gout, x, want_bias):
     return gwp, gb
 
 
+def wgrad_torch(desc, gout, x, kind, w_shape, stride, want_bias):
+    """Weight (torch layout, fp32) and bias gradient of one layer; the unpack is
+    fused into the kernel's final reduction pass (sel_conv_wgrad_unpacked)."""
+    lib = L.lib()
+    ws = L.workspace(lib.sel_conv_wgrad_workspace(ctypes.byref(desc)), x.device)
+    gw = torch.empty(w_shape, dtype=torch.float32, device=x.device)
+    gb = torch.empty(desc.bias_period, dtype=torch.float32, device=x.device) if want_bias else None
+    if kind == PACK_CONVT:
+        cin, cout, k = w_shape
+    else:
+        cout, cin, k = w_shape
+    L.call("sel_conv_wgrad_unpacked", ctypes.byref(desc), _code(x.dtype), L.ptr(gout), L.ptr(x), kind, cout, cin,
+           k, stride, L.ptr(gw), L.ptr(gb), L.ptr(ws), ws.numel(), L.stream())
+    return gw, gb
+
+
 def unpack(kind, gwp, w_shape, stride):
     gw = torch.empty(w_shape, dtype=torch.float32, device=gwp.device)
     if kind == PACK_CONVT:
@@ -330,10 +346,9 @@ class ConvLayerFn(torch.autograd.Function):
                        L.ptr(gx), L.stream())
             gx = gx.view(x.shape)
         if ctx.needs_input_grad[1] or (has_bias and ctx.needs_input_grad[2]):
-            gwp, gbv = wgrad(desc, gy, x, has_bias and ctx.needs_input_grad[2])
-            if ctx.needs_input_grad[1]:
-                gw = unpack(kind, gwp, w_shape, stride)
-            gb = gbv
+            gw, gb = wgrad_torch(desc, gy, x, kind, w_shape, stride, has_bias and ctx.needs_input_grad[2])
+            if not ctx.needs_input_grad[1]:
+                gw = None
         return gx, gw, gb, None, None, None
 
 
@@ -376,13 +391,13 @@ class ResidualUnitFn(torch.autograd.Function):
         gh = prim(d2.adjoint(), gf, wd2, aux=h)
         gw1 = gb1 = gw2 = gb2 = None
         if ctx.needs_input_grad[3] or ctx.needs_input_grad[4]:
-            gwp2, gb2 = wgrad(d2, gf, h, d2.bias_period > 0 and ctx.needs_input_grad[4])
-            gw2 = unpack(PACK_FWD, gwp2, s2, 1) if ctx.needs_input_grad[3] else None
+            gw2, gb2 = wgrad_torch(d2, gf, h, PACK_FWD, s2, 1, d2.bias_period > 0 and ctx.needs_input_grad[4])
+            gw2 = gw2 if ctx.needs_input_grad[3] else None
         gx = None
         if ctx.needs_input_grad[0]:
             # dL/dx = g + (conv_adjoint(gh)) * ELU'(x)
             gx = prim(d1.adjoint(), gh, wd1, aux=xf, res=gf).view(B, T, C)
         if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
-            gwp1, gb1 = wgrad(d1, gh, xf, d1.bias_period > 0 and ctx.needs_input_grad[2])
-            gw1 = unpack(PACK_FWD, gwp1, s1, 1) if ctx.needs_input_grad[1] else None
+            gw1, gb1 = wgrad_torch(d1, gh, xf, PACK_FWD, s1, 1, d1.bias_period > 0 and ctx.needs_input_grad[2])
+            gw1 = gw1 if ctx.needs_input_grad[1] else None
         return gx, gw1, gb1, gw2, gb2, None

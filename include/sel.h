@@ -164,6 +164,12 @@ int sel_conv_fwd(const sel_conv_desc* d, int in_dtype, int out_dtype, const void
 size_t sel_conv_wgrad_workspace(const sel_conv_desc* d);
 int sel_conv_wgrad(const sel_conv_desc* d, int dtype, const void* gout, const void* in,
                    float* gwpack, float* gbias, void* ws, size_t ws_bytes, sel_stream_t stream);
+/* sel_conv_wgrad with the weight gradient written straight into the torch layout
+ * of the layer's fp32 weight (kind/cout/cin/k/stride as in sel_pack_weight): the
+ * unpack is fused into the final reduction pass. */
+int sel_conv_wgrad_unpacked(const sel_conv_desc* d, int dtype, const void* gout, const void* in, int kind,
+                            int cout, int cin, int k, int stride, float* gw, float* gbias, void* ws,
+                            size_t ws_bytes, sel_stream_t stream);
 /* Repack fp32 torch weights (kind SEL_PACK_*) into Wp (dtype), and the dgrad
  * form of a packed Wp[N][K][C] -> Wd[C][K][N] with taps reversed (the adjoint is
  * the same primitive with pad' = (K-1)*dil - pad). */
