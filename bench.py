@@ -129,7 +129,12 @@ def c3_setup(dev, B, world, local):
                  optimizer={"generator": opt}, scheduler={"generator": sched}, config=cfg, device=dev)
     clean, noise = synthetic_batch(B, SR, seed=93 + 2 * int(os.environ.get("RANK", "0")))
     clean, noise = clean.to(dev), noise.to(dev)
-    mixed = add_noise(clean, noise, 15)
+    if world > 1:
+        # batch-global add_noise norms over all ranks' shards (data_utils.py:15-16)
+        from sel.dist import add_noise_global
+        mixed = add_noise_global(clean, noise, 15)
+    else:
+        mixed = add_noise(clean, noise, 15)
 
     def step():
         with precision(torch.bfloat16):
