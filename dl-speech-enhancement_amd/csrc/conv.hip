@@ -291,7 +291,6 @@ __global__ __launch_bounds__(256) void k_conv_fwd_bf16(Args a, const __bf16* __r
   constexpr int TM = WTM / 32, TN = WTN / 32;
   constexpr int XV = ((BM + F4_HALOMAX) * 4 + 255) / 256;
   constexpr int WV = (KMAX * BN * 4 + 255) / 256;
-  constexpr int OP = BN + 4;
   extern __shared__ __align__(16) unsigned char smem[];
   __bf16* const xs = reinterpret_cast<__bf16*>(smem);
   const int halo = (a.K - 1) * a.dil;
@@ -311,8 +310,9 @@ __global__ __launch_bounds__(256) void k_conv_fwd_bf16(Args a, const __bf16* __r
   const int n0 = blockIdx.y * BN;
   const int nchunk = a.C / CK;
 
-  // staging row r <-> input time t0 - pad + r of sample b
-  int64_t xrow[XV];
+  // staging row r <-> input time t0 - pad + r of sample b; per-thread source
+  // pointers computed once (chunks only add the channel offset)
+  const __bf16* xsrc[XV];
   bool xok[XV];
 #pragma unroll
   for (int u = 0; u < XV; ++u) {
@@ -321,22 +321,24 @@ __global__ __launch_bounds__(256) void k_conv_fwd_bf16(Args a, const __bf16* __r
     const bool inside = ti >= 0 && ti < a.T;
     xok[u] = r < span && (inside || a.pad_mode == SEL_PAD_REPLICATE);
     ti = ti < 0 ? 0 : (ti >= a.T ? a.T - 1 : ti);
-    xrow[u] = b * a.T + ti;
+    xsrc[u] = in + (b * a.T + ti) * a.C + ((tid + u * 256) & 3) * 8;
+  }
+  const __bf16* wsrc[WV];
+  bool wok[WV];
+#pragma unroll
+  for (int u = 0; u < WV; ++u) {
+    const int v = tid + u * 256;
+    const int k = v / (BN * 4), n = (v >> 2) % BN;
+    const bool ok = k < a.K && n0 + n < a.N;
+    wok[u] = ok;
+    wsrc[u] = wp + (int64_t(ok ? n0 + n : 0) * a.K + (ok ? k : 0)) * a.C + (v & 3) * 8;
   }
   uint4 xr[XV], wr[WV];
   auto load = [&](int c0) {
 #pragma unroll
-    for (int u = 0; u < XV; ++u) {
-      const int c = c0 + ((tid + u * 256) & 3) * 8;
-      xr[u] = *reinterpret_cast<const uint4*>(in + xrow[u] * a.C + c);  // masked in store()
-    }
+    for (int u = 0; u < XV; ++u) xr[u] = *reinterpret_cast<const uint4*>(xsrc[u] + c0);  // masked in store()
 #pragma unroll
-    for (int u = 0; u < WV; ++u) {
-      const int v = tid + u * 256;
-      const int k = v / (BN * 4), n = (v >> 2) % BN, c = c0 + (v & 3) * 8;
-      const bool ok = k < a.K && n0 + n < a.N;
-      wr[u] = *reinterpret_cast<const uint4*>(wp + (int64_t(ok ? n0 + n : 0) * a.K + (ok ? k : 0)) * a.C + c);
-    }
+    for (int u = 0; u < WV; ++u) wr[u] = *reinterpret_cast<const uint4*>(wsrc[u] + c0);
   };
   auto store = [&]() {
 #pragma unroll
@@ -357,7 +359,7 @@ __global__ __launch_bounds__(256) void k_conv_fwd_bf16(Args a, const __bf16* __r
     for (int u = 0; u < WV; ++u) {
       const int v = tid + u * 256;
       const int k = v / (BN * 4), n = (v >> 2) % BN;
-      const uint4 val = n0 + n < a.N ? wr[u] : make_uint4(0, 0, 0, 0);
+      const uint4 val = wok[u] ? wr[u] : make_uint4(0, 0, 0, 0);
       if (k < a.K) *reinterpret_cast<uint4*>(ws + (k * BN + n) * P + (v & 3) * 8) = val;
     }
   };
@@ -395,71 +397,68 @@ __global__ __launch_bounds__(256) void k_conv_fwd_bf16(Args a, const __bf16* __r
           const bf16x8 af = *reinterpret_cast<const bf16x8*>(xs + lr[i] + kofs);
 #pragma unroll
           for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf[j], af, acc[i][j], 0, 0, 0);
         }
       }
     }
   }
 
-  // epilogue: C/D of 32x32x16: col = lane & 31, row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)
-  __syncthreads();
-  float* ot = reinterpret_cast<float*>(smem);
+  // epilogue straight from the accumulators (operands were swapped, so C/D is
+  // out^T): lane -> output row m = lane & 31 of its 32-row tile, element r ->
+  // n = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5): four runs of 4 consecutive
+  // channels, each stored as one 8-B (bf16) / 16-B (fp32) vector.
+  const bool bias_vec = bias && a.bias_period && (a.bias_period % 4) == 0;
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
+  for (int i = 0; i < TM; ++i) {
+    const int r = wm * WTM + i * 32 + (lane & 31);
+    if (r >= mrows) continue;
+    const int64_t m = m0 + r;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      const int col = wn * WTN + j * 32 + (lane & 31);
 #pragma unroll
-      for (int r = 0; r < 16; ++r)
-        ot[(wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * OP + col] = acc[i][j][r];
-    }
-  __syncthreads();
-  constexpr int V = Vec16<TO>::n;
-  const bool vec_ok = (a.N % V) == 0;
-  // bias index: one modulo per V-vector (period % V == 0 keeps a vector inside one period)
-  const bool bias_vec = bias && a.bias_period && (a.bias_period % V) == 0;
-  for (int idx = tid; idx < BM * (BN / V); idx += 256) {
-    const int r = idx / (BN / V), cv = (idx % (BN / V)) * V;
-    const int64_t m = m0 + r;
-    const int n = n0 + cv;
-    if (r >= mrows || n >= a.N) continue;
-    const int64_t o = m * a.N + n;
-    float v[V];
-    if (bias_vec) {
-      const float* bp = bias + (n % a.bias_period);
+      for (int g = 0; g < 4; ++g) {
+        const int n = n0 + wn * WTN + j * 32 + 8 * g + 4 * (lane >> 5);
+        if (n >= a.N) continue;
+        const int64_t o = m * a.N + n;
+        float v[4];
 #pragma unroll
-      for (int e = 0; e < V; ++e) v[e] = ot[r * OP + cv + e] + bp[e];
-    } else {
+        for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * g + e];
+        if (bias_vec) {
+          const float4 bv = *reinterpret_cast<const float4*>(bias + (n % a.bias_period));
+          v[0] += bv.x, v[1] += bv.y, v[2] += bv.z, v[3] += bv.w;
+        } else if (bias && a.bias_period) {
 #pragma unroll
-      for (int e = 0; e < V; ++e) {
-        const int ne = n + e;
-        const float bv = (bias && a.bias_period && ne < a.N) ? bias[ne % a.bias_period] : 0.f;
-        v[e] = ot[r * OP + cv + e] + bv;
-      }
-    }
-    if (vec_ok) {
-      if (aux) {
-        TO av[V];
-        *reinterpret_cast<uint4*>(av) = *reinterpret_cast<const uint4*>(aux + o);
+          for (int e = 0; e < 4; ++e)
+            if (n + e < a.N) v[e] += bias[(n + e) % a.bias_period];
+        }
+        if (a.N % 4 == 0) {
+          if (aux) {
+            TO av[4];
+            if constexpr (sizeof(TO) == 2) *reinterpret_cast<uint2*>(av) = *reinterpret_cast<const uint2*>(aux + o);
+            else *reinterpret_cast<uint4*>(av) = *reinterpret_cast<const uint4*>(aux + o);
 #pragma unroll
-        for (int e = 0; e < V; ++e) v[e] *= elu_grad_fast(to_f(av[e]));
-      }
-      if (res) {
-        TO rv[V];
-        *reinterpret_cast<uint4*>(rv) = *reinterpret_cast<const uint4*>(res + o);
+            for (int e = 0; e < 4; ++e) v[e] *= elu_grad_fast(to_f(av[e]));
+          }
+          if (res) {
+            TO rv[4];
+            if constexpr (sizeof(TO) == 2) *reinterpret_cast<uint2*>(rv) = *reinterpret_cast<const uint2*>(res + o);
+            else *reinterpret_cast<uint4*>(rv) = *reinterpret_cast<const uint4*>(res + o);
 #pragma unroll
-        for (int e = 0; e < V; ++e) v[e] += to_f(rv[e]);
-      }
-      TO ov[V];
+            for (int e = 0; e < 4; ++e) v[e] += to_f(rv[e]);
+          }
+          TO ov[4];
 #pragma unroll
-      for (int e = 0; e < V; ++e) ov[e] = from_f<TO>(v[e]);
-      *reinterpret_cast<uint4*>(out + o) = *reinterpret_cast<uint4*>(ov);
-    } else {
-      for (int e = 0; e < V && n + e < a.N; ++e) {
-        float x = v[e];
-        if (aux) x *= elu_grad_fast(to_f(aux[o + e]));
-        if (res) x += to_f(res[o + e]);
-        out[o + e] = from_f<TO>(x);
+          for (int e = 0; e < 4; ++e) ov[e] = from_f<TO>(v[e]);
+          if constexpr (sizeof(TO) == 2) *reinterpret_cast<uint2*>(out + o) = *reinterpret_cast<uint2*>(ov);
+          else *reinterpret_cast<uint4*>(out + o) = *reinterpret_cast<uint4*>(ov);
+        } else {
+          for (int e = 0; e < 4 && n + e < a.N; ++e) {
+            float x = v[e];
+            if (aux) x *= elu_grad_fast(to_f(aux[o + e]));
+            if (res) x += to_f(res[o + e]);
+            out[o + e] = from_f<TO>(x);
+          }
+        }
       }
     }
   }
@@ -1513,9 +1512,7 @@ template <int BM, int BN, int WAVES_M, int KMAX, typename TO>
 int launch_fwd4(const Args& a, const void* in, const void* wp, const float* bias, const void* aux,
                 const void* res, void* out, hipStream_t s) {
   const int span = BM + (a.K - 1) * a.dil;
-  const size_t stage = (size_t(span) + size_t(a.K) * BN) * F4_P * 2;
-  const size_t epi = size_t(BM) * (BN + 4) * 4;
-  const size_t lds = stage > epi ? stage : epi;
+  const size_t lds = (size_t(span) + size_t(a.K) * BN) * F4_P * 2;
   const int64_t tiles = (a.rows / a.T) * ((a.T + BM - 1) / BM);  // sample-aligned tiles
   dim3 grid(unsigned(tiles), unsigned((a.N + BN - 1) / BN));
   if (grid.x == 0) return SEL_OK;
