@@ -465,6 +465,196 @@ __global__ __launch_bounds__(256) void k_conv_fwd_bf16(Args a, const __bf16* __r
 }
 
 // ---------------------------------------------------------------------------
+// Weight-stationary streaming conv for the thin layers (32/64/96 input and
+// 32/64 output channels: the residual-unit convs at T = 24000 / 8000, their
+// dgrads, the first strided layer and the last transposed layer's dgrad).
+// These are HBM-bound, yet the tiled kernel above re-stages every tap of the
+// weight slice for each 128-row tile (for a 64x64 k7 layer, 3x the tile's
+// activation bytes through L2 and LDS), and its neighbouring tiles land on
+// different XCDs, so the causal halo is re-fetched from HBM (rocprofv3 PMC:
+// 1.85x the algorithmic read bytes at 32 channels, profiles/r1_c3_pmc_traffic.md).
+// Here each wave keeps the MFMA A-fragments of its 32-channel output slice
+// for ALL taps and input channels in VGPRs (K*C/16 fragments, loaded once
+// per block), and the block streams a CONTIGUOUS range of sample-aligned
+// R-row tiles (the halo re-read hits the block's own XCD L2):
+//   stage rows + causal halo (ELU applied, padding resolved) in LDS
+//   -> K*C/16*TM MFMAs per wave while the next tile's rows are in flight
+//   -> accumulators -> LDS (fp32) -> one fully coalesced 16-B epilogue pass
+//      (bias, ELU'(aux), residual) over the tile's contiguous output rows.
+// ---------------------------------------------------------------------------
+template <int C, int N, int K, int R>
+struct Thin {
+  static constexpr int PLANES = C / 32;
+  static constexpr int NS = N / 32, RG = 4 / NS;
+  static constexpr int WR = R / RG, TM = WR / 32;
+  static constexpr int SPAN = R + F4_HALOMAX;
+  static constexpr int CV = C / 8;  // 16-B vectors per staged row
+  static constexpr int XV = (SPAN * CV + 255) / 256;
+  static constexpr int OP = N + 4;  // fp32 out-tile pitch (conflict-free b128)
+  static constexpr size_t LDS_STAGE = size_t(PLANES) * SPAN * F4_P * 2;
+  static constexpr size_t LDS_OUT = size_t(R) * OP * 4;
+  static constexpr size_t LDS = LDS_STAGE > LDS_OUT ? LDS_STAGE : LDS_OUT;
+  static_assert(N == 32 || N == 64, "thin kernel: N in {32, 64}");
+  static_assert(C % 32 == 0 && WR % 32 == 0, "thin kernel tiling");
+  static_assert(LDS <= 64 * 1024, "thin kernel LDS");
+};
+
+template <int C, int N, int K, int R>
+__global__ __launch_bounds__(256) void k_conv_thin_bf16(Args a, const __bf16* __restrict__ in,
+                                                        const __bf16* __restrict__ wp,
+                                                        const float* __restrict__ bias,
+                                                        const __bf16* __restrict__ aux,
+                                                        const __bf16* __restrict__ res, __bf16* __restrict__ out,
+                                                        int tiles_per_block) {
+  using G = Thin<C, N, K, R>;
+  constexpr int P = F4_P;
+  constexpr int CV = G::CV;
+  extern __shared__ __align__(16) unsigned char smem[];
+  __bf16* const xs = reinterpret_cast<__bf16*>(smem);  // [PLANES][SPAN][P]
+  float* const ot = reinterpret_cast<float*>(smem);      // [R][OP], aliases xs
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ns = wave % G::NS, rg = wave / G::NS;
+  const int span = R + (K - 1) * a.dil;
+  const int tps = (a.T + R - 1) / R;
+  const int64_t ntiles = (a.rows / a.T) * tps;
+  // XCD-contiguous tile ranges: the grid is a multiple of 8 and block b runs on
+  // XCD b % 8, so virtual block (b % 8) * (grid / 8) + b / 8 gives each XCD one
+  // contiguous run of tiles, walked in dispatch order -> a tile's causal halo
+  // was just fetched into the same L2 by its predecessor
+  const int64_t vb = int64_t(blockIdx.x % 8) * (gridDim.x / 8) + blockIdx.x / 8;
+  const int64_t tile0 = vb * tiles_per_block;
+  const int64_t tile_end = tile0 + tiles_per_block < ntiles ? tile0 + tiles_per_block : ntiles;
+  if (tile0 >= tile_end) return;  // block-uniform
+
+  // A fragments of output slice ns: wf[k][g] = Wp[n][k][16g + 8*(lane>>5) .. +8]
+  bf16x8 wf[K][C / 16];
+  {
+    const __bf16* wrow = wp + int64_t(ns * 32 + (lane & 31)) * K * C + 8 * (lane >> 5);
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+#pragma unroll
+      for (int g = 0; g < C / 16; ++g) wf[k][g] = *reinterpret_cast<const bf16x8*>(wrow + k * C + 16 * g);
+  }
+
+  uint4 xr[G::XV];
+  bool xok[G::XV];
+  auto load = [&](int64_t tile) {
+    const int64_t b = tile / tps;
+    const int t0 = int(tile % tps) * R;
+#pragma unroll
+    for (int u = 0; u < G::XV; ++u) {
+      const int v = tid + u * 256;
+      const int r = v / CV, c = (v % CV) * 8;
+      int ti = t0 - a.pad + r;
+      const bool inside = ti >= 0 && ti < a.T;
+      xok[u] = r < span && (inside || a.pad_mode == SEL_PAD_REPLICATE);
+      ti = ti < 0 ? 0 : (ti >= a.T ? a.T - 1 : ti);
+      if ((u * 256) / CV < span)  // block-uniform: batches wholly past the halo are never fetched
+        xr[u] = *reinterpret_cast<const uint4*>(in + (b * a.T + ti) * C + c);  // masked in store()
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int u = 0; u < G::XV; ++u) {
+      const int v = tid + u * 256;
+      const int r = v / CV, c = (v % CV) * 8;
+      if (r >= span) continue;
+      uint4 val = xok[u] ? xr[u] : make_uint4(0, 0, 0, 0);
+      if (a.in_elu) {
+        __bf16* t = reinterpret_cast<__bf16*>(&val);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) t[e] = __bf16(elu_fast(float(t[e])));
+      }
+      *reinterpret_cast<uint4*>(xs + ((c >> 5) * G::SPAN + r) * P + (c & 31)) = val;
+    }
+  };
+
+  const bool bias_vec = bias && a.bias_period && (a.bias_period % 8) == 0;
+  load(tile0);
+  for (int64_t tile = tile0; tile < tile_end; ++tile) {
+    __syncthreads();  // the previous tile's epilogue is done with ot (= xs)
+    store();
+    __syncthreads();
+    if (tile + 1 < tile_end) load(tile + 1);
+
+    floatx16 acc[G::TM];
+#pragma unroll
+    for (int i = 0; i < G::TM; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
+    const __bf16* xw = xs + (rg * G::WR + (lane & 31)) * P + 8 * (lane >> 5);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+#pragma unroll
+      for (int g = 0; g < C / 16; ++g) {
+        const __bf16* xb = xw + ((g >> 1) * G::SPAN + k * a.dil) * P + 16 * (g & 1);
+#pragma unroll
+        for (int i = 0; i < G::TM; ++i) {
+          const bf16x8 xf = *reinterpret_cast<const bf16x8*>(xb + i * 32 * P);
+          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[k][g], xf, acc[i], 0, 0, 0);
+        }
+      }
+    }
+
+    // accumulators (out^T: lane -> row, element r -> channel) -> fp32 tile in LDS
+    __syncthreads();  // every wave is done reading xs
+#pragma unroll
+    for (int i = 0; i < G::TM; ++i) {
+      const int row = rg * G::WR + i * 32 + (lane & 31);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int n = ns * 32 + 8 * g + 4 * (lane >> 5);
+        *reinterpret_cast<floatx4*>(ot + row * G::OP + n) =
+            floatx4{acc[i][4 * g], acc[i][4 * g + 1], acc[i][4 * g + 2], acc[i][4 * g + 3]};
+      }
+    }
+    __syncthreads();
+
+    // coalesced epilogue: a sample-aligned tile's output rows are contiguous in HBM
+    const int64_t b = tile / tps;
+    const int t0 = int(tile % tps) * R;
+    const int mrows = a.T - t0 < R ? a.T - t0 : R;
+    const int64_t obase = (b * a.T + t0) * N;
+    constexpr int GN = N / 8;
+    for (int idx = tid; idx < mrows * GN; idx += 256) {
+      const int r = idx / GN, n = (idx % GN) * 8;
+      const floatx4 lo = *reinterpret_cast<const floatx4*>(ot + r * G::OP + n);
+      const floatx4 hi = *reinterpret_cast<const floatx4*>(ot + r * G::OP + n + 4);
+      float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      if (bias_vec) {
+        const float4 b0 = *reinterpret_cast<const float4*>(bias + (n % a.bias_period));
+        const float4 b1 = *reinterpret_cast<const float4*>(bias + (n % a.bias_period) + 4);
+        v[0] += b0.x, v[1] += b0.y, v[2] += b0.z, v[3] += b0.w;
+        v[4] += b1.x, v[5] += b1.y, v[6] += b1.z, v[7] += b1.w;
+      } else if (bias && a.bias_period) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += bias[(n + e) % a.bias_period];
+      }
+      const int64_t o = obase + int64_t(r) * N + n;
+      if (aux) {
+        uint4 raw = *reinterpret_cast<const uint4*>(aux + o);
+        const __bf16* av = reinterpret_cast<const __bf16*>(&raw);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] *= elu_grad_fast(float(av[e]));
+      }
+      if (res) {
+        uint4 raw = *reinterpret_cast<const uint4*>(res + o);
+        const __bf16* rv = reinterpret_cast<const __bf16*>(&raw);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += float(rv[e]);
+      }
+      uint4 ov;
+      __bf16* op = reinterpret_cast<__bf16*>(&ov);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) op[e] = __bf16(v[e]);
+      *reinterpret_cast<uint4*>(out + o) = ov;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Single-input-channel layers (the encoder's first conv 1->32 k7, and the dgrad
 // of the decoder's last conv 32->1 k7): an implicit GEMM with a reduction of
 // only K taps would leave MFMA idle and stage a 1-wide tile, so this is a
@@ -1558,9 +1748,76 @@ int fwd4_variant(int v, const Args& a, const void* in, const void* wp, const flo
   return launch_fwd4<256, 64, 4, KMAX, TO>(a, in, wp, bias, aux, res, out, s);
 }
 
+// Weight-stationary thin kernel (tune key 4: 0 = use where legal, 1 = off;
+// key 5: target workgroup count, 0 = 1024).  Returns kNotThin when the shape
+// has no instance.
+constexpr int kNotThin = 1;
+
+template <int C, int N, int K, int R>
+int launch_thin(const Args& a, const void* in, const void* wp, const float* bias, const void* aux,
+                const void* res, void* out, hipStream_t s) {
+  using G = Thin<C, N, K, R>;
+  const int64_t ntiles = (a.rows / a.T) * ((a.T + R - 1) / R);
+  if (ntiles == 0) return SEL_OK;
+  const int64_t target = tune(5) > 0 ? tune(5) : 1024;
+  const int64_t tpb = std::max<int64_t>(1, (ntiles + target - 1) / target);
+  const unsigned nb = unsigned(((ntiles + tpb - 1) / tpb + 7) / 8 * 8);  // multiple of 8 (XCD map)
+  hipLaunchKernelGGL((k_conv_thin_bf16<C, N, K, R>), dim3(nb), dim3(256), G::LDS, s, a,
+                     static_cast<const __bf16*>(in), static_cast<const __bf16*>(wp), bias,
+                     static_cast<const __bf16*>(aux), static_cast<const __bf16*>(res), static_cast<__bf16*>(out),
+                     int(tpb));
+  SEL_LAUNCH_CHECK();
+  return SEL_OK;
+}
+
+// the (i, C, N, K) instances with their default / alternative tile rows:
+// residual-unit k7 / 1x1 at 32 and 64 channels, the first strided conv
+// (96 -> 64, 3 taps) and the last transposed conv's dgrad (96 -> 64, 2 taps).
+// A/B knobs: tune key 7 bit i = instance i off (tiled kernel instead),
+// key 6 bit i = instance i on its alternative tile rows
+#define SEL_THIN_SHAPES(X) X(0, 32, 32, 7, 256, 128) X(1, 32, 32, 1, 256, 128) X(2, 64, 64, 7, 128, 64) \
+  X(3, 64, 64, 1, 128, 64) X(4, 96, 64, 3, 128, 64) X(5, 96, 64, 2, 128, 64)
+
+int thin_index(const Args& a) {
+  if (tune(4) == 1 || (a.K - 1) * a.dil > F4_HALOMAX) return -1;
+#define SEL_THIN_IDX(I_, C_, N_, K_, R_, R2_) \
+  if (a.C == C_ && a.N == N_ && a.K == K_) return (tune(7) >> I_) & 1 ? -1 : I_;
+  SEL_THIN_SHAPES(SEL_THIN_IDX)
+#undef SEL_THIN_IDX
+  return -1;
+}
+
+bool thin_ok(const Args& a) { return thin_index(a) >= 0; }
+
+int thin_rows(const Args& a) {
+  const int i = thin_index(a);
+#define SEL_THIN_R(I_, C_, N_, K_, R_, R2_) if (i == I_) return (tune(6) >> I_) & 1 ? R2_ : R_;
+  SEL_THIN_SHAPES(SEL_THIN_R)
+#undef SEL_THIN_R
+  return 0;
+}
+
+int dispatch_thin(const Args& a, const void* in, const void* wp, const float* bias, const void* aux,
+                  const void* res, void* out, hipStream_t s) {
+  const int i = thin_index(a);
+  if (i < 0) return kNotThin;
+  const bool alt = (tune(6) >> i) & 1;
+#define SEL_THIN_LAUNCH(I_, C_, N_, K_, R_, R2_)                                             \
+  if (i == I_)                                                                               \
+    return alt ? launch_thin<C_, N_, K_, R2_>(a, in, wp, bias, aux, res, out, s)            \
+               : launch_thin<C_, N_, K_, R_>(a, in, wp, bias, aux, res, out, s);
+  SEL_THIN_SHAPES(SEL_THIN_LAUNCH)
+#undef SEL_THIN_LAUNCH
+  return kNotThin;
+}
+
 template <typename TI, typename TO>
 int dispatch_fwd(const Args& a, const void* in, const void* wp, const float* bias, const void* aux,
                  const void* res, void* out, hipStream_t s) {
+  if constexpr (sizeof(TI) == 2 && sizeof(TO) == 2) {
+    const int rc = dispatch_thin(a, in, wp, bias, aux, res, out, s);
+    if (rc != kNotThin) return rc;
+  }
   if constexpr (sizeof(TI) == 2) {
     if (a.C == 1 && a.N % 8 == 0 && a.N <= C1_NMAX && a.K <= C1_KMAX && (a.K - 1) * a.dil <= C1_HALO &&
         tune(3) == 0) {
@@ -1709,8 +1966,9 @@ extern "C" {
 
 int sel_conv_fwd_kernel_id(const sel_conv_desc* d, int in_dtype, int out_dtype) {
   if (!d || in_dtype != SEL_BF16) return -1;
-  (void)out_dtype;
   const Args a = to_args(d);
+  if (out_dtype == SEL_BF16 && thin_ok(a))  // thin: 1e9 + ((R/32*1000 + C)*1000 + N)*10 + K
+    return 1000000000 + ((thin_rows(a) / 32 * 1000 + a.C) * 1000 + a.N) * 10 + a.K;
   const int v = fwd4_choice(a);
   if (v < 0) return -1;
   const int kmax = a.K == 1 ? 1 : (a.K <= 3 ? 3 : 8);

@@ -107,6 +107,10 @@ def lib():
                 rc = L.sel_init()
                 if rc != 0:
                     raise SelError(f"sel_init failed ({rc}): {L.sel_last_error().decode()}")
+                # kernel-selection knobs for A/B measurements: SEL_TUNE="4=1,6=1"
+                for kv in filter(None, os.environ.get("SEL_TUNE", "").split(",")):
+                    k, v = kv.split("=")
+                    L.sel_tune(int(k), int(v))
                 _initialized = True
     return L
 

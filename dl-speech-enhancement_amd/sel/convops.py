@@ -234,6 +234,10 @@ def fwd_kernel_name(desc, in_dtype, out_dtype):
     kid = L.lib().sel_conv_fwd_kernel_id(ctypes.byref(desc), _code(in_dtype), _code(out_dtype))
     if kid < 0:
         return f"k_conv_fwd<{in_dtype}>"
+    if kid >= 10 ** 9:  # weight-stationary thin kernel: 1e9 + ((R/32*1000 + C)*1000 + N)*10 + K
+        kid -= 10 ** 9
+        k, n, c, r = kid % 10, (kid // 10) % 1000, (kid // 10000) % 1000, 32 * (kid // 10000000)
+        return f"k_conv_thin_bf16<{c}, {n}, {k}, {r}>"
     kmax, kid = kid % 10, kid // 10
     wm, kid = kid % 10, kid // 10
     bm, bn = kid // 1000, kid % 1000

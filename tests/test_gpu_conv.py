@@ -237,3 +237,64 @@ def test_single_channel_kernel_matches_generic(gpu, C, N, K, dil, elu, aux, res)
             lib.sel_tune(3, prev)
     e = ((outs[0] - outs[1]).norm() / outs[1].norm()).item()
     assert e < 4e-3, e
+
+
+# (C, N, K, dil, pad_mode, in_elu, aux, res, bias, B, T): every thin-kernel instance in
+# its forward and adjoint forms, plus ragged T (tails shorter than one tile) and T < halo
+THIN_SHAPES = [(32, 32, 7, 9, 0, 1, 0, 0, 0, 3, 1000), (32, 32, 7, 9, 0, 0, 1, 1, 0, 2, 777),
+               (32, 32, 1, 1, 0, 1, 0, 1, 0, 3, 1000), (32, 32, 1, 1, 0, 0, 1, 0, 0, 2, 300),
+               (64, 64, 7, 3, 0, 1, 0, 0, 0, 3, 800), (64, 64, 7, 1, 0, 0, 1, 1, 0, 2, 130),
+               (64, 64, 1, 1, 0, 1, 0, 1, 0, 3, 800), (96, 64, 3, 1, 0, 0, 0, 0, 64, 4, 333),
+               (96, 64, 2, 1, 0, 0, 0, 0, 0, 2, 500), (32, 32, 7, 9, 0, 1, 0, 0, 0, 2, 40)]
+
+
+@pytest.mark.parametrize("shape", THIN_SHAPES, ids=lambda s: "C{}N{}K{}d{}e{}a{}r{}T{}".format(*s[:3], s[3], *s[5:8],
+                                                                                               s[10]))
+def test_thin_kernel_matches_tiled(gpu, shape):
+    """The weight-stationary thin kernel (tune key 4 = 0) against the tiled kernel
+    (key 4 = 1) on the same bf16 operands, causal (pad (K-1)*dil) and adjoint
+    (pad 0) forms: both accumulate in fp32 (different order) and round once to
+    bf16 -> within one bf16 ulp (4e-3 norm-wise), and against an fp64 reference
+    of the same bf16 operands within bf16 output rounding (4e-3)."""
+    from sel import _lib as L
+    from sel import convops as CO
+    C, N, K, dil, mode, elu, aux, res, bias, B, T = shape
+    torch.manual_seed(C + N + K + T)
+    lib = L.lib()
+    for pad in ((K - 1) * dil, 0):
+        d = CO.ConvDesc(B * T, T, C, N, K, dil, pad, mode, elu, bias)
+        x = torch.randn(B * T, C, device=gpu).to(torch.bfloat16)
+        wp = (0.2 * torch.randn(N, K, C, device=gpu)).to(torch.bfloat16)
+        b = torch.randn(bias, device=gpu) if bias else None
+        a_ = torch.randn(B * T, N, device=gpu).to(torch.bfloat16) if aux else None
+        r_ = torch.randn(B * T, N, device=gpu).to(torch.bfloat16) if res else None
+        assert CO.fwd_kernel_name(d, torch.bfloat16, torch.bfloat16).startswith("k_conv_thin_bf16")
+        outs = []
+        for v in (0, 1):
+            prev = lib.sel_tune(4, v)
+            try:
+                outs.append(CO.prim(d, x, wp, bias=b, aux=a_, res=r_).double())
+            finally:
+                lib.sel_tune(4, prev)
+        e = ((outs[0] - outs[1]).norm() / outs[1].norm()).item()
+        assert e < 4e-3, (pad, e)
+        # fp64 reference of the same bf16 operands
+        xa = x.double().view(B, T, C)
+        if elu:
+            xa = torch.where(xa > 0, xa, torch.expm1(xa)).to(torch.bfloat16).double()
+        ref = torch.zeros(B, T, N, dtype=torch.float64, device=gpu)
+        for k in range(K):
+            idx = torch.arange(T, device=gpu) + k * dil - pad
+            ok = (idx >= 0) & (idx < T)
+            xs = torch.zeros(B, T, C, dtype=torch.float64, device=gpu)
+            xs[:, ok] = xa[:, idx[ok]]
+            ref += torch.einsum("btc,nc->btn", xs, wp[:, k, :].double())
+        ref = ref.view(B * T, N)
+        if bias:
+            ref += b.double().repeat(N // bias)
+        if aux:
+            ref *= torch.where(a_.double() > 0, 1.0, torch.exp(a_.double()))
+        if res:
+            ref += r_.double()
+        e = ((outs[0] - ref).norm() / ref.norm()).item()
+        assert e < 4e-3, (pad, e)

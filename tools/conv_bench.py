@@ -26,6 +26,9 @@ SHAPES = [
     ("down0 96->64 k3", 512000, 8000, 96, 64, 3, 1, 2, Z, 0, 0, 0, 1),
     ("RU64 k7d3 fwd", 512000, 8000, 64, 64, 7, 3, 18, Z, 1, 0, 0, 0),
     ("RU64 1x1 fwd", 512000, 8000, 64, 64, 1, 1, 0, Z, 1, 0, 1, 0),
+    ("RU64 k7d3 dgrad", 512000, 8000, 64, 64, 7, 3, 0, Z, 0, 1, 1, 0),
+    ("RU64 1x1 dgrad", 512000, 8000, 64, 64, 1, 1, 0, Z, 0, 1, 0, 0),
+    ("up3 dgrad 96->64 k2", 512000, 8000, 96, 64, 2, 1, 0, Z, 0, 0, 0, 0),
     ("up3 64->96 k2 rep", 512000, 8000, 64, 96, 2, 1, 1, R, 0, 0, 0, 1),
     ("RU128 k7d9 fwd", 128000, 2000, 128, 128, 7, 9, 54, Z, 1, 0, 0, 0),
     ("down1 256->128 k3", 128000, 2000, 256, 128, 3, 1, 2, Z, 0, 0, 0, 1),
@@ -47,7 +50,15 @@ def run(shape, variant, iters=20):
     b = torch.randn(N, device=dev) if bias else None
     a_ = torch.randn(rows, N, device=dev).to(torch.bfloat16) if aux else None
     r_ = torch.randn(rows, N, device=dev).to(torch.bfloat16) if res else None
-    L.lib().sel_tune(0, variant)
+    # variants 30-33 = the weight-stationary thin kernel (tune key 4 = 0):
+    # 30 default, 31 one tile per workgroup (key 5), 32 alternative tile rows
+    # (key 6), 33 both; any other variant runs with the thin kernel off so the
+    # tiled variants stay comparable
+    thin = 30 <= variant <= 33
+    L.lib().sel_tune(4, 0 if thin else 1)
+    L.lib().sel_tune(5, 1 << 30 if variant in (31, 33) else 0)
+    L.lib().sel_tune(6, 63 if variant in (32, 33) else 0)
+    L.lib().sel_tune(0, 0 if thin else variant)
     try:
         for _ in range(3):
             y = CO.prim(d, x, wp, bias=b, aux=a_, res=r_)
@@ -66,7 +77,7 @@ def run(shape, variant, iters=20):
 
 
 def main():
-    variants = [int(v) for v in sys.argv[1:]] or [0, 1, 5, 6, 21, 22, 23, 24, 25, 26]
+    variants = [int(v) for v in sys.argv[1:]] or [30, 0, 21, 22, 23, 24]
     L.lib()
     print("| shape | " + " | ".join(f"v{v}" for v in variants) + " | best | GB/s | TF/s |")
     print("|---" * (len(variants) + 4) + "|")
@@ -83,7 +94,8 @@ def main():
         cells = " | ".join("-" if t is None else f"{t:.1f}" for t in times)
         print(f"| {name} | {cells} | v{best_v} | {nbytes / best_t / 1e3:.0f} | {flops / best_t / 1e6:.0f} |",
               flush=True)
-    L.lib().sel_tune(0, 0)
+    for key in (0, 4, 5, 6, 7):
+        L.lib().sel_tune(key, 0)
 
 
 if __name__ == "__main__" and os.environ.get("WGRAD", "0") != "1":
