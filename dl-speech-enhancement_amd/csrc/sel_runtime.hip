@@ -41,6 +41,17 @@ static int do_init() {
       twN[k] = make_float2(float(std::cos(a)), float(std::sin(a)));
     }
   }
+  for (int L = spec::kMinLog; L <= spec::kFftMaxLog; ++L) {
+    for (int p = 1; p < spec::fft_npass(L); ++p) {
+      const int R = spec::fft_radix(L, p), Ns = spec::fft_ns(L, p);
+      float2* t = tw.data() + spec::twp_off(L, p);
+      for (int k = 0; k < Ns; ++k)
+        for (int r = 1; r < R; ++r) {
+          const double a = -2.0 * M_PI * double(r) * double(k) / double(R * Ns);
+          t[k * (R - 1) + r - 1] = make_float2(float(std::cos(a)), float(std::sin(a)));
+        }
+    }
+  }
   SEL_HIP(spec::upload_twiddles(tw.data(), tw.size()));
   return SEL_OK;
 }

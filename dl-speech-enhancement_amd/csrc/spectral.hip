@@ -39,14 +39,26 @@ __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
 __device__ __forceinline__ float2 cmni(float2 a) { return make_float2(a.y, -a.x); }
 __device__ __forceinline__ float2 conjf2(float2 a) { return make_float2(a.x, -a.y); }
 
+// Wave-FFT geometry: a frame is owned by LPF = M/8 lanes (8 points per lane):
+// a quarter / half / whole wave for n_fft 256 / 512 / 1024, so those
+// transforms run without a block barrier, and two waves (s_barrier between
+// passes) for 2048.  A 256-lane block holds FPB = 256/LPF frames per
+// iteration and walks `iters` consecutive frame groups (window and twiddles
+// stay in registers across them).
 template <int LOGN>
 struct Geo {
   static constexpr int N = 1 << LOGN;
   static constexpr int M = N / 2;
-  static constexpr int TPF = N / 8;                       // lanes per frame
-  static constexpr int FPB = TPF >= 256 ? 1 : 256 / TPF;  // frames per block
-  static constexpr int BLOCK = TPF * FPB;
-  static constexpr int BUF = M + 8;                       // complex slots per LDS buffer
+  static constexpr int PPL = fft_ppl(LOGN);  // complex points per lane
+  static constexpr int LPF = M / PPL;         // lanes per frame
+  static constexpr int FPB = 256 / LPF;       // frames per block iteration
+  static constexpr int BLOCK = 256;
+  static constexpr int NP = fft_npass(LOGN);
+  static constexpr int R0 = fft_radix(LOGN, 0), R1 = fft_radix(LOGN, 1), R2 = fft_radix(LOGN, 2),
+                       R3 = fft_radix(LOGN, 3);
+  static constexpr int NS1 = R0, NS2 = R0 * R1, NS3 = R0 * R1 * R2;
+  static constexpr int PADN = M + M / 8;  // padded complex slots per frame (pidx)
+  static_assert(R0 * R1 * R2 * R3 == M && PPL == 8 && LPF <= 256, "wave FFT schedule");
 };
 
 struct FrameArgs {
@@ -60,248 +72,557 @@ __device__ __forceinline__ int64_t reflect_index(int64_t j, int64_t T) {
   return j;
 }
 
-// Windowed, reflect-padded frame -> packed complex buffer (even + i*odd).
+// one pad slot per 8 complex values: the radix-8/16 Stockham stores (a lane's 8
+// or 16 outputs contiguous, lanes 64-128 B apart) spread over all 64 banks
+__device__ __forceinline__ int pidx(int i) { return i + (i >> 3); }
+
+// orders this lane's LDS accesses around cross-lane exchanges inside the wave
+// (DS instructions of one wave execute in order; this stops the compiler from
+// moving them across the exchange point)
+__device__ __forceinline__ void wave_lds_fence() {
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// exchange point of one frame's lanes: in-wave fence, or a block barrier when
+// the frame spans two waves (n_fft 2048)
 template <int LOGN>
-__device__ __forceinline__ void load_frame(const float* __restrict__ x, const FrameArgs& a, int f,
-                                           const float* __restrict__ window, float2* buf, int t,
-                                           bool active) {
-  using G = Geo<LOGN>;
-  const int64_t base = int64_t(f) * a.hop - a.P;
+__device__ __forceinline__ void frame_fence() {
+  if constexpr (Geo<LOGN>::LPF > 64) __syncthreads();
+  else wave_lds_fence();
+}
+
+// ---- in-register DFTs (forward, exp(-2 pi i nk/R)), natural-order output ----
+__device__ __forceinline__ void dft2(float2& a0, float2& a1) {
+  const float2 t = a0;
+  a0 = cadd(t, a1);
+  a1 = csub(t, a1);
+}
+__device__ __forceinline__ void dft4(float2& a0, float2& a1, float2& a2, float2& a3) {
+  const float2 t0 = cadd(a0, a2), t1 = csub(a0, a2), t2 = cadd(a1, a3), t3 = cmni(csub(a1, a3));
+  a0 = cadd(t0, t2);
+  a1 = cadd(t1, t3);
+  a2 = csub(t0, t2);
+  a3 = csub(t1, t3);
+}
+constexpr float kS2 = 0.70710678118654752440f;  // sqrt(1/2)
+constexpr float kC8 = 0.92387953251128675613f;  // cos(pi/8)
+constexpr float kS8 = 0.38268343236508977173f;  // sin(pi/8)
+// x * exp(-i pi/4), x * exp(-3i pi/4)
+__device__ __forceinline__ float2 w8_1(float2 x) { return make_float2(kS2 * (x.x + x.y), kS2 * (x.y - x.x)); }
+__device__ __forceinline__ float2 w8_3(float2 x) { return make_float2(kS2 * (x.y - x.x), -kS2 * (x.x + x.y)); }
+__device__ __forceinline__ float2 cmulc(float2 x, float c, float s) {  // x * (c + i s)
+  return make_float2(fmaf(x.x, c, -x.y * s), fmaf(x.x, s, x.y * c));
+}
+
+__device__ __forceinline__ void dft8(float2 (&a)[8]) {
+  float2 b[4], c[4];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int m = t + q * G::TPF;
-    const int n0 = 2 * m, n1 = n0 + 1;
-    float v0 = 0.f, v1 = 0.f;
-    if (active) {
-      const int w0 = n0 - a.left, w1 = n1 - a.left;
-      if (w0 >= 0 && w0 < a.win) v0 = window[w0] * x[reflect_index(base + n0, a.T)];
-      if (w1 >= 0 && w1 < a.win) v1 = window[w1] * x[reflect_index(base + n1, a.T)];
-    }
-    buf[m] = make_float2(v0, v1);
+  for (int n = 0; n < 4; ++n) {
+    b[n] = cadd(a[n], a[n + 4]);
+    c[n] = csub(a[n], a[n + 4]);
+  }
+  c[1] = w8_1(c[1]);
+  c[2] = cmni(c[2]);
+  c[3] = w8_3(c[3]);
+  dft4(b[0], b[1], b[2], b[3]);
+  dft4(c[0], c[1], c[2], c[3]);
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    a[2 * m] = b[m];
+    a[2 * m + 1] = c[m];
   }
 }
 
-// In-LDS forward complex FFT of M = N/2 points (Stockham autosort, natural order).
-// All block lanes must call it (contains __syncthreads). Returns the result buffer.
-template <int LOGN>
-__device__ __forceinline__ float2* fft_half(float2* src, float2* dst, int t) {
-  using G = Geo<LOGN>;
-  constexpr int M = G::M;
-  const float2* __restrict__ twM = g_tw + tw_off(LOGN);
-  int Ns = 1;
+__device__ __forceinline__ void dft16(float2 (&a)[16]) {
+  float2 b[8], c[8];
 #pragma unroll
-  for (int pass = 0; pass < (LOGN - 1) / 2; ++pass) {
-    const int j = t;
-    const int k = j & (Ns - 1);
-    float2 v0 = src[j], v1 = src[j + M / 4], v2 = src[j + M / 2], v3 = src[j + 3 * M / 4];
-    if (pass > 0) {
-      const int step = M / (4 * Ns);
-      v1 = cmul(v1, twM[k * step]);
-      v2 = cmul(v2, twM[2 * k * step]);
-      v3 = cmul(v3, twM[3 * k * step]);
-    }
-    const float2 t0 = cadd(v0, v2), t1 = csub(v0, v2), t2 = cadd(v1, v3), t3 = cmni(csub(v1, v3));
-    const int d = (j - k) * 4 + k;
-    dst[d] = cadd(t0, t2);
-    dst[d + Ns] = cadd(t1, t3);
-    dst[d + 2 * Ns] = csub(t0, t2);
-    dst[d + 3 * Ns] = csub(t1, t3);
-    __syncthreads();
-    float2* tmp = src;
-    src = dst;
-    dst = tmp;
-    Ns *= 4;
+  for (int n = 0; n < 8; ++n) {
+    b[n] = cadd(a[n], a[n + 8]);
+    c[n] = csub(a[n], a[n + 8]);
   }
-  if ((LOGN - 1) & 1) {  // final radix-2 pass, Ns = M/2
+  // c[n] *= exp(-2 pi i n / 16)
+  c[1] = cmulc(c[1], kC8, -kS8);
+  c[2] = w8_1(c[2]);
+  c[3] = cmulc(c[3], kS8, -kC8);
+  c[4] = cmni(c[4]);
+  c[5] = cmulc(c[5], -kS8, -kC8);
+  c[6] = w8_3(c[6]);
+  c[7] = cmulc(c[7], -kC8, -kS8);
+  dft8(b);
+  dft8(c);
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int j = t + h * G::TPF;  // j < M/2 == Ns -> k == j
-      const float2 v0 = src[j];
-      const float2 v1 = cmul(src[j + M / 2], twM[j]);
-      dst[j] = cadd(v0, v1);
-      dst[j + M / 2] = csub(v0, v1);
-    }
-    __syncthreads();
-    src = dst;
-  }
-  return src;
-}
-
-// Real split: X_k for this lane's bins k = t + q*TPF (q < 4) and X_M (lane 0).
-template <int LOGN>
-__device__ __forceinline__ void real_split(const float2* Z, int t, float2 (&X)[4], float2& XM) {
-  using G = Geo<LOGN>;
-  constexpr int M = G::M;
-  const float2* __restrict__ twN = g_tw + tw_off(LOGN) + M;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int k = t + q * G::TPF;
-    if (k == 0) {
-      const float2 z0 = Z[0];
-      X[q] = make_float2(z0.x + z0.y, 0.f);
-      XM = make_float2(z0.x - z0.y, 0.f);
-    } else {
-      const float2 zk = Z[k], zm = Z[M - k];
-      const float2 e = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y));
-      const float2 o = make_float2(0.5f * (zk.y + zm.y), -0.5f * (zk.x - zm.x));
-      X[q] = cadd(e, cmul(twN[k], o));
-    }
+  for (int m = 0; m < 8; ++m) {
+    a[2 * m] = b[m];
+    a[2 * m + 1] = c[m];
   }
 }
 
-// Inverse of real_split for a gradient: given G_k (k = 0..M) in `Gb`, build the
-// half-size spectrum Z'_k, run the forward FFT on conj(Z') and return the
-// buffer holding conj(z'); r[2m] = R[m].x, r[2m+1] = -R[m].y with
-// r_n = Re sum_{k=0}^{M} G_k exp(+2 pi i k n / N).
+template <int R>
+__device__ __forceinline__ void dft(float2 (&a)[R]) {
+  if constexpr (R == 2) dft2(a[0], a[1]);
+  else if constexpr (R == 4) dft4(a[0], a[1], a[2], a[3]);
+  else if constexpr (R == 8) dft8(a);
+  else dft16(a);
+}
+
+// Per-lane twiddles, loaded once per kernel: pass p's base twiddles
+// W_{R*NS}^{r*(l mod NS)} (r = 1..R-1) and the split twiddle W_N^l.  A lane's
+// other butterflies / bins differ by a lane-uniform factor read from the same
+// tables (scalar loads): W^{r*(l + LPF*u mod NS)} = W^{r*l} * W^{r*(LPF*u mod NS)},
+// W_N^{l + LPF*q} = W_N^l * W_N^{LPF*q}.
 template <int LOGN>
-__device__ __forceinline__ float2* c2r_grad(float2* Gb, float2* other, int t) {
+struct LaneTw {
+  using G = Geo<LOGN>;
+  // register-resident for PPL = 8; for PPL = 16 the pass twiddles are re-read
+  // from the (L1-resident) table each frame, through a pointer made opaque per
+  // use so the compiler cannot hoist them into registers it does not have
+  static constexpr bool RES = G::PPL == 8;
+  float2 p1[RES ? G::R1 - 1 : 1], p2[RES ? G::R2 - 1 : 1], p3[G::R3 > 1 ? G::R3 - 1 : 1], n;
+  const float2* g1;
+  const float2* g2;
+  __device__ __forceinline__ void load(int l) {
+    g1 = g_tw + twp_off(LOGN, 1) + (l & (G::NS1 - 1)) * (G::R1 - 1);
+    g2 = g_tw + twp_off(LOGN, 2) + (l & (G::NS2 - 1)) * (G::R2 - 1);
+    if constexpr (RES) {
+#pragma unroll
+      for (int r = 1; r < G::R1; ++r) p1[r - 1] = g1[r - 1];
+#pragma unroll
+      for (int r = 1; r < G::R2; ++r) p2[r - 1] = g2[r - 1];
+    }
+    if constexpr (G::R3 > 1) {
+#pragma unroll
+      for (int r = 1; r < G::R3; ++r) p3[r - 1] = g_tw[twp_off(LOGN, 3) + (l & (G::NS3 - 1)) * (G::R3 - 1) + r - 1];
+    }
+    n = g_tw[tw_off(LOGN) + G::M + l];
+  }
+  __device__ __forceinline__ const float2* t1() const {
+    if constexpr (RES) return p1;
+    const float2* p = g1;
+    asm volatile("" : "+v"(p));
+    return p;
+  }
+  __device__ __forceinline__ const float2* t2() const {
+    if constexpr (RES) return p2;
+    const float2* p = g2;
+    asm volatile("" : "+v"(p));
+    return p;
+  }
+};
+
+// W_N^k for this lane's bin k = l + LPF*q
+template <int LOGN>
+__device__ __forceinline__ float2 split_tw(const LaneTw<LOGN>& tw, int q) {
+  using G = Geo<LOGN>;
+  return q == 0 ? tw.n : cmul(tw.n, g_tw[tw_off(LOGN) + G::M + G::LPF * q]);
+}
+
+// One Stockham pass (radix R, stride NS) from registers to the frame's LDS
+// buffer.  Lane l's points are q = u + r*NB <-> butterfly j = l + LPF*u,
+// input j + r*M/R; output (j - j%NS)*R + j%NS + r*NS.
+template <int LOGN, int R, int NS, int PASS>
+__device__ __forceinline__ void fft_pass_store(float2 (&v)[Geo<LOGN>::PPL], float2* z, int l, const float2* twb) {
+  using G = Geo<LOGN>;
+  constexpr int NB = G::PPL / R;
+#pragma unroll
+  for (int u = 0; u < NB; ++u) {
+    const int j = l + G::LPF * u;
+    const int k = j & (NS - 1);
+    float2 a[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) a[r] = v[u + r * NB];
+    if constexpr (NS > 1) {
+      const int kf = (G::LPF * u) & (NS - 1);  // lane-uniform part of k
+#pragma unroll
+      for (int r = 1; r < R; ++r) {
+        float2 t = twb[r - 1];
+        if (NS > G::LPF && u > 0) t = cmul(t, g_tw[twp_off(LOGN, PASS) + kf * (R - 1) + r - 1]);
+        a[r] = cmul(a[r], t);
+      }
+    }
+    dft<R>(a);
+    // padded destination: pidx(base + r*NS) = pidx(base) + r*NS*9/8 when 8 | NS;
+    // for NS == 1 (R >= 8) base = j*R is a multiple of 8
+    const int base = (j - k) * R + k;
+    const int pb = pidx(base);
+#pragma unroll
+    for (int r = 0; r < R; ++r) z[NS >= 8 ? pb + r * NS * 9 / 8 : pb + r + (r >> 3)] = a[r];
+  }
+}
+
+template <int LOGN, int R>
+__device__ __forceinline__ void fft_pass_load(float2 (&v)[Geo<LOGN>::PPL], const float2* z, int l) {
+  using G = Geo<LOGN>;
+  constexpr int NB = G::PPL / R;
+  const int pl = pidx(l);  // LPF*u + r*M/R is a multiple of 8 -> linear offsets
+#pragma unroll
+  for (int u = 0; u < NB; ++u)
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[u + r * NB] = z[pl + (G::LPF * u + r * (G::M / R)) * 9 / 8];
+}
+
+// Half-size complex FFT of the frame whose points m = l + LPF*q sit in v[q]
+// (q < PPL); leaves Z in natural order in z[pidx(.)].  Wave-local: no barrier.
+template <int LOGN>
+__device__ __forceinline__ void fft_half(float2 (&v)[Geo<LOGN>::PPL], float2* z, int l, const LaneTw<LOGN>& tw) {
+  using G = Geo<LOGN>;
+  fft_pass_store<LOGN, G::R0, 1, 0>(v, z, l, nullptr);
+  frame_fence<LOGN>();
+  fft_pass_load<LOGN, G::R1>(v, z, l);
+  frame_fence<LOGN>();
+  fft_pass_store<LOGN, G::R1, G::NS1, 1>(v, z, l, tw.t1());
+  frame_fence<LOGN>();
+  fft_pass_load<LOGN, G::R2>(v, z, l);
+  frame_fence<LOGN>();
+  fft_pass_store<LOGN, G::R2, G::NS2, 2>(v, z, l, tw.t2());
+  frame_fence<LOGN>();
+  if constexpr (G::NP == 4) {
+    fft_pass_load<LOGN, G::R3>(v, z, l);
+    frame_fence<LOGN>();
+    fft_pass_store<LOGN, G::R3, G::NS3, 3>(v, z, l, tw.p3);
+    frame_fence<LOGN>();
+  }
+}
+
+// This lane's window pairs (w(2m - left), w(2m + 1 - left)), m = l + LPF*q:
+// register-resident for PPL = 8, re-read per frame (L1 hits) for PPL = 16,
+// whose FFT working set leaves no room for them.
+template <int LOGN, bool RESIDENT = (Geo<LOGN>::PPL == 8)>
+struct Win {
+  using G = Geo<LOGN>;
+  float2 w[RESIDENT ? G::PPL : 1];
+  const float* __restrict__ win;
+  int left, n, l;
+  __device__ __forceinline__ float2 fetch(int q) const {
+    const int w0 = 2 * (l + G::LPF * q) - left, w1 = w0 + 1;
+    return make_float2(w0 >= 0 && w0 < n ? win[w0] : 0.f, w1 >= 0 && w1 < n ? win[w1] : 0.f);
+  }
+  __device__ __forceinline__ void init(const float* window, const FrameArgs& a, int l_) {
+    win = window;
+    left = a.left;
+    n = a.win;
+    l = l_;
+    if constexpr (RESIDENT) {
+#pragma unroll
+      for (int q = 0; q < G::PPL; ++q) w[q] = fetch(q);
+    }
+  }
+  __device__ __forceinline__ float2 get(int q) const {
+    if constexpr (RESIDENT) return w[q];
+    else return fetch(q);
+  }
+};
+
+// Raw sample pairs (x[2m], x[2m+1]) of frame f of signal b, reflect-padded,
+// m = l + LPF*q.  Interior frames: one coalesced 8-B load per point off one
+// base address; edge frames: per-sample reflected loads through a buffer
+// resource over the whole (B, T) batch (32-bit offsets, one VGPR per address;
+// the host keeps B*T*4 < 2^31).  Issued one frame ahead
+// of the transform that consumes them.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t signal_rsrc(const float* x, const FrameArgs& a) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x), 0, int(a.B * a.T * 4), 0x00020000);
+}
+
+template <int LOGN>
+__device__ __forceinline__ void fetch_frame(const float* __restrict__ x, __amdgpu_buffer_rsrc_t xr, const FrameArgs& a,
+                                            int64_t b, int f, int l, bool active, float2 (&raw)[Geo<LOGN>::PPL]) {
+  using G = Geo<LOGN>;
+  const int T = int(a.T);
+  const int base = f * a.hop - a.P;
+  const int sig = int(b) * T;
+  const float* xs = x + sig + base;
+  if (active && base >= 0 && base + G::N <= T && (reinterpret_cast<uintptr_t>(xs) & 7) == 0) {
+    // (raw_buffer_load_b64 returned wrong pairs here on gfx950: plain 8-B global loads)
+    const float2* x2 = reinterpret_cast<const float2*>(xs) + l;
+#pragma unroll
+    for (int q = 0; q < G::PPL; ++q) raw[q] = x2[G::LPF * q];
+  } else if (active) {
+#pragma unroll
+    for (int q = 0; q < G::PPL; ++q) {
+      // reflect(j) = min(|j|, 2(T-1) - |j|) for -(T-1) <= j <= 2(T-1)
+      int n0 = abs(base + 2 * (l + G::LPF * q)), n1 = abs(base + 2 * (l + G::LPF * q) + 1);
+      n0 = min(n0, 2 * (T - 1) - n0);
+      n1 = min(n1, 2 * (T - 1) - n1);
+      raw[q] = make_float2(__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, (sig + n0) * 4, 0, 0)),
+                           __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, (sig + n1) * 4, 0, 0)));
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < G::PPL; ++q) raw[q] = make_float2(0.f, 0.f);
+  }
+}
+
+template <int LOGN>
+__device__ __forceinline__ void window_frame(const float2 (&raw)[Geo<LOGN>::PPL], const Win<LOGN>& wn,
+                                             float2 (&v)[Geo<LOGN>::PPL]) {
+#pragma unroll
+  for (int q = 0; q < Geo<LOGN>::PPL; ++q) {
+    const float2 w = wn.get(q);
+    v[q] = make_float2(raw[q].x * w.x, raw[q].y * w.y);
+  }
+}
+
+// Real split: X_k for this lane's bins k = l + LPF*q (q < PPL) and X_M (valid on l == 0).
+template <int LOGN>
+__device__ __forceinline__ void real_split(const float2* z, int l, const LaneTw<LOGN>& tw, float2 (&X)[Geo<LOGN>::PPL],
+                                           float2& XM) {
   using G = Geo<LOGN>;
   constexpr int M = G::M;
-  const float2* __restrict__ twN = g_tw + tw_off(LOGN) + M;
+  // linear LDS addressing off two per-lane bases: pidx(l + c) = pidx(l) + 9c/8 and
+  // pidx(M - l - c) = pidx(-l) + 9(M - c)/8 for c a multiple of 8 (bin 0 pairs with itself)
+  const int pl = pidx(l), pn = -l + ((-l) >> 3);
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int k = t + q * G::TPF;
+  for (int q = 0; q < G::PPL; ++q) {
+    const int im = q == 0 ? (l == 0 ? 0 : pn + G::PADN) : pn + (M - G::LPF * q) * 9 / 8;
+    const float2 zk = z[pl + G::LPF * q * 9 / 8], zm = z[im];
+    const float2 e = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y));
+    const float2 o = make_float2(0.5f * (zk.y + zm.y), -0.5f * (zk.x - zm.x));
+    X[q] = cadd(e, cmul(split_tw<LOGN>(tw, q), o));  // k = 0: e + o = (z0.x + z0.y, 0)
+    if (q == 0) XM = make_float2(zk.x - zk.y, 0.f);  // meaningful for k = 0 only
+  }
+  frame_fence<LOGN>();
+}
+
+// Gradient through real_split + FFT: given G_k for this lane's bins (Gq[q],
+// k = l + LPF*q) and G_M (GM, on l == 0), r_n = Re sum_{k=0}^{M} G_k exp(+2 pi i k n / N)
+// for this lane's points: out[q] = (r[2m], r[2m+1]), m = l + LPF*q.
+template <int LOGN>
+__device__ __forceinline__ void c2r_grad(float2 (&Gq)[Geo<LOGN>::PPL], float2 GM, float2* z, int l,
+                                         const LaneTw<LOGN>& tw, float2 (&out)[Geo<LOGN>::PPL]) {
+  using G = Geo<LOGN>;
+  constexpr int M = G::M;
+  const int pl = pidx(l);
+#pragma unroll
+  for (int q = 0; q < G::PPL; ++q) z[pl + G::LPF * q * 9 / 8] = Gq[q];
+  if (l == 0) z[G::PADN - 1] = GM;  // a pad slot (pidx never maps there)
+  frame_fence<LOGN>();
+  const int pn = -l + ((-l) >> 3);
+#pragma unroll
+  for (int q = 0; q < G::PPL; ++q) {
+    const int k = l + G::LPF * q;
+    // G_{M-k}; bin 0 pairs with G_M in slot PADN - 1
+    const int im = q == 0 ? (l == 0 ? G::PADN - 1 : pn + G::PADN) : pn + (M - G::LPF * q) * 9 / 8;
+    const float2 gk = Gq[q], gm = z[im];
     float2 zp;
     if (k == 0) {
-      const float h0 = Gb[0].x, hm = Gb[M].x;
-      zp = make_float2(h0 + hm, h0 - hm);
+      zp = make_float2(gk.x + gm.x, gk.x - gm.x);
     } else {
-      const float2 gk = Gb[k], gm = Gb[M - k];
       const float2 s = make_float2(gk.x + gm.x, gk.y - gm.y);  // gk + conj(gm)
       const float2 d = make_float2(gk.x - gm.x, gk.y + gm.y);  // gk - conj(gm)
-      const float2 wd = cmul(conjf2(twN[k]), d);                // W^-k * d
-      // 0.5 * (s + i * wd)
+      const float2 wd = cmul(conjf2(split_tw<LOGN>(tw, q)), d);  // W^-k * d
       zp = make_float2(0.5f * (s.x - wd.y), 0.5f * (s.y + wd.x));
     }
-    other[k] = conjf2(zp);
+    out[q] = conjf2(zp);
   }
-  __syncthreads();
-  return fft_half<LOGN>(other, Gb, t);
+  frame_fence<LOGN>();
+  fft_half<LOGN>(out, z, l, tw);
+#pragma unroll
+  for (int q = 0; q < G::PPL; ++q) {
+    const float2 r = z[pl + G::LPF * q * 9 / 8];
+    out[q] = make_float2(r.x, -r.y);
+  }
+  frame_fence<LOGN>();
 }
 
-// Windowed frame-gradient slab: ws[(frame)*win + (n - left)] = window * r_n.
+// Windowed frame-gradient slab row: slab[n - left] = w(n - left) * r_n.
 template <int LOGN>
-__device__ __forceinline__ void store_frame_grad(const float2* R, const FrameArgs& a,
-                                                 const float* __restrict__ window,
-                                                 float* __restrict__ slab, int t, bool active) {
+__device__ __forceinline__ void store_frame_grad(const float2 (&r)[Geo<LOGN>::PPL], const FrameArgs& a,
+                                                 const Win<LOGN>& wn, float* __restrict__ slab, int l, bool active) {
   using G = Geo<LOGN>;
   if (!active) return;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int m = t + q * G::TPF;
-    const float2 r = R[m];
-    const int w0 = 2 * m - a.left, w1 = w0 + 1;
-    if (w0 >= 0 && w0 < a.win) slab[w0] = window[w0] * r.x;
-    if (w1 >= 0 && w1 < a.win) slab[w1] = window[w1] * (-r.y);
+  for (int q = 0; q < G::PPL; ++q) {
+    const int w0 = 2 * (l + G::LPF * q) - a.left, w1 = w0 + 1;
+    const float2 w = wn.get(q);
+    if (w0 >= 0 && w0 < a.win) slab[w0] = w.x * r[q].x;
+    if (w1 >= 0 && w1 < a.win) slab[w1] = w.y * r[q].y;
   }
 }
 
-__device__ __forceinline__ float clamp_sqrt(float p, float floor_) { return sqrtf(fmaxf(p, floor_)); }
+// v_sqrt_f32 / v_rsq_f32 (1 ulp): the IEEE sqrtf expansion costs ~10 VALU per bin
+__device__ __forceinline__ float clamp_sqrt(float p, float floor_) { return __builtin_amdgcn_sqrtf(fmaxf(p, floor_)); }
+__device__ __forceinline__ float rsqrt_(float p) { return __builtin_amdgcn_rsqf(p); }
 __device__ __forceinline__ float pw(float2 z) { return z.x * z.x + z.y * z.y; }
 
 // -------------------------------------------------------------------------
 // Kernels
 // -------------------------------------------------------------------------
 
-#define FRAME_PROLOGUE(LOGN)                                               \
-  using G = Geo<LOGN>;                                                     \
-  __shared__ float2 lds[G::FPB][2][G::BUF];                                \
-  const int g = threadIdx.x / G::TPF;                                      \
-  const int t = threadIdx.x % G::TPF;                                      \
-  const int64_t fr = int64_t(blockIdx.x) * G::FPB + g;                    \
-  const bool active = fr < a.B * a.F;                                      \
-  const int64_t b = active ? fr / a.F : 0;                                 \
-  const int f = active ? int(fr % a.F) : 0;                                \
-  float2* buf0 = lds[g][0];                                                \
-  float2* buf1 = lds[g][1];
+// register budget of the frame kernels: >= 2 waves per SIMD (<= 256 VGPRs; the
+// 4-wave budget made hipcc spill, and the spilling builds computed wrong results)
+#ifndef SEL_FFT_WAVES
+#define SEL_FFT_WAVES 2
+#endif
+#define SEL_FFT_OCC __attribute__((amdgpu_waves_per_eu(SEL_FFT_WAVES)))
+
+// Frame ownership: block b, iteration it -> frames (b*iters + it)*FPB + slot;
+// the next frame's samples are fetched before the current one is transformed.
+#define FRAME_PROLOGUE(LOGN, EXTRA_FLOATS)                                          \
+  using G = Geo<LOGN>;                                                              \
+  extern __shared__ __align__(16) float2 lds_dyn[];                                 \
+  const int slot = threadIdx.x / G::LPF, l = threadIdx.x % G::LPF;                  \
+  float2* z = lds_dyn + slot * (G::PADN + (EXTRA_FLOATS) / 2);                      \
+  const int nframes = int(a.B * a.F);                                               \
+  const int fr0 = int(blockIdx.x) * iters * G::FPB + slot;                          \
+  Win<LOGN> wn;                                                                     \
+  wn.init(window, a, l);                                                            \
+  LaneTw<LOGN> tw;                                                                  \
+  tw.load(l);
+
+// A wave's current frame: flat index, signal, frame-in-signal (32-bit: the host
+// keeps B*T < 2^29, so B*F < 2^31).  Consecutive iterations advance by FPB
+// frames without a division.
+struct FramePos {
+  int fr, b, f;
+  bool active;
+  __device__ __forceinline__ void init(int fr_, int nframes, int F) {
+    fr = fr_;
+    active = fr < nframes;
+    b = active ? fr / F : 0;
+    f = active ? fr - b * F : 0;
+  }
+  __device__ __forceinline__ void advance(int step, int nframes, int F) {
+    fr += step;
+    f += step;
+    while (f >= F) {  // step = FPB <= 16: a few rounds at most
+      f -= F;
+      ++b;
+    }
+    active = fr < nframes;
+    if (!active) b = f = 0;
+  }
+};
+
+// for it in [0, iters): P = this frame; RAW (and RAWY) hold its fetched samples on
+// entry to the body, and the next frame's fetch is already in flight
+#define FRAME_LOOP_BEGIN(X, RAW, PF)                                     \
+  float2 RAW[G::PPL];                                                    \
+  const __amdgpu_buffer_rsrc_t X##_rsrc = signal_rsrc(X, a);             \
+  FramePos P;                                                            \
+  P.init(fr0, nframes, a.F);                                             \
+  if constexpr (PF) fetch_frame<LOGN>(X, X##_rsrc, a, P.b, P.f, l, P.active, RAW); \
+  for (int it = 0; it < iters; ++it) {                                   \
+    if constexpr (!(PF)) fetch_frame<LOGN>(X, X##_rsrc, a, P.b, P.f, l, P.active, RAW); \
+    float2 v[G::PPL];                                                    \
+    window_frame<LOGN>(RAW, wn, v);                                      \
+    const FramePos cur = P;                                              \
+    if (it + 1 < iters) {                                                \
+      P.advance(G::FPB, nframes, a.F);                                   \
+      if constexpr (PF) fetch_frame<LOGN>(X, X##_rsrc, a, P.b, P.f, l, P.active, RAW); \
+    }                                                                    \
+    const int64_t fr = cur.fr, b = cur.b;                                \
+    const int f = cur.f;                                                 \
+    const bool active = cur.active;                                      \
+    (void)b;
+
+// one-frame-ahead prefetch only where the registers allow it (PPL = 8, one signal)
+#define SEL_PF (G::PPL == 8)
+
+#define FRAME_LOOP_END }
 
 template <int LOGN>
-__global__ __launch_bounds__(Geo<LOGN>::BLOCK) void k_stft_mag_fwd(
-    const float* __restrict__ x, FrameArgs a, const float* __restrict__ window, float floor_,
-    float* __restrict__ mag) {
-  FRAME_PROLOGUE(LOGN)
-  load_frame<LOGN>(x + b * a.T, a, f, window, buf0, t, active);
-  __syncthreads();
-  const float2* Z = fft_half<LOGN>(buf0, buf1, t);
-  float2 X[4], XM;
-  real_split<LOGN>(Z, t, X, XM);
-  if (!active) return;
-  constexpr int K = G::M + 1;
-  float* out = mag + fr * K;
+__global__ __launch_bounds__(256) SEL_FFT_OCC void k_stft_mag_fwd(const float* __restrict__ x, FrameArgs a,
+                                                      const float* __restrict__ window, float floor_,
+                                                      float* __restrict__ mag, int iters) {
+  FRAME_PROLOGUE(LOGN, 0)
+  FRAME_LOOP_BEGIN(x, raw, SEL_PF)
+  (void)f;
+  fft_half<LOGN>(v, z, l, tw);
+  float2 X[G::PPL], XM;
+  real_split<LOGN>(z, l, tw, X, XM);
+  if (active) {
+    constexpr int K = G::M + 1;
+    float* out = mag + fr * K + l;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) out[t + q * G::TPF] = clamp_sqrt(pw(X[q]), floor_);
-  if (t == 0) out[G::M] = clamp_sqrt(pw(XM), floor_);
+    for (int q = 0; q < G::PPL; ++q) out[G::LPF * q] = clamp_sqrt(pw(X[q]), floor_);
+    if (l == 0) out[G::M] = clamp_sqrt(pw(XM), floor_);
+  }
+  FRAME_LOOP_END
 }
 
 template <int LOGN>
-__global__ __launch_bounds__(Geo<LOGN>::BLOCK) void k_stft_mag_bwd(
-    const float* __restrict__ x, FrameArgs a, const float* __restrict__ window, float floor_,
-    const float* __restrict__ gmag, float* __restrict__ slab) {
-  FRAME_PROLOGUE(LOGN)
-  load_frame<LOGN>(x + b * a.T, a, f, window, buf0, t, active);
-  __syncthreads();
-  float2* Z = fft_half<LOGN>(buf0, buf1, t);
-  float2 X[4], XM;
-  real_split<LOGN>(Z, t, X, XM);
-  __syncthreads();  // everyone done reading Z before it is overwritten with G
+__global__ __launch_bounds__(256) SEL_FFT_OCC void k_stft_mag_bwd(const float* __restrict__ x, FrameArgs a,
+                                                      const float* __restrict__ window, float floor_,
+                                                      const float* __restrict__ gmag, float* __restrict__ slab,
+                                                      int iters) {
+  FRAME_PROLOGUE(LOGN, 0)
+  FRAME_LOOP_BEGIN(x, raw, false)
+  (void)f;
+  fft_half<LOGN>(v, z, l, tw);
+  float2 X[G::PPL], XM;
+  real_split<LOGN>(z, l, tw, X, XM);
   constexpr int K = G::M + 1;
   const float* gm = gmag + (active ? fr : 0) * K;
-  float2* Gb = Z;
-  float2* other = (Z == buf0) ? buf1 : buf0;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int k = t + q * G::TPF;
+  for (int q = 0; q < G::PPL; ++q) {
     const float p = pw(X[q]);
-    const float s = (active && p >= floor_) ? gm[k] / sqrtf(p) : 0.f;
-    Gb[k] = make_float2(s * X[q].x, s * X[q].y);
+    const float s = (active && p >= floor_) ? gm[l + G::LPF * q] * rsqrt_(p) : 0.f;
+    X[q] = make_float2(s * X[q].x, s * X[q].y);
   }
-  if (t == 0) {
+  {
     const float p = pw(XM);
-    const float s = (active && p >= floor_) ? gm[G::M] / sqrtf(p) : 0.f;
-    Gb[G::M] = make_float2(s * XM.x, s * XM.y);
+    const float s = (active && l == 0 && p >= floor_) ? gm[G::M] * rsqrt_(p) : 0.f;
+    XM = make_float2(s * XM.x, s * XM.y);
   }
-  __syncthreads();
-  const float2* R = c2r_grad<LOGN>(Gb, other, t);
-  store_frame_grad<LOGN>(R, a, window, slab + (active ? fr : 0) * a.win, t, active);
+  c2r_grad<LOGN>(X, XM, z, l, tw, v);
+  store_frame_grad<LOGN>(v, a, wn, slab + (active ? fr : 0) * a.win, l, active);
+  FRAME_LOOP_END
 }
 
-// Fused STFT loss forward: both signals' spectra in LDS, block partial sums
+// |Y| of the reference signal's frame (windowed points in v) into ym[]
+// (PPL bins + bin M on l == 0)
+template <int LOGN>
+__device__ __forceinline__ void ref_mag(float2 (&v)[Geo<LOGN>::PPL], int l, float2* z, const LaneTw<LOGN>& tw,
+                                        float floor_, float (&ym)[Geo<LOGN>::PPL + 1]) {
+  using G = Geo<LOGN>;
+  fft_half<LOGN>(v, z, l, tw);
+  float2 X[G::PPL], XM;
+  real_split<LOGN>(z, l, tw, X, XM);
+#pragma unroll
+  for (int q = 0; q < G::PPL; ++q) ym[q] = clamp_sqrt(pw(X[q]), floor_);
+  ym[G::PPL] = clamp_sqrt(pw(XM), floor_);
+}
+
+// the reference signal's windowed frame at the current position (no prefetch)
+#define Y_FRAME(VY)                                                        \
+  float2 VY[G::PPL];                                                       \
+  {                                                                        \
+    float2 rawy[G::PPL];                                                   \
+    fetch_frame<LOGN>(y, y_rsrc, a, cur.b, cur.f, l, cur.active, rawy);    \
+    window_frame<LOGN>(rawy, wn, VY);                                      \
+  }
+
+// Fused STFT loss forward: both signals' spectra, block partial sums
 // {sum (ym-xm)^2, sum ym^2, sum |ln ym - ln xm|} (stft_loss.py:56, :77).
 template <int LOGN>
-__global__ __launch_bounds__(Geo<LOGN>::BLOCK) void k_stft_loss_fwd(
-    const float* __restrict__ x, const float* __restrict__ y, FrameArgs a,
-    const float* __restrict__ window, float floor_, double* __restrict__ partials) {
-  FRAME_PROLOGUE(LOGN)
+__global__ __launch_bounds__(256) SEL_FFT_OCC void k_stft_loss_fwd(const float* __restrict__ x, const float* __restrict__ y,
+                                                       FrameArgs a, const float* __restrict__ window,
+                                                       float floor_, double* __restrict__ partials, int iters) {
+  FRAME_PROLOGUE(LOGN, 0)
   __shared__ double red[16];
-  float ym[5];
-  {
-    load_frame<LOGN>(y + b * a.T, a, f, window, buf0, t, active);
-    __syncthreads();
-    const float2* Z = fft_half<LOGN>(buf0, buf1, t);
-    float2 X[4], XM;
-    real_split<LOGN>(Z, t, X, XM);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) ym[q] = clamp_sqrt(pw(X[q]), floor_);
-    ym[4] = clamp_sqrt(pw(XM), floor_);
-    __syncthreads();
-  }
-  load_frame<LOGN>(x + b * a.T, a, f, window, buf0, t, active);
-  __syncthreads();
-  const float2* Z = fft_half<LOGN>(buf0, buf1, t);
-  float2 X[4], XM;
-  real_split<LOGN>(Z, t, X, XM);
   float s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  const __amdgpu_buffer_rsrc_t y_rsrc = signal_rsrc(y, a);
+  FRAME_LOOP_BEGIN(x, raw, false)
+  (void)f;
+  (void)fr;
+  Y_FRAME(vy)
+  float ym[G::PPL + 1];
+  ref_mag<LOGN>(vy, l, z, tw, floor_, ym);
+  fft_half<LOGN>(v, z, l, tw);
+  float2 X[G::PPL], XM;
+  real_split<LOGN>(z, l, tw, X, XM);
   if (active) {
 #pragma unroll
-    for (int q = 0; q < 5; ++q) {
-      if (q == 4 && t != 0) break;
-      const float xm = clamp_sqrt(pw(q < 4 ? X[q] : XM), floor_);
+    for (int q = 0; q <= G::PPL; ++q) {
+      if (q == G::PPL && l != 0) break;
+      const float xm = clamp_sqrt(pw(q < G::PPL ? X[q] : XM), floor_);
       const float d = ym[q] - xm;
       s1 += d * d;
       s2 += ym[q] * ym[q];
       s3 += fabsf(logf(ym[q]) - logf(xm));
     }
   }
+  FRAME_LOOP_END
   const double r1 = block_sum<double>(s1, red);
   const double r2 = block_sum<double>(s2, red);
   const double r3 = block_sum<double>(s3, red);
@@ -313,47 +634,35 @@ __global__ __launch_bounds__(Geo<LOGN>::BLOCK) void k_stft_loss_fwd(
 }
 
 template <int LOGN>
-__global__ __launch_bounds__(Geo<LOGN>::BLOCK) void k_stft_loss_bwd(
-    const float* __restrict__ x, const float* __restrict__ y, FrameArgs a,
-    const float* __restrict__ window, float floor_, const float* __restrict__ coef,
-    float* __restrict__ slab) {
-  FRAME_PROLOGUE(LOGN)
-  float ym[5];
-  {
-    load_frame<LOGN>(y + b * a.T, a, f, window, buf0, t, active);
-    __syncthreads();
-    const float2* Z = fft_half<LOGN>(buf0, buf1, t);
-    float2 X[4], XM;
-    real_split<LOGN>(Z, t, X, XM);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) ym[q] = clamp_sqrt(pw(X[q]), floor_);
-    ym[4] = clamp_sqrt(pw(XM), floor_);
-    __syncthreads();
-  }
-  load_frame<LOGN>(x + b * a.T, a, f, window, buf0, t, active);
-  __syncthreads();
-  float2* Z = fft_half<LOGN>(buf0, buf1, t);
-  float2 X[4], XM;
-  real_split<LOGN>(Z, t, X, XM);
-  __syncthreads();
+__global__ __launch_bounds__(256) SEL_FFT_OCC void k_stft_loss_bwd(const float* __restrict__ x, const float* __restrict__ y,
+                                                       FrameArgs a, const float* __restrict__ window,
+                                                       float floor_, const float* __restrict__ coef,
+                                                       float* __restrict__ slab, int iters) {
+  FRAME_PROLOGUE(LOGN, 0)
   const float ca = coef[0], cb = coef[1];
-  float2* Gb = Z;
-  float2* other = (Z == buf0) ? buf1 : buf0;
+  const __amdgpu_buffer_rsrc_t y_rsrc = signal_rsrc(y, a);
+  FRAME_LOOP_BEGIN(x, raw, false)
+  (void)f;
+  Y_FRAME(vy)
+  float ym[G::PPL + 1];
+  ref_mag<LOGN>(vy, l, z, tw, floor_, ym);
+  fft_half<LOGN>(v, z, l, tw);
+  float2 X[G::PPL + 1];
+  real_split<LOGN>(z, l, tw, reinterpret_cast<float2(&)[G::PPL]>(X), X[G::PPL]);
 #pragma unroll
-  for (int q = 0; q < 5; ++q) {
-    if (q == 4 && t != 0) break;
-    const float2 Xq = q < 4 ? X[q] : XM;
-    const float p = pw(Xq);
+  for (int q = 0; q <= G::PPL; ++q) {
+    const float p = pw(X[q]);
     const float xm = clamp_sqrt(p, floor_);
     const float lx = logf(xm), ly = logf(ym[q]);
     const float sg = lx > ly ? 1.f : (lx < ly ? -1.f : 0.f);
     const float gx = ca * (xm - ym[q]) + cb * sg / xm;
-    const float s = (active && p >= floor_) ? gx / xm : 0.f;
-    Gb[q < 4 ? t + q * G::TPF : G::M] = make_float2(s * Xq.x, s * Xq.y);
+    const bool ok = active && p >= floor_ && (q < G::PPL || l == 0);
+    const float s = ok ? gx / xm : 0.f;
+    X[q] = make_float2(s * X[q].x, s * X[q].y);
   }
-  __syncthreads();
-  const float2* R = c2r_grad<LOGN>(Gb, other, t);
-  store_frame_grad<LOGN>(R, a, window, slab + (active ? fr : 0) * a.win, t, active);
+  c2r_grad<LOGN>(reinterpret_cast<float2(&)[G::PPL]>(X), X[G::PPL], z, l, tw, v);
+  store_frame_grad<LOGN>(v, a, wn, slab + (active ? fr : 0) * a.win, l, active);
+  FRAME_LOOP_END
 }
 
 __device__ __forceinline__ float log_k(float v, int kind) {
@@ -373,53 +682,55 @@ struct MelArgs {
 
 // log-mel forward (mel_loss.py:84-94): stft -> |X| (floor eps) -> melmat -> floor eps -> log.
 template <int LOGN>
-__global__ __launch_bounds__(Geo<LOGN>::BLOCK) void k_logmel_fwd(
-    const float* __restrict__ x, FrameArgs a, const float* __restrict__ window, MelArgs ma,
-    float* __restrict__ out) {
-  FRAME_PROLOGUE(LOGN)
-  load_frame<LOGN>(x + b * a.T, a, f, window, buf0, t, active);
-  __syncthreads();
-  float2* Z = fft_half<LOGN>(buf0, buf1, t);
-  float2 X[4], XM;
-  real_split<LOGN>(Z, t, X, XM);
-  float* magb = reinterpret_cast<float*>((Z == buf0) ? buf1 : buf0);
+__global__ __launch_bounds__(256) SEL_FFT_OCC void k_logmel_fwd(const float* __restrict__ x, FrameArgs a,
+                                                    const float* __restrict__ window, MelArgs ma,
+                                                    float* __restrict__ out, int iters) {
+  FRAME_PROLOGUE(LOGN, 0)
+  float* magb = reinterpret_cast<float*>(z);
+  FRAME_LOOP_BEGIN(x, raw, SEL_PF)
+  (void)fr;
+  fft_half<LOGN>(v, z, l, tw);
+  float2 X[G::PPL], XM;
+  real_split<LOGN>(z, l, tw, X, XM);
 #pragma unroll
-  for (int q = 0; q < 4; ++q) magb[t + q * G::TPF] = clamp_sqrt(pw(X[q]), ma.eps);
-  if (t == 0) magb[G::M] = clamp_sqrt(pw(XM), ma.eps);
-  __syncthreads();
-  if (!active) return;
-  for (int m = t; m < ma.nm; m += G::TPF) {
-    const int2 r = ma.range[m];
-    float s = 0.f;
-    for (int k = r.x; k < r.y; ++k) s = fmaf(magb[k], ma.melmat[k * ma.nm + m], s);
-    out[(b * ma.nm + m) * a.F + f] = log_k(fmaxf(s, ma.eps), ma.log_kind);
+  for (int q = 0; q < G::PPL; ++q) magb[l + G::LPF * q] = clamp_sqrt(pw(X[q]), ma.eps);
+  if (l == 0) magb[G::M] = clamp_sqrt(pw(XM), ma.eps);
+  frame_fence<LOGN>();
+  if (active) {
+    for (int m = l; m < ma.nm; m += G::LPF) {
+      const int2 r = ma.range[m];
+      float s = 0.f;
+      for (int k = r.x; k < r.y; ++k) s = fmaf(magb[k], ma.melmat[k * ma.nm + m], s);
+      out[(b * ma.nm + m) * a.F + f] = log_k(fmaxf(s, ma.eps), ma.log_kind);
+    }
   }
+  frame_fence<LOGN>();
+  FRAME_LOOP_END
 }
 
 // log-mel backward. gsel: if ref != nullptr, upstream = g_scale * sign(gout - ref)
-// (L1 backward, mel_loss.py:153); else upstream = gout.
+// (L1 backward, mel_loss.py:153); else upstream = gout.  Each frame owns
+// PADN complex slots (spectrum, then |X|, then G) + nm floats (dL/dmel).
 template <int LOGN>
-__global__ __launch_bounds__(Geo<LOGN>::BLOCK) void k_logmel_bwd(
-    const float* __restrict__ x, FrameArgs a, const float* __restrict__ window, MelArgs ma,
-    const int2* __restrict__ krange, const float* __restrict__ gout,
-    const float* __restrict__ ref, const float* __restrict__ gscale, float gmul,
-    float* __restrict__ slab) {
-  FRAME_PROLOGUE(LOGN)
-  load_frame<LOGN>(x + b * a.T, a, f, window, buf0, t, active);
-  __syncthreads();
-  float2* Z = fft_half<LOGN>(buf0, buf1, t);
-  float2 X[4], XM;
-  real_split<LOGN>(Z, t, X, XM);
-  float2* other = (Z == buf0) ? buf1 : buf0;
-  float* magb = reinterpret_cast<float*>(other);
-  float* glin = magb + G::M + 4;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) magb[t + q * G::TPF] = clamp_sqrt(pw(X[q]), ma.eps);
-  if (t == 0) magb[G::M] = clamp_sqrt(pw(XM), ma.eps);
-  __syncthreads();
+__global__ __launch_bounds__(256) SEL_FFT_OCC void k_logmel_bwd(const float* __restrict__ x, FrameArgs a,
+                                                    const float* __restrict__ window, MelArgs ma,
+                                                    const int2* __restrict__ krange, const float* __restrict__ gout,
+                                                    const float* __restrict__ ref, const float* __restrict__ gscale,
+                                                    float gmul, float* __restrict__ slab, int iters, int glin_floats) {
+  FRAME_PROLOGUE(LOGN, glin_floats)
+  float* magb = reinterpret_cast<float*>(z);
+  float* glin = reinterpret_cast<float*>(z + G::PADN);
   const float gs = ref ? gscale[0] * gmul : 0.f;
-  for (int m = t; m < ma.nm; m += G::TPF) {
-    float v = 0.f;
+  FRAME_LOOP_BEGIN(x, raw, false)
+  fft_half<LOGN>(v, z, l, tw);
+  float2 X[G::PPL + 1];
+  real_split<LOGN>(z, l, tw, reinterpret_cast<float2(&)[G::PPL]>(X), X[G::PPL]);
+#pragma unroll
+  for (int q = 0; q < G::PPL; ++q) magb[l + G::LPF * q] = clamp_sqrt(pw(X[q]), ma.eps);
+  if (l == 0) magb[G::M] = clamp_sqrt(pw(X[G::PPL]), ma.eps);
+  frame_fence<LOGN>();
+  for (int m = l; m < ma.nm; m += G::LPF) {
+    float gv = 0.f;
     if (active) {
       const int2 r = krange[m];
       float s = 0.f;
@@ -433,27 +744,26 @@ __global__ __launch_bounds__(Geo<LOGN>::BLOCK) void k_logmel_bwd(
         up = gout[o];
       }
       const float mel = fmaxf(s, ma.eps);
-      v = (s >= ma.eps) ? up / (mel * dlog_k(ma.log_kind)) : 0.f;
+      gv = (s >= ma.eps) ? up / (mel * dlog_k(ma.log_kind)) : 0.f;
     }
-    glin[m] = v;
+    glin[m] = gv;
   }
-  __syncthreads();
-  float2* Gb = Z;
+  frame_fence<LOGN>();
 #pragma unroll
-  for (int q = 0; q < 5; ++q) {
-    if (q == 4 && t != 0) break;
-    const int k = q < 4 ? t + q * G::TPF : G::M;
-    const float2 Xq = q < 4 ? X[q] : XM;
+  for (int q = 0; q <= G::PPL; ++q) {
+    const int k = q < G::PPL ? l + G::LPF * q : G::M;
     const int2 r = ma.range[k];
     float gmag = 0.f;
     for (int m = r.x; m < r.y; ++m) gmag = fmaf(ma.melmat[k * ma.nm + m], glin[m], gmag);
-    const float p = pw(Xq);
-    const float s = (active && p >= ma.eps) ? gmag / sqrtf(p) : 0.f;
-    Gb[k] = make_float2(s * Xq.x, s * Xq.y);
+    const float p = pw(X[q]);
+    const bool ok = active && p >= ma.eps && (q < G::PPL || l == 0);
+    const float s = ok ? gmag * rsqrt_(p) : 0.f;
+    X[q] = make_float2(s * X[q].x, s * X[q].y);
   }
-  __syncthreads();
-  const float2* R = c2r_grad<LOGN>(Gb, other, t);
-  store_frame_grad<LOGN>(R, a, window, slab + (active ? fr : 0) * a.win, t, active);
+  frame_fence<LOGN>();  // magb / glin reads done before c2r overwrites the slots
+  c2r_grad<LOGN>(reinterpret_cast<float2(&)[G::PPL]>(X), X[G::PPL], z, l, tw, v);
+  store_frame_grad<LOGN>(v, a, wn, slab + (active ? fr : 0) * a.win, l, active);
+  FRAME_LOOP_END
 }
 
 // Overlap-add of frame-gradient slabs + adjoint of the reflect pad -> g_x (B,T).
@@ -594,6 +904,9 @@ int check_frame(int64_t B, int64_t T, int n_fft, int hop, int win, int& logn) {
   SEL_REQUIRE(logn >= kMinLog && logn <= kMaxLog - 1, SEL_ERR_UNSUPPORTED,
               "n_fft=%d outside [256, 2048]", n_fft);
   SEL_REQUIRE(hop > 0, SEL_ERR_ARG, "hop must be > 0");
+  // frame loads address the batch through 32-bit buffer offsets
+  SEL_REQUIRE(B * T < (int64_t(1) << 29), SEL_ERR_UNSUPPORTED,
+              "batch of %lld x %lld samples exceeds 2 GiB per call: split the batch", (long long)B, (long long)T);
   SEL_REQUIRE(win > 0 && win <= n_fft, SEL_ERR_ARG, "win_length=%d must be in (0, n_fft=%d]", win, n_fft);
   // torch.stft(center=True, pad_mode='reflect') requires pad < input length
   SEL_REQUIRE(T > n_fft / 2, SEL_ERR_ARG,
@@ -614,30 +927,44 @@ FrameArgs frame_args(int64_t B, int64_t T, int n_fft, int hop, int win) {
   return a;
 }
 
-// dispatch helper: one template kernel family over LOGN in [8, 11]
-#define SEL_FRAME_DISPATCH(logn, nframes, stream, KER, ...)                                  \
+// Launch plan of the wave-FFT kernels: FPB frames per block iteration, `iters`
+// iterations per block (enough blocks to fill 256 CUs 8 deep first).
+template <int LOGN>
+unsigned frame_grid(int64_t nframes, int& iters) {
+  using G = Geo<LOGN>;
+  const int64_t groups = (nframes + G::FPB - 1) / G::FPB;
+  iters = int(std::max<int64_t>(1, std::min<int64_t>(8, groups / 2048)));
+  return unsigned((groups + iters - 1) / iters);
+}
+
+unsigned frame_grid_rt(int logn, int64_t nframes, int& iters) {
+  switch (logn) {
+    case 8: return frame_grid<8>(nframes, iters);
+    case 9: return frame_grid<9>(nframes, iters);
+    case 10: return frame_grid<10>(nframes, iters);
+    default: return frame_grid<11>(nframes, iters);
+  }
+}
+
+// dispatch helper: one template kernel family over LOGN in [8, 11]; the kernel's
+// trailing arguments are (iters, ...EXTRA); EXTRA_FLOATS = per-frame LDS floats
+// beyond the spectrum slots
+#define SEL_FRAME_CASE(L, nframes, stream, extra, KER, ...)                                   \
+  case L: {                                                                                   \
+    using G = Geo<L>;                                                                         \
+    int iters;                                                                                \
+    const unsigned grid = frame_grid<L>(nframes, iters);                                      \
+    const size_t lds = size_t(G::FPB) * (G::PADN * sizeof(float2) + size_t(extra) * sizeof(float)); \
+    if (grid) hipLaunchKernelGGL(KER<L>, dim3(grid), dim3(256), lds, stream, __VA_ARGS__, iters); \
+  } break;
+
+#define SEL_FRAME_DISPATCH_X(logn, nframes, stream, extra, KER, ...)                          \
   do {                                                                                       \
     switch (logn) {                                                                          \
-      case 8: {                                                                              \
-        using G = Geo<8>;                                                                    \
-        dim3 grid(unsigned((nframes + G::FPB - 1) / G::FPB));                                \
-        if (grid.x) hipLaunchKernelGGL(KER<8>, grid, dim3(G::BLOCK), 0, stream, __VA_ARGS__);   \
-      } break;                                                                               \
-      case 9: {                                                                              \
-        using G = Geo<9>;                                                                    \
-        dim3 grid(unsigned((nframes + G::FPB - 1) / G::FPB));                                \
-        if (grid.x) hipLaunchKernelGGL(KER<9>, grid, dim3(G::BLOCK), 0, stream, __VA_ARGS__);   \
-      } break;                                                                               \
-      case 10: {                                                                             \
-        using G = Geo<10>;                                                                   \
-        dim3 grid(unsigned((nframes + G::FPB - 1) / G::FPB));                                \
-        if (grid.x) hipLaunchKernelGGL(KER<10>, grid, dim3(G::BLOCK), 0, stream, __VA_ARGS__);  \
-      } break;                                                                               \
-      case 11: {                                                                             \
-        using G = Geo<11>;                                                                   \
-        dim3 grid(unsigned((nframes + G::FPB - 1) / G::FPB));                                \
-        if (grid.x) hipLaunchKernelGGL(KER<11>, grid, dim3(G::BLOCK), 0, stream, __VA_ARGS__);  \
-      } break;                                                                               \
+      SEL_FRAME_CASE(8, nframes, stream, extra, KER, __VA_ARGS__)                            \
+      SEL_FRAME_CASE(9, nframes, stream, extra, KER, __VA_ARGS__)                            \
+      SEL_FRAME_CASE(10, nframes, stream, extra, KER, __VA_ARGS__)                           \
+      SEL_FRAME_CASE(11, nframes, stream, extra, KER, __VA_ARGS__)                           \
       default:                                                                               \
         ::sel::set_error("unsupported log2(n_fft)=%d", logn);                                \
         return SEL_ERR_UNSUPPORTED;                                                          \
@@ -645,17 +972,18 @@ FrameArgs frame_args(int64_t B, int64_t T, int n_fft, int hop, int win) {
     SEL_LAUNCH_CHECK();                                                                      \
   } while (0)
 
-int frames_per_block(int logn) {
-  switch (logn) {
-    case 8: return Geo<8>::FPB;
-    case 9: return Geo<9>::FPB;
-    case 10: return Geo<10>::FPB;
-    default: return Geo<11>::FPB;
-  }
-}
+#define SEL_FRAME_DISPATCH(logn, nframes, stream, KER, ...) \
+  SEL_FRAME_DISPATCH_X(logn, nframes, stream, 0, KER, __VA_ARGS__)
 
+// upper bound on the block count of any launch plan (workspace sizing)
 int64_t n_blocks(int logn, int64_t nframes) {
-  const int fpb = frames_per_block(logn);
+  int fpb;
+  switch (logn) {
+    case 8: fpb = Geo<8>::FPB; break;
+    case 9: fpb = Geo<9>::FPB; break;
+    case 10: fpb = Geo<10>::FPB; break;
+    default: fpb = Geo<11>::FPB;
+  }
   return (nframes + fpb - 1) / fpb;
 }
 
@@ -759,7 +1087,8 @@ int sel_stft_loss_fwd(const float* x, const float* y, int64_t B, int64_t T, int 
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   double* part = static_cast<double*>(ws);
   SEL_FRAME_DISPATCH(logn, nf, s, k_stft_loss_fwd, x, y, a, window, 1e-7f, part);
-  const int nb = int(n_blocks(logn, nf));
+  int iters;
+  const int nb = int(frame_grid_rt(logn, nf, iters));
   hipLaunchKernelGGL(k_finish_partials, dim3(1), dim3(256), 0, s, part, nb, 3, sums, nullptr, 0.0);
   SEL_LAUNCH_CHECK();
   return SEL_OK;
@@ -854,8 +1183,30 @@ int sel_logmel_bwd(const float* x, int64_t B, int64_t T, int n_fft, int hop, int
   const int64_t nf = B * a.F;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   float* slab = static_cast<float*>(ws);
-  SEL_FRAME_DISPATCH(logn, nf, s, k_logmel_bwd, x, a, window, ma,
-                     reinterpret_cast<const int2*>(krange), g_out, ref, g_scale, g_mul, slab);
+  // per-frame dL/dmel floats after the spectrum slots; iters is passed before it
+  const int glin = (n_mels + 3) / 4 * 4;
+  switch (logn) {
+#define SEL_LOGMEL_BWD_CASE(L)                                                                          \
+    case L: {                                                                                           \
+      using G = Geo<L>;                                                                                 \
+      int iters;                                                                                        \
+      const unsigned grid = frame_grid<L>(nf, iters);                                                   \
+      const size_t lds = size_t(G::FPB) * (G::PADN * sizeof(float2) + size_t(glin) * sizeof(float));    \
+      if (grid)                                                                                         \
+        hipLaunchKernelGGL(k_logmel_bwd<L>, dim3(grid), dim3(256), lds, s, x, a, window, ma,           \
+                           reinterpret_cast<const int2*>(krange), g_out, ref, g_scale, g_mul, slab, iters, \
+                           glin);                                                                       \
+    } break;
+    SEL_LOGMEL_BWD_CASE(8)
+    SEL_LOGMEL_BWD_CASE(9)
+    SEL_LOGMEL_BWD_CASE(10)
+    SEL_LOGMEL_BWD_CASE(11)
+#undef SEL_LOGMEL_BWD_CASE
+    default:
+      ::sel::set_error("unsupported log2(n_fft)=%d", logn);
+      return SEL_ERR_UNSUPPORTED;
+  }
+  SEL_LAUNCH_CHECK();
   return ola(slab, a, g_x, s);
 }
 

@@ -32,7 +32,7 @@ def spec_close(a, b, rtol=1e-4, floor=1e-5):
     assert not bad.any(), f"{bad.sum()} elements out of bound; worst {np.abs(a - b)[bad].max()}"
 
 
-def cond_close(ours, ref32, ref64, slack=3.0, floor=1e-4):
+def cond_close(ours, ref32, ref64, slack=3.0, floor=1e-4, ref64_for_ref=None):
     """For ill-conditioned gradients: the log-magnitude / log-mel gradients are
     dominated by bins just above the power floor, where any fp32 FFT (torch's
     included) carries ~1e-3 relative error, amplified by the 1/|X|^2 of the
@@ -43,9 +43,10 @@ def cond_close(ours, ref32, ref64, slack=3.0, floor=1e-4):
     FFT has the same RMS error as torch's (2.3e-7 vs 2.2e-7 on windowed noise),
     so the remaining spread is which near-floor bins each rounding pattern hits."""
     o, r, t = (_np(v).astype(np.float64) for v in (ours, ref32, ref64))
+    tr = t if ref64_for_ref is None else _np(ref64_for_ref).astype(np.float64)
     nt = np.linalg.norm(t)
     e_ours = np.linalg.norm(o - t) / nt
-    e_ref = np.linalg.norm(r - t) / nt
+    e_ref = np.linalg.norm(r - tr) / np.linalg.norm(tr)
     assert e_ours <= max(slack * e_ref, floor), (e_ours, e_ref)
 
 
@@ -180,23 +181,43 @@ def test_mel_matches_reference_golden(gpu):
     loss.backward()
     scalar_close(loss, g["mel24.loss"])
     mt = ml.mel_transfers[0]
+    with torch.no_grad():
+        ours_d = [mt(yh) - mt(y)]
     cond_close(yg.grad, g["mel24.grad"], _mel_grad64(g["y_hat"], g["y"], [(2048, 300, 2048)],
-                                                     [mt.melmat.cpu()], None))
+                                                     [mt.melmat.cpu()], None, ours_d=ours_d),
+               ref64_for_ref=_mel_grad64(g["y_hat"], g["y"], [(2048, 300, 2048)], [mt.melmat.cpu()], None))
     mld = MultiMelSpectrogramLoss().to(gpu)
     yg = yh.clone().requires_grad_(True)
     loss = mld(yg, y)
     loss.backward()
     scalar_close(loss, g["meldef.loss"])
-    cond_close(yg.grad, g["meldef.grad"], _mel_grad64(g["y_hat"], g["y"], RES,
-                                                      [m.melmat.cpu() for m in mld.mel_transfers], 10.0))
+    with torch.no_grad():
+        ours_d = [mt(yh) - mt(y) for mt in mld.mel_transfers]
+    melmats = [m.melmat.cpu() for m in mld.mel_transfers]
+    cond_close(yg.grad, g["meldef.grad"], _mel_grad64(g["y_hat"], g["y"], RES, melmats, 10.0, ours_d=ours_d),
+               ref64_for_ref=_mel_grad64(g["y_hat"], g["y"], RES, melmats, 10.0))
 
 
-def _mel_grad64(yh, y, res, melmats, log_base, up=None):
+def _mel_grad64(yh, y, res, melmats, log_base, up=None, ours_d=None, tie_tol=1e-5):
+    """fp64 gradient of the mel loss (or of <melspec, up>).  With `ours_d` (per
+    resolution, our fp32 mel(y_hat) - mel(y)), the L1 subgradient at near-ties
+    |mel64(y_hat) - mel64(y)| < tie_tol (a few fp32 ulps of the log-mel: the sign
+    there is decided by rounding, in the reference's fp32 path as in ours) takes
+    our sign, so the comparison checks the backward arithmetic, not the tie-break."""
     from oracle import ref_ops as R
     x = torch.as_tensor(yh).double().requires_grad_(True)
     yy = torch.as_tensor(y).double()
     wins = [R.hann(w).double() for _, _, w in res]
-    if up is None:
+    if up is None and ours_d is not None:
+        total = 0.0
+        for (n, h, w), win, mm, d32 in zip(res, wins, melmats, ours_d):
+            mh = R.melspec(x, n, h, w, win, mm.double(), 1e-10, log_base)
+            with torch.no_grad():
+                d64 = mh - R.melspec(yy, n, h, w, win, mm.double(), 1e-10, log_base)
+                sg = torch.where(d64.abs() < tie_tol, torch.sign(d32.double().cpu()), torch.sign(d64))
+            total = total + (mh * sg).sum() / mh.numel()
+        (total / len(res)).backward()
+    elif up is None:
         R.multi_mel_loss(x, yy, res, wins, [m.double() for m in melmats], 1e-10, log_base).backward()
     else:
         (n, h, w), = res

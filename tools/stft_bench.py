@@ -41,6 +41,12 @@ def main():
     x = 0.1 * torch.randn(B, T, device=dev)
     y = 0.1 * torch.randn(B, T, device=dev)
     print(f"B={B} T={T}")
+    # measured HBM peak: device-to-device copy of 2 GiB (read + write bytes)
+    src = torch.empty(2 ** 29, device=dev)
+    dst = torch.empty_like(src)
+    sc = timed(lambda: dst.copy_(src), iters=10)
+    print(f"measured copy bandwidth: {2 * src.numel() * 4 / sc / 1e9:.0f} GB/s (2 GiB D2D copy)")
+    del src, dst
     print("| kernel | n_fft/hop/win | us | alg. bytes | GB/s | % of 8 TB/s | GFLOP/s |")
     print("|---|---|---|---|---|---|---|")
     for n, h, w in RES:
