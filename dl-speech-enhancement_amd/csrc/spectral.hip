@@ -45,6 +45,11 @@ __device__ __forceinline__ float2 conjf2(float2 a) { return make_float2(a.x, -a.
 // passes) for 2048.  A 256-lane block holds FPB = 256/LPF frames per
 // iteration and walks `iters` consecutive frame groups (window and twiddles
 // stay in registers across them).
+// LDS padding of a frame's complex slots: one pad slot per 2^SEL_PSH
+#ifndef SEL_PSH
+#define SEL_PSH 4
+#endif
+
 template <int LOGN>
 struct Geo {
   static constexpr int N = 1 << LOGN;
@@ -57,7 +62,8 @@ struct Geo {
   static constexpr int R0 = fft_radix(LOGN, 0), R1 = fft_radix(LOGN, 1), R2 = fft_radix(LOGN, 2),
                        R3 = fft_radix(LOGN, 3);
   static constexpr int NS1 = R0, NS2 = R0 * R1, NS3 = R0 * R1 * R2;
-  static constexpr int PADN = M + M / 8;  // padded complex slots per frame (pidx)
+  // complex slots per frame: M padded by pidx, + a spare slot (G_M in c2r_grad)
+  static constexpr int PADN = M + (M >> SEL_PSH) + 2;
   static_assert(R0 * R1 * R2 * R3 == M && PPL == 8 && LPF <= 256, "wave FFT schedule");
 };
 
@@ -74,7 +80,13 @@ __device__ __forceinline__ int64_t reflect_index(int64_t j, int64_t T) {
 
 // one pad slot per 8 complex values: the radix-8/16 Stockham stores (a lane's 8
 // or 16 outputs contiguous, lanes 64-128 B apart) spread over all 64 banks
-__device__ __forceinline__ int pidx(int i) { return i + (i >> 3); }
+__device__ __forceinline__ int pidx(int i) { return i + (i >> SEL_PSH); }
+// pidx(i + c) = pidx(i) + padc(c) whenever c is a multiple of 2^SEL_PSH
+__host__ __device__ constexpr int padc(int c) { return c + (c >> SEL_PSH); }
+// pidx(l + c) from pl = pidx(l): linear (an immediate offset) when the unrolled c allows it
+__device__ __forceinline__ int padd(int pl, int l, int c) {
+  return (c & ((1 << SEL_PSH) - 1)) == 0 ? pl + padc(c) : pidx(l + c);
+}
 
 // orders this lane's LDS accesses around cross-lane exchanges inside the wave
 // (DS instructions of one wave execute in order; this stops the compiler from
@@ -171,6 +183,10 @@ __device__ __forceinline__ void dft(float2 (&a)[R]) {
 // other butterflies / bins differ by a lane-uniform factor read from the same
 // tables (scalar loads): W^{r*(l + LPF*u mod NS)} = W^{r*l} * W^{r*(LPF*u mod NS)},
 // W_N^{l + LPF*q} = W_N^l * W_N^{LPF*q}.
+#ifndef SEL_SPLIT_TW_RES
+#define SEL_SPLIT_TW_RES 1
+#endif
+
 template <int LOGN>
 struct LaneTw {
   using G = Geo<LOGN>;
@@ -179,6 +195,10 @@ struct LaneTw {
   // use so the compiler cannot hoist them into registers it does not have
   static constexpr bool RES = G::PPL == 8;
   float2 p1[RES ? G::R1 - 1 : 1], p2[RES ? G::R2 - 1 : 1], p3[G::R3 > 1 ? G::R3 - 1 : 1], n;
+  // W_N^{l + LPF*q} exactly rounded from the table, where a frame fits one wave
+  // (at n_fft 2048 the 16 extra VGPRs cost a wave of occupancy: factorised)
+  static constexpr bool NQ = SEL_SPLIT_TW_RES && G::LPF <= 64;
+  float2 nq[NQ ? G::PPL : 1];
   const float2* g1;
   const float2* g2;
   __device__ __forceinline__ void load(int l) {
@@ -195,6 +215,10 @@ struct LaneTw {
       for (int r = 1; r < G::R3; ++r) p3[r - 1] = g_tw[twp_off(LOGN, 3) + (l & (G::NS3 - 1)) * (G::R3 - 1) + r - 1];
     }
     n = g_tw[tw_off(LOGN) + G::M + l];
+    if constexpr (NQ) {
+#pragma unroll
+      for (int q = 0; q < G::PPL; ++q) nq[q] = g_tw[tw_off(LOGN) + G::M + l + G::LPF * q];
+    }
   }
   __device__ __forceinline__ const float2* t1() const {
     if constexpr (RES) return p1;
@@ -214,7 +238,8 @@ struct LaneTw {
 template <int LOGN>
 __device__ __forceinline__ float2 split_tw(const LaneTw<LOGN>& tw, int q) {
   using G = Geo<LOGN>;
-  return q == 0 ? tw.n : cmul(tw.n, g_tw[tw_off(LOGN) + G::M + G::LPF * q]);
+  if constexpr (LaneTw<LOGN>::NQ) return tw.nq[q];
+  else return q == 0 ? tw.n : cmul(tw.n, g_tw[tw_off(LOGN) + G::M + G::LPF * q]);
 }
 
 // One Stockham pass (radix R, stride NS) from registers to the frame's LDS
@@ -241,12 +266,12 @@ __device__ __forceinline__ void fft_pass_store(float2 (&v)[Geo<LOGN>::PPL], floa
       }
     }
     dft<R>(a);
-    // padded destination: pidx(base + r*NS) = pidx(base) + r*NS*9/8 when 8 | NS;
-    // for NS == 1 (R >= 8) base = j*R is a multiple of 8
+    // padded destination pidx(base + r*NS): linear in r when 2^PSH | NS; for
+    // NS == 1, base = 8j and the r < 8 outputs stay inside one 8-slot run
     const int base = (j - k) * R + k;
     const int pb = pidx(base);
 #pragma unroll
-    for (int r = 0; r < R; ++r) z[NS >= 8 ? pb + r * NS * 9 / 8 : pb + r + (r >> 3)] = a[r];
+    for (int r = 0; r < R; ++r) z[NS == 1 ? pb + r : padd(pb, base, r * NS)] = a[r];
   }
 }
 
@@ -254,11 +279,11 @@ template <int LOGN, int R>
 __device__ __forceinline__ void fft_pass_load(float2 (&v)[Geo<LOGN>::PPL], const float2* z, int l) {
   using G = Geo<LOGN>;
   constexpr int NB = G::PPL / R;
-  const int pl = pidx(l);  // LPF*u + r*M/R is a multiple of 8 -> linear offsets
+  const int pl = pidx(l);
 #pragma unroll
   for (int u = 0; u < NB; ++u)
 #pragma unroll
-    for (int r = 0; r < R; ++r) v[u + r * NB] = z[pl + (G::LPF * u + r * (G::M / R)) * 9 / 8];
+    for (int r = 0; r < R; ++r) v[u + r * NB] = z[padd(pl, l, G::LPF * u + r * (G::M / R))];
 }
 
 // Half-size complex FFT of the frame whose points m = l + LPF*q sit in v[q]
@@ -368,13 +393,14 @@ __device__ __forceinline__ void real_split(const float2* z, int l, const LaneTw<
                                            float2& XM) {
   using G = Geo<LOGN>;
   constexpr int M = G::M;
-  // linear LDS addressing off two per-lane bases: pidx(l + c) = pidx(l) + 9c/8 and
-  // pidx(M - l - c) = pidx(-l) + 9(M - c)/8 for c a multiple of 8 (bin 0 pairs with itself)
-  const int pl = pidx(l), pn = -l + ((-l) >> 3);
+  // LDS addressing off two per-lane bases: pidx(l + c) = pidx(l) + padc(c) and
+  // pidx(M - l - c) = pidx(-l) + padc(M - c) (bin 0 pairs with itself)
+  const int pl = pidx(l), pn = pidx(-l);
 #pragma unroll
   for (int q = 0; q < G::PPL; ++q) {
-    const int im = q == 0 ? (l == 0 ? 0 : pn + G::PADN) : pn + (M - G::LPF * q) * 9 / 8;
-    const float2 zk = z[pl + G::LPF * q * 9 / 8], zm = z[im];
+    const int c = M - G::LPF * q;
+    const int im = q == 0 ? (l == 0 ? 0 : padd(pn, -l, M)) : padd(pn, -l, c);
+    const float2 zk = z[padd(pl, l, G::LPF * q)], zm = z[im];
     const float2 e = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y));
     const float2 o = make_float2(0.5f * (zk.y + zm.y), -0.5f * (zk.x - zm.x));
     X[q] = cadd(e, cmul(split_tw<LOGN>(tw, q), o));  // k = 0: e + o = (z0.x + z0.y, 0)
@@ -393,15 +419,15 @@ __device__ __forceinline__ void c2r_grad(float2 (&Gq)[Geo<LOGN>::PPL], float2 GM
   constexpr int M = G::M;
   const int pl = pidx(l);
 #pragma unroll
-  for (int q = 0; q < G::PPL; ++q) z[pl + G::LPF * q * 9 / 8] = Gq[q];
-  if (l == 0) z[G::PADN - 1] = GM;  // a pad slot (pidx never maps there)
+  for (int q = 0; q < G::PPL; ++q) z[padd(pl, l, G::LPF * q)] = Gq[q];
+  if (l == 0) z[G::PADN - 1] = GM;  // the spare slot (pidx never maps there)
   frame_fence<LOGN>();
-  const int pn = -l + ((-l) >> 3);
+  const int pn = pidx(-l);
 #pragma unroll
   for (int q = 0; q < G::PPL; ++q) {
     const int k = l + G::LPF * q;
-    // G_{M-k}; bin 0 pairs with G_M in slot PADN - 1
-    const int im = q == 0 ? (l == 0 ? G::PADN - 1 : pn + G::PADN) : pn + (M - G::LPF * q) * 9 / 8;
+    // G_{M-k}; bin 0 pairs with G_M in the spare slot PADN - 1
+    const int im = q == 0 ? (l == 0 ? G::PADN - 1 : padd(pn, -l, M)) : padd(pn, -l, M - G::LPF * q);
     const float2 gk = Gq[q], gm = z[im];
     float2 zp;
     if (k == 0) {
@@ -418,7 +444,7 @@ __device__ __forceinline__ void c2r_grad(float2 (&Gq)[Geo<LOGN>::PPL], float2 GM
   fft_half<LOGN>(out, z, l, tw);
 #pragma unroll
   for (int q = 0; q < G::PPL; ++q) {
-    const float2 r = z[pl + G::LPF * q * 9 / 8];
+    const float2 r = z[padd(pl, l, G::LPF * q)];
     out[q] = make_float2(r.x, -r.y);
   }
   frame_fence<LOGN>();
@@ -516,7 +542,10 @@ struct FramePos {
     (void)b;
 
 // one-frame-ahead prefetch only where the registers allow it (PPL = 8, one signal)
-#define SEL_PF (G::PPL == 8)
+#ifndef SEL_FFT_PF
+#define SEL_FFT_PF 1
+#endif
+#define SEL_PF (SEL_FFT_PF && G::PPL == 8)
 
 #define FRAME_LOOP_END }
 

@@ -70,6 +70,28 @@ def main():
                   f"{2 * 4 * B * T / s2 / 1e9:.0f} | - | {2 * flops / s2 / 1e9:.0f} |", flush=True)
         except Exception as e:  # noqa: BLE001
             print(f"| stft_loss_fwd | {n}/{h}/{w} | n/a ({str(e)[:60]}) |")
+        # magnitude backward (the kernel alone: slab + overlap-add) given dL/d|X|
+        gm = torch.randn(B, F, K, device=dev)
+        gx = torch.empty_like(x)
+        ws = torch.empty(lib_ws(B, T, n, h, w), dtype=torch.uint8, device=dev)
+        s3 = timed(lambda: L.call("sel_stft_mag_bwd", L.ptr(x), B, T, n, h, w, L.ptr(win), 1e-7, L.ptr(gm),
+                                  L.ptr(gx), L.ptr(ws), ws.numel(), L.stream()))
+        print(f"| stft_mag_bwd | {n}/{h}/{w} | {s3 * 1e6:.1f} | - | - | - | {flops / s3 / 1e9:.0f} |", flush=True)
+    # the C3 mel loss: 45 * L1(logmel(y_hat), logmel(y)), 2048/300/2048, fwd + bwd at B=64
+    from losses import MultiMelSpectrogramLoss
+    ml = MultiMelSpectrogramLoss(fs=24000, fft_sizes=[2048], hop_sizes=[300], win_lengths=[None],
+                                 num_mels=80, fmin=0, fmax=12000, log_base=None).to(dev)
+    yh = (0.1 * torch.randn(64, 1, T, device=dev)).requires_grad_(True)
+    yc = 0.1 * torch.randn(64, 1, T, device=dev)
+
+    def mel_step():
+        ml(yh, yc).backward()
+    s4 = timed(mel_step)
+    print(f"| mel loss fwd+bwd (B=64) | 2048/300/2048 | {s4 * 1e6:.1f} | - | - | - | - |", flush=True)
+
+
+def lib_ws(B, T, n, h, w):
+    return int(L.lib().sel_stft_bwd_workspace(B, T, n, h, w))
 
 
 if __name__ == "__main__":
