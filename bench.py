@@ -208,7 +208,7 @@ def pmc_traffic(tag, B, steps_cfg="c3"):
     frag = _mangled_fragment(tag)
     with open(PMC_FILE) as f:
         table = json.load(f)
-    hits = [v for k, v in table.items() if frag in k]
+    hits = [v for k, v in table.items() if frag in k or k.split("(")[0].endswith(tag)]
     if len(hits) != 1:
         return None
     return hits[0]["traffic_bytes_per_launch"]
@@ -243,6 +243,43 @@ def roofline(cfg, timer, dom, B, steps):
               "share_of_timed_conv_ms": round(ms / sum(v[1] for v in summ.values()), 3),
               "traffic": pmc_traffic(tag, B, cfg), "traffic_unit": "bytes/launch (rocprofv3 PMC, profiles/)"})
     return r
+
+
+def stft_kernel_roofline(dev):
+    """North-star STFT target: the |X| kernel (sel_stft_mag_fwd, the a1 row) at
+    SURVEY §8d's HBM-measurement size (B = 512 x 1 s, beyond the 256 MB Infinity
+    Cache), 1024/120/600, timed with HIP events on its launch stream, against
+    the 8 TB/s spec and against this box's measured copy bandwidth."""
+    from sel import _lib as L
+    B, T, (n, h, w) = 512, SR, STFT_RES[0]
+    F, K = 1 + T // h, n // 2 + 1
+    x = 0.1 * torch.randn(B, T, device=dev)
+    win = torch.hann_window(w, device=dev)
+    mag = torch.empty(B, F, K, device=dev)
+    src = torch.empty(2 ** 28, device=dev)
+    dst = torch.empty_like(src)
+
+    def timed(fn, iters=10):
+        for _ in range(2):
+            fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(iters):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / iters * 1e-3
+
+    t_copy = timed(lambda: dst.copy_(src))
+    copy_gbs = 2 * src.numel() * 4 / t_copy / 1e9
+    t = timed(lambda: L.call("sel_stft_mag_fwd", L.ptr(x), B, T, n, h, w, L.ptr(win), 1e-7, L.ptr(mag),
+                             L.stream()))
+    nbytes = 4 * B * (T + F * K)
+    gbs = nbytes / t / 1e9
+    return {"kernel": "k_stft_mag_fwd<10>", "shape": f"B={B} x {T}, n_fft/hop/win {n}/{h}/{w}",
+            "avg_launch_us": round(t * 1e6, 1), "alg_bytes": nbytes, "achieved": round(gbs, 1), "unit": "GB/s",
+            "frac_of_spec": round(gbs / HBM_PEAK_GBS, 4), "measured_copy_GBs": round(copy_gbs, 1),
+            "frac_of_measured": round(gbs / copy_gbs, 4)}
 
 
 def main():
@@ -307,6 +344,7 @@ def main():
     frames = world * B * SR / HOP * args.steps
     value = frames / elapsed
     roof = roofline(cfg, timer, dom, B, args.steps)
+    stft_roof = stft_kernel_roofline(dev) if world == 1 else None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         ncores = len(os.sched_getaffinity(0))
@@ -323,7 +361,7 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": dtype, "data": "synthetic",
             "config": {"workload": workload, "global_batch": world * B, "seq_len": SR,
                        "parallelism": f"dp{world}"},
-            "roofline": roof, "cpu_baseline": cpu,
+            "roofline": roof, "cpu_baseline": cpu, "stft_kernel": stft_roof,
         }
         print(json.dumps(out), flush=True)
     if world > 1:
