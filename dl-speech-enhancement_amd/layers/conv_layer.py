@@ -126,6 +126,26 @@ class CausalConv1d(NonCausalConv1d):
     def forward(self, x):
         return _run_layer(x, self.conv.weight, self.conv.bias, CO.PACK_FWD, self.stride, self.dilation)
 
+    @torch.no_grad()
+    def inference(self, x):
+        """Streaming step (conv_layer.py:144-147): conv over cat(pad_buffer, x),
+        keeping the last pad_length input samples.  Runs the causal forward kernel
+        on a shifted input: with its own (K-1)d zero pad in front,
+        forward(cat(0^j, buffer, x))[..., m:] equals the valid conv of
+        cat(buffer, x), where j = 0 and m = pad_length / stride for stride 1, and
+        j = 1, m = 2 for the kernel-2s stride-s downsampling convs."""
+        if self.pad_length == 0:
+            raise NotImplementedError("sel: streaming a kernel-1 CausalConv1d (reference keeps the whole input)")
+        xb = torch.cat((self.pad_buffer.to(x.dtype).expand(x.shape[0], -1, -1), x), -1)
+        self.pad_buffer = xb[:, :, -self.pad_length:].contiguous()
+        s = self.stride
+        if s == 1:
+            return self.forward(xb)[:, :, self.pad_length:]
+        if self.pad_length != 2 * s - 1:
+            raise NotImplementedError("sel: streaming strided CausalConv1d is lowered for kernel_size == 2*stride")
+        xz = torch.cat((xb.new_zeros(xb.shape[0], xb.shape[1], 1), xb), -1)
+        return self.forward(xz)[:, :, 2:]
+
     def reset_buffer(self):
         self.pad_buffer.zero_()
 
@@ -148,6 +168,16 @@ class CausalConvTranspose1d(NonCausalConvTranspose1d):
 
     def forward(self, x):
         return _run_layer(x, self.deconv.weight, self.deconv.bias, CO.PACK_CONVT, self.stride, 1)
+
+    @torch.no_grad()
+    def inference(self, x):
+        """Streaming step (conv_layer.py:185-188): deconv(cat(pad_buffer, x))[s:-s].
+        The forward kernel replicates its input's first sample in front, so
+        forward(cat(buffer, x))[..., s:] is exactly that (the duplicated leading
+        sample only reaches the s outputs that are dropped)."""
+        xb = torch.cat((self.pad_buffer.to(x.dtype).expand(x.shape[0], -1, -1), x), -1)
+        self.pad_buffer = xb[:, :, -self.pad_length:].contiguous()
+        return self.forward(xb)[:, :, self.stride:]
 
     def reset_buffer(self):
         self.pad_buffer.zero_()

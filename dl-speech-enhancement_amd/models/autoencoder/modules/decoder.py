@@ -8,6 +8,12 @@ _KINDS = {"causal": (CausalResidualUnit, CausalConvTranspose1d, CausalConv1d),
           "noncausal": (NonCausalResidualUnit, NonCausalConvTranspose1d, NonCausalConv1d)}
 
 
+def _check_causal(mode, name):
+    """models/utils.py check_mode: streaming methods exist for the causal mode only."""
+    if mode != "causal":
+        raise NotImplementedError(f"{name} is not supported in {mode} mode (causal only)")
+
+
 def _kinds(mode):
     if mode not in _KINDS:
         raise NotImplementedError(f"Mode ({mode}) is not supported!")
@@ -30,6 +36,13 @@ class DecoderBlock(torch.nn.Module):
         x = self.conv(x)
         for ru in self.res_units:
             x = ru(x)
+        return x
+
+    def inference(self, x):
+        _check_causal(self.mode, "inference")
+        x = self.conv.inference(x)
+        for ru in self.res_units:
+            x = ru.inference(x)
         return x
 
 
@@ -58,3 +71,11 @@ class Decoder(torch.nn.Module):
         for blk in self.conv_blocks:
             x = blk(x)
         return self.conv2(x)
+
+    def decode(self, z):
+        """Streaming decoder step (decoder.py:123-128)."""
+        _check_causal(self.mode, "decode")
+        x = z if self.skip_conv1 else self.conv1.inference(z)
+        for blk in self.conv_blocks:
+            x = blk.inference(x)
+        return self.conv2.inference(x)

@@ -7,6 +7,12 @@ from models.autoencoder.modules.residual_unit import CausalResidualUnit, NonCaus
 _KINDS = {"causal": (CausalResidualUnit, CausalConv1d), "noncausal": (NonCausalResidualUnit, NonCausalConv1d)}
 
 
+def _check_causal(mode, name):
+    """models/utils.py check_mode: streaming methods exist for the causal mode only."""
+    if mode != "causal":
+        raise NotImplementedError(f"{name} is not supported in {mode} mode (causal only)")
+
+
 def _kinds(mode):
     if mode not in _KINDS:
         raise NotImplementedError(f"Mode ({mode}) is not supported!")
@@ -29,6 +35,12 @@ class EncoderBlock(torch.nn.Module):
         for ru in self.res_units:
             x = ru(x)
         return self.conv(x)
+
+    def inference(self, x):
+        _check_causal(self.mode, "inference")
+        for ru in self.res_units:
+            x = ru.inference(x)
+        return self.conv.inference(x)
 
 
 class Encoder(torch.nn.Module):
@@ -53,4 +65,12 @@ class Encoder(torch.nn.Module):
         x = self.conv(x)
         for blk in self.conv_blocks:
             x = blk(x)
+        return x
+
+    def encode(self, x):
+        """Streaming encoder step (encoder.py:118-123)."""
+        _check_causal(self.mode, "encode")
+        x = self.conv.inference(x)
+        for blk in self.conv_blocks:
+            x = blk.inference(x)
         return x

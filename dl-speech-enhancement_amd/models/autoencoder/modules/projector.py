@@ -18,3 +18,9 @@ class Projector(torch.nn.Module):
 
     def forward(self, x):
         return self.project(x)
+
+    def encode(self, x):
+        """Streaming step (projector.py:52-54)."""
+        if self.mode != "causal":
+            raise NotImplementedError(f"encode is not supported in {self.mode} mode (causal only)")
+        return self.project.inference(x)

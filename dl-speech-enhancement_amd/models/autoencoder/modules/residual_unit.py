@@ -4,6 +4,7 @@ forward = x + conv2(ELU(conv1(ELU(x)))) (reference :43-46), executed as one
 fused autograd op (sel.convops.ResidualUnitFn): ELU is applied while the conv
 input tile is staged, the residual add in the 1x1 conv's epilogue.
 """
+import torch
 import torch.nn as nn
 
 from layers.conv_layer import CausalConv1d, Conv1d1x1, NonCausalConv1d
@@ -43,3 +44,9 @@ class CausalResidualUnit(NonCausalResidualUnit):
         c1, c2 = self.conv1.conv, self.conv2
         y = CO.ResidualUnitFn.apply(xc, c1.weight, c1.bias, c2.weight, c2.bias, c1.dilation[0])
         return y.transpose(1, 2)
+
+    @torch.no_grad()
+    def inference(self, x):
+        """Streaming step (residual_unit.py:78-81): conv1 carries its pad_buffer."""
+        y = self.conv1.inference(self.activation(x))
+        return x + self.conv2(self.activation(y))

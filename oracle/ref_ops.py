@@ -271,6 +271,81 @@ def generator_forward(P, x, geo, pqc=True, codebook_num=8):
 
 
 # --------------------------------------------------------------------------
+# streaming  (layers/conv_layer.py:144-191, models/autoencoder/AudioDec.py:106-191)
+# --------------------------------------------------------------------------
+
+def stream_causal_conv1d(S, key, x, w, b=None, stride=1, dilation=1):
+    """conv_layer.py:144-147 — conv over cat(pad_buffer, x); keep the last (k-1)d."""
+    pad = (w.shape[-1] - 1) * dilation
+    buf = S.get(key, torch.zeros(x.shape[0], x.shape[1], pad, dtype=x.dtype))
+    xb = torch.cat([buf, x], -1)
+    S[key] = xb[:, :, -pad:]
+    return F.conv1d(xb, w, b, stride=stride, dilation=dilation)
+
+
+def stream_conv_transpose1d(S, key, x, w, b=None, stride=1):
+    """conv_layer.py:185-188 — deconv(cat(pad_buffer, x))[s:-s]; keep the last sample."""
+    buf = S.get(key, torch.zeros(x.shape[0], x.shape[1], 1, dtype=x.dtype))
+    xb = torch.cat([buf, x], -1)
+    S[key] = xb[:, :, -1:]
+    return F.conv_transpose1d(xb, w, b, stride=stride)[:, :, stride:-stride]
+
+
+def stream_residual_unit(S, key, x, w1, w2, dilation):
+    """residual_unit.py:78-81 — conv1 streams, the 1x1 conv2 does not."""
+    y = stream_causal_conv1d(S, key, elu(x), w1, None, 1, dilation)
+    return x + F.conv1d(elu(y), w2)
+
+
+def stream_encode(P, S, x, geo, dilations=(1, 3, 9), project=True):
+    """AudioDec.py:160-166 -> encoder.py:118-123, projector.py:52-54 (without_PQC
+    AudioDec.py:160-166: encoder only, project=False)."""
+    enc, _ = geo
+    h = stream_causal_conv1d(S, "encoder.conv", x, P["encoder.conv.conv.weight"])
+    for i, (ci, co, s) in enumerate(enc):
+        pre = f"encoder.conv_blocks.{i}"
+        for j, d in enumerate(dilations):
+            ru = f"{pre}.res_units.{j}"
+            h = stream_residual_unit(S, f"{ru}.conv1", h, P[f"{ru}.conv1.conv.weight"], P[f"{ru}.conv2.weight"], d)
+        h = stream_causal_conv1d(S, f"{pre}.conv", h, P[f"{pre}.conv.conv.weight"], P.get(f"{pre}.conv.conv.bias"),
+                                 stride=s)
+    if not project:
+        return h
+    return stream_causal_conv1d(S, "projector.project", h, P["projector.project.conv.weight"])
+
+
+def stream_quantize(z, embeds):
+    """quantizer.py:42-44 -> vq_module.py:136-149 with flatten_idx: stage i's index + K*i."""
+    _, _, _, inds = rvq_forward(z.transpose(2, 1), embeds)
+    K = embeds[0].shape[1]
+    inds = inds + K * torch.arange(len(embeds)).view(-1, *([1] * (inds.dim() - 1)))
+    return inds.squeeze(1)
+
+
+def stream_lookup(idx, embeds):
+    """vq_module.py:151-162: sum over stages of the flattened codebook rows."""
+    book = torch.cat([e.transpose(0, 1) for e in embeds], 0)
+    return F.embedding(idx, book).sum(0, keepdim=True)
+
+
+def stream_decode(P, S, zq, geo, dilations=(1, 3, 9), pqc=True):
+    """AudioDec.py:178-179 -> decoder.py:123-128 on zq (B, L, D); without_PQC
+    decoder.py:125-132 skips conv1."""
+    _, dec = geo
+    h = zq.transpose(2, 1)
+    if pqc:
+        h = stream_causal_conv1d(S, "decoder.conv1", h, P["decoder.conv1.conv.weight"])
+    for i, (ci, co, s) in enumerate(dec):
+        pre = f"decoder.conv_blocks.{i}"
+        h = stream_conv_transpose1d(S, f"{pre}.conv", h, P[f"{pre}.conv.deconv.weight"],
+                                    P.get(f"{pre}.conv.deconv.bias"), s)
+        for j, d in enumerate(dilations):
+            ru = f"{pre}.res_units.{j}"
+            h = stream_residual_unit(S, f"{ru}.conv1", h, P[f"{ru}.conv1.conv.weight"], P[f"{ru}.conv2.weight"], d)
+    return stream_causal_conv1d(S, "decoder.conv2", h, P["decoder.conv2.conv.weight"])
+
+
+# --------------------------------------------------------------------------
 # step glue  (dataloader/data_utils.py, train_denoise.py, trainerGAN.py)
 # --------------------------------------------------------------------------
 

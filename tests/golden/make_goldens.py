@@ -87,7 +87,32 @@ def _grads(module, prefix="g."):
     return {prefix + k: _np(p.grad) for k, p in module.named_parameters() if p.grad is not None}
 
 
-def make(ref, out):
+def make_stream(pqc_mod, clean, noise, gp, out):
+    """StreamGenerator at reduced width: initial_encoder/decoder on zeros, then six
+    600-sample chunks (2 latent frames each) through encode -> quantize -> lookup ->
+    decode, recording every intermediate and the final pad_buffers."""
+    torch.manual_seed(93)
+    G = pqc_mod.StreamGenerator(**gp)
+    G.eval()
+    d = _sd(G)
+    x = torch.from_numpy(clean[0][:3600] + 0.1 * noise[0][:3600]).float().view(1, 1, -1)
+    d["x"] = _np(x)
+    with torch.no_grad():
+        zq0 = G.initial_encoder(600, "cpu")
+        G.initial_decoder(zq0)
+        d["init.zq"] = _np(zq0)
+        for c in range(6):
+            xc = x[:, :, 600 * c:600 * (c + 1)]
+            z = G.encode(xc)
+            idx = G.quantize(z)
+            zq = G.lookup(idx)
+            y = G.decode(zq)
+            d.update({f"z.{c}": _np(z), f"idx.{c}": _np(idx), f"zq.{c}": _np(zq), f"y.{c}": _np(y)})
+    d.update({"buf." + k: _np(v) for k, v in G.state_dict().items() if k.endswith("pad_buffer")})
+    np.savez_compressed(os.path.join(out, "stream.npz"), **d)
+
+
+def make(ref, out, only=None):
     du = _install_stubs(ref)
     stft_mod = _load("ref_stft_loss", os.path.join(ref, "losses", "stft_loss.py"))
     mel_mod = _load("ref_mel_loss", os.path.join(ref, "losses", "mel_loss.py"))
@@ -98,6 +123,9 @@ def make(ref, out):
 
     clean, noise = _audio(ref)
     os.makedirs(out, exist_ok=True)
+    if only == "stream":
+        gp = dict(encode_channels=4, decode_channels=4, code_dim=64, codebook_num=2, codebook_size=64)
+        return make_stream(pqc_mod, clean, noise, gp, out)
     torch.manual_seed(93)
 
     # ---------------- melmat (losses/mel_loss.py:54-61) ----------------
@@ -309,6 +337,9 @@ def make(ref, out):
         d.update(_sd(G, f"sd{step + 1}."))
     np.savez_compressed(os.path.join(out, "train_step.npz"), **d)
 
+    # ---------------- streaming (AudioDec.py:106-191, conv_layer.py:144-191) ----------------
+    make_stream(pqc_mod, clean, noise, gp, out)
+
     # ---------------- add_noise (dataloader/data_utils.py:12-22) ----------------
     cl = torch.from_numpy(np.stack([clean[0][:4800], clean[1][:4800]])).unsqueeze(1)
     nz = torch.from_numpy(np.stack([noise[0][:4800], noise[1][:4800]])).unsqueeze(1)
@@ -322,8 +353,9 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
     ap.add_argument("--out", default=HERE)
+    ap.add_argument("--only", default=None, help="regenerate one fixture family (stream)")
     a = ap.parse_args()
-    make(a.ref, a.out)
+    make(a.ref, a.out, a.only)
     for f in sorted(os.listdir(a.out)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(a.out, f)))

@@ -182,3 +182,30 @@ def test_train_step():
         close(tn, g[f"gradnorm.{s}"], rtol=1e-4)
         for k in train:
             close(P[k], g[f"sd{s + 1}.{k}"], rtol=1e-5, atol=1e-7)
+
+
+def test_stream_generator():
+    """StreamGenerator (AudioDec.py:106-191): initial encode/decode on zeros, then
+    six 600-sample chunks through encode -> quantize -> lookup -> decode, each
+    conv carrying its pad_buffer (conv_layer.py:144-191)."""
+    g = golden("stream")
+    P = {k[3:]: T(v) for k, v in g.items() if k.startswith("sd.")}
+    geo = R.generator_geometry(encode_channels=4, decode_channels=4)
+    embeds = [P[f"quantizer.codebook.layers.{i}.embed"] for i in range(2)]
+    S = {}
+    z0 = R.stream_encode(P, S, torch.zeros(1, 1, 600), geo)
+    zq0 = R.stream_lookup(R.stream_quantize(z0, embeds), embeds)
+    close(zq0, g["init.zq"], rtol=1e-5, atol=1e-6)
+    R.stream_decode(P, S, zq0, geo)
+    x = T(g["x"])
+    for c in range(6):
+        z = R.stream_encode(P, S, x[:, :, 600 * c:600 * (c + 1)], geo)
+        close(z, g[f"z.{c}"], rtol=1e-5, atol=1e-6)
+        idx = R.stream_quantize(z, embeds)
+        np.testing.assert_array_equal(idx.numpy(), g[f"idx.{c}"])
+        zq = R.stream_lookup(idx, embeds)
+        close(zq, g[f"zq.{c}"], rtol=1e-5, atol=1e-6)
+        close(R.stream_decode(P, S, zq, geo), g[f"y.{c}"], rtol=1e-5, atol=1e-6)
+    for k, v in g.items():
+        if k.startswith("buf."):
+            close(S[k[4:-len(".pad_buffer")]], v, rtol=1e-5, atol=1e-6)
