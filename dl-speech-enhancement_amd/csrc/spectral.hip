@@ -409,6 +409,34 @@ __device__ __forceinline__ void real_split(const float2* z, int l, const LaneTw<
   frame_fence<LOGN>();
 }
 
+// |X|^2 for bin pairs (forward-only epilogues): lane l's bins k = l + LPF*q and
+// M - k (q < PPL/2) share zk, zm and one twiddle product, since
+// X_{M-k} = conj(e_k - W^k o_k) while X_k = e_k + W^k o_k; p[q] <- |X_k|^2,
+// p[PPL/2 + q] <- |X_{M-k}|^2 (k = 0 pairs with the Nyquist bin M), and pmid <-
+// |X_{M/2}|^2 = |Z_{M/2}|^2 (valid on l == 0).
+template <int LOGN>
+__device__ __forceinline__ void split_pairs(const float2* z, int l, const LaneTw<LOGN>& tw,
+                                            float (&p)[Geo<LOGN>::PPL], float& pmid) {
+  using G = Geo<LOGN>;
+  constexpr int M = G::M, H = G::PPL / 2;
+  const int pl = pidx(l), pn = pidx(-l);
+#pragma unroll
+  for (int q = 0; q < H; ++q) {
+    const int im = q == 0 ? (l == 0 ? 0 : padd(pn, -l, M)) : padd(pn, -l, M - G::LPF * q);
+    const float2 zk = z[padd(pl, l, G::LPF * q)], zm = z[im];
+    const float ex = zk.x + zm.x, ey = zk.y - zm.y;  // 2 e_k
+    const float ox = zk.y + zm.y, oy = zm.x - zk.x;  // 2 o_k
+    const float2 w = split_tw<LOGN>(tw, q);
+    const float wox = w.x * ox - w.y * oy, woy = w.x * oy + w.y * ox;
+    const float ax = ex + wox, ay = ey + woy, bx = ex - wox, by = ey - woy;
+    p[q] = 0.25f * (ax * ax + ay * ay);
+    p[H + q] = 0.25f * (bx * bx + by * by);
+  }
+  const float2 zc = z[pidx(M / 2)];
+  pmid = zc.x * zc.x + zc.y * zc.y;
+  frame_fence<LOGN>();
+}
+
 // Gradient through real_split + FFT: given G_k for this lane's bins (Gq[q],
 // k = l + LPF*q) and G_M (GM, on l == 0), r_n = Re sum_{k=0}^{M} G_k exp(+2 pi i k n / N)
 // for this lane's points: out[q] = (r[2m], r[2m+1]), m = l + LPF*q.
@@ -557,14 +585,17 @@ __global__ __launch_bounds__(256) SEL_FFT_OCC void k_stft_mag_fwd(const float* _
   FRAME_LOOP_BEGIN(x, raw, SEL_PF)
   (void)f;
   fft_half<LOGN>(v, z, l, tw);
-  float2 X[G::PPL], XM;
-  real_split<LOGN>(z, l, tw, X, XM);
+  float pwr[G::PPL], pmid;
+  split_pairs<LOGN>(z, l, tw, pwr, pmid);
   if (active) {
-    constexpr int K = G::M + 1;
-    float* out = mag + fr * K + l;
+    constexpr int K = G::M + 1, H = G::PPL / 2;
+    float* out = mag + fr * K;
 #pragma unroll
-    for (int q = 0; q < G::PPL; ++q) out[G::LPF * q] = clamp_sqrt(pw(X[q]), floor_);
-    if (l == 0) out[G::M] = clamp_sqrt(pw(XM), floor_);
+    for (int q = 0; q < H; ++q) {
+      out[l + G::LPF * q] = clamp_sqrt(pwr[q], floor_);
+      out[G::M - l - G::LPF * q] = clamp_sqrt(pwr[H + q], floor_);
+    }
+    if (l == 0) out[G::M / 2] = clamp_sqrt(pmid, floor_);
   }
   FRAME_LOOP_END
 }
@@ -600,16 +631,24 @@ __global__ __launch_bounds__(256) SEL_FFT_OCC void k_stft_mag_bwd(const float* _
 
 // |Y| of the reference signal's frame (windowed points in v) into ym[]
 // (PPL bins + bin M on l == 0)
-template <int LOGN>
+template <int LOGN, bool PAIRED>
 __device__ __forceinline__ void ref_mag(float2 (&v)[Geo<LOGN>::PPL], int l, float2* z, const LaneTw<LOGN>& tw,
                                         float floor_, float (&ym)[Geo<LOGN>::PPL + 1]) {
   using G = Geo<LOGN>;
   fft_half<LOGN>(v, z, l, tw);
-  float2 X[G::PPL], XM;
-  real_split<LOGN>(z, l, tw, X, XM);
+  if constexpr (PAIRED) {  // split_pairs' bins (the fused forward)
+    float pwr[G::PPL], pmid;
+    split_pairs<LOGN>(z, l, tw, pwr, pmid);
 #pragma unroll
-  for (int q = 0; q < G::PPL; ++q) ym[q] = clamp_sqrt(pw(X[q]), floor_);
-  ym[G::PPL] = clamp_sqrt(pw(XM), floor_);
+    for (int q = 0; q < G::PPL; ++q) ym[q] = clamp_sqrt(pwr[q], floor_);
+    ym[G::PPL] = clamp_sqrt(pmid, floor_);
+  } else {  // real_split's bins k = l + LPF*q, then M (the backward)
+    float2 X[G::PPL], XM;
+    real_split<LOGN>(z, l, tw, X, XM);
+#pragma unroll
+    for (int q = 0; q < G::PPL; ++q) ym[q] = clamp_sqrt(pw(X[q]), floor_);
+    ym[G::PPL] = clamp_sqrt(pw(XM), floor_);
+  }
 }
 
 // the reference signal's windowed frame at the current position (no prefetch)
@@ -636,15 +675,15 @@ __global__ __launch_bounds__(256) SEL_FFT_OCC void k_stft_loss_fwd(const float* 
   (void)fr;
   Y_FRAME(vy)
   float ym[G::PPL + 1];
-  ref_mag<LOGN>(vy, l, z, tw, floor_, ym);
+  ref_mag<LOGN, true>(vy, l, z, tw, floor_, ym);
   fft_half<LOGN>(v, z, l, tw);
-  float2 X[G::PPL], XM;
-  real_split<LOGN>(z, l, tw, X, XM);
+  float pwr[G::PPL], pmid;
+  split_pairs<LOGN>(z, l, tw, pwr, pmid);  // same bin pairing as ref_mag's ym
   if (active) {
 #pragma unroll
     for (int q = 0; q <= G::PPL; ++q) {
       if (q == G::PPL && l != 0) break;
-      const float xm = clamp_sqrt(pw(q < G::PPL ? X[q] : XM), floor_);
+      const float xm = clamp_sqrt(q < G::PPL ? pwr[q] : pmid, floor_);
       const float d = ym[q] - xm;
       s1 += d * d;
       s2 += ym[q] * ym[q];
@@ -674,7 +713,7 @@ __global__ __launch_bounds__(256) SEL_FFT_OCC void k_stft_loss_bwd(const float* 
   (void)f;
   Y_FRAME(vy)
   float ym[G::PPL + 1];
-  ref_mag<LOGN>(vy, l, z, tw, floor_, ym);
+  ref_mag<LOGN, false>(vy, l, z, tw, floor_, ym);
   fft_half<LOGN>(v, z, l, tw);
   float2 X[G::PPL + 1];
   real_split<LOGN>(z, l, tw, reinterpret_cast<float2(&)[G::PPL]>(X), X[G::PPL]);
@@ -719,11 +758,14 @@ __global__ __launch_bounds__(256) SEL_FFT_OCC void k_logmel_fwd(const float* __r
   FRAME_LOOP_BEGIN(x, raw, SEL_PF)
   (void)fr;
   fft_half<LOGN>(v, z, l, tw);
-  float2 X[G::PPL], XM;
-  real_split<LOGN>(z, l, tw, X, XM);
+  float pwr[G::PPL], pmid;
+  split_pairs<LOGN>(z, l, tw, pwr, pmid);
 #pragma unroll
-  for (int q = 0; q < G::PPL; ++q) magb[l + G::LPF * q] = clamp_sqrt(pw(X[q]), ma.eps);
-  if (l == 0) magb[G::M] = clamp_sqrt(pw(XM), ma.eps);
+  for (int q = 0; q < G::PPL / 2; ++q) {
+    magb[l + G::LPF * q] = clamp_sqrt(pwr[q], ma.eps);
+    magb[G::M - l - G::LPF * q] = clamp_sqrt(pwr[G::PPL / 2 + q], ma.eps);
+  }
+  if (l == 0) magb[G::M / 2] = clamp_sqrt(pmid, ma.eps);
   frame_fence<LOGN>();
   if (active) {
     for (int m = l; m < ma.nm; m += G::LPF) {
