@@ -322,7 +322,7 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    timer = _lib.KernelTimer([dom])
+    timer = _lib.KernelTimer([dom] + (["sel_resunit_fwd"] if cfg == "c3" else []))
     _lib.TIMER = timer
     torch.cuda.synchronize()
     if world > 1:

@@ -655,6 +655,201 @@ __global__ __launch_bounds__(256) void k_conv_thin_bf16(Args a, const __bf16* __
 }
 
 // ---------------------------------------------------------------------------
+// Fused residual-unit forward for the thin layers (residual_unit.py:43-46 with
+// conv1 = causal K-tap dilated C->C, conv2 = 1x1 C->C, no bias in AudioDec):
+//   h   = conv1(ELU(x))                       -> HBM (saved for the backward)
+//   out = x + conv2(ELU(h))                   -> HBM
+// One pass over the tile: conv1 as in k_conv_thin_bf16 (weights in VGPRs,
+// ELU at staging), its accumulators -> fp32 tile in LDS -> coalesced h store
+// AND ELU(bf16(h)) staged straight into a second LDS tile that feeds conv2's
+// MFMAs (its weights also in VGPRs); the residual is re-read from L2 in the
+// final coalesced epilogue.  vs. two primitive calls this drops the h re-read
+// and one x re-read from HBM (5 -> 3 activation-sized tensors per unit).
+// ---------------------------------------------------------------------------
+template <int C, int K, int R>
+struct RuThin {
+  using G = Thin<C, C, K, R>;
+  static constexpr size_t LDS_HS = size_t(G::PLANES) * R * F4_P * 2;
+  static constexpr size_t LDS = G::LDS + LDS_HS;
+  static_assert(LDS <= 64 * 1024, "fused residual unit LDS");
+};
+
+template <int C, int K, int R>
+__global__ __launch_bounds__(256) void k_ru_thin_bf16(Args a, const __bf16* __restrict__ in,
+                                                      const __bf16* __restrict__ w1p, const float* __restrict__ b1,
+                                                      const __bf16* __restrict__ w2p, const float* __restrict__ b2,
+                                                      __bf16* __restrict__ hout, __bf16* __restrict__ out,
+                                                      int tiles_per_block) {
+  using G = Thin<C, C, K, R>;
+  constexpr int P = F4_P;
+  constexpr int CV = G::CV;
+  constexpr int N = C;
+  extern __shared__ __align__(16) unsigned char smem[];
+  __bf16* const xs = reinterpret_cast<__bf16*>(smem);                   // [PLANES][SPAN][P]
+  float* const ot = reinterpret_cast<float*>(smem);                     // [R][OP], aliases xs
+  __bf16* const hs = reinterpret_cast<__bf16*>(smem + G::LDS);          // [PLANES][R][P]
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ns = wave % G::NS, rg = wave / G::NS;
+  const int span = R + (K - 1) * a.dil;
+  const int tps = (a.T + R - 1) / R;
+  const int64_t ntiles = (a.rows / a.T) * tps;
+  const int64_t vb = int64_t(blockIdx.x % 8) * (gridDim.x / 8) + blockIdx.x / 8;
+  const int64_t tile0 = vb * tiles_per_block;
+  const int64_t tile_end = tile0 + tiles_per_block < ntiles ? tile0 + tiles_per_block : ntiles;
+  if (tile0 >= tile_end) return;  // block-uniform
+
+  bf16x8 wf[K][C / 16], wf2[C / 16];
+  {
+    const __bf16* wrow = w1p + int64_t(ns * 32 + (lane & 31)) * K * C + 8 * (lane >> 5);
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+#pragma unroll
+      for (int g = 0; g < C / 16; ++g) wf[k][g] = *reinterpret_cast<const bf16x8*>(wrow + k * C + 16 * g);
+    const __bf16* wrow2 = w2p + int64_t(ns * 32 + (lane & 31)) * C + 8 * (lane >> 5);
+#pragma unroll
+    for (int g = 0; g < C / 16; ++g) wf2[g] = *reinterpret_cast<const bf16x8*>(wrow2 + 16 * g);
+  }
+
+  uint4 xr[G::XV];
+  bool xok[G::XV];
+  auto load = [&](int64_t tile) {
+    const int64_t b = tile / tps;
+    const int t0 = int(tile % tps) * R;
+#pragma unroll
+    for (int u = 0; u < G::XV; ++u) {
+      const int v = tid + u * 256;
+      const int r = v / CV, c = (v % CV) * 8;
+      int ti = t0 - a.pad + r;
+      xok[u] = r < span && ti >= 0 && ti < a.T;
+      ti = ti < 0 ? 0 : (ti >= a.T ? a.T - 1 : ti);
+      if ((u * 256) / CV < span) xr[u] = *reinterpret_cast<const uint4*>(in + (b * a.T + ti) * C + c);
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int u = 0; u < G::XV; ++u) {
+      const int v = tid + u * 256;
+      const int r = v / CV, c = (v % CV) * 8;
+      if (r >= span) continue;
+      uint4 val = xok[u] ? xr[u] : make_uint4(0, 0, 0, 0);
+      __bf16* t = reinterpret_cast<__bf16*>(&val);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) t[e] = __bf16(elu_fast(float(t[e])));
+      *reinterpret_cast<uint4*>(xs + ((c >> 5) * G::SPAN + r) * P + (c & 31)) = val;
+    }
+  };
+  // accumulators (out^T: lane -> row, element -> channel) -> fp32 tile in LDS
+  auto acc_to_ot = [&](const floatx16 (&acc)[G::TM]) {
+#pragma unroll
+    for (int i = 0; i < G::TM; ++i) {
+      const int row = rg * G::WR + i * 32 + (lane & 31);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int n = ns * 32 + 8 * g + 4 * (lane >> 5);
+        *reinterpret_cast<floatx4*>(ot + row * G::OP + n) =
+            floatx4{acc[i][4 * g], acc[i][4 * g + 1], acc[i][4 * g + 2], acc[i][4 * g + 3]};
+      }
+    }
+  };
+  constexpr int GN = N / 8;
+
+  load(tile0);
+  for (int64_t tile = tile0; tile < tile_end; ++tile) {
+    __syncthreads();  // the previous tile's epilogue is done with ot (= xs)
+    store();
+    __syncthreads();
+    if (tile + 1 < tile_end) load(tile + 1);
+    const int64_t b = tile / tps;
+    const int t0 = int(tile % tps) * R;
+    const int mrows = a.T - t0 < R ? a.T - t0 : R;
+    const int64_t obase = (b * a.T + t0) * N;
+
+    // conv1
+    floatx16 acc[G::TM];
+#pragma unroll
+    for (int i = 0; i < G::TM; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
+    {
+      const __bf16* xw = xs + (rg * G::WR + (lane & 31)) * P + 8 * (lane >> 5);
+#pragma unroll
+      for (int k = 0; k < K; ++k)
+#pragma unroll
+        for (int g = 0; g < C / 16; ++g) {
+          const __bf16* xb = xw + ((g >> 1) * G::SPAN + k * a.dil) * P + 16 * (g & 1);
+#pragma unroll
+          for (int i = 0; i < G::TM; ++i)
+            acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[k][g], *reinterpret_cast<const bf16x8*>(xb + i * 32 * P),
+                                                             acc[i], 0, 0, 0);
+        }
+    }
+    __syncthreads();  // every wave is done reading xs
+    acc_to_ot(acc);
+    __syncthreads();
+    // h epilogue: + b1, store h (bf16), stage ELU(h) for conv2
+    for (int idx = tid; idx < R * GN; idx += 256) {
+      const int r = idx / GN, n = (idx % GN) * 8;
+      const floatx4 lo = *reinterpret_cast<const floatx4*>(ot + r * G::OP + n);
+      const floatx4 hi = *reinterpret_cast<const floatx4*>(ot + r * G::OP + n + 4);
+      float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      if (b1) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += b1[n + e];
+      }
+      uint4 hv, ev;
+      __bf16* hp = reinterpret_cast<__bf16*>(&hv);
+      __bf16* ep = reinterpret_cast<__bf16*>(&ev);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        hp[e] = __bf16(v[e]);
+        ep[e] = __bf16(elu_fast(float(hp[e])));
+      }
+      if (r < mrows) *reinterpret_cast<uint4*>(hout + obase + int64_t(r) * N + n) = hv;
+      *reinterpret_cast<uint4*>(hs + ((n >> 5) * R + r) * P + (n & 31)) = ev;
+    }
+    __syncthreads();
+    // conv2 (1x1)
+#pragma unroll
+    for (int i = 0; i < G::TM; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
+    {
+      const __bf16* hw = hs + (rg * G::WR + (lane & 31)) * P + 8 * (lane >> 5);
+#pragma unroll
+      for (int g = 0; g < C / 16; ++g) {
+        const __bf16* hb = hw + (g >> 1) * R * P + 16 * (g & 1);
+#pragma unroll
+        for (int i = 0; i < G::TM; ++i)
+          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf2[g], *reinterpret_cast<const bf16x8*>(hb + i * 32 * P),
+                                                           acc[i], 0, 0, 0);
+      }
+    }
+    acc_to_ot(acc);  // ot is free: the h epilogue read it before the last barrier
+    __syncthreads();
+    for (int idx = tid; idx < mrows * GN; idx += 256) {
+      const int r = idx / GN, n = (idx % GN) * 8;
+      const floatx4 lo = *reinterpret_cast<const floatx4*>(ot + r * G::OP + n);
+      const floatx4 hi = *reinterpret_cast<const floatx4*>(ot + r * G::OP + n + 4);
+      float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      if (b2) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += b2[n + e];
+      }
+      const int64_t o = obase + int64_t(r) * N + n;
+      uint4 raw = *reinterpret_cast<const uint4*>(in + o);
+      const __bf16* rv = reinterpret_cast<const __bf16*>(&raw);
+      uint4 ov;
+      __bf16* op = reinterpret_cast<__bf16*>(&ov);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) op[e] = __bf16(v[e] + float(rv[e]));
+      *reinterpret_cast<uint4*>(out + o) = ov;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Single-input-channel layers (the encoder's first conv 1->32 k7, and the dgrad
 // of the decoder's last conv 32->1 k7): an implicit GEMM with a reduction of
 // only K taps would leave MFMA idle and stage a 1-wide tile, so this is a
@@ -1811,6 +2006,30 @@ int dispatch_thin(const Args& a, const void* in, const void* wp, const float* bi
   return kNotThin;
 }
 
+// Fused residual-unit forward instances: (C, K, R) = (32, 7, 128), (64, 7, 64).
+template <int C, int K, int R>
+int launch_ru_thin(const Args& a, const void* in, const void* w1p, const float* b1, const void* w2p,
+                   const float* b2, void* h, void* out, hipStream_t s) {
+  using RU = RuThin<C, K, R>;
+  const int64_t ntiles = (a.rows / a.T) * ((a.T + R - 1) / R);
+  if (ntiles == 0) return SEL_OK;
+  const int64_t target = 1024;
+  const int64_t tpb = std::max<int64_t>(1, (ntiles + target - 1) / target);
+  const unsigned nb = unsigned(((ntiles + tpb - 1) / tpb + 7) / 8 * 8);  // multiple of 8 (XCD map)
+  hipLaunchKernelGGL((k_ru_thin_bf16<C, K, R>), dim3(nb), dim3(256), RU::LDS, s, a,
+                     static_cast<const __bf16*>(in), static_cast<const __bf16*>(w1p), b1,
+                     static_cast<const __bf16*>(w2p), b2, static_cast<__bf16*>(h), static_cast<__bf16*>(out),
+                     int(tpb));
+  SEL_LAUNCH_CHECK();
+  return SEL_OK;
+}
+
+bool ru_fused_ok(const Args& a) {
+  return (a.C == 32 || a.C == 64) && a.N == a.C && a.K == 7 && a.pad == (a.K - 1) * a.dil &&
+         a.pad_mode == SEL_PAD_ZERO && a.in_elu == 1 && (a.K - 1) * a.dil <= F4_HALOMAX &&
+         (a.bias_period == 0 || a.bias_period == a.N);
+}
+
 template <typename TI, typename TO>
 int dispatch_fwd(const Args& a, const void* in, const void* wp, const float* bias, const void* aux,
                  const void* res, void* out, hipStream_t s) {
@@ -1990,6 +2209,21 @@ int sel_conv_fwd(const sel_conv_desc* d, int in_dtype, int out_dtype, const void
     return dispatch_fwd<__bf16, float>(a, in, wpack, bias, aux, res, out, s);
   set_error("unsupported dtype combination in=%d out=%d", in_dtype, out_dtype);
   return SEL_ERR_UNSUPPORTED;
+}
+
+/* Fused residual unit forward (residual_unit.py:43-46): h = conv1(ELU(x)) and
+ * out = x + conv1x1(ELU(h)) in one pass (bf16, C = N in {32, 64}, K = 7, causal
+ * zero pad, ELU prologue; d1 describes conv1, its bias_period 0 or N).  Returns
+ * SEL_ERR_UNSUPPORTED for other shapes (callers then use two sel_conv_fwd calls). */
+int sel_resunit_fwd(const sel_conv_desc* d1, int dtype, const void* x, const void* w1pack, const float* b1,
+                    const void* w2pack, const float* b2, void* h, void* out, sel_stream_t stream) {
+  if (int rc = check_desc(d1)) return rc;
+  const Args a = to_args(d1);
+  SEL_REQUIRE(dtype == SEL_BF16 && ru_fused_ok(a), SEL_ERR_UNSUPPORTED,
+              "sel_resunit_fwd: fused path needs bf16, C = N in {32, 64}, K = 7, causal zero pad, ELU prologue");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (a.C == 32) return launch_ru_thin<32, 7, 128>(a, x, w1pack, b1, w2pack, b2, h, out, s);
+  return launch_ru_thin<64, 7, 64>(a, x, w1pack, b1, w2pack, b2, h, out, s);
 }
 
 size_t sel_conv_wgrad_workspace(const sel_conv_desc* d) {

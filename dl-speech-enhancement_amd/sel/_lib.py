@@ -44,6 +44,7 @@ SIGNATURES = {
                              P, P, P, F32, P, P, SZ, P]),
     "sel_conv_fwd_kernel_id": (I32, [P, I32, I32]),
     "sel_conv_fwd": (I32, [P, I32, I32, P, P, P, P, P, P, P]),
+    "sel_resunit_fwd": (I32, [P, I32, P, P, P, P, P, P, P, P]),
     "sel_conv_wgrad_workspace": (SZ, [P]),
     "sel_conv_wgrad": (I32, [P, I32, P, P, P, P, P, SZ, P]),
     "sel_pack_weight": (I32, [I32, P, I32, I32, I32, I32, I32, P, P]),

@@ -11,6 +11,7 @@ Reference semantics (file:line under the reference root):
 * CausalResidualUnit      models/autoencoder/modules/residual_unit.py:43-80
 """
 import ctypes
+import os
 import threading
 import weakref
 from contextlib import contextmanager
@@ -356,6 +357,35 @@ class ConvLayerFn(torch.autograd.Function):
         return gx, gw, gb, None, None, None
 
 
+# fused residual-unit forward (sel_resunit_fwd) for the 32/64-channel units; the
+# fusion is OFF by default: measured slower than the two calls
+RU_FUSED = os.environ.get("SEL_RU_FUSED", "0") == "1"
+
+
+def ru_fused_ok(d1, dtype):
+    """Mirror of the C side's eligibility (conv.hip ru_fused_ok)."""
+    return (RU_FUSED and dtype == torch.bfloat16 and d1.C == d1.N and d1.C in (32, 64) and d1.K == 7
+            and d1.pad == 6 * d1.dil and d1.pad_mode == PAD_ZERO and d1.in_elu == 1 and 6 * d1.dil <= 64
+            and d1.bias_period in (0, d1.N))
+
+
+def resunit_fwd(d1, xf, wp1, b1, wp2, b2):
+    """h = conv1(ELU(x)), out = x + conv1x1(ELU(h)) in one launch (both (rows, C) bf16)."""
+    h = torch.empty((d1.rows, d1.N), dtype=xf.dtype, device=xf.device)
+    out = torch.empty_like(h)
+    L.call("sel_resunit_fwd", ctypes.byref(d1), _code(xf.dtype), L.ptr(xf), L.ptr(wp1), L.ptr(b1), L.ptr(wp2),
+           L.ptr(b2), L.ptr(h), L.ptr(out), L.stream(), meta=lambda: _ru_meta(d1, xf, wp1, wp2))
+    return h, out
+
+
+def _ru_meta(d1, xf, wp1, wp2):
+    """Algorithmic bytes: read x once, write h and out, read both packed weights."""
+    es = xf.element_size()
+    nbytes = 3 * d1.rows * d1.C * es + (wp1.numel() + wp2.numel()) * es
+    flops = 2.0 * d1.rows * d1.N * d1.C * (d1.K + 1)
+    return f"k_ru_thin_bf16<{d1.C}, 7, {128 if d1.C == 32 else 64}>", nbytes, flops
+
+
 class ResidualUnitFn(torch.autograd.Function):
     """x + conv1x1(ELU(causal_conv_k(ELU(x)))) fused into two primitive calls
     forward and four backward (residual_unit.py:43-46)."""
@@ -375,8 +405,11 @@ class ResidualUnitFn(torch.autograd.Function):
         bb1 = b1.detach().float().contiguous() if b1 is not None else None
         bb2 = b2.detach().float().contiguous() if b2 is not None else None
         xf = x.view(B * T, C)
-        h = prim(d1, xf, wp1, bias=bb1)
-        out = prim(d2, h, wp2, bias=bb2, res=xf)
+        if ru_fused_ok(d1, x.dtype):
+            h, out = resunit_fwd(d1, xf, wp1, bb1, wp2, bb2)
+        else:
+            h = prim(d1, xf, wp1, bias=bb1)
+            out = prim(d2, h, wp2, bias=bb2, res=xf)
         ctx.save_for_backward(x, h, wd1, wd2)
         ctx.meta = (d1, d2, tuple(w1.shape), tuple(w2.shape))
         return out.view(B, T, C)

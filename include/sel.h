@@ -161,6 +161,13 @@ int sel_conv_fwd_kernel_id(const sel_conv_desc* d, int in_dtype, int out_dtype);
 int sel_conv_fwd(const sel_conv_desc* d, int in_dtype, int out_dtype, const void* in,
                  const void* wpack, const float* bias, const void* aux, const void* res,
                  void* out, sel_stream_t stream);
+/* Fused residual unit forward (replaces the two sel_conv_fwd calls of
+ * models/autoencoder/modules/residual_unit.py:43-46, conv_layer.py:19-23 + :139-142):
+ * h = conv1(ELU(x)) [saved for the backward] and out = x + conv1x1(ELU(h)), bf16,
+ * C = N in {32, 64}, K = 7, causal zero pad; d1 describes conv1 (in_elu = 1).
+ * Returns SEL_ERR_UNSUPPORTED for any other shape. */
+int sel_resunit_fwd(const sel_conv_desc* d1, int dtype, const void* x, const void* w1pack, const float* b1,
+                    const void* w2pack, const float* b2, void* h, void* out, sel_stream_t stream);
 /* weight/bias gradient of the same primitive: gwpack[N][K][C] (fp32) and, when
  * gbias != NULL, gbias[bias_period] = sum over rows and phases of gout. */
 size_t sel_conv_wgrad_workspace(const sel_conv_desc* d);

@@ -298,3 +298,56 @@ def test_thin_kernel_matches_tiled(gpu, shape):
             ref += r_.double()
         e = ((outs[0] - ref).norm() / ref.norm()).item()
         assert e < 4e-3, (pad, e)
+
+
+# (C, dil, bias, B, T): the fused residual-unit forward's instances at the
+# AudioDec dilations, ragged tails (T not a multiple of the tile rows) and T < halo
+RU_SHAPES = [(32, 1, 0, 2, 1000), (32, 3, 0, 3, 777), (32, 9, 1, 2, 1000), (32, 9, 0, 2, 40),
+             (64, 1, 0, 2, 500), (64, 3, 1, 3, 333), (64, 9, 0, 2, 260)]
+
+
+@pytest.mark.parametrize("shape", RU_SHAPES, ids=lambda s: "C{}d{}b{}B{}T{}".format(*s))
+def test_fused_residual_unit_matches_two_calls(gpu, shape):
+    """sel_resunit_fwd (one launch) against the two-primitive path (conv1 with
+    ELU prologue, then 1x1 with ELU prologue + residual) on the same bf16
+    operands: h and out within one bf16 ulp norm-wise (4e-3), and against an
+    fp64 reference of the same operands within bf16 rounding (1e-2)."""
+    from sel import convops as CO
+    C, dil, bias, B, T = shape
+    torch.manual_seed(C + dil + T)
+    x = (0.5 * torch.randn(B * T, C, device=gpu)).to(torch.bfloat16)
+    w1 = 0.1 * torch.randn(C, C, 7, device=gpu)
+    w2 = 0.2 * torch.randn(C, C, 1, device=gpu)
+    b1 = torch.randn(C, device=gpu) if bias else None
+    b2 = torch.randn(C, device=gpu) if bias else None
+    d1 = CO.ConvDesc(B * T, T, C, C, 7, dil, 6 * dil, CO.PAD_ZERO, 1, C if bias else 0)
+    d2 = CO.ConvDesc(B * T, T, C, C, 1, 1, 0, CO.PAD_ZERO, 1, C if bias else 0)
+    wp1 = CO.pack(CO.PACK_FWD, w1, 1, torch.bfloat16)
+    wp2 = CO.pack(CO.PACK_FWD, w2, 1, torch.bfloat16)
+    assert CO.ru_fused_ok(d1, torch.bfloat16)
+    h, out = CO.resunit_fwd(d1, x, wp1, b1, wp2, b2)
+    h_ref = CO.prim(d1, x, wp1, bias=b1)
+    out_ref = CO.prim(d2, h_ref, wp2, bias=b2, res=x)
+    for a_, b_ in ((h, h_ref), (out, out_ref)):
+        e = ((a_.float() - b_.float()).norm() / b_.float().norm()).item()
+        assert e < 4e-3, e
+    # fp64 reference of the same bf16 operands
+    elu = lambda v: torch.where(v > 0, v, torch.expm1(v))
+    xa = elu(x.double()).to(torch.bfloat16).double().view(B, T, C)
+    w1q = wp1.double().view(C, 7, C)
+    hr = torch.zeros(B, T, C, dtype=torch.float64, device=gpu)
+    for k in range(7):
+        idx = torch.arange(T, device=gpu) + k * dil - 6 * dil
+        ok = idx >= 0
+        xs = torch.zeros(B, T, C, dtype=torch.float64, device=gpu)
+        xs[:, ok] = xa[:, idx[ok]]
+        hr += torch.einsum("btc,nc->btn", xs, w1q[:, k, :])
+    if bias:
+        hr += b1.double()
+    ha = elu(hr.to(torch.bfloat16).double()).to(torch.bfloat16).double()
+    outr = x.double().view(B, T, C) + torch.einsum("btc,nc->btn", ha, wp2.double().view(C, C))
+    if bias:
+        outr += b2.double()
+    for a_, b_ in ((h, hr), (out, outr)):
+        e = ((a_.double().view(B, T, C) - b_).norm() / b_.norm()).item()
+        assert e < 1e-2, e
