@@ -32,3 +32,39 @@ class CollaterAudioPair(CollaterAudio):
         xs, ns = [b[0] for b in batch], [b[1] for b in batch]
         starts, ends = self._random_segment(xs)
         return self._cut(ns, starts, ends), self._cut(xs, starts, ends)
+
+
+class DeviceCollaterAudio(CollaterAudio):
+    """Device data pipeline (SURVEY §8 f3): items are (raw (T, C) float32, rate);
+    each whole file is resampled on the GPU (sel.resample: torchaudio's
+    sinc_interp_hann, AudioDataset.py:28-33), then the reference's filter and
+    random crops (:33-60, same numpy draws) are cut on the device -> (B, C, T)."""
+
+    def __init__(self, batch_length=9600, sample_rate=24000, device="cuda"):
+        super().__init__(batch_length)
+        self.sample_rate = sample_rate
+        self.device = torch.device(device)
+
+    def _to_rate(self, item):
+        from sel.resample import resample
+        x, sr = item
+        xt = torch.from_numpy(np.ascontiguousarray(x)).to(self.device, non_blocking=True)
+        return resample(xt.transpose(0, 1), sr, self.sample_rate).transpose(0, 1)  # (T', C)
+
+    def _cut(self, xs, starts, ends):
+        return torch.stack([x[s:e] for x, s, e in zip(xs, starts, ends)]).transpose(2, 1).contiguous()
+
+    def __call__(self, batch):
+        return super().__call__([self._to_rate(b) for b in batch])
+
+
+class DeviceCollaterAudioPair(DeviceCollaterAudio):
+    """(noisy, clean) pairs, both resampled on the device, cut at the same offsets."""
+
+    def __call__(self, batch):
+        batch = [(self._to_rate(b[0]), self._to_rate(b[1])) for b in batch]
+        batch = [b for b in batch if len(b[0]) > self.batch_length and len(b[0]) == len(b[1])]
+        assert len(batch) > 0, "No qualified audio pairs.!"
+        xs, ns = [b[0] for b in batch], [b[1] for b in batch]
+        starts, ends = self._random_segment(xs)
+        return self._cut(ns, starts, ends), self._cut(xs, starts, ends)

@@ -6,7 +6,7 @@ import numpy as np
 import torch
 from torch.utils.data import DataLoader, random_split
 
-from dataloader.collater import CollaterAudio
+from dataloader.collater import CollaterAudio, DeviceCollaterAudio
 from sel import _lib as L
 
 
@@ -31,7 +31,18 @@ def seed_worker(worker_id):
     random.seed(worker_seed)
 
 
+def _device_mode(dataset):
+    while hasattr(dataset, "dataset"):  # random_split Subset -> the AudioDataset
+        dataset = dataset.dataset
+    return getattr(dataset, "resample_device", False), getattr(dataset, "sample_rate", None)
+
+
 def create_dataloader(dataset, batch_size, batch_length, generator, sampler=None):
+    on_device, rate = _device_mode(dataset)
+    if on_device:  # GPU resampling + crops in the main process (no workers: the collater uses the GPU)
+        return DataLoader(dataset, batch_size=batch_size, shuffle=sampler is None, sampler=sampler,
+                          generator=generator if sampler is None else None,
+                          collate_fn=DeviceCollaterAudio(batch_length, rate), drop_last=True)
     return DataLoader(dataset, batch_size=batch_size, shuffle=sampler is None, sampler=sampler,
                       generator=generator if sampler is None else None, collate_fn=CollaterAudio(batch_length),
                       worker_init_fn=seed_worker, drop_last=True, pin_memory=torch.cuda.is_available())

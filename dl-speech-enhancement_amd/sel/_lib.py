@@ -65,6 +65,10 @@ SIGNATURES = {
     "sel_mix_noise": (I32, [P, P, I64, P, F32, P, P]),
     "sel_snr_fwd": (I32, [P, P, I64, I64, P, P, P]),
     "sel_snr_bwd": (I32, [P, P, I64, I64, P, P, P, P]),
+    "sel_resample_plan": (I32, [I32, I32, I32, F32, P, P]),
+    "sel_resample_out_len": (I64, [I64, I32, I32]),
+    "sel_resample_kernel": (I32, [I32, I32, I32, F32, P]),
+    "sel_resample": (I32, [P, I64, I64, I32, I32, I32, F32, P, P, P]),
 }
 
 _lock = threading.Lock()

@@ -248,6 +248,19 @@ int sel_snr_fwd(const float* pred, const float* target, int64_t B, int64_t T, do
 int sel_snr_bwd(const float* pred, const float* target, int64_t B, int64_t T, const double* sums,
                 const float* g_out, float* g_pred, sel_stream_t stream);
 
+/* ---- data pipeline: band-limited resampling ----
+ * replaces torchaudio.functional.resample(x, orig, new) at dataloader/AudioDataset.py:28-33
+ * (defaults: sinc_interp_hann, lowpass_filter_width 6, rolloff 0.99; torchaudio 2.1.1
+ * restated).  x (n_wavs, len) fp32 -> y (n_wavs, sel_resample_out_len(len, ...)).
+ * The tap table [phases][taps] is caller-owned: fill it on the host with
+ * sel_resample_kernel and copy it to the device. */
+int sel_resample_plan(int orig_freq, int new_freq, int lowpass_filter_width, float rolloff, int* phases,
+                      int* taps);
+int64_t sel_resample_out_len(int64_t len, int orig_freq, int new_freq);
+int sel_resample_kernel(int orig_freq, int new_freq, int lowpass_filter_width, float rolloff, float* table);
+int sel_resample(const float* x, int64_t n_wavs, int64_t len, int orig_freq, int new_freq, int lowpass_filter_width,
+                 float rolloff, const float* table, float* y, sel_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

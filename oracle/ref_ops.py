@@ -346,6 +346,35 @@ def stream_decode(P, S, zq, geo, dilations=(1, 3, 9), pqc=True):
 
 
 # --------------------------------------------------------------------------
+# data pipeline  (dataloader/AudioDataset.py:25-36 -> torchaudio.functional.resample)
+# --------------------------------------------------------------------------
+
+def resample(x, orig_freq, new_freq, lowpass_filter_width=6, rolloff=0.99):
+    """torchaudio 2.1.1 functional.resample, sinc_interp_hann (third-party, absent
+    here: restated from its published _get_sinc_resample_kernel /
+    _apply_sinc_resample_kernel; parity unpinned by any reference fixture)."""
+    if orig_freq == new_freq:
+        return x
+    g = math.gcd(int(orig_freq), int(new_freq))
+    o, n = int(orig_freq) // g, int(new_freq) // g
+    base = min(o, n) * rolloff
+    width = math.ceil(lowpass_filter_width * o / base)
+    idx = torch.arange(-width, width + o, dtype=torch.float64)[None, None] / o
+    t = torch.arange(0, -n, -1, dtype=torch.float64)[:, None, None] / n + idx
+    t = (t * base).clamp(-lowpass_filter_width, lowpass_filter_width)
+    window = torch.cos(t * math.pi / lowpass_filter_width / 2) ** 2
+    t = t * math.pi
+    kern = torch.where(t == 0, torch.ones_like(t), torch.sin(t) / t) * window * (base / o)
+    shape = x.shape
+    w = x.reshape(-1, shape[-1]).double()
+    length = w.shape[-1]
+    w = F.pad(w, (width, width + o))
+    y = F.conv1d(w[:, None], kern, stride=o).transpose(1, 2).reshape(w.shape[0], -1)
+    target = math.ceil(n * length / o)
+    return y[..., :target].reshape(*shape[:-1], target).to(x.dtype)
+
+
+# --------------------------------------------------------------------------
 # step glue  (dataloader/data_utils.py, train_denoise.py, trainerGAN.py)
 # --------------------------------------------------------------------------
 
