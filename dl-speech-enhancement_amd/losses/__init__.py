@@ -1,2 +1,3 @@
 from .mel_loss import *  # NOQA
 from .stft_loss import *  # NOQA
+from .waveform_loss import *  # NOQA

@@ -69,6 +69,9 @@ SIGNATURES = {
     "sel_resample_out_len": (I64, [I64, I32, I32]),
     "sel_resample_kernel": (I32, [I32, I32, I32, F32, P]),
     "sel_resample": (I32, [P, I64, I64, I32, I32, I32, F32, P, P, P]),
+    "sel_shape_loss_workspace": (SZ, [I64, I64, I32]),
+    "sel_shape_loss_fwd": (I32, [P, P, I64, I64, I32, P, P, P, P, SZ, P]),
+    "sel_shape_loss_bwd": (I32, [P, I64, I64, I32, P, P, P, F32, P, P]),
 }
 
 _lock = threading.Lock()

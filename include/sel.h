@@ -261,6 +261,16 @@ int sel_resample_kernel(int orig_freq, int new_freq, int lowpass_filter_width, f
 int sel_resample(const float* x, int64_t n_wavs, int64_t len, int orig_freq, int new_freq, int lowpass_filter_width,
                  float rolloff, const float* table, float* y, sel_stream_t stream);
 
+/* ---- waveform shape loss (losses/waveform_loss.py:15-74), one window length per call ----
+ * L1(maxpool_w(|y_hat|), maxpool_w(|y|)) over (rows, T) -> out[0]; argidx/dsign
+ * (rows * (T / w) each) carry the argmax and sign(diff) to the backward, which
+ * ADDS g_out[0] * g_mul * d loss / d y_hat into g_yhat (y is not differentiated). */
+size_t sel_shape_loss_workspace(int64_t rows, int64_t T, int win);
+int sel_shape_loss_fwd(const float* y_hat, const float* y, int64_t rows, int64_t T, int win, int32_t* argidx,
+                       float* dsign, float* out, void* ws, size_t ws_bytes, sel_stream_t stream);
+int sel_shape_loss_bwd(const float* y_hat, int64_t rows, int64_t T, int win, const int32_t* argidx,
+                       const float* dsign, const float* g_out, float g_mul, float* g_yhat, sel_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

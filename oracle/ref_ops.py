@@ -346,6 +346,23 @@ def stream_decode(P, S, zq, geo, dilations=(1, 3, 9), pqc=True):
 
 
 # --------------------------------------------------------------------------
+# waveform shape loss  (losses/waveform_loss.py:15-74)
+# --------------------------------------------------------------------------
+
+def waveform_shape_loss(y_hat, y, winlen):
+    """waveform_loss.py:26-38 — L1(maxpool_w(|y_hat|), maxpool_w(|y|))."""
+    return F.l1_loss(F.max_pool1d(torch.abs(y_hat), winlen), F.max_pool1d(torch.abs(y), winlen))
+
+
+def multi_window_shape_loss(y_hat, y, winlen=(300, 200, 100)):
+    """waveform_loss.py:58-74 — mean over the window lengths."""
+    loss = 0.0
+    for w in winlen:
+        loss = loss + waveform_shape_loss(y_hat, y, w)
+    return loss / len(winlen)
+
+
+# --------------------------------------------------------------------------
 # data pipeline  (dataloader/AudioDataset.py:25-36 -> torchaudio.functional.resample)
 # --------------------------------------------------------------------------
 

@@ -112,6 +112,24 @@ def make_stream(pqc_mod, clean, noise, gp, out):
     np.savez_compressed(os.path.join(out, "stream.npz"), **d)
 
 
+def make_waveform(ref, clean, noise, out):
+    """losses/waveform_loss.py: MultiWindowShapeLoss (default windows) and a
+    single WaveformShapeLoss(160) whose window does not divide T."""
+    wl = _load("ref_waveform_loss", os.path.join(ref, "losses", "waveform_loss.py"))
+    T = 4810
+    y = torch.from_numpy(np.stack([clean[0][:T], clean[1][:T]])).unsqueeze(1)
+    yh = torch.from_numpy(np.stack([clean[0][:T] + 0.2 * noise[0][:T],
+                                    clean[1][:T] + 0.2 * noise[1][:T]]).astype(np.float32)).unsqueeze(1)
+    d = {"y": _np(y), "y_hat": _np(yh)}
+    for tag, mod in (("multi", wl.MultiWindowShapeLoss()), ("w160", wl.WaveformShapeLoss(160))):
+        x = yh.clone().requires_grad_(True)
+        loss = mod(x, y)
+        loss.backward()
+        d[f"{tag}.loss"] = _np(loss)
+        d[f"{tag}.grad"] = _np(x.grad)
+    np.savez_compressed(os.path.join(out, "waveform.npz"), **d)
+
+
 def make(ref, out, only=None):
     du = _install_stubs(ref)
     stft_mod = _load("ref_stft_loss", os.path.join(ref, "losses", "stft_loss.py"))
@@ -126,6 +144,8 @@ def make(ref, out, only=None):
     if only == "stream":
         gp = dict(encode_channels=4, decode_channels=4, code_dim=64, codebook_num=2, codebook_size=64)
         return make_stream(pqc_mod, clean, noise, gp, out)
+    if only == "waveform":
+        return make_waveform(ref, clean, noise, out)
     torch.manual_seed(93)
 
     # ---------------- melmat (losses/mel_loss.py:54-61) ----------------
@@ -339,6 +359,8 @@ def make(ref, out, only=None):
 
     # ---------------- streaming (AudioDec.py:106-191, conv_layer.py:144-191) ----------------
     make_stream(pqc_mod, clean, noise, gp, out)
+    # ---------------- waveform shape loss (losses/waveform_loss.py:15-74) ----------------
+    make_waveform(ref, clean, noise, out)
 
     # ---------------- add_noise (dataloader/data_utils.py:12-22) ----------------
     cl = torch.from_numpy(np.stack([clean[0][:4800], clean[1][:4800]])).unsqueeze(1)
@@ -353,7 +375,7 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
     ap.add_argument("--out", default=HERE)
-    ap.add_argument("--only", default=None, help="regenerate one fixture family (stream)")
+    ap.add_argument("--only", default=None, help="regenerate one fixture family (stream, waveform)")
     a = ap.parse_args()
     make(a.ref, a.out, a.only)
     for f in sorted(os.listdir(a.out)):

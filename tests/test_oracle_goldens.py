@@ -209,3 +209,15 @@ def test_stream_generator():
     for k, v in g.items():
         if k.startswith("buf."):
             close(S[k[4:-len(".pad_buffer")]], v, rtol=1e-5, atol=1e-6)
+
+
+def test_waveform_shape_loss():
+    """losses/waveform_loss.py: multi-window and a window that leaves a tail."""
+    g = golden("waveform")
+    for tag, fn in (("multi", lambda a, b: R.multi_window_shape_loss(a, b)),
+                    ("w160", lambda a, b: R.waveform_shape_loss(a, b, 160))):
+        x = T(g["y_hat"]).requires_grad_(True)
+        loss = fn(x, T(g["y"]))
+        close(loss, g[f"{tag}.loss"], rtol=1e-6, atol=1e-8)
+        loss.backward()
+        close(x.grad, g[f"{tag}.grad"], rtol=1e-6, atol=1e-9)
