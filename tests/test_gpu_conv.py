@@ -307,7 +307,7 @@ RU_SHAPES = [(32, 1, 0, 2, 1000), (32, 3, 0, 3, 777), (32, 9, 1, 2, 1000), (32, 
 
 
 @pytest.mark.parametrize("shape", RU_SHAPES, ids=lambda s: "C{}d{}b{}B{}T{}".format(*s))
-def test_fused_residual_unit_matches_two_calls(gpu, shape):
+def test_fused_residual_unit_matches_two_calls(gpu, shape, monkeypatch):
     """sel_resunit_fwd (one launch) against the two-primitive path (conv1 with
     ELU prologue, then 1x1 with ELU prologue + residual) on the same bf16
     operands: h and out within one bf16 ulp norm-wise (4e-3), and against an
@@ -324,6 +324,7 @@ def test_fused_residual_unit_matches_two_calls(gpu, shape):
     d2 = CO.ConvDesc(B * T, T, C, C, 1, 1, 0, CO.PAD_ZERO, 1, C if bias else 0)
     wp1 = CO.pack(CO.PACK_FWD, w1, 1, torch.bfloat16)
     wp2 = CO.pack(CO.PACK_FWD, w2, 1, torch.bfloat16)
+    monkeypatch.setattr(CO, "RU_FUSED", True)  # off by default in the product path
     assert CO.ru_fused_ok(d1, torch.bfloat16)
     h, out = CO.resunit_fwd(d1, x, wp1, b1, wp2, b2)
     h_ref = CO.prim(d1, x, wp1, bias=b1)
