@@ -279,12 +279,37 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 constexpr int F4_HALOMAX = 64;
 constexpr int F4_P = 40;  // staged row pitch (bf16 elements) = 80 B
 
+// XCD-aware block order for multi-column-tile launches (1-D grid of
+// row tiles x ncol): workgroups are dealt round-robin over the 8 XCDs, so the
+// ncol column tiles of one row tile are given ids 8 apart (one XCD, adjacent in
+// that XCD's dispatch order) and share the input tile through its L2 instead
+// of each XCD fetching it from HBM.  ncol == 0 means a 2-D (row, column) grid.
+__device__ __forceinline__ void xcd_tile(int ncol, int64_t& mt, int& nt) {
+  if (ncol == 0) {
+    mt = blockIdx.x;
+    nt = blockIdx.y;
+    return;
+  }
+  const int64_t L = blockIdx.x;
+  const int64_t mtiles = int64_t(gridDim.x) / ncol;
+  const int64_t full = (mtiles / 8) * 8 * ncol;
+  if (L < full) {
+    const int64_t q = L >> 3;
+    nt = int(q % ncol);
+    mt = (q / ncol) * 8 + (L & 7);
+  } else {
+    const int64_t r = L - full;
+    nt = int(r % ncol);
+    mt = (mtiles / 8) * 8 + r / ncol;
+  }
+}
+
 template <int BM, int BN, int WAVES_M, int KMAX, typename TO>
 __global__ __launch_bounds__(256) void k_conv_fwd_bf16(Args a, const __bf16* __restrict__ in,
                                                        const __bf16* __restrict__ wp,
                                                        const float* __restrict__ bias,
                                                        const TO* __restrict__ aux, const TO* __restrict__ res,
-                                                       TO* __restrict__ out) {
+                                                       TO* __restrict__ out, int ncol) {
   constexpr int P = F4_P;
   constexpr int WAVES_N = 4 / WAVES_M;
   constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
@@ -303,11 +328,14 @@ __global__ __launch_bounds__(256) void k_conv_fwd_bf16(Args a, const __bf16* __r
   // the causal zero / replicate padding is resolved once while staging and the
   // MFMA loop needs no per-tap row validity (blocks past T are clipped at store)
   const int tps = (a.T + BM - 1) / BM;
-  const int64_t b = blockIdx.x / tps;
-  const int t0 = int(blockIdx.x % tps) * BM;
+  int64_t mt;
+  int nt;
+  xcd_tile(ncol, mt, nt);
+  const int64_t b = mt / tps;
+  const int t0 = int(mt % tps) * BM;
   const int64_t m0 = b * a.T + t0;
   const int mrows = a.T - t0 < BM ? a.T - t0 : BM;
-  const int n0 = blockIdx.y * BN;
+  const int n0 = nt * BN;
   const int nchunk = a.C / CK;
 
   // staging row r <-> input time t0 - pad + r of sample b; per-thread source
@@ -1899,14 +1927,17 @@ int launch_fwd4(const Args& a, const void* in, const void* wp, const float* bias
   const int span = BM + (a.K - 1) * a.dil;
   const size_t lds = (size_t(span) + size_t(a.K) * BN) * F4_P * 2;
   const int64_t tiles = (a.rows / a.T) * ((a.T + BM - 1) / BM);  // sample-aligned tiles
-  dim3 grid(unsigned(tiles), unsigned((a.N + BN - 1) / BN));
-  if (grid.x == 0) return SEL_OK;
+  const int ncol = (a.N + BN - 1) / BN;
+  if (tiles == 0) return SEL_OK;
+  // tune key 8 = 1: plain 2-D grid instead of the XCD-aware 1-D order
+  const bool xcd = ncol > 1 && tune(8) == 0 && tiles * ncol < (int64_t(1) << 31);
+  const dim3 grid = xcd ? dim3(unsigned(tiles * ncol)) : dim3(unsigned(tiles), unsigned(ncol));
   auto kern = k_conv_fwd_bf16<BM, BN, WAVES_M, KMAX, TO>;
   if (lds > 64 * 1024)
     SEL_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
   hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, a, static_cast<const __bf16*>(in),
                      static_cast<const __bf16*>(wp), bias, static_cast<const TO*>(aux), static_cast<const TO*>(res),
-                     static_cast<TO*>(out));
+                     static_cast<TO*>(out), xcd ? ncol : 0);
   SEL_LAUNCH_CHECK();
   return SEL_OK;
 }

@@ -1,13 +1,14 @@
 // Residual VQ (layers/vq_module.py:61-88 eval mode, ResidualVQ :119-134) on gfx950.
 //
 // Rows are independent through all stages, so one workgroup carries a block of
-// 16 rows through every stage with the residual kept in LDS: per stage each
-// lane scores 4 codes against the 16 rows (codebook streamed from L2,
-// coalesced over k), a wavefront argmin with lowest-index tie-break picks the
-// code, and the row update (straight-through value r + (q - r), next residual,
-// running sum) is done in LDS.  Cross-row quantities (commitment SSE, code
-// histogram for the perplexity) go to deterministic per-block partials and
-// integer atomics.
+// rows through every stage with the residual kept in LDS: per stage the block
+// scores every code against its rows, an argmin with lowest-index tie-break
+// picks the code, and the row update (straight-through value r + (q - r), next
+// residual, running sum) is done in LDS.  Cross-row quantities (commitment SSE,
+// code histogram for the perplexity) go to deterministic per-block partials and
+// integer atomics.  Three kernels with one arithmetic (bit-identical results,
+// tune key 2): k_rvq_mfma (default, f32-input matrix cores), k_rvq_fwd2
+// (codebook staged through LDS, fp32 VALU) and k_rvq_fwd (direct, any D).
 #include <algorithm>
 
 #include "sel_common.h"
@@ -345,6 +346,245 @@ __global__ __launch_bounds__(T2) void k_rvq_fwd2(const float* __restrict__ x, in
   }
 }
 
+// Matrix-core variant (default; D % 4 == 0, D <= 64): the 16-row residual
+// block is the A operand of v_mfma_f32_16x16x4_f32 (lane l holds
+// r[row l&15][d = 4j + (l>>4)] for k-step j: 16 VGPRs at D = 64, loaded from
+// LDS once per stage) and the codebook is the B operand.  k_rvq_prep lays each
+// stage's codebook out in B-fragment order (per 16-code tile: [j/4][lane][j%4],
+// so a lane's operands for four k-steps are one coalesced 16-byte load) and
+// computes |e|^2.  Each of the 8 waves scores every 8th code tile with the
+// next tile's operands in flight, starting at a block-dependent tile so the
+// 320 blocks do not all hit the same L2 lines at once.  The code histogram is a
+// separate pass over the indices (k_rvq_hist), off the per-stage critical path.
+// The f32-input MFMA is bit-for-bit a k-ordered fmaf chain, so with d ascending
+// from a zero accumulator every dot product, |e|^2 and |r|^2 (the same
+// wave_sum) is the one k_rvq_fwd computes: all variants pick the same codes and
+// produce the same outputs.
+constexpr int RM = 16;
+constexpr int TM = 512;
+constexpr int NWM = TM / 64;
+constexpr int DM = 64;
+using f32x4 = __attribute__((ext_vector_type(4))) float;
+
+struct MfmaGeo {
+  int ntile, nj4;  // 16-code tiles; groups of four k-steps (4 dims each)
+  __host__ __device__ MfmaGeo(int D, int K) : ntile((K + 15) / 16), nj4((D / 4 + 3) / 4) {}
+  __host__ __device__ int64_t tile_floats() const { return int64_t(nj4) * 256; }
+  __host__ __device__ int64_t stage_floats() const { return int64_t(ntile) * tile_floats(); }
+};
+
+// one thread per (stage, tile, j4, lane): four B operands, zero-padded past D and K
+__global__ __launch_bounds__(256) void k_rvq_prep(const float* __restrict__ embeds, int S, int D, int K,
+                                                  float* __restrict__ ep, float* __restrict__ en) {
+  const MfmaGeo g(D, K);
+  const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  const int64_t total = int64_t(S) * g.stage_floats() / 4;
+  if (i < total) {
+    const int lane = int(i & 63);
+    const int64_t q = i >> 6;
+    const int j4 = int(q % g.nj4);
+    const int64_t st = q / g.nj4;  // s * ntile + tile
+    const int tile = int(st % g.ntile);
+    const int64_t s = st / g.ntile;
+    const int k = tile * 16 + (lane & 15);
+    const float* E = embeds + s * D * K;
+    float v[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int d = 4 * (4 * j4 + e) + (lane >> 4);
+      v[e] = (d < D && k < K) ? E[int64_t(d) * K + k] : 0.f;
+    }
+    reinterpret_cast<float4*>(ep)[i] = make_float4(v[0], v[1], v[2], v[3]);
+  }
+  if (i < int64_t(S) * K) {  // |e|^2: fmaf over d ascending from 0 (k_rvq_fwd's en)
+    const int64_t s = i / K, k = i - s * K;
+    const float* E = embeds + s * D * K + k;
+    float v = 0.f;
+#pragma unroll 16
+    for (int d = 0; d < D; ++d) v = fmaf(E[int64_t(d) * K], E[int64_t(d) * K], v);
+    en[i] = v;
+  }
+}
+
+constexpr int SM = 16;  // max stages of the matrix-core variant (per-stage state in LDS)
+
+__global__ __launch_bounds__(TM) __attribute__((amdgpu_waves_per_eu(4))) void k_rvq_mfma(
+    const float* __restrict__ x, int64_t N, int D, const float* __restrict__ embeds, int S, int K,
+    const float* __restrict__ ep_all, const float* __restrict__ en_all, float* __restrict__ out,
+    int64_t* __restrict__ idx, double* __restrict__ partials) {
+  __shared__ float resT[DM * RM];  // [d][row]: the A-fragment reads hit 64 distinct banks
+  __shared__ float acc_o[RM * DM];
+  __shared__ float xn[RM];
+  __shared__ float red_d[NWM][RM];
+  __shared__ int red_k[NWM][RM];
+  __shared__ int sel_k[SM][RM];    // chosen codes, written to idx after the last stage
+  __shared__ float sq_t[SM][TM];   // per-thread SSE per stage, reduced after the last stage
+  __shared__ double red[16];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int col = lane & 15, h = lane >> 4;
+  const int64_t r0 = int64_t(blockIdx.x) * RM;
+  for (int i = tid; i < RM * D; i += TM) {
+    const int r = i / D, d = i % D;
+    const int64_t row = r0 + r;
+    resT[d * RM + r] = row < N ? x[row * D + d] : 0.f;
+    acc_o[r * D + d] = 0.f;
+  }
+  const int ns = D / 4;
+  const MfmaGeo g(D, K);
+  const int ntile = g.ntile, nj4 = g.nj4;
+  const int rot = int((blockIdx.x * 4u) % unsigned(ntile));  // L2 de-synchronisation across blocks
+  // wave w scores tiles w, w + 8, ... in a block-rotated order with the next
+  // tile's operands in flight (one tile keeps the kernel at 4 waves/SIMD); the
+  // last tile of a stage prefetches the next stage's first one
+  auto tile_of = [&](int p) {
+    const int t = p + rot;
+    return t >= ntile ? t - ntile : t;
+  };
+  float4 cur[DM / 16], nxt[DM / 16];
+  auto load = [&](int st, int p, float4 (&b)[DM / 16]) {
+    const float4* src = reinterpret_cast<const float4*>(ep_all + int64_t(st) * g.stage_floats()) +
+                        int64_t(tile_of(p)) * (nj4 * 64) + lane;
+#pragma unroll
+    for (int j4 = 0; j4 < DM / 16; ++j4) b[j4] = j4 < nj4 ? src[j4 * 64] : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  if (wave < ntile) load(0, wave, cur);
+  __syncthreads();
+
+  for (int s = 0; s < S; ++s) {
+    const float* __restrict__ E = embeds + int64_t(s) * D * K;
+    const float* __restrict__ enS = en_all + int64_t(s) * K;
+    for (int r = wave; r < RM; r += NWM) {
+      float v = 0.f;
+      for (int d = lane; d < D; d += 64) v = fmaf(resT[d * RM + r], resT[d * RM + r], v);
+      v = wave_sum(v);
+      if (lane == 0) xn[r] = v;
+    }
+    float a[DM / 4];
+#pragma unroll
+    for (int j = 0; j < DM / 4; ++j) a[j] = j < ns ? resT[(4 * j + h) * RM + col] : 0.f;
+    __syncthreads();
+    float xr[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) xr[i] = xn[4 * h + i];
+    float bd[4];
+    int bk[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      bd[i] = __builtin_inff();
+      bk[i] = 0x7fffffff;
+    }
+    for (int p = wave; p < ntile; p += NWM) {
+      if (p + NWM < ntile)
+        load(s, p + NWM, nxt);
+      else if (s + 1 < S)
+        load(s + 1, wave, nxt);
+      f32x4 c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < DM / 4; ++j) {
+        if (j < ns) {
+          const float4 bv = cur[j >> 2];
+          const float bj = (j & 3) == 0 ? bv.x : (j & 3) == 1 ? bv.y : (j & 3) == 2 ? bv.z : bv.w;
+          c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], bj, c, 0, 0, 0);
+        }
+      }
+      const int k = tile_of(p) * 16 + col;
+      const bool kin = k < K;
+      const float ek = kin ? enS[k] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {  // C/D map: col = lane & 15 (code), row = 4 (lane >> 4) + i
+        const float dist = (xr[i] - 2.f * c[i]) + ek;
+        const bool take = kin && better(dist, k, bd[i], bk[i]);
+        bd[i] = take ? dist : bd[i];
+        bk[i] = take ? k : bk[i];
+      }
+#pragma unroll
+      for (int j4 = 0; j4 < DM / 16; ++j4) cur[j4] = nxt[j4];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float d0 = bd[i];
+      int k0 = bk[i];
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) {  // the 16 lanes of one row group
+        const float d1 = __shfl_xor(d0, o, 64);
+        const int k1 = __shfl_xor(k0, o, 64);
+        if (better(d1, k1, d0, k0)) {
+          d0 = d1;
+          k0 = k1;
+        }
+      }
+      if (col == 0) {
+        red_d[wave][4 * h + i] = d0;
+        red_k[wave][4 * h + i] = k0;
+      }
+    }
+    __syncthreads();
+    if (tid < RM) {
+      float d0 = red_d[0][tid];
+      int k0 = red_k[0][tid];
+      for (int w = 1; w < NWM; ++w)
+        if (better(red_d[w][tid], red_k[w][tid], d0, k0)) {
+          d0 = red_d[w][tid];
+          k0 = red_k[w][tid];
+        }
+      sel_k[s][tid] = k0;
+    }
+    __syncthreads();
+    float sq = 0.f;
+    for (int i = tid; i < RM * D; i += TM) {
+      const int r = i / D, d = i % D;
+      if (r0 + r >= N) continue;
+      const float q = E[int64_t(d) * K + sel_k[s][r]];
+      const float rv = resT[d * RM + r];
+      const float diff = q - rv;
+      sq = fmaf(diff, diff, sq);
+      const float qst = rv + diff;
+      resT[d * RM + r] = rv - qst;
+      acc_o[r * D + d] += qst;
+    }
+    sq_t[s][tid] = sq;
+    __syncthreads();
+  }
+  for (int i = tid; i < RM * D; i += TM) {
+    const int r = i / D, d = i % D;
+    const int64_t row = r0 + r;
+    if (row < N) out[row * D + d] = acc_o[r * D + d];
+  }
+  for (int i = tid; i < S * RM; i += TM) {
+    const int st = i / RM, r = i % RM;
+    if (r0 + r < N) idx[int64_t(st) * N + r0 + r] = sel_k[st][r];
+  }
+  for (int st = 0; st < S; ++st) {
+    const double bs = block_sum<double>(double(sq_t[st][tid]), red);
+    if (tid == 0) partials[int64_t(st) * gridDim.x + blockIdx.x] = bs;
+  }
+}
+
+// code histogram of one stage's indices: LDS bins, then one global add per bin
+constexpr int kHistRows = 4096;
+constexpr int kHistMaxK = 8192;
+__global__ __launch_bounds__(512) void k_rvq_hist(const int64_t* __restrict__ idx, int64_t N, int K,
+                                                  int32_t* __restrict__ counts) {
+  __shared__ int32_t bins[kHistMaxK];
+  const int s = blockIdx.y;
+  for (int k = threadIdx.x; k < K; k += blockDim.x) bins[k] = 0;
+  __syncthreads();
+  const int64_t a = int64_t(blockIdx.x) * kHistRows, b = std::min<int64_t>(N, a + kHistRows);
+  for (int64_t i = a + threadIdx.x; i < b; i += blockDim.x) atomicAdd(&bins[idx[int64_t(s) * N + i]], 1);
+  __syncthreads();
+  for (int k = threadIdx.x; k < K; k += blockDim.x)
+    if (bins[k]) atomicAdd(&counts[int64_t(s) * K + k], bins[k]);
+}
+
+inline size_t en_offset(int64_t N, int S) {
+  const int64_t nb = (N + ROWS - 1) / ROWS;  // >= every variant's block count (16 / 20 rows)
+  return (size_t(nb) * size_t(S) * sizeof(double) + 255) & ~size_t(255);
+}
+inline size_t ep_offset(int64_t N, int S, int K) {
+  return (en_offset(N, S) + size_t(S) * size_t(K) * sizeof(float) + 255) & ~size_t(255);
+}
+
 __global__ __launch_bounds__(256) void k_rvq_sqerr(const double* __restrict__ partials, int nb,
                                                    double* __restrict__ sqerr) {
   __shared__ double red[16];
@@ -402,9 +642,9 @@ using namespace sel::vq;
 extern "C" {
 
 size_t sel_rvq_workspace(int64_t N, int S, int K) {
-  (void)K;
-  const int64_t nb = (N + ROWS - 1) / ROWS;  // >= the staged kernel's block count (20 rows)
-  return size_t(nb) * size_t(S) * sizeof(double) + 16;
+  // per-block SSE partials, then |e|^2 per (stage, code) for the matrix-core variant
+  // + the B-fragment-ordered codebook copy for the matrix-core variant (any D <= 64)
+  return ep_offset(N, S, K) + size_t(S) * size_t(MfmaGeo(DM, K).stage_floats()) * sizeof(float);
 }
 
 int sel_rvq_fwd(const float* x, int64_t N, int D, const float* embeds, int S, int K, float* out, int64_t* idx,
@@ -414,10 +654,25 @@ int sel_rvq_fwd(const float* x, int64_t N, int D, const float* embeds, int S, in
   SEL_REQUIRE(ws_bytes >= sel_rvq_workspace(N, S, K), SEL_ERR_WORKSPACE, "workspace too small");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   SEL_HIP(hipMemsetAsync(counts, 0, size_t(S) * K * sizeof(int32_t), s));
-  const bool staged = D % DC == 0 && K % 4 == 0 && tune(2) == 0;
-  const int nb = int((N + (staged ? R2 : ROWS) - 1) / (staged ? R2 : ROWS));
+  // tune key 2: 0 = matrix-core kernel where it applies, 1 = direct, 2 = staged
+  const int variant = tune(2);
+  const bool mfma = D % 4 == 0 && D <= DM && K <= kHistMaxK && S <= SM && variant == 0;
+  const bool staged = !mfma && D % DC == 0 && K % 4 == 0 && variant != 1;
+  const int rows = mfma ? RM : staged ? R2 : ROWS;
+  const int nb = int((N + rows - 1) / rows);
   double* part = static_cast<double*>(ws);
-  if (nb > 0 && staged) {
+  if (nb > 0 && mfma) {
+    float* en = reinterpret_cast<float*>(static_cast<char*>(ws) + en_offset(N, S));
+    float* ep = reinterpret_cast<float*>(static_cast<char*>(ws) + ep_offset(N, S, K));
+    const int64_t nprep = std::max<int64_t>(int64_t(S) * MfmaGeo(D, K).stage_floats() / 4, int64_t(S) * K);
+    hipLaunchKernelGGL(k_rvq_prep, dim3(unsigned((nprep + 255) / 256)), dim3(256), 0, s, embeds, S, D, K, ep, en);
+    SEL_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_rvq_mfma, dim3(nb), dim3(TM), 0, s, x, N, D, embeds, S, K, ep, en, out, idx, part);
+    SEL_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_rvq_hist, dim3(unsigned((N + kHistRows - 1) / kHistRows), unsigned(S)), dim3(512), 0, s,
+                       idx, N, K, counts);
+    SEL_LAUNCH_CHECK();
+  } else if (nb > 0 && staged) {
     const size_t lds = (size_t(2) * MAXD * R2 + size_t(2) * DC * KP) * sizeof(float);
     SEL_HIP(hipFuncSetAttribute((const void*)k_rvq_fwd2, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
     hipLaunchKernelGGL(k_rvq_fwd2, dim3(nb), dim3(T2), lds, s, x, N, D, embeds, S, K, out, idx, counts, part);

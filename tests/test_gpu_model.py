@@ -165,12 +165,13 @@ def test_full_width_generator_bf16_vs_oracle(gpu):
             nclose(p.grad, P[name].grad, 1e-1, name)
 
 
-@pytest.mark.parametrize("N,D,K,S", [(5120, 64, 1024, 8), (333, 64, 1000, 3), (40, 16, 64, 2)])
+@pytest.mark.parametrize("N,D,K,S", [(5120, 64, 1024, 8), (333, 64, 1000, 3), (40, 16, 64, 2), (77, 12, 40, 3)])
 def test_rvq_kernels_bit_identical(gpu, N, D, K, S):
-    """The staged-codebook RVQ kernel (default) and the direct one (tune key 2 = 1)
-    evaluate every distance with the same fp32 operation order, so indices and
-    outputs must be bit-identical (the fp64 SSE partials are grouped by block
-    size, 20 vs 16 rows: losses agree to 1e-6)."""
+    """The matrix-core RVQ kernel (default, tune key 2 = 0), the direct one (= 1)
+    and the staged-codebook one (= 2) evaluate every distance with the same fp32
+    operation order (the f32-input MFMA is a k-ordered fmaf chain), so indices
+    and outputs must be bit-identical (the fp64 SSE partials are grouped by block
+    size, 16 vs 20 rows: losses agree to 1e-6)."""
     from sel import _lib as L
     from sel.vqops import ResidualVQFn
     torch.manual_seed(N + K)
@@ -178,12 +179,13 @@ def test_rvq_kernels_bit_identical(gpu, N, D, K, S):
     emb = torch.randn(S, D, K, device=gpu)
     lib = L.lib()
     outs = []
-    for v in (0, 1):
+    for v in (1, 0, 2):
         prev = lib.sel_tune(2, v)
         try:
             outs.append([t.clone() for t in ResidualVQFn.apply(x, emb, 1.0)])
         finally:
             lib.sel_tune(2, prev)
-    (o0, l0, p0, i0), (o1, l1, p1, i1) = outs
-    assert torch.equal(i0, i1) and torch.equal(o0, o1) and torch.equal(p0, p1)
-    torch.testing.assert_close(l0, l1, rtol=1e-6, atol=0)
+    o1, l1, p1, i1 = outs[0]
+    for o0, l0, p0, i0 in outs[1:]:
+        assert torch.equal(i0, i1) and torch.equal(o0, o1) and torch.equal(p0, p1)
+        torch.testing.assert_close(l0, l1, rtol=1e-6, atol=0)

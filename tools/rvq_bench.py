@@ -14,11 +14,11 @@ from sel.vqops import ResidualVQFn  # noqa: E402
 
 def main():
     dev = torch.device("cuda")
-    N, D, K, S = 5120, 64, 1024, 8
+    N, D, K, S = (int(v) for v in os.environ.get("RVQ_SHAPE", "5120,64,1024,8").split(","))
     x = torch.randn(N, D, device=dev)
     emb = torch.randn(S, D, K, device=dev)
     lib = L.lib()
-    for v in (0, 1):
+    for v in (int(v) for v in os.environ.get("RVQ_VARIANTS", "0,2,1").split(",")):  # 0 matrix-core, 2 staged, 1 direct
         lib.sel_tune(2, v)
         for _ in range(3):
             ResidualVQFn.apply(x, emb, 1.0)
@@ -29,7 +29,7 @@ def main():
             ResidualVQFn.apply(x, emb, 1.0)
         e1.record()
         torch.cuda.synchronize()
-        print(f"variant {v}: {e0.elapsed_time(e1) / 20 * 1e3:.1f} us per RVQ forward (+finish)", flush=True)
+        print(f"{(N, D, K, S)} variant {v}: {e0.elapsed_time(e1) / 20 * 1e3:.1f} us per RVQ forward (+finish)", flush=True)
     lib.sel_tune(2, 0)
 
 
