@@ -102,7 +102,7 @@ def c2_cpu_baseline(B_sample=4, steps=3):
 C3_CONFIG = "symAD_libritts_24000_hop300"
 
 
-def c3_setup(dev, B, world, local):
+def c3_setup(dev, B, world, local, graph=False):
     from sel import configs
     from sel.convops import precision
     from models.autoencoder.AudioDec import Generator
@@ -123,7 +123,10 @@ def c3_setup(dev, B, world, local):
             p.requires_grad = False
         model["generator"] = DDP(G, device_ids=[local], broadcast_buffers=False, bucket_cap_mb=16)
     mel = MultiMelSpectrogramLoss(**cfg["mel_loss_params"]).to(dev)
-    opt = torch.optim.Adam(G.parameters(), **cfg["generator_optimizer_params"])
+    opt_kw = dict(cfg["generator_optimizer_params"])
+    if graph:
+        opt_kw["capturable"] = True  # step count on device: the update replays inside a HIP graph
+    opt = torch.optim.Adam(G.parameters(), **opt_kw)
     sched = torch.optim.lr_scheduler.StepLR(opt, **cfg["generator_scheduler_params"])
     tr = Trainer(steps=0, epochs=0, data_loader={}, model=model, criterion={"mel": mel},
                  optimizer={"generator": opt}, scheduler={"generator": sched}, config=cfg, device=dev)
@@ -238,7 +241,7 @@ def roofline(cfg, timer, dom, B, steps):
         ach = nbytes / (ms * 1e-3) / 1e9
         r = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
              "frac": round(ach / HBM_PEAK_GBS, 4)}
-    r.update({"kernel": tag, "launches": n, "avg_launch_us": round(1e3 * ms / n, 2),
+    r.update({"kernel": tag, "launches": n, "event_timed_steps": 1, "avg_launch_us": round(1e3 * ms / n, 2),
               "bytes_per_launch": int(nbytes / n), "flops_per_launch": int(flops / n),
               "share_of_timed_conv_ms": round(ms / sum(v[1] for v in summ.values()), 3),
               "traffic": pmc_traffic(tag, B, cfg), "traffic_unit": "bytes/launch (rocprofv3 PMC, profiles/)"})
@@ -323,12 +326,15 @@ def main():
     if world > 1:
         dist.barrier()
     timer = _lib.KernelTimer([dom] + (["sel_resunit_fwd"] if cfg == "c3" else []))
-    _lib.TIMER = timer
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
+        # per-launch HIP events only in the last timed step: an event pair around
+        # every conv launch of every step costs ~0.6 ms/step (C3) of its own
+        if i == args.steps - 1:
+            _lib.TIMER = timer
         step()
     torch.cuda.synchronize()
     if world > 1:
@@ -343,7 +349,7 @@ def main():
     ms_per_step = 1e3 * elapsed / args.steps
     frames = world * B * SR / HOP * args.steps
     value = frames / elapsed
-    roof = roofline(cfg, timer, dom, B, args.steps)
+    roof = roofline(cfg, timer, dom, B, 1)  # the timer covered the last timed step
     stft_roof = stft_kernel_roofline(dev) if world == 1 else None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
