@@ -522,7 +522,7 @@ struct Thin {
   static constexpr size_t LDS_STAGE = size_t(PLANES) * SPAN * F4_P * 2;
   static constexpr size_t LDS_OUT = size_t(R) * OP * 4;
   static constexpr size_t LDS = LDS_STAGE > LDS_OUT ? LDS_STAGE : LDS_OUT;
-  static_assert(N == 32 || N == 64, "thin kernel: N in {32, 64}");
+  static_assert(N == 32 || N == 64 || N == 128, "thin kernel: N in {32, 64, 128}");
   static_assert(C % 32 == 0 && WR % 32 == 0, "thin kernel tiling");
   static_assert(LDS <= 64 * 1024, "thin kernel LDS");
 };
@@ -2002,11 +2002,12 @@ int launch_thin(const Args& a, const void* in, const void* wp, const float* bias
 
 // the (i, C, N, K) instances with their default / alternative tile rows:
 // residual-unit k7 / 1x1 at 32 and 64 channels, the first strided conv
-// (96 -> 64, 3 taps) and the last transposed conv's dgrad (96 -> 64, 2 taps).
+// (96 -> 64, 3 taps), the last transposed conv's dgrad (96 -> 64, 2 taps) and
+// the 128-channel residual-unit 1x1 (one 32-channel output slice per wave).
 // A/B knobs: tune key 7 bit i = instance i off (tiled kernel instead),
 // key 6 bit i = instance i on its alternative tile rows
 #define SEL_THIN_SHAPES(X) X(0, 32, 32, 7, 256, 128) X(1, 32, 32, 1, 256, 128) X(2, 64, 64, 7, 128, 64) \
-  X(3, 64, 64, 1, 128, 64) X(4, 96, 64, 3, 128, 64) X(5, 96, 64, 2, 128, 64)
+  X(3, 64, 64, 1, 128, 64) X(4, 96, 64, 3, 128, 64) X(5, 96, 64, 2, 128, 64) X(6, 128, 128, 1, 64, 32)
 
 int thin_index(const Args& a) {
   if (tune(4) == 1 || (a.K - 1) * a.dil > F4_HALOMAX) return -1;

@@ -245,7 +245,8 @@ THIN_SHAPES = [(32, 32, 7, 9, 0, 1, 0, 0, 0, 3, 1000), (32, 32, 7, 9, 0, 0, 1, 1
                (32, 32, 1, 1, 0, 1, 0, 1, 0, 3, 1000), (32, 32, 1, 1, 0, 0, 1, 0, 0, 2, 300),
                (64, 64, 7, 3, 0, 1, 0, 0, 0, 3, 800), (64, 64, 7, 1, 0, 0, 1, 1, 0, 2, 130),
                (64, 64, 1, 1, 0, 1, 0, 1, 0, 3, 800), (96, 64, 3, 1, 0, 0, 0, 0, 64, 4, 333),
-               (96, 64, 2, 1, 0, 0, 0, 0, 0, 2, 500), (32, 32, 7, 9, 0, 1, 0, 0, 0, 2, 40)]
+               (96, 64, 2, 1, 0, 0, 0, 0, 0, 2, 500), (32, 32, 7, 9, 0, 1, 0, 0, 0, 2, 40),
+               (128, 128, 1, 1, 0, 1, 0, 1, 0, 3, 1000), (128, 128, 1, 1, 0, 0, 1, 0, 0, 2, 333)]
 
 
 @pytest.mark.parametrize("shape", THIN_SHAPES, ids=lambda s: "C{}N{}K{}d{}e{}a{}r{}T{}".format(*s[:3], s[3], *s[5:8],
