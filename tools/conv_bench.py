@@ -31,6 +31,10 @@ SHAPES = [
     ("up3 dgrad 96->64 k2", 512000, 8000, 96, 64, 2, 1, 0, Z, 0, 0, 0, 0),
     ("up3 64->96 k2 rep", 512000, 8000, 64, 96, 2, 1, 1, R, 0, 0, 0, 1),
     ("RU128 k7d9 fwd", 128000, 2000, 128, 128, 7, 9, 54, Z, 1, 0, 0, 0),
+    ("RU128 k7d9 dgrad", 128000, 2000, 128, 128, 7, 9, 0, Z, 0, 1, 1, 0),
+    ("RU128 1x1 fwd", 128000, 2000, 128, 128, 1, 1, 0, Z, 1, 0, 1, 0),
+    ("RU256 1x1 fwd", 25600, 400, 256, 256, 1, 1, 0, Z, 1, 0, 1, 0),
+    ("RU256 1x1 dgrad", 25600, 400, 256, 256, 1, 1, 0, Z, 0, 1, 0, 0),
     ("down1 256->128 k3", 128000, 2000, 256, 128, 3, 1, 2, Z, 0, 0, 0, 1),
     ("RU256 k7d1 fwd", 25600, 400, 256, 256, 7, 1, 6, Z, 1, 0, 0, 0),
     ("RU256 k7 dgrad", 25600, 400, 256, 256, 7, 1, 0, Z, 0, 1, 1, 0),
