@@ -2186,7 +2186,8 @@ WgPlan wgrad_plan(const sel_conv_desc* d, int mode) {
   p.tiles_per_sample = (d->T + bm - 1) / bm;
   p.n_tiles = (d->rows / d->T) * p.tiles_per_sample;
   const int64_t blocks = int64_t((d->N + bn - 1) / bn) * ((d->C + bc - 1) / bc);
-  const int64_t target = mode == 3 ? 512 : 768;
+  // tune key 10 > 0: workgroup-count target override (A/B sweeps)
+  const int64_t target = tune(10) > 0 ? tune(10) : (mode == 3 ? 512 : 768);
   int64_t want = std::max<int64_t>(1, (target + blocks - 1) / blocks);
   if (mode == 3) want = (want + 7) / 8 * 8;  // splits on x: blocks of one row range share an XCD
   const int64_t per_split = (int64_t(d->N) * d->K * d->C + d->N) * 4;

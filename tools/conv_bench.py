@@ -133,6 +133,19 @@ def run_wgrad(shape, variant, iters=10):
 
 
 def main_wgrad():
+    targets = [int(t) for t in os.environ.get("WG_TARGETS", "").split(",") if t]
+    if targets:  # sweep the workgroup-count target (tune key 10) of the default path
+        print("\n| wgrad shape | " + " | ".join(f"t{t}" for t in targets) + " |")
+        print("|---" * (len(targets) + 1) + "|")
+        for sh in WG_SHAPES:
+            cells = []
+            for t in targets:
+                L.lib().sel_tune(10, t)
+                us = run_wgrad(sh, 0)
+                cells.append("-" if us is None else f"{us:.1f}")
+            L.lib().sel_tune(10, 0)
+            print(f"| {sh[0]} | " + " | ".join(cells) + " |", flush=True)
+        return
     print("\n| wgrad shape | fast (us) | generic (us) | GB/s | TF/s |\n|---|---|---|---|---|")
     for sh in WG_SHAPES:
         name, rows, T, C, N, K, dil, pad, mode, elu, aux, res, bias = sh
