@@ -522,6 +522,12 @@ struct Thin {
   static constexpr size_t LDS_STAGE = size_t(PLANES) * SPAN * F4_P * 2;
   static constexpr size_t LDS_OUT = size_t(R) * OP * 4;
   static constexpr size_t LDS = LDS_STAGE > LDS_OUT ? LDS_STAGE : LDS_OUT;
+  // epilogue-operand prefetch: EJ 16-B vectors per lane and operand, held in
+  // VGPRs across the MFMA phase.  Only where it costs no occupancy (measured
+  // with -Rpass-analysis=kernel-resource-usage): the 32-channel k7 instance
+  // at 256 rows stays at 2 waves/SIMD; every other instance would drop a wave.
+  static constexpr int EJ = (R * (N / 8) + 255) / 256;
+  static constexpr bool EPF = C == 32 && N == 32 && K == 7 && R == 256;
   static_assert(N == 32 || N == 64 || N == 128, "thin kernel: N in {32, 64, 128}");
   static_assert(C % 32 == 0 && WR % 32 == 0, "thin kernel tiling");
   static_assert(LDS <= 64 * 1024, "thin kernel LDS");
@@ -533,7 +539,7 @@ __global__ __launch_bounds__(256) void k_conv_thin_bf16(Args a, const __bf16* __
                                                         const float* __restrict__ bias,
                                                         const __bf16* __restrict__ aux,
                                                         const __bf16* __restrict__ res, __bf16* __restrict__ out,
-                                                        int tiles_per_block) {
+                                                        int tiles_per_block, int epi_pf) {
   using G = Thin<C, N, K, R>;
   constexpr int P = F4_P;
   constexpr int CV = G::CV;
@@ -607,6 +613,26 @@ __global__ __launch_bounds__(256) void k_conv_thin_bf16(Args a, const __bf16* __
     __syncthreads();
     if (tile + 1 < tile_end) load(tile + 1);
 
+    // this tile's epilogue operands (ELU'(aux), residual), fetched before the
+    // MFMA phase so their HBM latency hides behind it instead of stalling the
+    // epilogue (N <= 64: <= 8 16-B vectors per lane per operand)
+    const int64_t eb = tile / tps;
+    const int et0 = int(tile % tps) * R;
+    const int emrows = a.T - et0 < R ? a.T - et0 : R;
+    const int64_t eobase = (eb * a.T + et0) * N;
+    uint4 apf[G::EPF ? G::EJ : 1], rpf[G::EPF ? G::EJ : 1];
+    if constexpr (G::EPF) {
+      if (epi_pf) {
+#pragma unroll
+        for (int j = 0; j < G::EJ; ++j) {
+          const int idx = tid + j * 256, r = idx / (N / 8), n = (idx % (N / 8)) * 8;
+          const int64_t o = eobase + int64_t(r) * N + n;
+          if (aux && r < emrows) apf[j] = *reinterpret_cast<const uint4*>(aux + o);
+          if (res && r < emrows) rpf[j] = *reinterpret_cast<const uint4*>(res + o);
+        }
+      }
+    }
+
     floatx16 acc[G::TM];
 #pragma unroll
     for (int i = 0; i < G::TM; ++i)
@@ -646,7 +672,7 @@ __global__ __launch_bounds__(256) void k_conv_thin_bf16(Args a, const __bf16* __
     const int mrows = a.T - t0 < R ? a.T - t0 : R;
     const int64_t obase = (b * a.T + t0) * N;
     constexpr int GN = N / 8;
-    for (int idx = tid; idx < mrows * GN; idx += 256) {
+    auto epilogue = [&](int idx, const uint4* apv, const uint4* rpv) {
       const int r = idx / GN, n = (idx % GN) * 8;
       const floatx4 lo = *reinterpret_cast<const floatx4*>(ot + r * G::OP + n);
       const floatx4 hi = *reinterpret_cast<const floatx4*>(ot + r * G::OP + n + 4);
@@ -662,13 +688,13 @@ __global__ __launch_bounds__(256) void k_conv_thin_bf16(Args a, const __bf16* __
       }
       const int64_t o = obase + int64_t(r) * N + n;
       if (aux) {
-        uint4 raw = *reinterpret_cast<const uint4*>(aux + o);
+        uint4 raw = apv ? *apv : *reinterpret_cast<const uint4*>(aux + o);
         const __bf16* av = reinterpret_cast<const __bf16*>(&raw);
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] *= elu_grad_fast(float(av[e]));
       }
       if (res) {
-        uint4 raw = *reinterpret_cast<const uint4*>(res + o);
+        uint4 raw = rpv ? *rpv : *reinterpret_cast<const uint4*>(res + o);
         const __bf16* rv = reinterpret_cast<const __bf16*>(&raw);
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] += float(rv[e]);
@@ -678,6 +704,13 @@ __global__ __launch_bounds__(256) void k_conv_thin_bf16(Args a, const __bf16* __
 #pragma unroll
       for (int e = 0; e < 8; ++e) op[e] = __bf16(v[e]);
       *reinterpret_cast<uint4*>(out + o) = ov;
+    };
+    if (G::EPF && epi_pf) {
+#pragma unroll
+      for (int j = 0; j < (G::EPF ? G::EJ : 1); ++j)
+        if (tid + j * 256 < mrows * GN) epilogue(tid + j * 256, &apf[j], &rpf[j]);
+    } else {
+      for (int idx = tid; idx < mrows * GN; idx += 256) epilogue(idx, nullptr, nullptr);
     }
   }
 }
@@ -2002,7 +2035,7 @@ int launch_thin(const Args& a, const void* in, const void* wp, const float* bias
   hipLaunchKernelGGL((k_conv_thin_bf16<C, N, K, R>), dim3(nb), dim3(256), G::LDS, s, a,
                      static_cast<const __bf16*>(in), static_cast<const __bf16*>(wp), bias,
                      static_cast<const __bf16*>(aux), static_cast<const __bf16*>(res), static_cast<__bf16*>(out),
-                     int(tpb));
+                     int(tpb), tune(11) == 0 ? 1 : 0);
   SEL_LAUNCH_CHECK();
   return SEL_OK;
 }
