@@ -528,6 +528,9 @@ struct Thin {
   // at 256 rows stays at 2 waves/SIMD; every other instance would drop a wave.
   static constexpr int EJ = (R * (N / 8) + 255) / 256;
   static constexpr bool EPF = C == 32 && N == 32 && K == 7 && R == 256;
+  // split tile loop (separate staging and out tiles in LDS): same instance
+  static constexpr bool SPLIT = EPF && LDS_STAGE + LDS_OUT <= 64 * 1024;
+  static constexpr size_t LDS_TOTAL = SPLIT ? LDS_STAGE + LDS_OUT : LDS;
   static_assert(N == 32 || N == 64 || N == 128, "thin kernel: N in {32, 64, 128}");
   static_assert(C % 32 == 0 && WR % 32 == 0, "thin kernel tiling");
   static_assert(LDS <= 64 * 1024, "thin kernel LDS");
@@ -545,7 +548,9 @@ __global__ __launch_bounds__(256) void k_conv_thin_bf16(Args a, const __bf16* __
   constexpr int CV = G::CV;
   extern __shared__ __align__(16) unsigned char smem[];
   __bf16* const xs = reinterpret_cast<__bf16*>(smem);  // [PLANES][SPAN][P]
-  float* const ot = reinterpret_cast<float*>(smem);      // [R][OP], aliases xs
+  // [R][OP] fp32 out tile: aliases xs, or follows it when the tile loop is split
+  float* const ot = reinterpret_cast<float*>(smem + (G::SPLIT ? G::LDS_STAGE : 0));
+  const bool split = G::SPLIT && (epi_pf & 2);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -607,11 +612,18 @@ __global__ __launch_bounds__(256) void k_conv_thin_bf16(Args a, const __bf16* __
 
   const bool bias_vec = bias && a.bias_period && (a.bias_period % 8) == 0;
   load(tile0);
-  for (int64_t tile = tile0; tile < tile_end; ++tile) {
-    __syncthreads();  // the previous tile's epilogue is done with ot (= xs)
+  if (split) {
     store();
     __syncthreads();
-    if (tile + 1 < tile_end) load(tile + 1);
+    if (tile0 + 1 < tile_end) load(tile0 + 1);
+  }
+  for (int64_t tile = tile0; tile < tile_end; ++tile) {
+    if (!split) {
+      __syncthreads();  // the previous tile's epilogue is done with ot (= xs)
+      store();
+      __syncthreads();
+      if (tile + 1 < tile_end) load(tile + 1);
+    }
 
     // this tile's epilogue operands (ELU'(aux), residual), fetched before the
     // MFMA phase so their HBM latency hides behind it instead of stalling the
@@ -622,7 +634,7 @@ __global__ __launch_bounds__(256) void k_conv_thin_bf16(Args a, const __bf16* __
     const int64_t eobase = (eb * a.T + et0) * N;
     uint4 apf[G::EPF ? G::EJ : 1], rpf[G::EPF ? G::EJ : 1];
     if constexpr (G::EPF) {
-      if (epi_pf) {
+      if (epi_pf & 1) {
 #pragma unroll
         for (int j = 0; j < G::EJ; ++j) {
           const int idx = tid + j * 256, r = idx / (N / 8), n = (idx % (N / 8)) * 8;
@@ -653,7 +665,7 @@ __global__ __launch_bounds__(256) void k_conv_thin_bf16(Args a, const __bf16* __
     }
 
     // accumulators (out^T: lane -> row, element r -> channel) -> fp32 tile in LDS
-    __syncthreads();  // every wave is done reading xs
+    __syncthreads();  // every wave is done reading xs (split: and the last epilogue with ot)
 #pragma unroll
     for (int i = 0; i < G::TM; ++i) {
       const int row = rg * G::WR + i * 32 + (lane & 31);
@@ -664,7 +676,11 @@ __global__ __launch_bounds__(256) void k_conv_thin_bf16(Args a, const __bf16* __
             floatx4{acc[i][4 * g], acc[i][4 * g + 1], acc[i][4 * g + 2], acc[i][4 * g + 3]};
       }
     }
+    // split loop: the next tile is staged beside this tile's out tile, so a
+    // tile costs two barriers and its epilogue overlaps the next MFMA phase
+    if (split && tile + 1 < tile_end) store();
     __syncthreads();
+    if (split && tile + 2 < tile_end) load(tile + 2);
 
     // coalesced epilogue: a sample-aligned tile's output rows are contiguous in HBM
     const int64_t b = tile / tps;
@@ -705,7 +721,7 @@ __global__ __launch_bounds__(256) void k_conv_thin_bf16(Args a, const __bf16* __
       for (int e = 0; e < 8; ++e) op[e] = __bf16(v[e]);
       *reinterpret_cast<uint4*>(out + o) = ov;
     };
-    if (G::EPF && epi_pf) {
+    if (G::EPF && (epi_pf & 1)) {
 #pragma unroll
       for (int j = 0; j < (G::EPF ? G::EJ : 1); ++j)
         if (tid + j * 256 < mrows * GN) epilogue(tid + j * 256, &apf[j], &rpf[j]);
@@ -2032,10 +2048,10 @@ int launch_thin(const Args& a, const void* in, const void* wp, const float* bias
   const int64_t target = tune(5) > 0 ? tune(5) : 1024;
   const int64_t tpb = std::max<int64_t>(1, (ntiles + target - 1) / target);
   const unsigned nb = unsigned(((ntiles + tpb - 1) / tpb + 7) / 8 * 8);  // multiple of 8 (XCD map)
-  hipLaunchKernelGGL((k_conv_thin_bf16<C, N, K, R>), dim3(nb), dim3(256), G::LDS, s, a,
+  hipLaunchKernelGGL((k_conv_thin_bf16<C, N, K, R>), dim3(nb), dim3(256), G::LDS_TOTAL, s, a,
                      static_cast<const __bf16*>(in), static_cast<const __bf16*>(wp), bias,
                      static_cast<const __bf16*>(aux), static_cast<const __bf16*>(res), static_cast<__bf16*>(out),
-                     int(tpb), tune(11) == 0 ? 1 : 0);
+                     int(tpb), 3 & ~tune(11));
   SEL_LAUNCH_CHECK();
   return SEL_OK;
 }

@@ -301,6 +301,38 @@ def test_thin_kernel_matches_tiled(gpu, shape):
         assert e < 4e-3, (pad, e)
 
 
+@pytest.mark.parametrize("epi", [0, 1, 2, 3])
+@pytest.mark.parametrize("shape", [(32, 32, 7, 9, 0, 1, 0, 0, 0, 3, 1000), (32, 32, 7, 9, 0, 0, 1, 1, 0, 2, 777),
+                                   (32, 32, 7, 1, 0, 0, 1, 0, 0, 5, 600)],
+                         ids=lambda s: "C{}N{}K{}d{}a{}r{}T{}".format(*s[:4], s[6], s[7], s[10]))
+def test_thin_kernel_multi_tile_loops(gpu, shape, epi):
+    """Many tiles per workgroup (tune key 5 = 3 workgroups): the thin kernel's
+    tile loop with and without the epilogue-operand prefetch and the split
+    (two-barrier) loop (tune key 11 bits), across batch boundaries and ragged
+    tails, equals the single-tile-per-workgroup launch bit for bit (same
+    per-tile arithmetic, only the schedule differs)."""
+    from sel import _lib as L
+    from sel import convops as CO
+    C, N, K, dil, mode, elu, aux, res, bias, B, T = shape
+    torch.manual_seed(T + epi)
+    lib = L.lib()
+    for pad in ((K - 1) * dil, 0):
+        d = CO.ConvDesc(B * T, T, C, N, K, dil, pad, mode, elu, bias)
+        x = torch.randn(B * T, C, device=gpu).to(torch.bfloat16)
+        wp = (0.2 * torch.randn(N, K, C, device=gpu)).to(torch.bfloat16)
+        a_ = torch.randn(B * T, N, device=gpu).to(torch.bfloat16) if aux else None
+        r_ = torch.randn(B * T, N, device=gpu).to(torch.bfloat16) if res else None
+        assert CO.fwd_kernel_name(d, torch.bfloat16, torch.bfloat16).startswith("k_conv_thin_bf16")
+        ref = CO.prim(d, x, wp, aux=a_, res=r_).clone()
+        p5, p11 = lib.sel_tune(5, 3), lib.sel_tune(11, epi)
+        try:
+            got = CO.prim(d, x, wp, aux=a_, res=r_).clone()
+        finally:
+            lib.sel_tune(5, p5)
+            lib.sel_tune(11, p11)
+        assert torch.equal(got, ref), (pad, (got.float() - ref.float()).abs().max().item())
+
+
 # (C, dil, bias, B, T): the fused residual-unit forward's instances at the
 # AudioDec dilations, ragged tails (T not a multiple of the tile rows) and T < halo
 RU_SHAPES = [(32, 1, 0, 2, 1000), (32, 3, 0, 3, 777), (32, 9, 1, 2, 1000), (32, 9, 0, 2, 40),
