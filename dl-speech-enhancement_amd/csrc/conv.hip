@@ -510,7 +510,7 @@ __global__ __launch_bounds__(256) void k_conv_fwd_bf16(Args a, const __bf16* __r
 //   -> accumulators -> LDS (fp32) -> one fully coalesced 16-B epilogue pass
 //      (bias, ELU'(aux), residual) over the tile's contiguous output rows.
 // ---------------------------------------------------------------------------
-template <int C, int N, int K, int R>
+template <int C, int N, int K, int R, bool E = false>
 struct Thin {
   static constexpr int PLANES = C / 32;
   static constexpr int NS = N / 32, RG = 4 / NS;
@@ -522,13 +522,12 @@ struct Thin {
   static constexpr size_t LDS_STAGE = size_t(PLANES) * SPAN * F4_P * 2;
   static constexpr size_t LDS_OUT = size_t(R) * OP * 4;
   static constexpr size_t LDS = LDS_STAGE > LDS_OUT ? LDS_STAGE : LDS_OUT;
-  // epilogue-operand prefetch: EJ 16-B vectors per lane and operand, held in
-  // VGPRs across the MFMA phase.  Only where it costs no occupancy (measured
-  // with -Rpass-analysis=kernel-resource-usage): the 32-channel k7 instance
-  // at 256 rows stays at 2 waves/SIMD; every other instance would drop a wave.
+  // E: epilogue-operand prefetch, EJ 16-B vectors per lane and operand held
+  // in VGPRs across the MFMA phase (costs up to 8*EJ VGPRs, i.e. occupancy on
+  // some instances: chosen per instance, kThinEpfDefault), plus the split
+  // tile loop (separate staging and out tiles in LDS) where both fit in 64 KB
   static constexpr int EJ = (R * (N / 8) + 255) / 256;
-  static constexpr bool EPF = C == 32 && N == 32 && K == 7 && R == 256;
-  // split tile loop (separate staging and out tiles in LDS): same instance
+  static constexpr bool EPF = E && EJ <= 8;
   static constexpr bool SPLIT = EPF && LDS_STAGE + LDS_OUT <= 64 * 1024;
   static constexpr size_t LDS_TOTAL = SPLIT ? LDS_STAGE + LDS_OUT : LDS;
   static_assert(N == 32 || N == 64 || N == 128, "thin kernel: N in {32, 64, 128}");
@@ -536,14 +535,14 @@ struct Thin {
   static_assert(LDS <= 64 * 1024, "thin kernel LDS");
 };
 
-template <int C, int N, int K, int R>
+template <int C, int N, int K, int R, bool E>
 __global__ __launch_bounds__(256) void k_conv_thin_bf16(Args a, const __bf16* __restrict__ in,
                                                         const __bf16* __restrict__ wp,
                                                         const float* __restrict__ bias,
                                                         const __bf16* __restrict__ aux,
                                                         const __bf16* __restrict__ res, __bf16* __restrict__ out,
                                                         int tiles_per_block, int epi_pf) {
-  using G = Thin<C, N, K, R>;
+  using G = Thin<C, N, K, R, E>;
   constexpr int P = F4_P;
   constexpr int CV = G::CV;
   extern __shared__ __align__(16) unsigned char smem[];
@@ -2039,16 +2038,16 @@ int fwd4_variant(int v, const Args& a, const void* in, const void* wp, const flo
 // has no instance.
 constexpr int kNotThin = 1;
 
-template <int C, int N, int K, int R>
+template <int C, int N, int K, int R, bool E>
 int launch_thin(const Args& a, const void* in, const void* wp, const float* bias, const void* aux,
                 const void* res, void* out, hipStream_t s) {
-  using G = Thin<C, N, K, R>;
+  using G = Thin<C, N, K, R, E>;
   const int64_t ntiles = (a.rows / a.T) * ((a.T + R - 1) / R);
   if (ntiles == 0) return SEL_OK;
   const int64_t target = tune(5) > 0 ? tune(5) : 1024;
   const int64_t tpb = std::max<int64_t>(1, (ntiles + target - 1) / target);
   const unsigned nb = unsigned(((ntiles + tpb - 1) / tpb + 7) / 8 * 8);  // multiple of 8 (XCD map)
-  hipLaunchKernelGGL((k_conv_thin_bf16<C, N, K, R>), dim3(nb), dim3(256), G::LDS_TOTAL, s, a,
+  hipLaunchKernelGGL((k_conv_thin_bf16<C, N, K, R, E>), dim3(nb), dim3(256), G::LDS_TOTAL, s, a,
                      static_cast<const __bf16*>(in), static_cast<const __bf16*>(wp), bias,
                      static_cast<const __bf16*>(aux), static_cast<const __bf16*>(res), static_cast<__bf16*>(out),
                      int(tpb), 3 & ~tune(11));
@@ -2084,15 +2083,29 @@ int thin_rows(const Args& a) {
   return 0;
 }
 
+// measured per layer (tools/conv_bench.py 30 34 35 36 37, profiles/r1_conv_bench_epf.md):
+// the prefetch pays on the k7 dgrads (ELU'(aux) operand) at 32 channels /
+// 256 rows (113 -> 88 us) and 64 channels / 64 rows (77 -> 72 us); on the
+// 1x1 and strided instances the VGPRs it takes cost more occupancy than it hides
+constexpr int kThinEpfDefault = 0b101;  // instances 0 and 2
+constexpr int kThinEpfAlt = 0b100;      // instance 2 on its 64-row tiles
+
 int dispatch_thin(const Args& a, const void* in, const void* wp, const float* bias, const void* aux,
                   const void* res, void* out, hipStream_t s) {
   const int i = thin_index(a);
   if (i < 0) return kNotThin;
-  const bool alt = (tune(6) >> i) & 1;
+  // epilogue prefetch + split loop: only for launches with epilogue operands
+  // (aux and/or res), per instance by kThinEpfDefault (key 12 bit i flips
+  // instance i, key 11 bit 0 forces it off); kThinEpfAlt instances run it on
+  // their alternative tile rows
+  const bool epf = (aux || res) && ((kThinEpfDefault ^ tune(12)) >> i & 1) && !(tune(11) & 1);
+  const bool alt = (((tune(6) >> i) & 1) != 0) != (epf && ((kThinEpfAlt >> i) & 1));
 #define SEL_THIN_LAUNCH(I_, C_, N_, K_, R_, R2_)                                             \
   if (i == I_)                                                                               \
-    return alt ? launch_thin<C_, N_, K_, R2_>(a, in, wp, bias, aux, res, out, s)            \
-               : launch_thin<C_, N_, K_, R_>(a, in, wp, bias, aux, res, out, s);
+    return epf ? (alt ? launch_thin<C_, N_, K_, R2_, true>(a, in, wp, bias, aux, res, out, s)   \
+                      : launch_thin<C_, N_, K_, R_, true>(a, in, wp, bias, aux, res, out, s))   \
+               : (alt ? launch_thin<C_, N_, K_, R2_, false>(a, in, wp, bias, aux, res, out, s)  \
+                      : launch_thin<C_, N_, K_, R_, false>(a, in, wp, bias, aux, res, out, s));
   SEL_THIN_SHAPES(SEL_THIN_LAUNCH)
 #undef SEL_THIN_LAUNCH
   return kNotThin;

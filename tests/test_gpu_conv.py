@@ -303,7 +303,8 @@ def test_thin_kernel_matches_tiled(gpu, shape):
 
 @pytest.mark.parametrize("epi", [0, 1, 2, 3])
 @pytest.mark.parametrize("shape", [(32, 32, 7, 9, 0, 1, 0, 0, 0, 3, 1000), (32, 32, 7, 9, 0, 0, 1, 1, 0, 2, 777),
-                                   (32, 32, 7, 1, 0, 0, 1, 0, 0, 5, 600)],
+                                   (32, 32, 7, 1, 0, 0, 1, 0, 0, 5, 600), (64, 64, 7, 3, 0, 0, 1, 1, 0, 3, 800),
+                                   (64, 64, 7, 1, 0, 0, 1, 0, 0, 2, 333)],
                          ids=lambda s: "C{}N{}K{}d{}a{}r{}T{}".format(*s[:4], s[6], s[7], s[10]))
 def test_thin_kernel_multi_tile_loops(gpu, shape, epi):
     """Many tiles per workgroup (tune key 5 = 3 workgroups): the thin kernel's

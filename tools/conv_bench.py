@@ -58,10 +58,16 @@ def run(shape, variant, iters=20):
     # 30 default, 31 one tile per workgroup (key 5), 32 alternative tile rows
     # (key 6), 33 both; any other variant runs with the thin kernel off so the
     # tiled variants stay comparable
-    thin = 30 <= variant <= 33
+    # 34/35: default rows with the epilogue prefetch (+ split loop) on / off for
+    # every instance with epilogue operands (key 12 flips kThinEpfDefault =
+    # 0b101, key 11 bit 0 = off); 36/37: the same with key 6 flipping every
+    # instance's tile rows (kThinEpfAlt instances flip back under 34/36)
+    thin = 30 <= variant <= 37
     L.lib().sel_tune(4, 0 if thin else 1)
     L.lib().sel_tune(5, 1 << 30 if variant in (31, 33) else 0)
-    L.lib().sel_tune(6, 63 if variant in (32, 33) else 0)
+    L.lib().sel_tune(6, 127 if variant in (32, 33, 36, 37) else 0)
+    L.lib().sel_tune(12, 127 ^ 0b101 if variant in (34, 36) else 0)
+    L.lib().sel_tune(11, 1 if variant in (35, 37) else 0)
     L.lib().sel_tune(0, 0 if thin else variant)
     try:
         for _ in range(3):
@@ -98,7 +104,7 @@ def main():
         cells = " | ".join("-" if t is None else f"{t:.1f}" for t in times)
         print(f"| {name} | {cells} | v{best_v} | {nbytes / best_t / 1e3:.0f} | {flops / best_t / 1e6:.0f} |",
               flush=True)
-    for key in (0, 4, 5, 6, 7):
+    for key in (0, 4, 5, 6, 7, 11, 12):
         L.lib().sel_tune(key, 0)
 
 
