@@ -211,10 +211,13 @@ def pmc_traffic(tag, B, steps_cfg="c3"):
     frag = _mangled_fragment(tag)
     with open(PMC_FILE) as f:
         table = json.load(f)
+    # a tag can cover several compiled variants (e.g. the thin kernel's
+    # epilogue-prefetch template flag: ...ELb0E / ...ELb1E): launch-weighted mean
     hits = [v for k, v in table.items() if frag in k or k.split("(")[0].endswith(tag)]
-    if len(hits) != 1:
+    if not hits:
         return None
-    return hits[0]["traffic_bytes_per_launch"]
+    n = sum(v["launches"] for v in hits)
+    return int(sum(v["traffic_bytes_per_launch"] * v["launches"] for v in hits) / n)
 
 
 def roofline(cfg, timer, dom, B, steps):
