@@ -1000,21 +1000,40 @@ FrameArgs frame_args(int64_t B, int64_t T, int n_fft, int hop, int win) {
 
 // Launch plan of the wave-FFT kernels: FPB frames per block iteration, `iters`
 // iterations per block (enough blocks to fill 256 CUs 8 deep first).
+// Frame groups per block.  A block pays a fixed prologue (per-lane twiddles and
+// window from the tables, the first frame's fetch) before its frame loop
+// pipelines, and blocks of one launch take near-equal time, so a grid slightly
+// larger than the resident-block capacity (`slots`) costs a whole extra round
+// for its tail.  Default: one round, iters = ceil(groups / slots) (measured at
+// B = 512, 1024/120/600: 117 us at 8 iters -> 98-100 us).  tune key 14: -1 = the
+// earlier rule (<= 8 iters, >= 2048 groups per iter), > 0 = fixed iters.
 template <int LOGN>
-unsigned frame_grid(int64_t nframes, int& iters) {
+unsigned frame_grid(int64_t nframes, int& iters, int64_t slots = 0) {
   using G = Geo<LOGN>;
   const int64_t groups = (nframes + G::FPB - 1) / G::FPB;
-  iters = int(std::max<int64_t>(1, std::min<int64_t>(8, groups / 2048)));
+  if (tune(14) > 0) {
+    iters = tune(14);
+  } else if (tune(14) == -1 || slots <= 0) {
+    iters = int(std::max<int64_t>(1, std::min<int64_t>(8, groups / 2048)));
+  } else {
+    iters = int(std::max<int64_t>(1, (groups + slots - 1) / slots));
+  }
   return unsigned((groups + iters - 1) / iters);
 }
 
-unsigned frame_grid_rt(int logn, int64_t nframes, int& iters) {
-  switch (logn) {
-    case 8: return frame_grid<8>(nframes, iters);
-    case 9: return frame_grid<9>(nframes, iters);
-    case 10: return frame_grid<10>(nframes, iters);
-    default: return frame_grid<11>(nframes, iters);
-  }
+// grid of the last SEL_FRAME_DISPATCH on this thread (per-block partial counts)
+thread_local unsigned t_last_frame_grid = 0;
+
+// resident-block capacity of a frame kernel at `lds` bytes per block (cached
+// per call site by the dispatch macro)
+template <typename KerT>
+int64_t frame_slots(KerT ker, size_t lds) {
+  int dev = 0, cus = 0, per_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ker, 256, lds) != hipSuccess)
+    return 0;
+  return int64_t(cus) * per_cu;
 }
 
 // dispatch helper: one template kernel family over LOGN in [8, 11]; the kernel's
@@ -1024,8 +1043,10 @@ unsigned frame_grid_rt(int logn, int64_t nframes, int& iters) {
   case L: {                                                                                   \
     using G = Geo<L>;                                                                         \
     int iters;                                                                                \
-    const unsigned grid = frame_grid<L>(nframes, iters);                                      \
     const size_t lds = size_t(G::FPB) * (G::PADN * sizeof(float2) + size_t(extra) * sizeof(float)); \
+    static const int64_t slots = frame_slots(KER<L>, lds);                                    \
+    const unsigned grid = frame_grid<L>(nframes, iters, slots);                               \
+    t_last_frame_grid = grid;                                                                 \
     if (grid) hipLaunchKernelGGL(KER<L>, dim3(grid), dim3(256), lds, stream, __VA_ARGS__, iters); \
   } break;
 
@@ -1158,8 +1179,7 @@ int sel_stft_loss_fwd(const float* x, const float* y, int64_t B, int64_t T, int 
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   double* part = static_cast<double*>(ws);
   SEL_FRAME_DISPATCH(logn, nf, s, k_stft_loss_fwd, x, y, a, window, 1e-7f, part);
-  int iters;
-  const int nb = int(frame_grid_rt(logn, nf, iters));
+  const int nb = int(t_last_frame_grid);  // one partial triple per block of that launch
   hipLaunchKernelGGL(k_finish_partials, dim3(1), dim3(256), 0, s, part, nb, 3, sums, nullptr, 0.0);
   SEL_LAUNCH_CHECK();
   return SEL_OK;
@@ -1261,8 +1281,8 @@ int sel_logmel_bwd(const float* x, int64_t B, int64_t T, int n_fft, int hop, int
     case L: {                                                                                           \
       using G = Geo<L>;                                                                                 \
       int iters;                                                                                        \
-      const unsigned grid = frame_grid<L>(nf, iters);                                                   \
       const size_t lds = size_t(G::FPB) * (G::PADN * sizeof(float2) + size_t(glin) * sizeof(float));    \
+      const unsigned grid = frame_grid<L>(nf, iters, frame_slots(k_logmel_bwd<L>, lds));               \
       if (grid)                                                                                         \
         hipLaunchKernelGGL(k_logmel_bwd<L>, dim3(grid), dim3(256), lds, s, x, a, window, ma,           \
                            reinterpret_cast<const int2*>(krange), g_out, ref, g_scale, g_mul, slab, iters, \
