@@ -2044,7 +2044,19 @@ int launch_thin(const Args& a, const void* in, const void* wp, const float* bias
   using G = Thin<C, N, K, R, E>;
   const int64_t ntiles = (a.rows / a.T) * ((a.T + R - 1) / R);
   if (ntiles == 0) return SEL_OK;
-  const int64_t target = tune(5) > 0 ? tune(5) : 1024;
+  // one round of resident workgroups (each pays the weight-fragment prologue
+  // once; a grid just past the resident capacity would add a whole round for
+  // its tail); tune key 5 > 0 overrides the workgroup target
+  static const int64_t slots = [] {
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_conv_thin_bf16<C, N, K, R, E>, 256, G::LDS_TOTAL) !=
+            hipSuccess)
+      return int64_t(0);
+    return int64_t(cus) * per_cu / 8 * 8;
+  }();
+  const int64_t target = tune(5) > 0 ? tune(5) : (slots > 0 ? slots : 1024);
   const int64_t tpb = std::max<int64_t>(1, (ntiles + target - 1) / target);
   const unsigned nb = unsigned(((ntiles + tpb - 1) / tpb + 7) / 8 * 8);  // multiple of 8 (XCD map)
   hipLaunchKernelGGL((k_conv_thin_bf16<C, N, K, R, E>), dim3(nb), dim3(256), G::LDS_TOTAL, s, a,
