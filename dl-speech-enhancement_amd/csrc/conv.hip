@@ -1680,8 +1680,29 @@ __global__ __launch_bounds__(256) void k_split_sum1(const float* __restrict__ pa
   if (i >= n) return;
   const int s0 = blockIdx.y * SPLIT_GROUP;
   const int s1 = s0 + SPLIT_GROUP < nsplit ? s0 + SPLIT_GROUP : nsplit;
+  const float* p = part + int64_t(s0) * n + i;
   float acc = 0.f;
-  for (int sp = s0; sp < s1; ++sp) acc += part[int64_t(sp) * n + i];
+  if (s1 - s0 == SPLIT_GROUP) {
+    // a full group: all 32 loads in flight at once (a serial chain of dependent
+    // adds made the compiler issue them a few at a time: latency-bound), then a
+    // fixed pairwise tree (deterministic)
+    float v[SPLIT_GROUP];
+#pragma unroll
+    for (int u = 0; u < SPLIT_GROUP; ++u) v[u] = p[int64_t(u) * n];
+#pragma unroll
+    for (int w = 1; w < SPLIT_GROUP; w *= 2)
+#pragma unroll
+      for (int u = 0; u < SPLIT_GROUP; u += 2 * w) v[u] += v[u + w];
+    acc = v[0];
+  } else {
+    int u = 0;
+    for (; u + 4 <= s1 - s0; u += 4) {
+      const float a0 = p[int64_t(u) * n], a1 = p[int64_t(u + 1) * n], a2 = p[int64_t(u + 2) * n],
+                  a3 = p[int64_t(u + 3) * n];
+      acc += (a0 + a1) + (a2 + a3);
+    }
+    for (; u < s1 - s0; ++u) acc += p[int64_t(u) * n];
+  }
   part2[int64_t(blockIdx.y) * n + i] = acc;
 }
 
