@@ -1857,8 +1857,15 @@ __global__ __launch_bounds__(256) void k_split_sum2_unpack(const float* __restri
   const int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x;
   if (i >= n_torch) return;
   const int64_t j = unpack_src(kind, i, cout, cin, K, s);
+  const float* p = part2 + j;
   float acc = 0.f;
-  for (int g = 0; g < ngroups; ++g) acc += part2[int64_t(g) * n + j];
+  int g = 0;
+  for (; g + 4 <= ngroups; g += 4) {  // 4 loads in flight, fixed order
+    const float a0 = p[int64_t(g) * n], a1 = p[int64_t(g + 1) * n], a2 = p[int64_t(g + 2) * n],
+                a3 = p[int64_t(g + 3) * n];
+    acc += (a0 + a1) + (a2 + a3);
+  }
+  for (; g < ngroups; ++g) acc += p[int64_t(g) * n];
   gw[i] = acc;
 }
 
