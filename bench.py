@@ -126,6 +126,10 @@ def c3_setup(dev, B, world, local, graph=False):
     opt_kw = dict(cfg["generator_optimizer_params"])
     if graph:
         opt_kw["capturable"] = True  # step count on device: the update replays inside a HIP graph
+    if os.environ.get("SEL_ADAM_FOREACH", "0") != "1":
+        # one fused multi-tensor Adam launch instead of torch's 7 foreach passes
+        # (128 us/step at C3, profiles/r1_c3_v22_kernel_stats.md); same update rule
+        opt_kw.setdefault("fused", True)
     opt = torch.optim.Adam(G.parameters(), **opt_kw)
     sched = torch.optim.lr_scheduler.StepLR(opt, **cfg["generator_scheduler_params"])
     tr = Trainer(steps=0, epochs=0, data_loader={}, model=model, criterion={"mel": mel},

@@ -78,8 +78,12 @@ class DenoiseStep:
                       else GeneratorAudioDec(**config["generator_params"]).to(device),
                       "discriminator": discriminator}
         gen = self.model["generator"]
+        # on the GPU: torch's fused multi-tensor Adam (one launch per step, same update rule)
+        opt_kw = dict(config["generator_optimizer_params"])
+        if next(gen.parameters()).is_cuda:
+            opt_kw.setdefault("fused", True)
         self.optimizer = {"generator": optimizer if optimizer is not None
-                          else torch.optim.Adam(gen.parameters(), **config["generator_optimizer_params"])}
+                          else torch.optim.Adam(gen.parameters(), **opt_kw)}
         self.measures = {"MAE": nn.L1Loss(), "SNR": SignalNoiseRatio(),
                          "Mel-loss": MultiMelSpectrogramLoss(**config["mel_loss_params"]).to(device)}
         self.discriminator_enabled = False
