@@ -45,6 +45,27 @@ def synthetic_batch(B, T, seed=93):
     return torch.from_numpy(clean), torch.from_numpy(noise)
 
 
+def _median_time(step, steps):
+    ts = []
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        step()
+        ts.append(time.perf_counter() - t0)
+    return float(np.median(ts))
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown CPU"
+
+
 # ---------------------------------------------------------------------------
 # c2: spectral losses only
 # ---------------------------------------------------------------------------
@@ -72,7 +93,7 @@ def c2_bytes_per_launch(name, B):
     return 2 * 4 * B * SR
 
 
-def c2_cpu_baseline(B_sample=4, steps=3):
+def c2_cpu_baseline(B_sample=4, steps=20):
     from oracle import ref_ops as R
     from oracle.melfilters import mel as melbank
     mm = torch.from_numpy(melbank(sr=24000, n_fft=2048, n_mels=80, fmin=0, fmax=24000).T.copy())
@@ -88,11 +109,9 @@ def c2_cpu_baseline(B_sample=4, steps=3):
             + 45.0 * (sc + mg)
         loss.backward()
     step()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        step()
-    dt = (time.perf_counter() - t0) / steps
-    return B_sample * SR / HOP / dt, f"oracle (PyTorch-CPU restatement) c2 losses fwd+bwd, B={B_sample}, {steps} steps"
+    dt = _median_time(step, steps)
+    return B_sample * SR / HOP / dt, (f"oracle (PyTorch-CPU restatement) c2 losses fwd+bwd, B={B_sample}, "
+                                      f"median of {steps} steps, on {_cpu_model()}")
 
 
 # ---------------------------------------------------------------------------
@@ -102,7 +121,7 @@ def c2_cpu_baseline(B_sample=4, steps=3):
 C3_CONFIG = "symAD_libritts_24000_hop300"
 
 
-def c3_setup(dev, B, world, local, graph=False):
+def c3_setup(dev, B, world, local, graph=False, dtype=torch.bfloat16):
     from sel import configs
     from sel.convops import precision
     from models.autoencoder.AudioDec import Generator
@@ -144,12 +163,12 @@ def c3_setup(dev, B, world, local, graph=False):
         mixed = add_noise(clean, noise, 15)
 
     def step():
-        with precision(torch.bfloat16):
+        with precision(dtype):
             tr._train_step((mixed, clean))
     return step
 
 
-def c3_cpu_baseline(B_sample=2, steps=2):
+def c3_cpu_baseline(B_sample=4, steps=20):
     """Oracle (op-for-op PyTorch-CPU restatement) of the same denoise-trainer step."""
     from oracle import ref_ops as R
     from oracle.melfilters import mel as melbank
@@ -178,12 +197,10 @@ def c3_cpu_baseline(B_sample=2, steps=2):
         loss.backward()
         opt.step()
     step()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        step()
-    dt = (time.perf_counter() - t0) / steps
+    dt = _median_time(step, steps)
     return B_sample * SR / HOP / dt, (f"oracle (PyTorch-CPU op-for-op restatement) denoise-trainer step, "
-                                      f"PQC generator fp32, B={B_sample} x 1 s, {steps} timed steps")
+                                      f"PQC generator fp32, B={B_sample} x 1 s, median of {steps} timed steps "
+                                      f"after 1 warm-up, on {_cpu_model()}")
 
 
 # ---------------------------------------------------------------------------
@@ -292,6 +309,63 @@ def stft_kernel_roofline(dev):
             "frac_of_measured": round(gbs / copy_gbs, 4)}
 
 
+def launch_cmd(n, port, argv):
+    """torch.distributed.run command line for N local ranks of this script."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def _relaunch(n):
+    """bench.py --gpus N outside torchrun: start N ranks under
+    torch.distributed.run as a CHILD process and exit with its code.  Runs
+    before anything initialises the GPU (device_count() does not on ROCm)."""
+    import socket
+    import subprocess
+    have = torch.cuda.device_count()
+    if have < n:
+        sys.exit(f"bench.py: --gpus {n} but only {have} GPU(s) visible")
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = launch_cmd(n, port, sys.argv[1:])
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    sys.exit(subprocess.call(cmd, env=env))
+
+
+def _timed_steps(step, steps, world, dev, timer=None):
+    """K steps bracketed by barrier + synchronize; per-step HIP events on the
+    current stream give the per-step durations (max over ranks per step)."""
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+    t0 = time.perf_counter()
+    evs[0].record()
+    for i in range(steps):
+        # per-launch HIP events only in the last timed step: an event pair around
+        # every conv launch of every step costs ~0.6 ms/step (C3) of its own
+        if timer is not None and i == steps - 1:
+            _lib().TIMER = timer
+        step()
+        evs[i + 1].record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    _lib().TIMER = None
+    per = torch.tensor([evs[i].elapsed_time(evs[i + 1]) for i in range(steps)] + [elapsed * 1e3],
+                       dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(per, op=dist.ReduceOp.MAX)
+    per = per.cpu().numpy()
+    return float(per[-1]) * 1e-3, per[:-1]
+
+
+def _lib():
+    from sel import _lib as L
+    return L
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -300,9 +374,14 @@ def main():
     ap.add_argument("--config", default="c3", choices=["c2", "c3"])
     ap.add_argument("--batch", type=int, default=0, help="per-GPU batch (default: config's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-fp32-companion", action="store_true")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        _relaunch(args.gpus)
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
@@ -316,47 +395,38 @@ def main():
     if cfg == "c2":
         step = c2_setup(dev, B)
         dom = "sel_stft_loss_fwd"
-        bytes_fn = c2_bytes_per_launch
         workload = "configs[1]: MR-STFT(3 res) + mel(2048/300/80) loss fwd+bwd, fp32, 1 s @ 24 kHz"
         dtype = "fp32"
     else:
         step = c3_setup(dev, B, world, local)
         dom = "sel_conv_fwd"
-        bytes_fn = None
         workload = (f"configs[2]/[3]: denoise-trainer step (trainer/denoise.py) on the PQC AudioDec generator, "
                     f"{C3_CONFIG} (derived), bf16 convs / fp32 losses, {B} x 1 s @ 24 kHz per GPU")
         dtype = "bf16"
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
     timer = _lib.KernelTimer([dom] + (["sel_resunit_fwd"] if cfg == "c3" else []))
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        # per-launch HIP events only in the last timed step: an event pair around
-        # every conv launch of every step costs ~0.6 ms/step (C3) of its own
-        if i == args.steps - 1:
-            _lib.TIMER = timer
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    _lib.TIMER = None
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed, per_step = _timed_steps(step, args.steps, world, dev, timer)
 
     ms_per_step = 1e3 * elapsed / args.steps
-    frames = world * B * SR / HOP * args.steps
-    value = frames / elapsed
+    frames_per_step = world * B * SR / HOP
+    value = frames_per_step * args.steps / elapsed
+    med_ms = float(np.median(per_step))
     roof = roofline(cfg, timer, dom, B, 1)  # the timer covered the last timed step
+
+    fp32 = None
+    if cfg == "c3" and not args.no_fp32_companion:
+        # the reference's own arithmetic (fp32 convs on the exact-fp32 MFMA path), same step
+        step32 = c3_setup(dev, B, world, local, dtype=torch.float32)
+        for _ in range(2):
+            step32()
+        e32, per32 = _timed_steps(step32, args.steps, world, dev)
+        fp32 = {"dtype": "fp32", "value": round(frames_per_step * args.steps / e32, 1), "unit": "frames/s",
+                "ms_per_step": round(1e3 * e32 / args.steps, 3),
+                "median_ms_per_step": round(float(np.median(per32)), 3)}
+        del step32
+
     stft_roof = stft_kernel_roofline(dev) if world == 1 else None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -370,11 +440,14 @@ def main():
         out = {
             "metric": "denoise-train frames/sec (24 kHz, hop 300)",
             "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+            "median_ms_per_step": round(med_ms, 3),
+            "value_at_median": round(frames_per_step / (med_ms * 1e-3), 1),
+            "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": dtype, "data": "synthetic",
             "config": {"workload": workload, "global_batch": world * B, "seq_len": SR,
                        "parallelism": f"dp{world}"},
-            "roofline": roof, "cpu_baseline": cpu, "stft_kernel": stft_roof,
+            "roofline": roof, "cpu_baseline": cpu, "fp32_companion": fp32, "stft_kernel": stft_roof,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -66,4 +66,15 @@ def get_dataloaders(dataset, splits=None, batch_size=8, batch_length=2 * 48000, 
     return out
 
 
+def set_epoch(loaders, epoch):
+    """Reshuffle the data-parallel shards for a new epoch (DistributedSampler
+    .set_epoch).  Single-process loaders reshuffle on their own: their shuffling
+    generator advances every epoch, as in the reference; without this call a
+    DistributedSampler would replay epoch 0's order forever."""
+    for dl in loaders:
+        sampler = getattr(dl, "sampler", None)
+        if hasattr(sampler, "set_epoch"):
+            sampler.set_epoch(epoch)
+
+
 _ = math  # math.exp semantics documented above

@@ -17,6 +17,7 @@ import weakref
 from contextlib import contextmanager
 
 import torch
+from torch.optim.optimizer import register_optimizer_step_post_hook as _register_optimizer_step_post_hook
 
 from . import _lib as L
 
@@ -142,7 +143,7 @@ def _packed_shape(kind, w, stride):
 
 
 class _PackEntry:
-    __slots__ = ("wref", "kind", "stride", "dtype", "version", "wp", "wd")
+    __slots__ = ("wref", "pid", "kind", "stride", "dtype", "version", "wp", "wd")
 
 
 class PackCache:
@@ -150,21 +151,37 @@ class PackCache:
     in ONE sel_pack_many launch per weight update instead of two launches per
     layer per step.
 
-    Validity is tracked with the parameter's version counter (bumped by every
-    in-place update through autograd-visible ops: optimizer steps, copy_,
-    load_state_dict).  A refresh repacks every stale entry into FRESH buffers,
-    so tensors saved by a graph that has not run backward yet are never
-    overwritten.  Code that mutates a weight through ``.data`` (which has its own
-    version counter) must call ``invalidate()``.
+    Two staleness signals, because neither alone is complete:
+    * the parameter's version counter, bumped by in-place updates through
+      autograd-visible ops (copy_, load_state_dict, foreach/for-loop Adam);
+    * a global optimizer step post-hook (``_optimizer_stepped``), because
+      torch's fused Adam (``fused=True``, the GPU default here) writes the
+      parameters in a kernel that does NOT bump ``_version`` — with the version
+      alone every later forward would silently reuse the step-0 packs.
+    A refresh repacks every stale entry into FRESH buffers, so tensors saved by
+    a graph that has not run backward yet are never overwritten.  Code that
+    mutates a weight through ``.data`` (which has its own version counter) must
+    call ``invalidate()``.
     """
 
     def __init__(self):
         self._entries = {}
+        self._by_param = {}  # id(param) -> [entry keys]
         self._lock = threading.Lock()
 
     def invalidate(self):
         with self._lock:
             self._entries.clear()
+            self._by_param.clear()
+
+    def mark_stale(self, params):
+        """Force a repack of every entry packed from one of `params`."""
+        with self._lock:
+            for p in params:
+                for key in self._by_param.get(id(p), ()):
+                    e = self._entries.get(key)
+                    if e is not None and e.wref() is p:
+                        e.version = None
 
     def get(self, kind, w, stride, dtype):
         key = (w.data_ptr(), kind, stride, dtype, tuple(w.shape), w.device)
@@ -174,9 +191,12 @@ class PackCache:
                 return e.wp, e.wd
             if e is None or e.wref() is not w:
                 e = _PackEntry()
-                e.wref, e.kind, e.stride, e.dtype = weakref.ref(w), kind, stride, dtype
+                e.wref, e.pid, e.kind, e.stride, e.dtype = weakref.ref(w), id(w), kind, stride, dtype
                 e.version, e.wp, e.wd = None, None, None
                 self._entries[key] = e
+                keys = self._by_param.setdefault(id(w), [])
+                if key not in keys:
+                    keys.append(key)
             self._refresh(w.device, dtype)
             return e.wp, e.wd
 
@@ -186,6 +206,11 @@ class PackCache:
             w = e.wref()
             if w is None:
                 del self._entries[key]
+                keys = self._by_param.get(e.pid)
+                if keys is not None and key in keys:
+                    keys.remove(key)
+                    if not keys:
+                        del self._by_param[e.pid]
                 continue
             if e.dtype == dtype and w.device == device and e.version != w._version:
                 stale.append((e, w))
@@ -214,6 +239,16 @@ class PackCache:
 
 
 PACKS = PackCache()
+
+
+def _optimizer_stepped(optimizer, args, kwargs):
+    """Global torch.optim post-step hook: every conv weight the optimizer owns
+    is repacked before its next use (see PackCache: fused Adam does not bump
+    the parameters' version counters)."""
+    PACKS.mark_stale(p for g in optimizer.param_groups for p in g["params"])
+
+
+_register_optimizer_step_post_hook(_optimizer_stepped)
 
 
 def prim(desc, x, wp, bias=None, aux=None, res=None, out_dtype=None):

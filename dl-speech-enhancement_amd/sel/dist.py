@@ -8,8 +8,10 @@ rank-local losses equals the single-device gradient on the global batch.  Two
 reference quantities are *batch-global* and need an explicit exchange:
   * add_noise (dataloader/data_utils.py:15-16): ||speech||, ||noise|| over the
     whole batch -> all-reduce the two sums of squares (add_noise_global);
-  * spectral convergence (losses/stft_loss.py:56): global Frobenius norms
-    (not used by any shipped config's step; documented in DESIGN.md).
+  * spectral convergence (losses/stft_loss.py:56): ||y-x||_F / ||y||_F over
+    the whole batch -> all-reduce the per-rank partial sums (sum (y-x)^2,
+    sum y^2, sum |ln y - ln x|, element count) before the ratio
+    (global_loss_sums; used by sel/spectral.py's STFT-loss autograd ops).
 """
 import os
 
@@ -53,6 +55,30 @@ def shard(t, rank=None, world=None):
         raise ValueError(f"global batch {t.shape[0]} not divisible by world size {world}")
     n = t.shape[0] // world
     return t[rank * n:(rank + 1) * n]
+
+
+# Spectral-convergence / log-magnitude losses over the GLOBAL batch when data
+# parallel (the reference's value on the concatenated batch).  Set False to get
+# rank-local losses (e.g. when only some ranks evaluate a loss).
+GLOBAL_BATCH_LOSSES = True
+
+
+def global_loss_sums(sums, n):
+    """Data-parallel exchange of the STFT-loss partial sums.
+
+    sums: float64 (3,) = [sum (y-x)^2, sum y^2, sum |ln y - ln x|] of this
+    rank's shard, n = its element count.  Returns (global sums, global n,
+    grad_scale).  The loss computed from the global sums is the same scalar on
+    every rank; DDP then AVERAGES the parameter gradients over the W ranks, so
+    each rank back-propagates W x d(global loss)/d(local sums) (grad_scale = W):
+    the average is then exactly the single-device gradient on the global batch
+    (the SC ratio is not a mean over shards)."""
+    if not (GLOBAL_BATCH_LOSSES and is_dist()) or dist.get_world_size() == 1:
+        return sums, n, 1.0
+    t = torch.cat([sums.detach().to(torch.float64), torch.tensor([float(n)], dtype=torch.float64,
+                                                                  device=sums.device)])
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return t[:3].contiguous(), int(round(t[3].item())), float(dist.get_world_size())
 
 
 def allreduce_sum_(t):

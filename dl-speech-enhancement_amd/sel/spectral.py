@@ -11,6 +11,7 @@ import numpy as np
 import torch
 
 from . import _lib as L
+from . import dist as D
 
 LOG_KIND = {None: 0, 2.0: 1, 10.0: 2}
 
@@ -76,18 +77,20 @@ class MagPairLoss(torch.autograd.Function):
         ws = L.workspace(lib.sel_mag_pair_workspace(n), xm.device)
         L.call("sel_mag_pair_sums", L.ptr(xm), L.ptr(ym), n, L.ptr(sums), L.ptr(ws), ws.numel(),
                                       L.stream())
+        sums, n_all, ctx.scale = D.global_loss_sums(sums, n)  # data parallel: global-batch SC
         out = torch.empty(2, dtype=torch.float32, device=xm.device)
-        L.call("sel_stft_loss_finish", L.ptr(sums), n, L.ptr(out), L.stream())
+        L.call("sel_stft_loss_finish", L.ptr(sums), n_all, L.ptr(out), L.stream())
         ctx.save_for_backward(xm, ym, sums)
+        ctx.n_all = n_all
         return out
 
     @staticmethod
     def backward(ctx, g):
         xm, ym, sums = ctx.saved_tensors
         lib = L.lib()
-        g = g.contiguous()
+        g = (g * ctx.scale if ctx.scale != 1.0 else g).contiguous()
         coef = torch.empty(4, dtype=torch.float32, device=xm.device)
-        L.call("sel_stft_loss_coef", L.ptr(sums), xm.numel(), L.ptr(g[0:1]), L.ptr(g[1:2]),
+        L.call("sel_stft_loss_coef", L.ptr(sums), ctx.n_all, L.ptr(g[0:1]), L.ptr(g[1:2]),
                                        L.ptr(coef), L.stream())
         gx = torch.empty_like(xm)
         gy = torch.empty_like(ym) if ctx.needs_input_grad[1] else None
@@ -112,6 +115,7 @@ class StftLoss(torch.autograd.Function):
         L.call("sel_stft_loss_fwd", L.ptr(x), L.ptr(y), B, T, n_fft, hop, win_length, L.ptr(window),
                                       L.ptr(sums), L.ptr(ws), ws.numel(), L.stream())
         n = B * _frames(T, hop) * (n_fft // 2 + 1)
+        sums, n, ctx.scale = D.global_loss_sums(sums, n)  # data parallel: global-batch SC
         out = torch.empty(2, dtype=torch.float32, device=x.device)
         L.call("sel_stft_loss_finish", L.ptr(sums), n, L.ptr(out), L.stream())
         ctx.save_for_backward(x, y, window, sums)
@@ -124,7 +128,7 @@ class StftLoss(torch.autograd.Function):
         n_fft, hop, win, n = ctx.cfg
         lib = L.lib()
         B, T = x.shape
-        g = g.contiguous()
+        g = (g * ctx.scale if ctx.scale != 1.0 else g).contiguous()
         coef = torch.empty(4, dtype=torch.float32, device=x.device)
         L.call("sel_stft_loss_coef", L.ptr(sums), n, L.ptr(g[0:1]), L.ptr(g[1:2]), L.ptr(coef),
                                        L.stream())

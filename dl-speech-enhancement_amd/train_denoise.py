@@ -31,7 +31,7 @@ import numpy as np
 import torch
 from torch import nn
 
-from dataloader.data_utils import add_noise
+from dataloader.data_utils import add_noise, set_epoch
 from losses import MultiMelSpectrogramLoss
 from models.autoencoder_without_PQC.AudioDec import Generator as GeneratorAudioDec
 from sel import configs as sel_configs
@@ -185,6 +185,7 @@ def main(argv=None):
 
     batch_length = 1 * SAMPLE_RATE
     batch_size = 4 if env == "LAPTOP" else int(config["batch_size"])
+    loaders = ()
     if env == "SYNTH":
         clean_it, noise_it = _synthetic_loaders(batch_size * world, batch_length, args.synthetic_batches,
                                                 config["seed"])
@@ -204,6 +205,7 @@ def main(argv=None):
                                     config["seed"], rank, world)
         train_pairs = lambda: zip(tc, tn)  # noqa: E731
         val_pairs = lambda: zip(vc, vn)  # noqa: E731
+        loaders = (tc, tn, vc, vn)
 
     def mix(clean, noise):
         snr = torch.randint(10, 20, (1,))
@@ -217,6 +219,7 @@ def main(argv=None):
     steps = train_steps = config["step"]
     start = time.perf_counter()
     for epoch in range(EPOCHS):
+        set_epoch(loaders, epoch)  # data parallel: new shard order every epoch
         if epoch > config["epoch_to_enable_noise_dropout_decay"]:
             NOISE_DROPOUT_RATE -= config["noise_dropout_rate_decay"]
         losses = []

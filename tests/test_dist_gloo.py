@@ -139,3 +139,46 @@ def test_shard_rejects_ragged():
     from sel import dist as D
     with pytest.raises(ValueError):
         D.shard(torch.arange(5), rank=0, world=2)
+
+
+def _mags():
+    g = torch.Generator().manual_seed(21)
+    xm = torch.rand(4, 31, 17, generator=g, dtype=torch.float64) + 0.05
+    ym = torch.rand(4, 31, 17, generator=g, dtype=torch.float64) + 0.05
+    return xm, ym
+
+
+def _sc_case(rank):
+    """Rank-local partial sums (the kernel's sel_mag_pair_sums, restated) ->
+    sel.dist.global_loss_sums -> SC / log-mag and the per-rank gradient the
+    autograd op back-propagates (the sel_stft_loss_coef formula with grad_scale)."""
+    from sel import dist as D
+    xm, ym = _mags()
+    x, y = D.shard(xm), D.shard(ym)
+    sums = torch.stack([((y - x) ** 2).sum(), (y ** 2).sum(), (torch.log(y) - torch.log(x)).abs().sum()])
+    sums_g, n_g, scale = D.global_loss_sums(sums, x.numel())
+    assert n_g == xm.numel() and scale == WORLD
+    n1, n2 = sums_g[0].sqrt(), sums_g[1].sqrt()
+    sc, mag = n1 / n2, sums_g[2] / n_g
+    # d/dx of sc and mag w.r.t. this shard, times grad_scale (stft_loss_coef + mag_pair_bwd)
+    gx = scale * ((x - y) / (n1 * n2) + torch.sign(torch.log(x) - torch.log(y)) / x / n_g)
+    return [torch.stack([sc, mag]), gx]
+
+
+def test_spectral_convergence_is_global_under_dp():
+    """losses/stft_loss.py:56 is a ratio of GLOBAL Frobenius norms: under data
+    parallelism the exchanged sums give the single-device value on the global
+    batch, and the DDP-averaged gradient (grad/W per shard) equals the
+    single-device gradient."""
+    out = _run(_sc_case)
+    xm, ym = _mags()
+    xr = xm.clone().requires_grad_(True)
+    sc, mag = R.spectral_convergence(xr, ym), R.log_stft_magnitude(xr, ym)
+    (sc + mag).backward()
+    for r in range(WORLD):
+        torch.testing.assert_close(out[r][0], torch.stack([sc, mag]).detach(), rtol=1e-12, atol=0)
+    got = torch.cat([out[0][1], out[1][1]]) / WORLD
+    torch.testing.assert_close(got, xr.grad, rtol=1e-10, atol=1e-14)
+    # rank-local SC (no exchange) differs: the exchange is load-bearing
+    loc = R.spectral_convergence(xm[:2], ym[:2])
+    assert abs(loc.item() - sc.item()) > 1e-4

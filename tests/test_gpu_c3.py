@@ -1,0 +1,190 @@
+"""Parity of the C3 (BASELINE configs[2]) bf16 path at the bench's own size.
+
+1. Every bf16 tile variant of the MFMA conv primitive (tune key 0 = 21..26,
+   conv.hip fwd4_variant) on the real C3 layer shapes in primitive form,
+   forward and dgrad (adjoint) forms, against an fp64 reference computed from
+   the SAME bf16 operands.  Both accumulate exact bf16 products (fp32 vs fp64
+   sums) and the kernel rounds once to bf16, so the bound is bf16 output
+   rounding: <= 4e-3 norm-wise, and elementwise |a-b| <= 8e-3|b| + 2e-3 max|b|.
+   The variant the dispatcher picks by default (key 0 = 0) must be bit-equal to
+   the forced one it names.
+   Shapes (B = 64, 1 s @ 24 kHz): RU128 k7 d1/3/9 at T=2000 (128k rows), RU256
+   k7 d1/3/9 at T=400 (25.6k rows; the 256-row tiles overrun every sample),
+   the 256-wide 1x1, the strided 128->256 s5 / 256->512 s5 layers (phase-packed
+   3-tap form), the transposed 512->256 s5 decoder layer (2 taps, replicate
+   pad), and their dgrads.  Reference layers: conv_layer.py:139-142, :180-183,
+   residual_unit.py:43-46.
+2. One full denoise-trainer step at B = 64 x 24000 in bf16 against the fp32
+   oracle on the same weights (trainer/denoise.py:52-84): y, z, the loss and
+   the encoder gradients, norm-wise (bounds in the test).
+"""
+import zlib
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+B = 64
+# (tag, C, N, K, dil, pad_mode, in_elu, bias_period, T, aux, res)
+FWD = [
+    ("ru128_k7_d1", 128, 128, 7, 1, 0, 1, 0, 2000, 0, 0),
+    ("ru128_k7_d9", 128, 128, 7, 9, 0, 1, 0, 2000, 0, 0),
+    ("ru256_k7_d1", 256, 256, 7, 1, 0, 1, 0, 400, 0, 0),
+    ("ru256_k7_d3", 256, 256, 7, 3, 0, 1, 0, 400, 0, 0),
+    ("ru256_k7_d9", 256, 256, 7, 9, 0, 1, 0, 400, 0, 0),
+    ("ru256_1x1", 256, 256, 1, 1, 0, 1, 0, 400, 0, 1),
+    ("down128_256_s5", 640, 256, 3, 1, 0, 0, 256, 400, 0, 0),
+    ("down256_512_s5", 1280, 512, 3, 1, 0, 0, 512, 80, 0, 0),
+    ("up512_256_s5", 512, 1280, 2, 1, 1, 0, 256, 80, 0, 0),
+]
+
+
+def _ref(x, wp, d, B_, bias=None, aux=None, res=None):
+    """fp64 primitive on the same (bf16) operands: out[b,t,n] = sum_k,c
+    act(x)[b, t + k*dil - pad, c] * wp[n,k,c] (+ bias, * ELU'(aux), + res)."""
+    T, C, N, K = d.T, d.C, d.N, d.K
+    xa = x.double().view(B_, T, C)
+    if d.in_elu:
+        xa = torch.where(xa > 0, xa, torch.expm1(xa)).to(torch.bfloat16).double()
+    out = torch.zeros(B_, T, N, dtype=torch.float64, device=x.device)
+    w = wp.double()
+    for k in range(K):
+        idx = torch.arange(T, device=x.device) + k * d.dil - d.pad
+        if d.pad_mode == 0:
+            ok = (idx >= 0) & (idx < T)
+            xs = torch.zeros(B_, T, C, dtype=torch.float64, device=x.device)
+            xs[:, ok] = xa[:, idx[ok]]
+        else:
+            xs = xa[:, idx.clamp(0, T - 1)]
+        out += torch.einsum("btc,nc->btn", xs, w[:, k, :])
+    out = out.view(B_ * T, N)
+    if bias is not None:
+        out += bias.double().repeat(N // bias.numel())
+    if aux is not None:
+        out *= torch.where(aux.double() > 0, 1.0, torch.exp(aux.double()))
+    if res is not None:
+        out += res.double()
+    return out
+
+
+def _check(got, ref, what):
+    g = got.double()
+    e = ((g - ref).norm() / ref.norm()).item()
+    assert e <= 4e-3, (what, e)
+    bad = (g - ref).abs() > 8e-3 * ref.abs() + 2e-3 * ref.abs().max()
+    assert not bad.any(), (what, int(bad.sum()), (g - ref).abs().max().item())
+
+
+def _operands(d, gen, dev, aux, res):
+    x = (0.5 * torch.randn(d.rows, d.C, generator=gen, device=dev)).to(torch.bfloat16)
+    wp = (torch.randn(d.N, d.K, d.C, generator=gen, device=dev) / (d.K * d.C) ** 0.5).to(torch.bfloat16)
+    b = torch.randn(d.bias_period, generator=gen, device=dev) if d.bias_period else None
+    a_ = torch.randn(d.rows, d.N, generator=gen, device=dev).to(torch.bfloat16) if aux else None
+    r_ = torch.randn(d.rows, d.N, generator=gen, device=dev).to(torch.bfloat16) if res else None
+    return x, wp, b, a_, r_
+
+
+@pytest.mark.parametrize("form", ["fwd", "dgrad"])
+@pytest.mark.parametrize("shape", FWD, ids=[s[0] for s in FWD])
+def test_fwd4_tile_variants_on_c3_shapes(gpu, shape, form):
+    from sel import _lib as L
+    from sel import convops as CO
+    tag, C, N, K, dil, mode, elu, bias, T, aux, res = shape
+    pad = (K - 1) * dil if mode == 0 else 1
+    d = CO.ConvDesc(B * T, T, C, N, K, dil, pad, mode, elu, bias)
+    if form == "dgrad":
+        # the backward uses the adjoint primitive on gout (pad' = (K-1)dil - pad,
+        # no prologue) with the ELU'(aux) and residual epilogue of a residual unit
+        d = d.adjoint()
+        aux = res = int(K > 1 and C == N)
+    gen = torch.Generator(device=gpu).manual_seed(zlib.crc32(f"{tag}/{form}".encode()))
+    x, wp, b, a_, r_ = _operands(d, gen, gpu, aux, res)
+    ref = _ref(x, wp, d, B, b, a_, r_)
+    lib = L.lib()
+    p4 = lib.sel_tune(4, 1)  # the weight-stationary thin kernel would pre-empt the tiled one
+    try:
+        default_name = CO.fwd_kernel_name(d, torch.bfloat16, torch.bfloat16)
+        assert default_name.startswith("k_conv_fwd_bf16"), default_name
+        default = CO.prim(d, x, wp, bias=b, aux=a_, res=r_).clone()
+        _check(default, ref, (form, "default", default_name))
+        matched = False
+        for v in range(21, 27):
+            p0 = lib.sel_tune(0, v)
+            try:
+                name = CO.fwd_kernel_name(d, torch.bfloat16, torch.bfloat16)
+                got = CO.prim(d, x, wp, bias=b, aux=a_, res=r_)
+            finally:
+                lib.sel_tune(0, p0)
+            _check(got, ref, (form, v, name))
+            if name == default_name:
+                matched = True
+                assert torch.equal(got, default), (form, v)
+        assert matched, default_name
+    finally:
+        lib.sel_tune(4, p4)
+
+
+def test_c3_denoise_step_bf16_vs_fp32_oracle(gpu):
+    """Full C3 step: PQC generator (symAD_libritts_24000_hop300), B = 64 x 1 s,
+    loss = lambda_vq * sum(vqloss) + 45 * mel, grads into the encoder/projector
+    (decoder + quantizer frozen, codebook eval) — bf16 convs vs the fp32 oracle.
+
+    Bounds (bf16 operands carry 2^-9 relative rounding per layer through ~30
+    layers): y 3e-2, z 3e-2, mel-loss term 5e-3 relative, encoder/projector
+    gradient (all trainable tensors concatenated) 6e-2 norm-wise, each tensor
+    1.5e-1.  VQ indices are not compared: z itself differs at the bf16 level, so
+    near-ties legitimately flip (the VQ kernel's exactness is tested on identical
+    z in test_gpu_model.py)."""
+    from oracle import ref_ops as R
+    from oracle.melfilters import mel as melbank
+    from losses import MultiMelSpectrogramLoss
+    from models.autoencoder.AudioDec import Generator
+    from sel import configs
+    from sel.convops import precision
+    cfg = configs.get("symAD_libritts_24000_hop300")
+    mp = cfg["mel_loss_params"]
+    torch.manual_seed(93)
+    G = Generator(**cfg["generator_params"])
+    P = {k: v.clone() for k, v in G.state_dict().items()}
+    train = [k for k in P if k.startswith(("encoder.", "projector.")) and k.endswith(("weight", "bias"))]
+    for k in train:
+        P[k].requires_grad_(True)
+    g = torch.Generator().manual_seed(5)
+    clean = 0.1 * torch.randn(B, 1, 24000, generator=g)
+    noisy = R.add_noise(clean, 0.1 * torch.randn(B, 1, 24000, generator=g), 15)
+    mm = torch.from_numpy(melbank(sr=mp["fs"], n_fft=2048, n_mels=80, fmin=mp["fmin"], fmax=mp["fmax"]).T.copy())
+    win = R.hann(2048) if mp["win_lengths"][0] is None else R.hann(mp["win_lengths"][0])
+    torch.set_num_threads(min(16, torch.get_num_threads()))
+    yr, zqr, zr, vqr, _ = R.generator_forward(P, noisy, R.generator_geometry(), pqc=True)
+    melr = R.multi_mel_loss(yr, clean, [(2048, 300, mp["win_lengths"][0] or 2048)], [win], [mm], 1e-10, None)
+    lossr = cfg["lambda_vq_loss"] * vqr.sum() + cfg["lambda_mel_loss"] * melr
+    lossr.backward()
+
+    G = G.to(gpu)
+    for p in list(G.quantizer.parameters()) + list(G.decoder.parameters()):
+        p.requires_grad_(False)
+    G.quantizer.codebook.eval()
+    mel = MultiMelSpectrogramLoss(**mp).to(gpu)
+    with precision(torch.bfloat16):
+        y, zq, z, vql, ppl = G(noisy.to(gpu))
+        meld = mel(y, clean.to(gpu))
+        loss = cfg["lambda_vq_loss"] * vql.sum() + cfg["lambda_mel_loss"] * meld
+        loss.backward()
+    rel = lambda a, b: ((a.detach().double().cpu() - b.detach().double()).norm() / b.detach().double().norm()).item()
+    ey, ez = rel(y, yr), rel(z, zr)
+    em = abs(meld.item() - melr.item()) / abs(melr.item())
+    params = dict(G.named_parameters())
+    num = den = 0.0
+    worst = (0.0, "")
+    for k in train:
+        gd, gr = params[k].grad.double().cpu(), P[k].grad.double()
+        num += ((gd - gr) ** 2).sum().item()
+        den += (gr ** 2).sum().item()
+        worst = max(worst, (rel(gd, gr), k))
+    eg = (num / den) ** 0.5
+    print(f"C3 bf16 vs fp32: y {ey:.2e} z {ez:.2e} mel {em:.2e} grad {eg:.2e} worst {worst}")
+    assert ey <= 3e-2 and ez <= 3e-2, (ey, ez)
+    assert em <= 5e-3, em
+    assert eg <= 6e-2, eg
+    assert worst[0] <= 1.5e-1, worst

@@ -109,3 +109,40 @@ def test_train_step_matches_golden(gpu):
                 p.copy_(torch.from_numpy(g[f"sd{s + 1}.{k}"]).to(gpu))
         assert flips <= 0.02 * tot, (s, flips, tot)
         assert (num / den) ** 0.5 <= 0.10, (s, (num / den) ** 0.5)
+
+
+@pytest.mark.parametrize("bf16", [False, True])
+def test_steps_without_copy_use_updated_weights(gpu, bf16):
+    """fused Adam writes the parameters without bumping their
+    version counters, so the packed conv weights must be refreshed by the
+    optimizer step hook.  After three DenoiseStep steps with nothing touching
+    the weights in between, the trained generator's forward must equal a fresh
+    generator's forward on the same (updated) weights, bit for bit."""
+    from models.autoencoder_without_PQC.AudioDec import Generator
+    from sel import configs
+    from sel.convops import precision
+    from train_denoise import DenoiseStep
+    gp = dict(encode_channels=8, decode_channels=8, code_dim=64, codebook_num=2, codebook_size=64)
+    torch.manual_seed(1)
+    G = Generator(**gp).to(gpu)
+    cfg = configs.get("symAD_24Mel")
+    cfg["generator_optimizer_params"]["lr"] = 1e-3  # visible updates in 3 steps
+    step = DenoiseStep(cfg, gpu, generator=G)
+    assert step.optimizer["generator"].defaults.get("fused"), "the GPU default is fused Adam"
+    g = torch.Generator().manual_seed(2)
+    xc = 0.1 * torch.randn(2, 1, 4800, generator=g)
+    xn = xc + 0.05 * torch.randn(2, 1, 4800, generator=g)
+    dt = torch.bfloat16 if bf16 else torch.float32
+    with precision(dt):
+        with torch.no_grad():
+            y0 = G(xn.to(gpu)).clone()
+        for _ in range(3):
+            step.model_step(xc, xn)
+        with torch.no_grad():
+            y1 = G(xn.to(gpu)).clone()
+            G2 = Generator(**gp)
+            G2.load_state_dict(G.state_dict())
+            G2 = G2.to(gpu)
+            y2 = G2(xn.to(gpu))
+    assert not torch.equal(y0, y1), "the weights did not move"
+    assert torch.equal(y1, y2), (y1 - y2).abs().max().item()

@@ -48,25 +48,86 @@ def test_rvq_matches_reference_golden(gpu):
     nclose(qi, g["fi.q"], 1e-6, "fi.q")
 
 
+TIE_ULPS = 64  # near-tie bound: 64 fp32 ulps of the row's largest top-2 distance
+
+
+def _oracle_margins(z, embeds):
+    """Per (stage, row): the oracle's top-2 distance margin and the tie bound
+    TIE_ULPS * ulp(max |top-2 distance|) (make_goldens.py records the same
+    margins for the golden; vq_module.py:64-69)."""
+    from oracle import ref_ops as R
+    res_ = z.reshape(-1, z.shape[-1])
+    margins, bounds = [], []
+    for e in embeds:
+        dist = R.vq_distance(res_, e)
+        top2 = torch.topk(-dist, 2, dim=1).values
+        margins.append(top2[:, 0] - top2[:, 1])
+        scale = top2.abs().max(1).values
+        bounds.append(TIE_ULPS * torch.finfo(torch.float32).eps * scale)
+        q, _, _, _ = R.vq_forward(res_, e)
+        res_ = res_ - q
+    return torch.stack(margins), torch.stack(bounds)
+
+
 def test_rvq_full_size_vs_oracle(gpu):
-    """C3 shape: N = 64*80 rows, 8 stages x 1024 codes x 64 dims."""
+    """C3 shape: N = 64*80 rows, 8 stages x 1024 codes x 64 dims.
+
+    Bit-exact VQ indices (north_star): an index may differ from the oracle's
+    only at the FIRST stage where that row diverges, and only where the
+    oracle's own top-2 margin there is a near-tie (<= TIE_ULPS fp32 ulps of the
+    distance scale; the cross term is a 64-term fp32 dot product summed in a
+    different order than MKL's sgemm).  Later stages of such a row see a
+    different residual and are excluded.  q, losses and perplexities are then
+    compared on the rows whose indices match at every stage, by re-running both
+    sides on exactly those rows (a row's arithmetic does not depend on other rows)."""
     from oracle import ref_ops as R
     from layers.vq_module import ResidualVQ
     torch.manual_seed(0)
     rvq = ResidualVQ(num_quantizers=8, dim=64, codebook_size=1024).eval()
     z = torch.randn(64, 80, 64) * 1.5
     embeds = [l.embed.clone() for l in rvq.layers]
-    qr, lr, pr, ir = R.rvq_forward(z, embeds)
+    _, _, _, ir = R.rvq_forward(z, embeds)
     rvq = rvq.to(gpu)
-    q, losses, ppls = rvq(z.to(gpu))
     _, idx = rvq.forward_index(z.to(gpu))
-    mism = (idx.cpu() != ir).sum().item()
-    # near-ties only: a stage-0 mismatch propagates to later stages of that row
-    assert mism <= 8, mism
-    if mism == 0:
-        nclose(q, qr, 1e-6, "q")
-        nclose(losses, lr, 1e-5, "losses")
-        nclose(ppls, pr, 1e-5, "ppls")
+    idx, ir = idx.cpu().reshape(8, -1), ir.reshape(8, -1)
+    margins, bounds = _oracle_margins(z, embeds)
+    mism = idx != ir
+    rows_bad = mism.any(0)
+    first = torch.where(rows_bad, mism.float().argmax(0), torch.full_like(rows_bad, -1, dtype=torch.long))
+    for row in torch.nonzero(rows_bad).flatten().tolist():
+        s = int(first[row])
+        assert margins[s, row] <= bounds[s, row], (row, s, margins[s, row].item(), bounds[s, row].item())
+    print(f"RVQ full size: {int(rows_bad.sum())} of {idx.shape[1]} rows diverge (all at oracle near-ties)")
+    ok = torch.nonzero(~rows_bad).flatten()
+    assert ok.numel() >= idx.shape[1] - 16
+    zs = z.reshape(-1, 64)[ok].reshape(1, -1, 64)
+    qr, lr, pr, ir2 = R.rvq_forward(zs, embeds)
+    q, losses, ppls = rvq(zs.to(gpu))
+    _, idx2 = rvq.forward_index(zs.to(gpu))
+    assert torch.equal(idx2.cpu().reshape(8, -1), ir2.reshape(8, -1))
+    nclose(q, qr, 1e-6, "q")
+    nclose(losses, lr, 1e-5, "losses")
+    nclose(ppls, pr, 1e-6, "ppls")
+
+
+def test_vq_training_mode_ema_matches_reference_golden(gpu):
+    """VectorQuantize in training mode (vq_module.py:74-80): EMA update of
+    cluster_size / embed_avg / embed (decay 0.8, Laplace eps 1e-5) plus q, loss
+    and perplexity, against the reference's own run (tests/golden/vq.npz ema.*)."""
+    from layers.vq_module import VectorQuantize
+    g = golden("vq")
+    vq = VectorQuantize(dim=64, codebook_size=256)
+    with torch.no_grad():
+        vq.embed.copy_(torch.from_numpy(g["ema.embed0"]))
+        vq.embed_avg.copy_(torch.from_numpy(g["ema.embed0"]))
+    vq = vq.to(gpu).train()
+    q, loss, ppl = vq(torch.from_numpy(g["ema.z"]).to(gpu))
+    nclose(q, g["ema.q"], 1e-6, "q")
+    nclose(loss, g["ema.loss"], 1e-5, "loss")
+    nclose(ppl, g["ema.ppl"], 1e-6, "ppl")
+    nclose(vq.cluster_size, g["ema.cluster_size"], 1e-6, "cluster_size")
+    nclose(vq.embed_avg, g["ema.embed_avg"], 1e-6, "embed_avg")
+    nclose(vq.embed, g["ema.embed1"], 1e-6, "embed")
 
 
 def _load(tag, dev):

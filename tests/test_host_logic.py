@@ -1,0 +1,101 @@
+"""CPU checks of host-side logic that needs no GPU: the packed-weight cache's
+staleness signals, the bench launcher, the trainer checkpoint layout and the
+data-parallel sampler epochs."""
+import os
+import sys
+
+import pytest
+import torch
+
+from conftest import REPO
+
+
+def _entry(cache, w, kind=0):
+    from sel import convops as CO
+    e = CO._PackEntry()
+    e.wref, e.pid, e.kind, e.stride, e.dtype = __import__("weakref").ref(w), id(w), kind, 1, torch.float32
+    e.version, e.wp, e.wd = w._version, None, None
+    key = (w.data_ptr(), kind, 1, torch.float32, tuple(w.shape), w.device)
+    cache._entries[key] = e
+    cache._by_param.setdefault(id(w), []).append(key)
+    return e
+
+
+@pytest.mark.parametrize("kw", [dict(fused=True), dict(foreach=True), dict(foreach=False)])
+def test_pack_cache_goes_stale_after_every_adam_flavour(kw):
+    """Fused Adam updates parameters without bumping ``_version``; the global
+    optimizer post-step hook must mark their packs stale anyway."""
+    from sel import convops as CO
+    w = torch.nn.Parameter(torch.randn(4, 3, 7))
+    other = torch.nn.Parameter(torch.randn(4, 3, 7))
+    e = _entry(CO.PACKS, w)
+    e2 = _entry(CO.PACKS, other)
+    try:
+        opt = torch.optim.Adam([w], lr=1e-2, **kw)
+        w.grad = torch.randn_like(w)
+        opt.step()
+        assert e.version is None or e.version != w._version
+        # a parameter the optimizer does not own keeps its pack
+        assert e2.version == other._version
+    finally:
+        CO.PACKS.invalidate()
+
+
+def test_fused_adam_really_skips_the_version_bump():
+    """Documents why the hook exists: if torch ever bumps the version in fused
+    Adam this test fails and the hook becomes belt-and-braces only."""
+    w = torch.nn.Parameter(torch.randn(8))
+    v0 = w._version
+    opt = torch.optim.Adam([w], lr=1e-2, fused=True)
+    w.grad = torch.randn_like(w)
+    before = w.detach().clone()
+    opt.step()
+    assert not torch.equal(before, w.detach())
+    assert w._version == v0
+
+
+def test_bench_launch_cmd_runs_n_ranks_of_itself():
+    sys.path.insert(0, REPO)
+    import bench
+    cmd = bench.launch_cmd(8, 29555, ["--gpus", "8", "--steps", "20"])
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nproc-per-node=8" in cmd and "--master-addr=127.0.0.1" in cmd and "--master-port=29555" in cmd
+    assert cmd[-5:] == [os.path.join(REPO, "bench.py"), "--gpus", "8", "--steps", "20"]
+
+
+def test_bench_launcher_starts_world_size_ranks(tmp_path):
+    """The relaunch command really yields WORLD_SIZE = N ranks with RANK 0..N-1
+    (gloo, CPU): run the same torch.distributed.run line on a probe script."""
+    import subprocess
+    probe = tmp_path / "probe.py"
+    probe.write_text("import os, torch.distributed as d\n"
+                     "d.init_process_group('gloo')\n"
+                     "print('RANK', os.environ['RANK'], os.environ['WORLD_SIZE'], d.get_world_size(), flush=True)\n"
+                     "d.destroy_process_group()\n")
+    sys.path.insert(0, REPO)
+    import bench
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = bench.launch_cmd(2, port, [])
+    cmd[-1] = str(probe)
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = sorted(l for l in out.stdout.splitlines() if l.startswith("RANK"))
+    assert lines == ["RANK 0 2 2", "RANK 1 2 2"], out.stdout
+
+
+def test_set_epoch_reshuffles_distributed_shards():
+    """every epoch must draw a new DistributedSampler order."""
+    from torch.utils.data import DataLoader, DistributedSampler
+    from dataloader.data_utils import set_epoch
+    ds = list(range(64))
+    s = DistributedSampler(ds, num_replicas=2, rank=0, shuffle=True, seed=82, drop_last=True)
+    dl = DataLoader(ds, batch_size=4, sampler=s)
+    plain = DataLoader(ds, batch_size=4, shuffle=True)
+    set_epoch((dl, plain), 0)
+    e0 = list(iter(s))
+    set_epoch((dl, plain), 1)
+    e1 = list(iter(s))
+    assert s.epoch == 1 and sorted(e0) != e0 and e0 != e1
