@@ -413,3 +413,161 @@ def snr_db(preds, target):
     noise = target - preds
     v = (torch.sum(target ** 2, dim=-1) + eps) / (torch.sum(noise ** 2, dim=-1) + eps)
     return (10 * torch.log10(v)).mean()
+
+
+# --------------------------------------------------------------------------
+# HiFi-GAN MSD + MPD discriminator  (models/vocoder/HiFiGAN.py:308-395,
+# models/vocoder/modules/discriminator.py:26-447) and the GAN losses
+# (losses/adversarial_loss.py:13-124, losses/feat_match_loss.py:13-55)
+# --------------------------------------------------------------------------
+
+def _wn(P, key):
+    """torch.nn.utils.weight_norm(dim=0): w = g * v / ||v|| (norm over all dims but 0)."""
+    if key + ".weight" in P:
+        return P[key + ".weight"]
+    g, v = P[key + ".weight_g"], P[key + ".weight_v"]
+    return g * v / v.flatten(1).norm(dim=1).view(-1, *([1] * (v.dim() - 1)))
+
+
+def scale_discriminator_plan(in_channels=1, out_channels=1, kernel_sizes=(15, 41, 5, 3), channels=128,
+                             max_downsample_channels=1024, max_groups=16, downsample_scales=(2, 2, 4, 4, 1),
+                             **_):
+    """Layer plan of HiFiGANScaleDiscriminator.__init__ (discriminator.py:257-324):
+    (cin, cout, k, stride, pad, groups, leaky) per layer."""
+    plan = [(in_channels, channels, kernel_sizes[0], 1, (kernel_sizes[0] - 1) // 2, 1, True)]
+    cin, cout, groups = channels, channels, 4
+    for s in downsample_scales:
+        plan.append((cin, cout, kernel_sizes[1], s, (kernel_sizes[1] - 1) // 2, groups, True))
+        cin = cout
+        cout = min(cin * 2, max_downsample_channels)
+        groups = min(groups * 4, max_groups)
+    cout = min(cin * 2, max_downsample_channels)
+    plan.append((cin, cout, kernel_sizes[2], 1, (kernel_sizes[2] - 1) // 2, 1, True))
+    plan.append((cout, out_channels, kernel_sizes[3], 1, (kernel_sizes[3] - 1) // 2, 1, False))
+    return plan
+
+
+def period_discriminator_plan(in_channels=1, out_channels=1, kernel_sizes=(5, 3), channels=32,
+                              downsample_scales=(3, 3, 3, 3, 1), max_downsample_channels=1024, **_):
+    """Layer plan of HiFiGANPeriodDiscriminator.__init__ (discriminator.py:69-97):
+    (cin, cout, k, stride, pad, leaky); the output conv uses kernel k1 - 1 with
+    padding (k1 - 1) // 2 (:91-97, as written)."""
+    plan = []
+    cin, cout = in_channels, channels
+    for s in downsample_scales:
+        plan.append((cin, cout, kernel_sizes[0], s, (kernel_sizes[0] - 1) // 2, True))
+        cin = cout
+        cout = min(cout * 4, max_downsample_channels)
+    plan.append((cout, out_channels, kernel_sizes[1] - 1, 1, (kernel_sizes[1] - 1) // 2, False))
+    return plan
+
+
+def scale_discriminator(P, pre, x, plan, slope=0.1):
+    """HiFiGANScaleDiscriminator.forward (:337-352): every layer's output is kept."""
+    outs = []
+    for i, (ci, co, k, s, p, g, leaky) in enumerate(plan):
+        key = f"{pre}.layers.{i}.0" if leaky else f"{pre}.layers.{i}"
+        x = F.conv1d(x, _wn(P, key), P.get(key + ".bias"), stride=s, padding=p, groups=g)
+        if leaky:
+            x = F.leaky_relu(x, slope)
+        outs.append(x)
+    return outs
+
+
+def period_discriminator(P, pre, x, period, plan, slope=0.1):
+    """HiFiGANPeriodDiscriminator.forward (:110-137): reflect-pad T to a multiple
+    of the period, view (B, C, T/p, p), (k, 1) Conv2d stack, flatten the last."""
+    b, c, t = x.shape
+    if t % period:
+        n_pad = period - t % period
+        x = F.pad(x, (0, n_pad), "reflect")
+        t += n_pad
+    x = x.view(b, c, t // period, period)
+    outs = []
+    n = len(plan)
+    for i, (ci, co, k, s, p, leaky) in enumerate(plan):
+        key = f"{pre}.convs.{i}.0" if i < n - 1 else f"{pre}.output_conv"
+        x = F.conv2d(x, _wn(P, key), P.get(key + ".bias"), stride=(s, 1), padding=(p, 0))
+        if leaky:
+            x = F.leaky_relu(x, slope)
+        outs.append(x)
+    outs[-1] = torch.flatten(outs[-1], 1, -1)
+    return outs
+
+
+def hifigan_discriminator(P, x, scales=3, scale_downsample_pooling_params=None, scale_discriminator_params=None,
+                          periods=(2, 3, 5, 7, 11), period_discriminator_params=None, **_):
+    """HiFiGAN.Discriminator.forward (HiFiGAN.py:380-395): MSD outputs (AvgPool1d
+    between scales, discriminator.py:432-447) followed by MPD outputs (:195-209)."""
+    pool = scale_downsample_pooling_params or {"kernel_size": 4, "stride": 2, "padding": 2}
+    sp = scale_discriminator_params or {}
+    pp = period_discriminator_params or {}
+    b, c, t = x.shape
+    if c != 1:
+        x = x.reshape(b * c, 1, t)
+    splan = scale_discriminator_plan(**sp)
+    slope = sp.get("nonlinear_activation_params", {}).get("negative_slope", 0.1)
+    outs = []
+    h = x
+    for i in range(scales):
+        outs.append(scale_discriminator(P, f"msd.discriminators.{i}", h, splan, slope))
+        h = F.avg_pool1d(h, **pool)
+    pplan = period_discriminator_plan(**pp)
+    pslope = pp.get("nonlinear_activation_params", {}).get("negative_slope", 0.1)
+    for i, p in enumerate(periods):
+        outs.append(period_discriminator(P, f"mpd.discriminators.{i}", x, p, pplan, pslope))
+    return outs
+
+
+def generator_adv_loss(outputs, average_by_discriminators=True, loss_type="mse"):
+    """GeneratorAdversarialLoss.forward (adversarial_loss.py:30-58)."""
+    crit = (lambda v: F.mse_loss(v, v.new_ones(v.size()))) if loss_type == "mse" else (lambda v: -v.mean())
+    if isinstance(outputs, (tuple, list)):
+        loss = 0.0
+        for i, o in enumerate(outputs):
+            if isinstance(o, (tuple, list)):
+                o = o[-1]
+            loss = loss + crit(o)
+        if average_by_discriminators:
+            loss = loss / (i + 1)
+        return loss
+    return crit(outputs)
+
+
+def discriminator_adv_loss(outputs_hat, outputs, average_by_discriminators=True, loss_type="mse"):
+    """DiscriminatorAdversarialLoss.forward (adversarial_loss.py:81-124) -> (real, fake)."""
+    if loss_type == "mse":
+        real_c = lambda v: F.mse_loss(v, v.new_ones(v.size()))  # noqa: E731
+        fake_c = lambda v: F.mse_loss(v, v.new_zeros(v.size()))  # noqa: E731
+    else:
+        real_c = lambda v: -torch.mean(torch.min(v - 1, v.new_zeros(v.size())))  # noqa: E731
+        fake_c = lambda v: -torch.mean(torch.min(-v - 1, v.new_zeros(v.size())))  # noqa: E731
+    if isinstance(outputs, (tuple, list)):
+        real = fake = 0.0
+        for i, (oh, o) in enumerate(zip(outputs_hat, outputs)):
+            if isinstance(oh, (tuple, list)):
+                oh, o = oh[-1], o[-1]
+            real = real + real_c(o)
+            fake = fake + fake_c(oh)
+        if average_by_discriminators:
+            real, fake = real / (i + 1), fake / (i + 1)
+        return real, fake
+    return real_c(outputs), fake_c(outputs_hat)
+
+
+def feat_match_loss(feats_hat, feats, average_by_layers=True, average_by_discriminators=True,
+                    include_final_outputs=False):
+    """FeatureMatchLoss.forward (feat_match_loss.py:29-55)."""
+    total = 0.0
+    for i, (fh, f) in enumerate(zip(feats_hat, feats)):
+        part = 0.0
+        if not include_final_outputs:
+            fh, f = fh[:-1], f[:-1]
+        for j, (a, b) in enumerate(zip(fh, f)):
+            part = part + F.l1_loss(a, b.detach())
+        if average_by_layers:
+            part = part / (j + 1)
+        total = total + part
+    if average_by_discriminators:
+        total = total / (i + 1)
+    return total

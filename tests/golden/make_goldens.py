@@ -12,8 +12,13 @@ Third-party pieces absent from this image and how they are handled:
   ``filters.mel`` is the restatement in ``oracle/melfilters.py``.
 * torchaudio / soundfile (dataloader package init) — ``dataloader/data_utils.py``
   and ``collater.py`` are loaded by file path with a stub package.
-* torchmetrics (SNR), clearml, tensorboardX — not needed: the step glue of
+* torchmetrics (SNR), clearml — not needed: the step glue of
   ``train_denoise.py:213-263`` is restated below from its source text.
+* tensorboardX (``trainer/trainerGAN.py:20``) — stub ``SummaryWriter`` (no-op)
+  so the reference ``trainer/denoise.Trainer`` itself runs (``--only trainer``).
+* torchaudio (``models/vocoder/modules/discriminator.py:23`` imports
+  ``functional.spectrogram``, used only by the UnivNet discriminator) — stub
+  module, so the HiFiGAN discriminator itself runs (``--only gan``).
 """
 import argparse
 import importlib.util
@@ -83,6 +88,10 @@ def _sd(module, prefix="sd."):
     return {prefix + k: _np(v) for k, v in module.state_dict().items()}
 
 
+def _params(module, prefix):
+    return {prefix + k: _np(p) for k, p in module.named_parameters()}
+
+
 def _grads(module, prefix="g."):
     return {prefix + k: _np(p.grad) for k, p in module.named_parameters() if p.grad is not None}
 
@@ -130,6 +139,191 @@ def make_waveform(ref, clean, noise, out):
     np.savez_compressed(os.path.join(out, "waveform.npz"), **d)
 
 
+def _install_trainer_stubs():
+    tbx = types.ModuleType("tensorboardX")
+
+    class SummaryWriter:  # no-op stand-in (logging only)
+        def __init__(self, *a, **k):
+            pass
+
+        def add_scalar(self, *a, **k):
+            pass
+
+    tbx.SummaryWriter = SummaryWriter
+    sys.modules["tensorboardX"] = tbx
+    ta = types.ModuleType("torchaudio")
+    ta.functional = types.SimpleNamespace(spectrogram=None)
+    sys.modules["torchaudio"] = ta
+    sys.modules["torchaudio.functional"] = ta.functional
+
+
+# reduced-width HiFiGAN discriminator: the vctk 48 kHz structure
+# (config/denoise/symAD_vctk_48000_hop300.yaml:49-82) at 1/8 .. 1/32 the channels
+D_PARAMS = dict(
+    scales=3, scale_downsample_pooling="AvgPool1d",
+    scale_downsample_pooling_params={"kernel_size": 4, "stride": 2, "padding": 2},
+    scale_discriminator_params={"in_channels": 1, "out_channels": 1, "kernel_sizes": [15, 41, 5, 3],
+                                "channels": 16, "max_downsample_channels": 32, "max_groups": 16, "bias": True,
+                                "downsample_scales": [4, 4, 4, 4, 1], "nonlinear_activation": "LeakyReLU",
+                                "nonlinear_activation_params": {"negative_slope": 0.1}},
+    follow_official_norm=True, periods=[2, 3, 5, 7, 11],
+    period_discriminator_params={"in_channels": 1, "out_channels": 1, "kernel_sizes": [5, 3], "channels": 4,
+                                 "downsample_scales": [3, 3, 3, 3, 1], "max_downsample_channels": 32,
+                                 "bias": True, "nonlinear_activation": "LeakyReLU",
+                                 "nonlinear_activation_params": {"negative_slope": 0.1},
+                                 "use_weight_norm": True, "use_spectral_norm": False})
+
+
+def gan_cotangent(shape, i, j):
+    """Deterministic cotangent for output (i, j) (regenerated by the tests, not stored)."""
+    return torch.randn(shape, generator=torch.Generator().manual_seed(1000 * i + j))
+
+
+def _flat_outs(outs, prefix):
+    d = {}
+    for i, o in enumerate(outs):
+        for j, t in enumerate(o):
+            d[f"{prefix}.{i}.{j}"] = _np(t)
+    return d
+
+
+def make_gan(ref, clean, noise, out):
+    """HiFiGAN MSD+MPD discriminator (models/vocoder/HiFiGAN.py:308-395), the
+    adversarial / feature-matching losses (losses/adversarial_loss.py,
+    feat_match_loss.py) and two GAN-mode train_denoise steps (:138-165, :213-263,
+    restated from the source text; discriminator enabled) at reduced width."""
+    _install_trainer_stubs()
+    hifi = importlib.import_module("models.vocoder.HiFiGAN")
+    adv = _load("ref_adversarial_loss", os.path.join(ref, "losses", "adversarial_loss.py"))
+    fm = _load("ref_feat_match_loss", os.path.join(ref, "losses", "feat_match_loss.py"))
+    mel_mod = _load("ref_mel_loss", os.path.join(ref, "losses", "mel_loss.py"))
+    npqc_mod = importlib.import_module("models.autoencoder_without_PQC.AudioDec")
+    T = 1200  # 25 ms at 48 kHz: MPD reflect-pads for periods 7 and 11 (1200 % p != 0)
+    torch.manual_seed(93)
+    D = hifi.Discriminator(**D_PARAMS)
+    d = _sd(D)
+    x = torch.from_numpy(np.stack([clean[0][:T] + 0.1 * noise[0][:T],
+                                   clean[1][:T] + 0.1 * noise[1][:T]]).astype(np.float32)).unsqueeze(1)
+    y = torch.from_numpy(np.stack([clean[0][:T], clean[1][:T]])).unsqueeze(1)
+    d["x"], d["y"] = _np(x), _np(y)
+    xg = x.clone().requires_grad_(True)
+    outs = D(xg)
+    d.update(_flat_outs(outs, "out"))
+    r = [[gan_cotangent(t.shape, i, j) for j, t in enumerate(o)] for i, o in enumerate(outs)]
+    sum((t * rr).sum() for o, ro in zip(outs, r) for t, rr in zip(o, ro)).backward()
+    d["grad_x"] = _np(xg.grad)
+    d.update(_grads(D))
+    with torch.no_grad():
+        outs_y = D(y)
+        outs_x = D(x)
+    gal = adv.GeneratorAdversarialLoss(average_by_discriminators=False)
+    dal = adv.DiscriminatorAdversarialLoss(average_by_discriminators=False)
+    fml = fm.FeatureMatchLoss(average_by_discriminators=False, average_by_layers=False,
+                              include_final_outputs=False)
+    d["loss.gen_adv"] = _np(gal(outs_x))
+    d["loss.gen_adv_avg"] = _np(adv.GeneratorAdversarialLoss()(outs_x))
+    d["loss.gen_adv_hinge"] = _np(adv.GeneratorAdversarialLoss(loss_type="hinge")(outs_x))
+    rl, fl = dal(outs_x, outs_y)
+    d["loss.dis_real"], d["loss.dis_fake"] = _np(rl), _np(fl)
+    rl, fl = adv.DiscriminatorAdversarialLoss(loss_type="hinge")(outs_x, outs_y)
+    d["loss.dis_real_hinge"], d["loss.dis_fake_hinge"] = _np(rl), _np(fl)
+    d["loss.feat_match"] = _np(fml(outs_x, outs_y))
+    d["loss.feat_match_default"] = _np(fm.FeatureMatchLoss()(outs_x, outs_y))
+    d["loss.feat_match_final"] = _np(fm.FeatureMatchLoss(include_final_outputs=True)(outs_x, outs_y))
+    # gradients of the two GAN loss terms w.r.t. the fake input
+    xg = x.clone().requires_grad_(True)
+    o_hat = D(xg)
+    (gal(o_hat) + 2.0 * fml(o_hat, outs_y)).backward()
+    d["grad_x.gen_terms"] = _np(xg.grad)
+    np.savez_compressed(os.path.join(out, "discriminator.npz"), **d)
+
+    # ---- two GAN-mode train_denoise steps (discriminator enabled) ----
+    gp = dict(encode_channels=4, decode_channels=4, code_dim=64, codebook_num=2, codebook_size=64)
+    p48 = dict(fs=48000, fft_sizes=[2048], hop_sizes=[300], win_lengths=[None], window="hann_window",
+               num_mels=80, fmin=0, fmax=24000, log_base=None)
+    # initial weights = generator_nopqc.npz sd (seed 93) and discriminator.npz sd (seed 93): not stored again
+    torch.manual_seed(93)
+    G = npqc_mod.Generator(**gp)
+    torch.manual_seed(93)
+    D = hifi.Discriminator(**D_PARAMS)
+    mel = mel_mod.MultiMelSpectrogramLoss(**p48)
+    og = torch.optim.Adam(G.parameters(), lr=1e-4, betas=(0.5, 0.9), weight_decay=0.0)
+    od = torch.optim.Adam(D.parameters(), lr=2e-4, betas=(0.5, 0.9), weight_decay=0.0)
+    g = {"x_noisy": _np(x), "x_clean": _np(y)}
+    lam_mel, lam_adv, lam_fm = 45.0, 1.0, 2.0
+    for step in range(2):
+        G.train()
+        D.train()
+        pred = G(x)
+        mel_loss = lam_mel * mel(pred, y)
+        p_ = D(pred)
+        with torch.no_grad():
+            p = D(y)
+        adv_loss = lam_adv * gal(pred)  # reference quirk (:147): the waveform, not p_
+        feat_loss = lam_fm * fml(p_, p)
+        gen_loss = mel_loss + adv_loss + feat_loss
+        og.zero_grad()
+        gen_loss.backward()
+        og.step()
+        with torch.no_grad():
+            pred2 = G(x)
+        p = D(y)
+        p_ = D(pred2.detach())
+        rl, fl = dal(p_, p)
+        dis_loss = (rl + fl) * lam_adv
+        od.zero_grad()
+        dis_loss.backward()
+        od.step()
+        g.update({f"mel.{step}": _np(mel_loss), f"adv.{step}": _np(adv_loss), f"fm.{step}": _np(feat_loss),
+                  f"gen.{step}": _np(gen_loss), f"dis.{step}": _np(dis_loss)})
+        g.update(_params(G, f"g_sd{step + 1}."))
+        g.update(_params(D, f"d_sd{step + 1}."))
+    np.savez_compressed(os.path.join(out, "gan_step.npz"), **g)
+
+
+def make_trainer(ref, clean, noise, out):
+    """trainer/denoise.Trainer._train_step (the reference class itself, :52-84)
+    on the reduced-width PQC generator for two steps, then its save_checkpoint
+    (trainerGAN.py:95-121) with a reduced HiFiGAN discriminator."""
+    _install_trainer_stubs()
+    sys.modules.pop("trainer", None)
+    den = importlib.import_module("trainer.denoise")
+    hifi = importlib.import_module("models.vocoder.HiFiGAN")
+    mel_mod = _load("ref_mel_loss", os.path.join(ref, "losses", "mel_loss.py"))
+    pqc_mod = importlib.import_module("models.autoencoder.AudioDec")
+    gp = dict(encode_channels=4, decode_channels=4, code_dim=64, codebook_num=2, codebook_size=64)
+    p24 = dict(fs=24000, fft_sizes=[2048], hop_sizes=[300], win_lengths=[2048], window="hann_window",
+               num_mels=80, fmin=0, fmax=12000, log_base=None)
+    T = 2400
+    xn = torch.from_numpy(np.stack([clean[0][:T] + 0.1 * noise[0][:T],
+                                    clean[1][:T] + 0.1 * noise[1][:T]]).astype(np.float32)).unsqueeze(1)
+    xc = torch.from_numpy(np.stack([clean[0][:T], clean[1][:T]])).unsqueeze(1)
+    torch.manual_seed(95)
+    G = pqc_mod.Generator(**gp)
+    D = hifi.Discriminator(**D_PARAMS)
+    cfg = {"outdir": None, "train_max_steps": 10, "use_mel_loss": True, "use_stft_loss": False,
+           "use_shape_loss": False, "lambda_mel_loss": 45.0, "lambda_vq_loss": 1.0, "generator_grad_norm": -1}
+    og = torch.optim.Adam(G.parameters(), lr=1e-4, betas=(0.5, 0.9), weight_decay=0.0)
+    od = torch.optim.Adam(D.parameters(), lr=2e-4, betas=(0.5, 0.9), weight_decay=0.0)
+    sg = torch.optim.lr_scheduler.StepLR(og, step_size=200000, gamma=1.0)
+    sd = torch.optim.lr_scheduler.MultiStepLR(od, milestones=[200000, 400000], gamma=0.5)
+    d = {"x_noisy": _np(xn), "x_clean": _np(xc)}
+    d.update(_sd(G, "sd0."))
+    tr = den.Trainer(steps=0, epochs=0, data_loader={}, model={"generator": G, "discriminator": D},
+                     criterion={"mel": mel_mod.MultiMelSpectrogramLoss(**p24)},
+                     optimizer={"generator": og, "discriminator": od},
+                     scheduler={"generator": sg, "discriminator": sd}, config=cfg)
+    tr.tqdm = types.SimpleNamespace(update=lambda n=1: None)
+    for step in range(2):
+        tr._train_step((xn, xc))
+        for k, v in tr.total_train_loss.items():
+            d[f"rec.{step}.{k}"] = np.array(v, dtype=np.float64)
+        tr.total_train_loss.clear()
+        d.update({f"sd{step + 1}.{k}": _np(p) for k, p in G.named_parameters() if p.requires_grad})
+    tr.save_checkpoint(os.path.join(out, "trainer_ckpt.pt"))
+    np.savez_compressed(os.path.join(out, "trainer_step.npz"), **d)
+
+
 def make(ref, out, only=None):
     du = _install_stubs(ref)
     stft_mod = _load("ref_stft_loss", os.path.join(ref, "losses", "stft_loss.py"))
@@ -146,6 +340,10 @@ def make(ref, out, only=None):
         return make_stream(pqc_mod, clean, noise, gp, out)
     if only == "waveform":
         return make_waveform(ref, clean, noise, out)
+    if only == "gan":
+        return make_gan(ref, clean, noise, out)
+    if only == "trainer":
+        return make_trainer(ref, clean, noise, out)
     torch.manual_seed(93)
 
     # ---------------- melmat (losses/mel_loss.py:54-61) ----------------
@@ -375,7 +573,7 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
     ap.add_argument("--out", default=HERE)
-    ap.add_argument("--only", default=None, help="regenerate one fixture family (stream, waveform)")
+    ap.add_argument("--only", default=None, help="regenerate one fixture family (stream, waveform, gan, trainer)")
     a = ap.parse_args()
     make(a.ref, a.out, a.only)
     for f in sorted(os.listdir(a.out)):

@@ -125,17 +125,26 @@ def test_fwd4_tile_variants_on_c3_shapes(gpu, shape, form):
         lib.sel_tune(4, p4)
 
 
-def test_c3_denoise_step_bf16_vs_fp32_oracle(gpu):
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+def test_c3_denoise_step_vs_fp32_oracle(gpu, dtype):
     """Full C3 step: PQC generator (symAD_libritts_24000_hop300), B = 64 x 1 s,
     loss = lambda_vq * sum(vqloss) + 45 * mel, grads into the encoder/projector
-    (decoder + quantizer frozen, codebook eval) — bf16 convs vs the fp32 oracle.
+    (decoder + quantizer frozen, codebook eval) — HIP convs (bf16 or the
+    exact-fp32 path) vs the fp32 oracle on the same weights.
 
-    Bounds (bf16 operands carry 2^-9 relative rounding per layer through ~30
-    layers): y 3e-2, z 3e-2, mel-loss term 5e-3 relative, encoder/projector
-    gradient (all trainable tensors concatenated) 6e-2 norm-wise, each tensor
-    1.5e-1.  VQ indices are not compared: z itself differs at the bf16 level, so
-    near-ties legitimately flip (the VQ kernel's exactness is tested on identical
-    z in test_gpu_model.py)."""
+    Forward: y, z and the mel term norm-wise.  Backward, two ways:
+    * same upstream gradient: both sides back-propagate the ORACLE's dL/dy and
+      dL/dvqloss, which isolates the conv stack's backward from the mel-L1
+      subgradient (sign(mel(y) - mel(x)) flips wherever |diff| is below the
+      forward error: measured 9e-2 end-to-end in bf16 on r2a, a property of the
+      L1 loss, not of the kernels);
+    * end to end (own loss): bounded loosely, for the record.
+    Bounds — bf16 (2^-9 operand rounding per layer, ~30 layers): y, z 3e-2,
+    mel 5e-3, same-upstream grad 3e-2 concatenated / 6e-2 worst tensor, end to
+    end 1.5e-1.  fp32: 1e-4 forward, 2e-3 gradients (summation order only).
+    VQ indices are not compared here: z differs at the bf16 level, so near-ties
+    may flip (the VQ kernel's exactness is tested on identical z,
+    test_gpu_model.py)."""
     from oracle import ref_ops as R
     from oracle.melfilters import mel as melbank
     from losses import MultiMelSpectrogramLoss
@@ -154,37 +163,55 @@ def test_c3_denoise_step_bf16_vs_fp32_oracle(gpu):
     clean = 0.1 * torch.randn(B, 1, 24000, generator=g)
     noisy = R.add_noise(clean, 0.1 * torch.randn(B, 1, 24000, generator=g), 15)
     mm = torch.from_numpy(melbank(sr=mp["fs"], n_fft=2048, n_mels=80, fmin=mp["fmin"], fmax=mp["fmax"]).T.copy())
-    win = R.hann(2048) if mp["win_lengths"][0] is None else R.hann(mp["win_lengths"][0])
+    wl = mp["win_lengths"][0] or 2048
     torch.set_num_threads(min(16, torch.get_num_threads()))
     yr, zqr, zr, vqr, _ = R.generator_forward(P, noisy, R.generator_geometry(), pqc=True)
-    melr = R.multi_mel_loss(yr, clean, [(2048, 300, mp["win_lengths"][0] or 2048)], [win], [mm], 1e-10, None)
+    yr.retain_grad()
+    vqr.retain_grad()
+    melr = R.multi_mel_loss(yr, clean, [(2048, 300, wl)], [R.hann(wl)], [mm], 1e-10, None)
     lossr = cfg["lambda_vq_loss"] * vqr.sum() + cfg["lambda_mel_loss"] * melr
     lossr.backward()
+    gy, gvq = yr.grad.clone(), vqr.grad.clone()
 
     G = G.to(gpu)
     for p in list(G.quantizer.parameters()) + list(G.decoder.parameters()):
         p.requires_grad_(False)
     G.quantizer.codebook.eval()
     mel = MultiMelSpectrogramLoss(**mp).to(gpu)
-    with precision(torch.bfloat16):
-        y, zq, z, vql, ppl = G(noisy.to(gpu))
-        meld = mel(y, clean.to(gpu))
-        loss = cfg["lambda_vq_loss"] * vql.sum() + cfg["lambda_mel_loss"] * meld
-        loss.backward()
+    params = dict(G.named_parameters())
     rel = lambda a, b: ((a.detach().double().cpu() - b.detach().double()).norm() / b.detach().double().norm()).item()
+
+    def grad_err():
+        num = den = 0.0
+        worst = (0.0, "")
+        for k in train:
+            gd, gr = params[k].grad.double().cpu(), P[k].grad.double()
+            num += ((gd - gr) ** 2).sum().item()
+            den += (gr ** 2).sum().item()
+            worst = max(worst, (rel(gd, gr), k))
+            params[k].grad = None
+        return (num / den) ** 0.5, worst
+
+    with precision(torch.bfloat16 if dtype == "bf16" else torch.float32):
+        xin = noisy.to(gpu)
+        y, zq, z, vql, ppl = G(xin)
+        meld = mel(y, clean.to(gpu))
+        ((y * gy.to(gpu)).sum() + (vql * gvq.to(gpu)).sum()).backward()
+        eg_same, worst_same = grad_err()
+        y, zq, z, vql, ppl = G(xin)
+        meld = mel(y, clean.to(gpu))
+        (cfg["lambda_vq_loss"] * vql.sum() + cfg["lambda_mel_loss"] * meld).backward()
+        eg_e2e, worst_e2e = grad_err()
     ey, ez = rel(y, yr), rel(z, zr)
     em = abs(meld.item() - melr.item()) / abs(melr.item())
-    params = dict(G.named_parameters())
-    num = den = 0.0
-    worst = (0.0, "")
-    for k in train:
-        gd, gr = params[k].grad.double().cpu(), P[k].grad.double()
-        num += ((gd - gr) ** 2).sum().item()
-        den += (gr ** 2).sum().item()
-        worst = max(worst, (rel(gd, gr), k))
-    eg = (num / den) ** 0.5
-    print(f"C3 bf16 vs fp32: y {ey:.2e} z {ez:.2e} mel {em:.2e} grad {eg:.2e} worst {worst}")
-    assert ey <= 3e-2 and ez <= 3e-2, (ey, ez)
-    assert em <= 5e-3, em
-    assert eg <= 6e-2, eg
-    assert worst[0] <= 1.5e-1, worst
+    print(f"C3 {dtype} vs fp32 oracle: y {ey:.2e} z {ez:.2e} mel {em:.2e} | same-upstream grad {eg_same:.2e} "
+          f"worst {worst_same} | end-to-end grad {eg_e2e:.2e} worst {worst_e2e}")
+    if dtype == "bf16":
+        assert ey <= 3e-2 and ez <= 3e-2, (ey, ez)
+        assert em <= 5e-3, em
+        assert eg_same <= 3e-2 and worst_same[0] <= 6e-2, (eg_same, worst_same)
+        assert eg_e2e <= 1.5e-1, eg_e2e
+    else:
+        assert ey <= 1e-4 and ez <= 1e-4 and em <= 1e-4, (ey, ez, em)
+        assert eg_same <= 2e-3 and worst_same[0] <= 5e-3, (eg_same, worst_same)
+        assert eg_e2e <= 5e-2, eg_e2e

@@ -221,3 +221,148 @@ def test_waveform_shape_loss():
         close(loss, g[f"{tag}.loss"], rtol=1e-6, atol=1e-8)
         loss.backward()
         close(x.grad, g[f"{tag}.grad"], rtol=1e-6, atol=1e-9)
+
+
+# ---------------------------------------------------------------- GAN mode
+D_PARAMS = dict(
+    scales=3, scale_downsample_pooling_params={"kernel_size": 4, "stride": 2, "padding": 2},
+    scale_discriminator_params={"in_channels": 1, "out_channels": 1, "kernel_sizes": [15, 41, 5, 3],
+                                "channels": 16, "max_downsample_channels": 32, "max_groups": 16,
+                                "downsample_scales": [4, 4, 4, 4, 1]},
+    periods=[2, 3, 5, 7, 11],
+    period_discriminator_params={"in_channels": 1, "out_channels": 1, "kernel_sizes": [5, 3], "channels": 4,
+                                 "downsample_scales": [3, 3, 3, 3, 1], "max_downsample_channels": 32})
+
+
+def gan_cotangent(shape, i, j):
+    """Same deterministic cotangents as tests/golden/make_goldens.gan_cotangent."""
+    return torch.randn(shape, generator=torch.Generator().manual_seed(1000 * i + j))
+
+
+def _dparams(g, prefix="sd."):
+    return {k[len(prefix):]: T(v).clone() for k, v in g.items() if k.startswith(prefix)}
+
+
+def test_hifigan_discriminator():
+    """HiFiGAN.Discriminator (HiFiGAN.py:308-395): all 8 x per-layer outputs and
+    the gradients of sum(out * r) w.r.t. the input and every parameter."""
+    g = golden("discriminator")
+    P = _dparams(g)
+    for v in P.values():
+        v.requires_grad_(True)
+    x = T(g["x"]).clone().requires_grad_(True)
+    outs = R.hifigan_discriminator(P, x, **D_PARAMS)
+    assert len(outs) == 8
+    tot = 0.0
+    for i, o in enumerate(outs):
+        for j, t in enumerate(o):
+            close(t, g[f"out.{i}.{j}"], rtol=1e-5, atol=1e-6)
+            tot = tot + (t * gan_cotangent(t.shape, i, j)).sum()
+    tot.backward()
+    close(x.grad, g["grad_x"], rtol=1e-4, atol=1e-5)
+    for k, v in P.items():
+        close(v.grad, g["g." + k], rtol=1e-4, atol=1e-5)
+
+
+def test_gan_losses():
+    """adversarial_loss.py (mse + hinge, averaged or not) and feat_match_loss.py."""
+    g = golden("discriminator")
+    P = _dparams(g)
+    with torch.no_grad():
+        oy = R.hifigan_discriminator(P, T(g["y"]), **D_PARAMS)
+        ox = R.hifigan_discriminator(P, T(g["x"]), **D_PARAMS)
+    close(R.generator_adv_loss(ox, False), g["loss.gen_adv"], rtol=1e-6)
+    close(R.generator_adv_loss(ox), g["loss.gen_adv_avg"], rtol=1e-6)
+    close(R.generator_adv_loss(ox, loss_type="hinge"), g["loss.gen_adv_hinge"], rtol=1e-6)
+    rl, fl = R.discriminator_adv_loss(ox, oy, False)
+    close(rl, g["loss.dis_real"], rtol=1e-6)
+    close(fl, g["loss.dis_fake"], rtol=1e-6)
+    rl, fl = R.discriminator_adv_loss(ox, oy, loss_type="hinge")
+    close(rl, g["loss.dis_real_hinge"], rtol=1e-6)
+    close(fl, g["loss.dis_fake_hinge"], rtol=1e-6)
+    close(R.feat_match_loss(ox, oy, False, False, False), g["loss.feat_match"], rtol=1e-6)
+    close(R.feat_match_loss(ox, oy), g["loss.feat_match_default"], rtol=1e-6)
+    close(R.feat_match_loss(ox, oy, include_final_outputs=True), g["loss.feat_match_final"], rtol=1e-6)
+    x = T(g["x"]).clone().requires_grad_(True)
+    oh = R.hifigan_discriminator(P, x, **D_PARAMS)
+    (R.generator_adv_loss(oh, False) + 2.0 * R.feat_match_loss(oh, oy, False, False, False)).backward()
+    close(x.grad, g["grad_x.gen_terms"], rtol=1e-4, atol=1e-7)
+
+
+def test_gan_step():
+    """Two GAN-mode train_denoise steps (:138-165, :213-263 with the discriminator
+    enabled; vctk 48 kHz loss weights): generator 45*mel + adv (the waveform quirk,
+    :147) + 2*feat-match, Adam(1e-4, (0.5, 0.9)); then the discriminator on the
+    regenerated output, Adam(2e-4, (0.5, 0.9))."""
+    g = golden("gan_step")
+    Gp = _dparams(golden("generator_nopqc"))
+    Dp = _dparams(golden("discriminator"))
+    gm = golden("melmat")
+    gtrain = [k for k in Gp if k.startswith(("encoder.", "decoder.conv_blocks", "decoder.conv2"))
+              and not k.endswith("pad_buffer")]
+    for k in gtrain:
+        Gp[k].requires_grad_(True)
+    for v in Dp.values():
+        v.requires_grad_(True)
+    og = torch.optim.Adam([Gp[k] for k in gtrain], lr=1e-4, betas=(0.5, 0.9), weight_decay=0.0)
+    od = torch.optim.Adam(list(Dp.values()), lr=2e-4, betas=(0.5, 0.9), weight_decay=0.0)
+    geo = R.generator_geometry(encode_channels=4, decode_channels=4)
+    mm = T(gm["melmat.48k_fmax24000"])
+    x, y = T(g["x_noisy"]), T(g["x_clean"])
+    for s in range(2):
+        pred = R.generator_forward(Gp, x, geo, pqc=False)
+        mel = 45.0 * R.multi_mel_loss(pred, y, [(2048, 300, 2048)], [R.hann(2048)], [mm], 1e-10, None)
+        p_ = R.hifigan_discriminator(Dp, pred, **D_PARAMS)
+        with torch.no_grad():
+            p = R.hifigan_discriminator(Dp, y, **D_PARAMS)
+        adv = R.generator_adv_loss(pred, False)
+        fm = 2.0 * R.feat_match_loss(p_, p, False, False, False)
+        gen = mel + adv + fm
+        og.zero_grad()
+        od.zero_grad()
+        gen.backward()
+        og.step()
+        with torch.no_grad():
+            pred2 = R.generator_forward(Gp, x, geo, pqc=False)
+        rl, fl = R.discriminator_adv_loss(R.hifigan_discriminator(Dp, pred2, **D_PARAMS),
+                                          R.hifigan_discriminator(Dp, y, **D_PARAMS), False)
+        dis = rl + fl
+        od.zero_grad()
+        dis.backward()
+        od.step()
+        for name, v in (("mel", mel), ("adv", adv), ("fm", fm), ("gen", gen), ("dis", dis)):
+            close(v, g[f"{name}.{s}"], rtol=1e-5 if s == 0 else 1e-4)
+        for k in gtrain:
+            close(Gp[k], g[f"g_sd{s + 1}.{k}"], rtol=1e-5, atol=1e-7)
+        for k, v in Dp.items():
+            close(v, g[f"d_sd{s + 1}.{k}"], rtol=1e-5, atol=1e-7)
+
+
+def test_denoise_trainer_step():
+    """trainer/denoise.Trainer._train_step (:52-84) run by the reference class
+    itself: PQC generator, codebook eval, lambda_vq * sum(vqloss) + 45 * mel
+    (libritts-24k mel params), decoder/quantizer frozen, Adam(1e-4, (0.5, 0.9))."""
+    g = golden("trainer_step")
+    P = _dparams(g, "sd0.")
+    train = [k for k in P if k.startswith(("encoder.", "projector.")) and k.endswith(("weight", "bias"))]
+    for k in train:
+        P[k].requires_grad_(True)
+    opt = torch.optim.Adam([P[k] for k in train], lr=1e-4, betas=(0.5, 0.9), weight_decay=0.0)
+    geo = R.generator_geometry(encode_channels=4, decode_channels=4)
+    mm = T(golden("melmat")["melmat.24k_fmax12000"])
+    xn, xc = T(g["x_noisy"]), T(g["x_clean"])
+    for s in range(2):
+        y, zq, z, vql, ppl = R.generator_forward(P, xn, geo, pqc=True, codebook_num=2)
+        mel = 45.0 * R.multi_mel_loss(y, xc, [(2048, 300, 2048)], [R.hann(2048)], [mm], 1e-10, None)
+        vq = vql.sum()
+        loss = vq + mel
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        close(mel, g[f"rec.{s}.train/mel_loss"], rtol=1e-5)
+        close(vq, g[f"rec.{s}.train/train/vqloss"], rtol=1e-5)
+        close(loss, g[f"rec.{s}.train/generator_loss"], rtol=1e-5)
+        for i in range(2):
+            close(ppl[i], g[f"rec.{s}.train/train/ppl_{i}"], rtol=1e-5)
+        for k in train:
+            close(P[k], g[f"sd{s + 1}.{k}"], rtol=1e-5, atol=1e-7)
