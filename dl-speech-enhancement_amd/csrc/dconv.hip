@@ -1,0 +1,1024 @@
+// HiFi-GAN multi-scale + multi-period discriminator on gfx950
+// (models/vocoder/HiFiGAN.py:308-395, models/vocoder/modules/discriminator.py:26-447)
+// and the GAN losses (losses/adversarial_loss.py, losses/feat_match_loss.py).
+//
+// Every discriminator layer — the grouped, strided k41 Conv1d of the MSD, the
+// (k,1) Conv2d of the MPD (a 1-D conv along T/p with the p columns as extra
+// sequences), the dense k5/k3/k2 output convs — and every adjoint is ONE
+// primitive (include/sel.h sel_dconv_desc):
+//
+//   out[b, j, col(g, o)] = sum_{i<K, r<S, c<Cg} Wp[g][o][i][r][c] * x[b, j+q0+i, r*Cs + g*Cg + c]
+//
+// over channels-last rows.  A stride-s conv is run on the PHASE VIEW of its
+// input (rows of s consecutive samples: x[b, s*t + r, c] = view[b, t, r*C + c],
+// a free reinterpretation when the row count is padded to a multiple of s), so
+// it becomes a stride-1 conv with ceil(K/s)+1 taps over s*C channels and no
+// wasted output rows; its adjoint is the same primitive on gout with So = s
+// output phases.  Groups index disjoint channel slices, so no MFMA lane ever
+// multiplies a structural zero of a grouped weight (a group narrower than the
+// 32-wide MFMA tile is padded to 32 output channels; only the MSD's 8-input /
+// 16-output-channel layer pays that, 2x on 4% of the flops).
+//
+//   MFMA kernel (Cg % 8 == 0): v_mfma_f32_32x32x16_bf16 (bf16 path) or
+//     v_mfma_f32_32x32x2_f32 (exact-fp32 parity path).  Reduction vectors are
+//     8 consecutive channels of one (tap, phase): each 32-lane half of a wave
+//     feeds one vector per MFMA.  The input span of a BM-row tile is staged once
+//     per 32-channel chunk and re-read by every tap; weights are staged per tap
+//     group.  Epilogue: + bias, LeakyReLU, or (+ res) * LeakyReLU'(aux) for the
+//     adjoint, rows past Tvalid written as exact zeros (the next layer's padding).
+//   VALU kernel: the 1-channel input / 1-channel output layers (first and last
+//     conv of every sub-discriminator and their adjoints), where a 32-wide MFMA
+//     tile would be 1/32 useful.
+//   Weight gradient: gW = sum_rows gout^T x as split-row partials (MFMA with
+//     transposing LDS reads for bf16, VALU for fp32 / thin layers), then one
+//     deterministic reduction fused with the unpack to the torch layout and the
+//     weight-norm backward (torch.nn.utils.weight_norm, used by the MPD).
+#include <algorithm>
+
+#include "sel_common.h"
+
+namespace sel {
+namespace dconv {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef short v8i16 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ float to_f(float v) { return v; }
+__device__ __forceinline__ float to_f(__bf16 v) { return float(v); }
+template <typename T> __device__ __forceinline__ T from_f(float v);
+template <> __device__ __forceinline__ float from_f<float>(float v) { return v; }
+template <> __device__ __forceinline__ __bf16 from_f<__bf16>(float v) { return __bf16(v); }
+
+__device__ __forceinline__ float leaky(float v, float s) { return v > 0.f ? v : v * s; }
+__device__ __forceinline__ float leaky_grad(float y, float s) { return y > 0.f ? 1.f : s; }
+
+using D = sel_dconv_desc;
+
+__device__ __forceinline__ int64_t in_col(const D& d, int g, int r, int c) {
+  return int64_t(r) * d.Cs + int64_t(g) * d.Cg + c;
+}
+__device__ __forceinline__ int64_t out_col(const D& d, int g, int o) {
+  const int ro = o / d.Ng, no = o - ro * d.Ng;
+  return int64_t(ro) * d.Ns + int64_t(g) * d.Ng + no;
+}
+
+template <typename T> struct Elt;
+template <> struct Elt<__bf16> { static constexpr int VEC = 8; static constexpr int P = 40; };  // 80-B LDS rows
+template <> struct Elt<float> { static constexpr int VEC = 4; static constexpr int P = 36; };   // 144-B LDS rows
+
+constexpr int CH = 32;  // reduction channels per staged chunk
+constexpr int KC = 8;   // taps per staged weight group
+
+// ---------------------------------------------------------------------------
+// MFMA primitive.  Block = BM output rows of one sequence x BN local output
+// channels of one group; 4 waves as 2 x 2 (wave tile BM/2 x BN/2, 32x32 MFMA
+// sub-tiles).  LDS: x span [BM + K - 1][P] of the current 32-channel chunk,
+// weights [BN][KC][P] of the current tap group.
+// ---------------------------------------------------------------------------
+template <typename T, int BM, int BN>
+__global__ __launch_bounds__(256) void k_dconv_mfma(D d, const T* __restrict__ x, const T* __restrict__ wp,
+                                                    const float* __restrict__ bias, const T* __restrict__ aux,
+                                                    const T* __restrict__ res, T* __restrict__ out) {
+  constexpr int P = Elt<T>::P;
+  constexpr int VEC = Elt<T>::VEC;
+  constexpr int WAVES_N = BN / 32, WAVES_M = 4 / WAVES_N;
+  constexpr int TM = BM / (32 * WAVES_M);
+  static_assert(TM >= 1 && WAVES_N * WAVES_M == 4, "tile");
+  extern __shared__ __align__(16) unsigned char smem[];
+  T* const xs = reinterpret_cast<T*>(smem);
+  const int span = BM + d.K - 1;
+  T* const ws = xs + span * P;  // [BN][KC][P]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+  const int tps = (d.Tvo + BM - 1) / BM;
+  const int b = blockIdx.x / tps;
+  const int j0 = (blockIdx.x % tps) * BM;
+  const int no_per_g = d.So * d.Ng;
+  const int ntile_g = (no_per_g + BN - 1) / BN;
+  const int g = blockIdx.y / ntile_g;
+  const int o0 = (blockIdx.y % ntile_g) * BN;
+  const int64_t xrow0 = int64_t(b) * d.Tvs;
+  const int nred = d.S * d.Cg;  // reduction channels per tap
+
+  floatx16 acc[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
+
+  // this lane's output rows (B operand column) and channel (A operand row)
+  int lrow[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) lrow[i] = wm * (BM / WAVES_M) + i * 32 + (lane & 31);
+  const int half = lane >> 5;
+  const int nw_ = wn * 32 + (lane & 31);
+  const int vpr = CH / VEC;
+
+  for (int cc = 0; cc < nred; cc += CH) {
+    const int chn = nred - cc < CH ? nred - cc : CH;  // multiple of 8 (host-checked)
+    __syncthreads();
+    // stage x span rows [j0 + q0, j0 + q0 + span) x chunk channels (vectors of VEC)
+    for (int idx = tid; idx < span * vpr; idx += 256) {
+      const int rr = idx / vpr, v = idx % vpr;
+      const int t = j0 + d.q0 + rr;
+      const int ch = cc + v * VEC;
+      uint4 val = make_uint4(0, 0, 0, 0);
+      if (t >= 0 && t < d.Tv && v * VEC < chn) {
+        const int rph = ch / d.Cg, c = ch - rph * d.Cg;
+        val = *reinterpret_cast<const uint4*>(x + (xrow0 + t) * d.ldx + in_col(d, g, rph, c));
+      }
+      *reinterpret_cast<uint4*>(xs + rr * P + v * VEC) = val;
+    }
+    for (int k0 = 0; k0 < d.K; k0 += KC) {
+      const int kn = d.K - k0 < KC ? d.K - k0 : KC;
+      if (k0) __syncthreads();
+      for (int idx = tid; idx < BN * KC * vpr; idx += 256) {
+        const int v = idx % vpr, kk = (idx / vpr) % KC, n = idx / (vpr * KC);
+        uint4 val = make_uint4(0, 0, 0, 0);
+        if (kk < kn && o0 + n < no_per_g && v * VEC < chn)
+          val = *reinterpret_cast<const uint4*>(
+              wp + ((int64_t(g) * no_per_g + o0 + n) * d.K + k0 + kk) * nred + cc + v * VEC);
+        *reinterpret_cast<uint4*>(ws + (n * KC + kk) * P + v * VEC) = val;
+      }
+      __syncthreads();
+      for (int kk = 0; kk < kn; ++kk) {
+        const int k = k0 + kk;
+        if constexpr (sizeof(T) == 2) {
+#pragma unroll
+          for (int h = 0; h < CH / 16; ++h) {
+            if (h * 16 >= chn) break;
+            const int co = 16 * h + 8 * half;
+            const bf16x8 bw = *reinterpret_cast<const bf16x8*>(ws + (nw_ * KC + kk) * P + co);
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+              const bf16x8 af = *reinterpret_cast<const bf16x8*>(xs + (lrow[i] + k) * P + co);
+              acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bw, af, acc[i], 0, 0, 0);
+            }
+          }
+        } else {
+          for (int c2 = 0; c2 < chn; c2 += 2) {
+            const int co = c2 + half;
+            const float bw = ws[(nw_ * KC + kk) * P + co];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+              const float af = xs[(lrow[i] + k) * P + co];
+              acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(bw, af, acc[i], 0, 0, 0);
+            }
+          }
+        }
+      }
+    }
+  }
+
+  // epilogue (operands swapped: lane -> output row lane & 31 of its sub-tile,
+  // element e -> channel (e & 3) + 8 (e >> 2) + 4 (lane >> 5) of the wave's 32)
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int j = j0 + lrow[i];
+    if (j >= d.Tvo) continue;
+    const int64_t orow = (int64_t(b) * d.Tvo + j) * d.ldo;
+    const bool valid = j < d.Tvalid;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int o = o0 + wn * 32 + (e & 3) + 8 * (e >> 2) + 4 * half;
+      if (o >= no_per_g) continue;
+      const int64_t col = out_col(d, g, o);
+      float v = 0.f;
+      if (valid) {
+        v = acc[i][e];
+        if (bias) v += bias[col];
+        if (res) v += to_f(res[orow + col]);
+        if (aux) v *= leaky_grad(to_f(aux[orow + col]), d.slope);
+        if (d.act) v = leaky(v, d.slope);
+      }
+      out[orow + col] = from_f<T>(v);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// VALU primitive (any Cg; used when S*Cg*K or the group output width is tiny).
+// One thread per (row, output channel); the reduction walks (i, r, c).
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void k_dconv_valu(D d, const T* __restrict__ x, const T* __restrict__ wp,
+                                                    const float* __restrict__ bias, const T* __restrict__ aux,
+                                                    const T* __restrict__ res, T* __restrict__ out) {
+  const int no_per_g = d.So * d.Ng;
+  const int64_t nout = int64_t(d.G) * no_per_g;
+  const int64_t total = int64_t(d.B) * d.Tvo * nout;
+  const int nred = d.S * d.Cg;
+  for (int64_t idx = int64_t(blockIdx.x) * 256 + threadIdx.x; idx < total; idx += int64_t(gridDim.x) * 256) {
+    const int64_t row = idx / nout;
+    const int oc = int(idx - row * nout);
+    const int g = oc / no_per_g, o = oc - g * no_per_g;
+    const int b = int(row / d.Tvo), j = int(row - int64_t(b) * d.Tvo);
+    const int64_t orow = row * d.ldo;
+    const int64_t col = out_col(d, g, o);
+    float v = 0.f;
+    if (j < d.Tvalid) {
+      const T* w = wp + (int64_t(g) * no_per_g + o) * d.K * nred;
+      for (int i = 0; i < d.K; ++i) {
+        const int t = j + d.q0 + i;
+        if (t < 0 || t >= d.Tv) continue;
+        const T* xr = x + (int64_t(b) * d.Tvs + t) * d.ldx;
+        for (int r = 0; r < d.S; ++r)
+          for (int c = 0; c < d.Cg; ++c) v += to_f(w[i * nred + r * d.Cg + c]) * to_f(xr[in_col(d, g, r, c)]);
+      }
+      if (bias) v += bias[col];
+      if (res) v += to_f(res[orow + col]);
+      if (aux) v *= leaky_grad(to_f(aux[orow + col]), d.slope);
+      if (d.act) v = leaky(v, d.slope);
+    }
+    out[orow + col] = from_f<T>(v);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Weight gradient partials.  gW[g][o][i][r][c] = sum over rows (b, j < Tvalid)
+// of gout[b, j, col(g, o)] * x[b, j + q0 + i, r*Cs + g*Cg + c]; bias partials
+// gb[col] = sum gout.  part[split][...] (fp32), reduced by k_dwgrad_finish.
+// ---------------------------------------------------------------------------
+// VALU: thread per weight element, rows of its split.
+template <typename T>
+__global__ __launch_bounds__(256) void k_dwgrad_valu(D d, const T* __restrict__ gout, const T* __restrict__ x,
+                                                     int rows_per_split, float* __restrict__ part,
+                                                     float* __restrict__ bpart) {
+  const int no_per_g = d.So * d.Ng;
+  const int nred = d.S * d.Cg;
+  const int64_t nw = int64_t(d.G) * no_per_g * d.K * nred;
+  const int64_t nb = bpart ? int64_t(d.G) * no_per_g : 0;
+  const int64_t total_rows = int64_t(d.B) * d.Tvalid;
+  const int64_t r0 = int64_t(blockIdx.y) * rows_per_split;
+  const int64_t r1 = r0 + rows_per_split < total_rows ? r0 + rows_per_split : total_rows;
+  for (int64_t idx = int64_t(blockIdx.x) * 256 + threadIdx.x; idx < nw + nb; idx += int64_t(gridDim.x) * 256) {
+    float acc = 0.f;
+    if (idx < nw) {
+      const int rc = int(idx % nred);
+      const int i = int((idx / nred) % d.K);
+      const int64_t go = idx / (int64_t(nred) * d.K);
+      const int g = int(go / no_per_g), o = int(go - int64_t(g) * no_per_g);
+      const int rph = rc / d.Cg, c = rc - rph * d.Cg;
+      const int64_t oc = out_col(d, g, o), ic = in_col(d, g, rph, c);
+      for (int64_t rr = r0; rr < r1; ++rr) {
+        const int b = int(rr / d.Tvalid), j = int(rr - int64_t(b) * d.Tvalid);
+        const int t = j + d.q0 + i;
+        if (t < 0 || t >= d.Tv) continue;
+        acc += to_f(gout[(int64_t(b) * d.Tvo + j) * d.ldo + oc]) * to_f(x[(int64_t(b) * d.Tvs + t) * d.ldx + ic]);
+      }
+      part[int64_t(blockIdx.y) * nw + idx] = acc;
+    } else {
+      const int64_t go = idx - nw;
+      const int g = int(go / no_per_g), o = int(go - int64_t(g) * no_per_g);
+      const int64_t oc = out_col(d, g, o);
+      for (int64_t rr = r0; rr < r1; ++rr) {
+        const int b = int(rr / d.Tvalid), j = int(rr - int64_t(b) * d.Tvalid);
+        acc += to_f(gout[(int64_t(b) * d.Tvo + j) * d.ldo + oc]);
+      }
+      bpart[int64_t(blockIdx.y) * nb + go] = acc;
+    }
+  }
+}
+
+// bf16 MFMA weight gradient (Cg % 8 == 0, group output width a multiple of 16).
+// Block = (16*NT local outputs o, 32 reduction channels (r, c), tap group of
+// <= WG_TAPS taps, split of 64-row tiles).  Both operands reduce over ROWS of the
+// row-major LDS tiles and are read with ds_read_b64_tr_b16 (gfx950 transposing
+// LDS read), v_mfma_f32_16x16x32_bf16.
+constexpr int WG_BM = 64;
+constexpr int WG_TAPS = 8;
+
+__device__ __forceinline__ v4i16 tr_read(const __bf16* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)(p));
+}
+__device__ __forceinline__ bf16x8 tr_frag(const __bf16* p, int pitch) {
+  const v4i16 lo = tr_read(p);
+  const v4i16 hi = tr_read(p + 16 * pitch);
+  const v8i16 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+template <int NT>
+__global__ __launch_bounds__(256) void k_dwgrad_mfma(D d, const __bf16* __restrict__ gout,
+                                                     const __bf16* __restrict__ x, int tiles_per_seq,
+                                                     int tiles_per_split, int ntg, float* __restrict__ part) {
+  constexpr int BN = 16 * NT;
+  constexpr int PG = BN + 16;  // (PG/2) dwords = 8 x odd: conflict-free transposing reads
+  constexpr int PX = 32 + 16;
+  constexpr int WPN = 4 / NT;  // waves per 16-wide output sub-tile
+  constexpr int MAXJ = (WG_TAPS * 2 + WPN - 1) / WPN;
+  extern __shared__ __align__(16) unsigned char smem[];
+  __bf16* const gs = reinterpret_cast<__bf16*>(smem);
+  __bf16* const xs = gs + WG_BM * PG;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nt = wave % NT, wsub = wave / NT;
+  const int no_per_g = d.So * d.Ng;
+  const int ntile_g = (no_per_g + BN - 1) / BN;
+  const int g = blockIdx.x / ntile_g;
+  const int o0 = (blockIdx.x % ntile_g) * BN;
+  const int nred = d.S * d.Cg;
+  const int cc = blockIdx.y * 32;
+  const int tgi = blockIdx.z % ntg, split = blockIdx.z / ntg;
+  const int k0 = tgi * WG_TAPS;
+  const int kn = d.K - k0 < WG_TAPS ? d.K - k0 : WG_TAPS;
+  const int span = WG_BM + kn - 1;
+  const int64_t ntiles = int64_t(d.B) * tiles_per_seq;
+  const int64_t tb = int64_t(split) * tiles_per_split;
+  const int64_t te = tb + tiles_per_split < ntiles ? tb + tiles_per_split : ntiles;
+  const int npairs = kn * 2;
+  const int gq = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+
+  floatx4 acc[MAXJ];
+#pragma unroll
+  for (int j = 0; j < MAXJ; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  for (int64_t tile = tb; tile < te; ++tile) {
+    const int b = int(tile / tiles_per_seq);
+    const int j0 = int(tile % tiles_per_seq) * WG_BM;
+    __syncthreads();
+    for (int idx = tid; idx < WG_BM * (BN / 8); idx += 256) {
+      const int rr = idx / (BN / 8), v = (idx % (BN / 8)) * 8;
+      const int j = j0 + rr;
+      __bf16 vals[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int o = o0 + v + e;
+        vals[e] = (j < d.Tvalid && o < no_per_g) ? gout[(int64_t(b) * d.Tvo + j) * d.ldo + out_col(d, g, o)]
+                                                 : __bf16(0.f);
+      }
+      *reinterpret_cast<uint4*>(gs + rr * PG + v) = *reinterpret_cast<uint4*>(vals);
+    }
+    for (int idx = tid; idx < span * 4; idx += 256) {
+      const int rr = idx >> 2, v = (idx & 3) * 8;
+      const int t = j0 + d.q0 + k0 + rr;
+      const int ch = cc + v;
+      uint4 val = make_uint4(0, 0, 0, 0);
+      if (t >= 0 && t < d.Tv && ch < nred) {
+        const int rph = ch / d.Cg, c = ch - rph * d.Cg;
+        val = *reinterpret_cast<const uint4*>(x + (int64_t(b) * d.Tvs + t) * d.ldx + in_col(d, g, rph, c));
+      }
+      *reinterpret_cast<uint4*>(xs + rr * PX + v) = val;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int grp = 0; grp < WG_BM / 32; ++grp) {
+      const bf16x8 A = tr_frag(gs + (grp * 32 + 4 * gq + q) * PG + nt * 16 + 4 * p, PG);
+#pragma unroll
+      for (int j = 0; j < MAXJ; ++j) {
+        const int pr = wsub + WPN * j;
+        if (pr >= npairs) break;
+        const int k = pr >> 1, ct = pr & 1;
+        const bf16x8 Bf = tr_frag(xs + (grp * 32 + 4 * gq + q + k) * PX + ct * 16 + 4 * p, PX);
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, Bf, acc[j], 0, 0, 0);
+      }
+    }
+  }
+  const int64_t nw = int64_t(d.G) * no_per_g * d.K * nred;
+  float* pdst = part + int64_t(split) * nw;
+#pragma unroll
+  for (int j = 0; j < MAXJ; ++j) {
+    const int pr = wsub + WPN * j;
+    if (pr >= npairs) break;
+    const int k = k0 + (pr >> 1), ct = pr & 1;
+    const int ch = cc + ct * 16 + (lane & 15);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int o = o0 + nt * 16 + 4 * (lane >> 4) + e;
+      if (o < no_per_g && ch < nred) pdst[((int64_t(g) * no_per_g + o) * d.K + k) * nred + ch] = acc[j][e];
+    }
+  }
+}
+
+// bias partials for the MFMA wgrad path: gb[col] over a split of rows
+template <typename T>
+__global__ __launch_bounds__(256) void k_dbias_part(D d, const T* __restrict__ gout, int rows_per_split,
+                                                    float* __restrict__ bpart) {
+  const int no_per_g = d.So * d.Ng;
+  const int64_t nb = int64_t(d.G) * no_per_g;
+  const int64_t total_rows = int64_t(d.B) * d.Tvalid;
+  const int64_t r0 = int64_t(blockIdx.y) * rows_per_split;
+  const int64_t r1 = r0 + rows_per_split < total_rows ? r0 + rows_per_split : total_rows;
+  for (int64_t go = int64_t(blockIdx.x) * 256 + threadIdx.x; go < nb; go += int64_t(gridDim.x) * 256) {
+    const int g = int(go / no_per_g), o = int(go - int64_t(g) * no_per_g);
+    const int64_t oc = out_col(d, g, o);
+    float acc = 0.f;
+    for (int64_t rr = r0; rr < r1; ++rr) {
+      const int b = int(rr / d.Tvalid), j = int(rr - int64_t(b) * d.Tvalid);
+      acc += to_f(gout[(int64_t(b) * d.Tvo + j) * d.ldo + oc]);
+    }
+    bpart[int64_t(blockIdx.y) * nb + go] = acc;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Weight packing (torch Conv1d / (k,1) Conv2d weight [N][Cg][Kt], optional
+// weight norm w = g * v / ||v||) into the phase-view forms:
+//   fwd  Wp[g][n][i][r][c] = w[g*Ng + n][c][s*(q0 + i) + r + pad]   (0 if out of [0, Kt))
+//   dgrad Wd[g][(r,c)][i'][n] = Wp[g][n][K-1-i'][r][c]
+// ---------------------------------------------------------------------------
+struct PackGeo {
+  int N, Cg, Kt, s, pad, G, K, q0;
+};
+
+__host__ __device__ inline PackGeo pack_geo(int N, int Cg, int Kt, int s, int pad, int G) {
+  PackGeo p{N, Cg, Kt, s, pad, G, 0, 0};
+  // q0 = floor(-pad / s), K = floor((Kt - 1 - pad) / s) - q0 + 1
+  const int a = -pad;
+  p.q0 = a >= 0 ? a / s : -((-a + s - 1) / s);
+  const int e = Kt - 1 - pad;
+  const int qe = e >= 0 ? e / s : -((-e + s - 1) / s);
+  p.K = qe - p.q0 + 1;
+  return p;
+}
+
+// one block per output channel n: ||v_n|| then the packed weights
+template <typename T>
+__global__ __launch_bounds__(256) void k_dpack(PackGeo pg, int mode, const float* __restrict__ w,
+                                               const float* __restrict__ wg, T* __restrict__ out) {
+  __shared__ float red[16];
+  const int n = blockIdx.x;
+  const int per = pg.Cg * pg.Kt;
+  float scale = 1.f;
+  if (wg) {
+    float ss = 0.f;
+    for (int e = threadIdx.x; e < per; e += 256) {
+      const float v = w[int64_t(n) * per + e];
+      ss += v * v;
+    }
+    ss = block_sum(ss, red);
+    if (threadIdx.x == 0) red[0] = ss;
+    __syncthreads();
+    scale = wg[n] / sqrtf(red[0]);
+  }
+  const int Ng = pg.N / pg.G, g = n / Ng, nl = n - g * Ng;
+  const int nred = pg.s * pg.Cg;
+  for (int e = threadIdx.x; e < pg.K * nred; e += 256) {
+    const int i = e / nred, rc = e - i * nred;
+    const int r = rc / pg.Cg, c = rc - r * pg.Cg;
+    const int k = pg.s * (pg.q0 + i) + r + pg.pad;
+    const float v = (k >= 0 && k < pg.Kt) ? w[(int64_t(n) * pg.Cg + c) * pg.Kt + k] * scale : 0.f;
+    if (mode == 0) {
+      out[((int64_t(g) * Ng + nl) * pg.K + i) * nred + rc] = from_f<T>(v);
+    } else {  // dgrad: [g][(r,c)][K-1-i][n]
+      out[((int64_t(g) * nred + rc) * pg.K + (pg.K - 1 - i)) * Ng + nl] = from_f<T>(v);
+    }
+  }
+}
+
+// Final wgrad reduction: sum the split partials, unpack to the torch layout,
+// and (weight norm) gv = (g/||v||) (gw - w_hat (w_hat . gw)), gg = w_hat . gw.
+// One block per output channel n.
+__global__ __launch_bounds__(256) void k_dwgrad_finish(PackGeo pg, const float* __restrict__ part, int nsplit,
+                                                       const float* __restrict__ bpart, int bsplit,
+                                                       const float* __restrict__ v, const float* __restrict__ wg,
+                                                       float* __restrict__ gw, float* __restrict__ gg,
+                                                       float* __restrict__ gb) {
+  __shared__ float red[16];
+  __shared__ float bc[2];
+  const int n = blockIdx.x;
+  const int per = pg.Cg * pg.Kt;
+  const int Ng = pg.N / pg.G, g = n / Ng, nl = n - g * Ng;
+  const int nred = pg.s * pg.Cg;
+  const int64_t nw = int64_t(pg.N) * pg.K * nred;
+  // pass 1: the reduced gradient of the effective weight, kept in gw
+  float dot = 0.f, vv = 0.f;
+  for (int e = threadIdx.x; e < per; e += 256) {
+    const int c = e / pg.Kt, k = e - c * pg.Kt;
+    // k = s*(q0+i) + r + pad
+    const int kk = k - pg.pad - pg.s * pg.q0;
+    const int i = kk / pg.s, r = kk - i * pg.s;
+    const int64_t src = ((int64_t(g) * Ng + nl) * pg.K + i) * nred + r * pg.Cg + c;
+    float acc = 0.f;
+    for (int sp = 0; sp < nsplit; ++sp) acc += part[int64_t(sp) * nw + src];
+    gw[int64_t(n) * per + e] = acc;
+    if (v) {
+      const float vv_ = v[int64_t(n) * per + e];
+      dot += vv_ * acc;
+      vv += vv_ * vv_;
+    }
+  }
+  if (gb && threadIdx.x == 0) {
+    float acc = 0.f;
+    for (int sp = 0; sp < bsplit; ++sp) acc += bpart[int64_t(sp) * pg.N + n];
+    gb[n] = acc;
+  }
+  if (!v) return;
+  dot = block_sum(dot, red);
+  if (threadIdx.x == 0) bc[0] = dot;
+  vv = block_sum(vv, red);
+  if (threadIdx.x == 0) bc[1] = vv;
+  __syncthreads();
+  const float nv = sqrtf(bc[1]);
+  const float gn = wg[n];
+  // w = gn * v / nv ; dL/dgn = (v . gw) / nv ; dL/dv = gn/nv * (gw - v (v . gw) / nv^2)
+  if (threadIdx.x == 0) gg[n] = bc[0] / nv;
+  const float a = gn / nv, bcoef = gn * bc[0] / (nv * nv * nv);
+  for (int e = threadIdx.x; e < per; e += 256) {
+    const int64_t o = int64_t(n) * per + e;
+    gw[o] = a * gw[o] - bcoef * v[o];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Data movement of the discriminator front-ends
+// ---------------------------------------------------------------------------
+// AvgPool1d(kernel 4, stride 2, padding 2, count_include_pad) between MSD scales
+// (discriminator.py:428-447): (B, T) fp32 -> (B, Tout_alloc) with zeros past To.
+__global__ void k_avgpool_fwd(const float* __restrict__ x, int B, int T, int ldx, int kw, int st, int pad,
+                              int To, int ldo, float* __restrict__ y) {
+  const int64_t total = int64_t(B) * ldo;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += int64_t(gridDim.x) * blockDim.x) {
+    const int b = int(i / ldo), t = int(i - int64_t(b) * ldo);
+    float v = 0.f;
+    if (t < To) {
+      for (int k = 0; k < kw; ++k) {
+        const int u = t * st + k - pad;
+        if (u >= 0 && u < T) v += x[int64_t(b) * ldx + u];
+      }
+      v /= float(kw);
+    }
+    y[i] = v;
+  }
+}
+
+__global__ void k_avgpool_bwd(const float* __restrict__ gy, int B, int T, int ldx, int kw, int st, int pad, int To,
+                              int ldo, float* __restrict__ gx) {
+  const int64_t total = int64_t(B) * ldx;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += int64_t(gridDim.x) * blockDim.x) {
+    const int b = int(i / ldx), u = int(i - int64_t(b) * ldx);
+    float v = 0.f;
+    if (u < T) {
+      // outputs t with t*st + k - pad == u, 0 <= k < kw
+      const int lo = (u + pad - kw + 1 + st - 1) / st > 0 ? (u + pad - kw + 1 + st - 1) / st : 0;
+      for (int t = lo; t * st - pad <= u && t < To; ++t) v += gy[int64_t(b) * ldo + t];
+      v /= float(kw);
+    }
+    gx[i] = v;
+  }
+}
+
+// MPD front-end (discriminator.py:120-126): reflect-pad T to a multiple of the
+// period p, view (B, 1, T/p, p) -> our (B*p, L_alloc) sequences (column-major
+// over the p columns), rows past L zero.  Backward folds the reflect pad.
+__global__ void k_mpd_fold(const float* __restrict__ x, int B, int T, int ldx, int p, int L, int Lalloc,
+                           float* __restrict__ y) {
+  const int64_t total = int64_t(B) * p * Lalloc;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t seq = i / Lalloc;
+    const int l = int(i - seq * Lalloc);
+    const int b = int(seq / p), col = int(seq - int64_t(b) * p);
+    float v = 0.f;
+    if (l < L) {
+      int u = l * p + col;
+      if (u >= T) u = 2 * (T - 1) - u;  // reflect (F.pad mode "reflect")
+      v = x[int64_t(b) * ldx + u];
+    }
+    y[i] = v;
+  }
+}
+
+__global__ void k_mpd_unfold(const float* __restrict__ gy, int B, int T, int ldx, int p, int L, int Lalloc,
+                             float* __restrict__ gx) {
+  const int64_t total = int64_t(B) * ldx;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += int64_t(gridDim.x) * blockDim.x) {
+    const int b = int(i / ldx), u = int(i - int64_t(b) * ldx);
+    float v = 0.f;
+    if (u < T) {
+      v = gy[(int64_t(b) * p + u % p) * Lalloc + u / p];
+      const int up = 2 * (T - 1) - u;  // padded position mirrored onto u
+      if (up >= T && up < L * p) v += gy[(int64_t(b) * p + up % p) * Lalloc + up / p];
+    }
+    gx[i] = v;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// GAN losses over strided (up to 4-D) views: sum |a - b| (feature matching) or
+// sum (a - target)^2 (LSGAN) / sum min(+-a - 1, 0) (hinge), fp64 block partials,
+// and their elementwise gradients written into a buffer of the same view.
+// ---------------------------------------------------------------------------
+struct View4 {
+  int64_t size[4];
+  int64_t stride[4];
+};
+
+__device__ __forceinline__ int64_t view_off(const View4& v, int64_t i) {
+  int64_t off = 0;
+#pragma unroll
+  for (int d = 3; d >= 0; --d) {
+    const int64_t q = i / v.size[d];
+    off += (i - q * v.size[d]) * v.stride[d];
+    i = q;
+  }
+  return off;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_gan_reduce(int kind, const T* __restrict__ a, View4 va,
+                                                    const T* __restrict__ b, View4 vb, float target, int64_t n,
+                                                    double* __restrict__ partials) {
+  __shared__ double red[16];
+  double s = 0.0;
+  for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256) {
+    const float x = to_f(a[view_off(va, i)]);
+    float v;
+    if (kind == 0) v = fabsf(x - to_f(b[view_off(vb, i)]));  // L1
+    else if (kind == 1) v = (x - target) * (x - target);     // MSE to target
+    else if (kind == 2) v = fminf(x - 1.f, 0.f);             // hinge real: min(x - 1, 0)
+    else if (kind == 3) v = fminf(-x - 1.f, 0.f);            // hinge fake: min(-x - 1, 0)
+    else v = x;                                              // plain sum (generator hinge: -mean)
+    s += double(v);
+  }
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) partials[blockIdx.x] = s;
+}
+
+__global__ void k_gan_finish(const double* __restrict__ partials, int nblocks, double scale, float* __restrict__ out,
+                             int accumulate) {
+  __shared__ double red[16];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < nblocks; i += blockDim.x) s += partials[i];
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) out[0] = float(s * scale) + (accumulate ? out[0] : 0.f);
+}
+
+// grad[i] (+)= coef * dv/da (coef is a device scalar: the upstream grad / n)
+template <typename T>
+__global__ __launch_bounds__(256) void k_gan_grad(int kind, const T* __restrict__ a, View4 va,
+                                                  const T* __restrict__ b, View4 vb, float target, int64_t n,
+                                                  const float* __restrict__ gscale, float mult,
+                                                  T* __restrict__ grad, View4 vg, int accumulate) {
+  const float c = gscale[0] * mult;
+  for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256) {
+    const float x = to_f(a[view_off(va, i)]);
+    float gv;
+    if (kind == 0) {
+      const float dlt = x - to_f(b[view_off(vb, i)]);
+      gv = dlt > 0.f ? c : (dlt < 0.f ? -c : 0.f);
+    } else if (kind == 1) {
+      gv = 2.f * (x - target) * c;
+    } else if (kind == 2) {
+      gv = x - 1.f < 0.f ? c : 0.f;
+    } else if (kind == 3) {
+      gv = -x - 1.f < 0.f ? -c : 0.f;
+    } else {
+      gv = c;
+    }
+    const int64_t o = view_off(vg, i);
+    grad[o] = from_f<T>(accumulate ? to_f(grad[o]) + gv : gv);
+  }
+}
+
+}  // namespace dconv
+}  // namespace sel
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+using namespace sel;
+using namespace sel::dconv;
+
+namespace {
+
+int check(const sel_dconv_desc* d) {
+  SEL_REQUIRE(d != nullptr, SEL_ERR_ARG, "null dconv descriptor");
+  SEL_REQUIRE(d->B > 0 && d->Tv >= 0 && d->Tvs >= d->Tv && d->Tvs > 0 && d->Tvo > 0 && d->Tvalid >= 0 && d->Tvalid <= d->Tvo && d->K > 0 &&
+                  d->S > 0 && d->Cg > 0 && d->G > 0 && d->So > 0 && d->Ng > 0,
+              SEL_ERR_ARG, "bad dconv shape B=%d Tv=%d Tvo=%d Tvalid=%d K=%d S=%d Cg=%d G=%d So=%d Ng=%d", d->B,
+              d->Tv, d->Tvo, d->Tvalid, d->K, d->S, d->Cg, d->G, d->So, d->Ng);
+  SEL_REQUIRE(int64_t(d->S - 1) * d->Cs + int64_t(d->G) * d->Cg <= d->ldx, SEL_ERR_ARG,
+              "input columns exceed the row pitch ldx=%d", d->ldx);
+  SEL_REQUIRE(int64_t(d->So - 1) * d->Ns + int64_t(d->G) * d->Ng <= d->ldo, SEL_ERR_ARG,
+              "output columns exceed the row pitch ldo=%d", d->ldo);
+  return SEL_OK;
+}
+
+bool mfma_ok(const sel_dconv_desc* d, int dtype) {
+  const int vec = dtype == SEL_BF16 ? 8 : 4;
+  // 8-channel (bf16) / 4-channel (fp32) vectors may not straddle a phase or a
+  // group, and the group's output width must fill at least half a 32-wide tile
+  return d->Cg % vec == 0 && d->Cs % vec == 0 && d->ldx % vec == 0 && (d->S * d->Cg) % 8 == 0 &&
+         d->So * d->Ng >= 16 && d->K <= 64;
+}
+
+template <typename T, int BM, int BN>
+int launch_mfma(const sel_dconv_desc* d, const void* x, const void* wp, const float* bias, const void* aux,
+                const void* res, void* out, hipStream_t s) {
+  constexpr int P = Elt<T>::P;
+  const size_t lds = (size_t(BM + d->K - 1) * P + size_t(BN) * KC * P) * sizeof(T);
+  SEL_REQUIRE(lds <= 160 * 1024, SEL_ERR_UNSUPPORTED, "dconv tile needs %zu B of LDS", lds);
+  const int tps = (d->Tvo + BM - 1) / BM;
+  const int ntg = (d->So * d->Ng + BN - 1) / BN;
+  dim3 grid(unsigned(int64_t(d->B) * tps), unsigned(ntg * d->G));
+  auto kern = k_dconv_mfma<T, BM, BN>;
+  if (lds > 64 * 1024)
+    SEL_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
+  hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, *d, static_cast<const T*>(x), static_cast<const T*>(wp), bias,
+                     static_cast<const T*>(aux), static_cast<const T*>(res), static_cast<T*>(out));
+  SEL_LAUNCH_CHECK();
+  return SEL_OK;
+}
+
+template <typename T>
+int launch_valu(const sel_dconv_desc* d, const void* x, const void* wp, const float* bias, const void* aux,
+                const void* res, void* out, hipStream_t s) {
+  const int64_t total = int64_t(d->B) * d->Tvo * d->G * d->So * d->Ng;
+  const unsigned blocks = unsigned(std::min<int64_t>((total + 255) / 256, 65536));
+  hipLaunchKernelGGL(k_dconv_valu<T>, dim3(blocks), dim3(256), 0, s, *d, static_cast<const T*>(x),
+                     static_cast<const T*>(wp), bias, static_cast<const T*>(aux), static_cast<const T*>(res),
+                     static_cast<T*>(out));
+  SEL_LAUNCH_CHECK();
+  return SEL_OK;
+}
+
+template <typename T>
+int dispatch_fwd(const sel_dconv_desc* d, const void* x, const void* wp, const float* bias, const void* aux,
+                 const void* res, void* out, hipStream_t s, int dtype) {
+  if (!mfma_ok(d, dtype) || tune(9) == 1) return launch_valu<T>(d, x, wp, bias, aux, res, out, s);
+  const int width = d->So * d->Ng;
+  const int64_t rows = int64_t(d->B) * d->Tvo;
+  // narrow groups: 32-wide tiles; short sequences / few rows: 64-row tiles
+  if (width <= 32) {
+    if (rows * d->G < 131072) return launch_mfma<T, 128, 32>(d, x, wp, bias, aux, res, out, s);
+    return launch_mfma<T, 256, 32>(d, x, wp, bias, aux, res, out, s);
+  }
+  if (rows * d->G * (width / 64) < 65536) return launch_mfma<T, 64, 64>(d, x, wp, bias, aux, res, out, s);
+  return launch_mfma<T, 128, 64>(d, x, wp, bias, aux, res, out, s);
+}
+
+struct WgPlanD {
+  bool mfma;
+  int nsplit, bsplit;
+  int rows_per_split, brows_per_split;
+  int tiles_per_seq, tiles_per_split, ntg, nt;
+};
+
+WgPlanD wg_plan(const sel_dconv_desc* d, int dtype) {
+  WgPlanD p{};
+  const int width = d->So * d->Ng;
+  const int nred = d->S * d->Cg;
+  p.mfma = dtype == SEL_BF16 && d->Cg % 8 == 0 && d->Cs % 8 == 0 && d->ldx % 8 == 0 && nred % 8 == 0 &&
+           width % 16 == 0 && tune(9) != 1;
+  const int64_t rows = int64_t(d->B) * d->Tvalid;
+  const int64_t nw = int64_t(d->G) * width * d->K * nred;
+  if (p.mfma) {
+    p.nt = width % 32 == 0 ? 2 : 1;
+    p.ntg = (d->K + WG_TAPS - 1) / WG_TAPS;
+    p.tiles_per_seq = (d->Tvalid + WG_BM - 1) / WG_BM;
+    const int64_t ntiles = int64_t(d->B) * p.tiles_per_seq;
+    const int64_t blocks = int64_t(d->G) * ((width + 16 * p.nt - 1) / (16 * p.nt)) * ((nred + 31) / 32) * p.ntg;
+    int64_t want = std::max<int64_t>(1, (1024 + blocks - 1) / blocks);
+    want = std::min<int64_t>(want, std::max<int64_t>(1, (int64_t(64) << 20) / (nw * 4)));
+    want = std::min<int64_t>(want, std::max<int64_t>(1, ntiles));
+    p.tiles_per_split = int((ntiles + want - 1) / want);
+    p.nsplit = int((ntiles + p.tiles_per_split - 1) / p.tiles_per_split);
+  } else {
+    const int64_t want_threads = int64_t(1) << 20;
+    int64_t want = std::max<int64_t>(1, want_threads / std::max<int64_t>(1, nw + int64_t(d->G) * width));
+    want = std::min<int64_t>(want, std::max<int64_t>(1, (int64_t(64) << 20) / ((nw + width * d->G) * 4)));
+    want = std::min<int64_t>(want, std::max<int64_t>(1, rows));
+    p.rows_per_split = int((rows + want - 1) / want);
+    p.nsplit = int((rows + p.rows_per_split - 1) / p.rows_per_split);
+  }
+  int64_t bwant = std::max<int64_t>(1, std::min<int64_t>(256, rows / 256));
+  p.brows_per_split = int((rows + bwant - 1) / bwant);
+  p.bsplit = int((rows + p.brows_per_split - 1) / std::max(1, p.brows_per_split));
+  if (p.bsplit < 1) p.bsplit = 1;
+  return p;
+}
+
+size_t wg_bytes(const sel_dconv_desc* d, const WgPlanD& p) {
+  const int64_t width = int64_t(d->So) * d->Ng;
+  const int64_t nw = int64_t(d->G) * width * d->K * d->S * d->Cg;
+  const int64_t nb = int64_t(d->G) * width;
+  return size_t(int64_t(p.nsplit) * nw + int64_t(std::max(p.bsplit, p.nsplit)) * nb) * sizeof(float) + 256;
+}
+
+hipError_t wgrad_fill(const sel_dconv_desc* d, int dtype, const WgPlanD& p, const void* gout, const void* x,
+                      float* part, float* bpart, hipStream_t s) {
+  const int width = d->So * d->Ng;
+  const int nred = d->S * d->Cg;
+  if (p.mfma) {
+    const int bn = 16 * p.nt;
+    dim3 grid(unsigned(d->G * ((width + bn - 1) / bn)), unsigned((nred + 31) / 32), unsigned(p.nsplit * p.ntg));
+    const size_t lds = (size_t(WG_BM) * (bn + 16) + size_t(WG_BM + WG_TAPS - 1) * 48) * sizeof(__bf16);
+    if (p.nt == 2)
+      hipLaunchKernelGGL(k_dwgrad_mfma<2>, grid, dim3(256), lds, s, *d, static_cast<const __bf16*>(gout),
+                         static_cast<const __bf16*>(x), p.tiles_per_seq, p.tiles_per_split, p.ntg, part);
+    else
+      hipLaunchKernelGGL(k_dwgrad_mfma<1>, grid, dim3(256), lds, s, *d, static_cast<const __bf16*>(gout),
+                         static_cast<const __bf16*>(x), p.tiles_per_seq, p.tiles_per_split, p.ntg, part);
+    if (bpart) {
+      const int64_t nb = int64_t(d->G) * width;
+      dim3 bg(unsigned((nb + 255) / 256), unsigned(p.bsplit));
+      hipLaunchKernelGGL(k_dbias_part<__bf16>, bg, dim3(256), 0, s, *d, static_cast<const __bf16*>(gout),
+                         p.brows_per_split, bpart);
+    }
+    return hipGetLastError();
+  }
+  const int64_t nw = int64_t(d->G) * width * d->K * nred;
+  const int64_t nb = bpart ? int64_t(d->G) * width : 0;
+  dim3 grid(unsigned(std::min<int64_t>((nw + nb + 255) / 256, 65535)), unsigned(p.nsplit));
+  if (dtype == SEL_BF16)
+    hipLaunchKernelGGL(k_dwgrad_valu<__bf16>, grid, dim3(256), 0, s, *d, static_cast<const __bf16*>(gout),
+                       static_cast<const __bf16*>(x), p.rows_per_split, part, bpart);
+  else
+    hipLaunchKernelGGL(k_dwgrad_valu<float>, grid, dim3(256), 0, s, *d, static_cast<const float*>(gout),
+                       static_cast<const float*>(x), p.rows_per_split, part, bpart);
+  return hipGetLastError();
+}
+
+int launch_blocks(int64_t n) { return int(std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192))); }
+
+bool view_ok(const int64_t* size, const int64_t* stride) { return size && stride; }
+
+View4 to_view(const int64_t* size, const int64_t* stride, int ndim) {
+  View4 v;
+  for (int i = 0; i < 4; ++i) {
+    const int src = i - (4 - ndim);
+    v.size[i] = src >= 0 ? size[src] : 1;
+    v.stride[i] = src >= 0 ? stride[src] : 0;
+  }
+  return v;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sel_dconv_fwd(const sel_dconv_desc* d, int dtype, const void* x, const void* wpack, const float* bias,
+                  const void* aux, const void* res, void* out, sel_stream_t stream) {
+  if (int rc = check(d)) return rc;
+  SEL_REQUIRE(x && wpack && out, SEL_ERR_ARG, "null pointer");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (dtype == SEL_BF16) return dispatch_fwd<__bf16>(d, x, wpack, bias, aux, res, out, s, dtype);
+  if (dtype == SEL_F32) return dispatch_fwd<float>(d, x, wpack, bias, aux, res, out, s, dtype);
+  set_error("sel_dconv_fwd: unsupported dtype %d", dtype);
+  return SEL_ERR_UNSUPPORTED;
+}
+
+int sel_dconv_uses_mfma(const sel_dconv_desc* d, int dtype) { return d && mfma_ok(d, dtype) && tune(9) != 1; }
+
+size_t sel_dconv_wgrad_workspace(const sel_dconv_desc* d, int dtype) {
+  if (!d || check(d) != SEL_OK) return 16;
+  return wg_bytes(d, wg_plan(d, dtype));
+}
+
+int sel_dconv_wgrad(const sel_dconv_desc* d, int dtype, const void* gout, const void* x, int N, int Cg, int Kt,
+                    int stride, int pad, const float* v, const float* wg, float* gw, float* gg, float* gb, void* ws,
+                    size_t ws_bytes, sel_stream_t stream) {
+  if (int rc = check(d)) return rc;
+  SEL_REQUIRE(dtype == SEL_BF16 || dtype == SEL_F32, SEL_ERR_UNSUPPORTED, "dtype %d", dtype);
+  SEL_REQUIRE(d->So == 1 && d->S == stride && d->G * d->Ng == N && d->Cg == Cg, SEL_ERR_ARG,
+              "sel_dconv_wgrad: descriptor must be the forward layer's");
+  const PackGeo pg = pack_geo(N, Cg, Kt, stride, pad, d->G);
+  SEL_REQUIRE(pg.K == d->K && pg.q0 == d->q0, SEL_ERR_ARG, "tap geometry mismatch (K %d vs %d, q0 %d vs %d)",
+              pg.K, d->K, pg.q0, d->q0);
+  SEL_REQUIRE(!v || (wg && gg), SEL_ERR_ARG, "weight norm needs v, g and gg");
+  const WgPlanD p = wg_plan(d, dtype);
+  SEL_REQUIRE(ws_bytes >= wg_bytes(d, p), SEL_ERR_WORKSPACE, "wgrad workspace too small");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  float* part = static_cast<float*>(ws);
+  const int64_t nw = int64_t(N) * d->K * d->S * d->Cg;
+  float* bpart = gb ? part + int64_t(p.nsplit) * nw : nullptr;
+  SEL_HIP(wgrad_fill(d, dtype, p, gout, x, part, bpart, s));
+  const int bsplit = p.mfma ? p.bsplit : p.nsplit;
+  hipLaunchKernelGGL(k_dwgrad_finish, dim3(N), dim3(256), 0, s, pg, part, p.nsplit, bpart, bsplit, v, wg, gw, gg,
+                     gb);
+  SEL_LAUNCH_CHECK();
+  return SEL_OK;
+}
+
+int sel_dconv_geometry(int Kt, int stride, int pad, int* K, int* q0) {
+  SEL_REQUIRE(Kt > 0 && stride > 0 && pad >= 0 && K && q0, SEL_ERR_ARG, "bad conv geometry");
+  const PackGeo pg = pack_geo(1, 1, Kt, stride, pad, 1);
+  *K = pg.K;
+  *q0 = pg.q0;
+  return SEL_OK;
+}
+
+int sel_dconv_pack(int mode, const float* w, const float* wg, int N, int Cg, int Kt, int stride, int pad, int G,
+                   int dtype, void* out, sel_stream_t stream) {
+  SEL_REQUIRE(w && out && N > 0 && Cg > 0 && Kt > 0 && stride > 0 && pad >= 0 && G > 0 && N % G == 0 &&
+                  (mode == 0 || mode == 1),
+              SEL_ERR_ARG, "bad dconv pack arguments");
+  const PackGeo pg = pack_geo(N, Cg, Kt, stride, pad, G);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (dtype == SEL_BF16)
+    hipLaunchKernelGGL(k_dpack<__bf16>, dim3(N), dim3(256), 0, s, pg, mode, w, wg, static_cast<__bf16*>(out));
+  else if (dtype == SEL_F32)
+    hipLaunchKernelGGL(k_dpack<float>, dim3(N), dim3(256), 0, s, pg, mode, w, wg, static_cast<float*>(out));
+  else {
+    set_error("sel_dconv_pack: dtype %d", dtype);
+    return SEL_ERR_UNSUPPORTED;
+  }
+  SEL_LAUNCH_CHECK();
+  return SEL_OK;
+}
+
+int sel_avgpool1d_fwd(const float* x, int B, int T, int ldx, int kernel, int stride, int pad, int To, int ldo,
+                      float* y, sel_stream_t stream) {
+  SEL_REQUIRE(x && y && B > 0 && T > 0 && ldx >= T && kernel > 0 && stride > 0 && ldo >= To && To > 0, SEL_ERR_ARG,
+              "bad avgpool arguments");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(k_avgpool_fwd, dim3(launch_blocks(int64_t(B) * ldo)), dim3(256), 0, s, x, B, T, ldx, kernel,
+                     stride, pad, To, ldo, y);
+  SEL_LAUNCH_CHECK();
+  return SEL_OK;
+}
+
+int sel_avgpool1d_bwd(const float* gy, int B, int T, int ldx, int kernel, int stride, int pad, int To, int ldo,
+                      float* gx, sel_stream_t stream) {
+  SEL_REQUIRE(gy && gx && B > 0 && T > 0 && ldx >= T && kernel > 0 && stride > 0 && ldo >= To, SEL_ERR_ARG,
+              "bad avgpool arguments");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(k_avgpool_bwd, dim3(launch_blocks(int64_t(B) * ldx)), dim3(256), 0, s, gy, B, T, ldx, kernel,
+                     stride, pad, To, ldo, gx);
+  SEL_LAUNCH_CHECK();
+  return SEL_OK;
+}
+
+int sel_mpd_fold(const float* x, int B, int T, int ldx, int period, int Lalloc, float* y, sel_stream_t stream) {
+  SEL_REQUIRE(x && y && B > 0 && period > 0 && T > period && ldx >= T, SEL_ERR_ARG, "bad mpd fold arguments");
+  const int L = (T + period - 1) / period;
+  SEL_REQUIRE(Lalloc >= L, SEL_ERR_ARG, "Lalloc %d < L %d", Lalloc, L);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(k_mpd_fold, dim3(launch_blocks(int64_t(B) * period * Lalloc)), dim3(256), 0, s, x, B, T, ldx,
+                     period, L, Lalloc, y);
+  SEL_LAUNCH_CHECK();
+  return SEL_OK;
+}
+
+int sel_mpd_unfold(const float* gy, int B, int T, int ldx, int period, int Lalloc, float* gx, sel_stream_t stream) {
+  SEL_REQUIRE(gy && gx && B > 0 && period > 0 && T > period && ldx >= T, SEL_ERR_ARG, "bad mpd unfold arguments");
+  const int L = (T + period - 1) / period;
+  SEL_REQUIRE(Lalloc >= L, SEL_ERR_ARG, "Lalloc %d < L %d", Lalloc, L);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(k_mpd_unfold, dim3(launch_blocks(int64_t(B) * ldx)), dim3(256), 0, s, gy, B, T, ldx, period, L,
+                     Lalloc, gx);
+  SEL_LAUNCH_CHECK();
+  return SEL_OK;
+}
+
+size_t sel_gan_workspace(void) { return 1024 * sizeof(double); }
+
+int sel_gan_reduce(int kind, int dtype, const void* a, const int64_t* a_size, const int64_t* a_stride,
+                   const void* b, const int64_t* b_size, const int64_t* b_stride, int ndim, float target,
+                   double scale, int accumulate, float* out, void* ws, size_t ws_bytes, sel_stream_t stream) {
+  SEL_REQUIRE(kind >= 0 && kind <= 4 && a && out && ndim >= 1 && ndim <= 4 && view_ok(a_size, a_stride),
+              SEL_ERR_ARG, "bad gan reduce arguments");
+  SEL_REQUIRE(kind != 0 || (b && view_ok(b_size, b_stride)), SEL_ERR_ARG, "L1 needs b");
+  SEL_REQUIRE(ws_bytes >= sel_gan_workspace(), SEL_ERR_WORKSPACE, "workspace too small");
+  int64_t n = 1;
+  for (int i = 0; i < ndim; ++i) {
+    n *= a_size[i];
+    if (kind == 0) SEL_REQUIRE(b_size[i] == a_size[i], SEL_ERR_ARG, "shape mismatch");
+  }
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const View4 va = to_view(a_size, a_stride, ndim);
+  const View4 vb = kind == 0 ? to_view(b_size, b_stride, ndim) : va;
+  const int nb = int(std::min<int64_t>(1024, std::max<int64_t>(1, (n + 255) / 256)));
+  double* part = static_cast<double*>(ws);
+  if (dtype == SEL_BF16)
+    hipLaunchKernelGGL(k_gan_reduce<__bf16>, dim3(nb), dim3(256), 0, s, kind, static_cast<const __bf16*>(a), va,
+                       static_cast<const __bf16*>(b ? b : a), vb, target, n, part);
+  else
+    hipLaunchKernelGGL(k_gan_reduce<float>, dim3(nb), dim3(256), 0, s, kind, static_cast<const float*>(a), va,
+                       static_cast<const float*>(b ? b : a), vb, target, n, part);
+  hipLaunchKernelGGL(k_gan_finish, dim3(1), dim3(256), 0, s, part, nb, scale, out, accumulate);
+  SEL_LAUNCH_CHECK();
+  return SEL_OK;
+}
+
+int sel_gan_grad(int kind, int dtype, const void* a, const int64_t* a_size, const int64_t* a_stride, const void* b,
+                 const int64_t* b_size, const int64_t* b_stride, int ndim, float target, const float* gscale,
+                 float mult, void* grad, const int64_t* g_stride, int accumulate, sel_stream_t stream) {
+  SEL_REQUIRE(kind >= 0 && kind <= 4 && a && grad && gscale && ndim >= 1 && ndim <= 4 && view_ok(a_size, a_stride) &&
+                  g_stride,
+              SEL_ERR_ARG, "bad gan grad arguments");
+  SEL_REQUIRE(kind != 0 || (b && view_ok(b_size, b_stride)), SEL_ERR_ARG, "L1 needs b");
+  int64_t n = 1;
+  for (int i = 0; i < ndim; ++i) n *= a_size[i];
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const View4 va = to_view(a_size, a_stride, ndim);
+  const View4 vb = kind == 0 ? to_view(b_size, b_stride, ndim) : va;
+  const View4 vg = to_view(a_size, g_stride, ndim);
+  const unsigned nb = unsigned(launch_blocks(n));
+  if (dtype == SEL_BF16)
+    hipLaunchKernelGGL(k_gan_grad<__bf16>, dim3(nb), dim3(256), 0, s, kind, static_cast<const __bf16*>(a), va,
+                       static_cast<const __bf16*>(b ? b : a), vb, target, n, gscale, mult,
+                       static_cast<__bf16*>(grad), vg, accumulate);
+  else
+    hipLaunchKernelGGL(k_gan_grad<float>, dim3(nb), dim3(256), 0, s, kind, static_cast<const float*>(a), va,
+                       static_cast<const float*>(b ? b : a), vb, target, n, gscale, mult, static_cast<float*>(grad),
+                       vg, accumulate);
+  SEL_LAUNCH_CHECK();
+  return SEL_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,43 @@
+"""HiFi-GAN discriminator — drop-in for the reference ``models/vocoder/HiFiGAN.py``
+``Discriminator`` (:308-395): MSD + MPD, outputs concatenated (MSD first).
+
+The HiFi-GAN *generator* of the same reference file (:28-305) is the vocoder
+of the codec's pre-training and is outside the denoise hot path (SURVEY §2 row
+13); only the discriminator GAN mode needs (BASELINE config C5) is built.
+"""
+import torch.nn as nn
+
+from models.vocoder.modules.discriminator import HiFiGANMultiPeriodDiscriminator, HiFiGANMultiScaleDiscriminator
+
+
+class Discriminator(nn.Module):
+    """HiFi-GAN multi-scale + multi-period discriminator module."""
+
+    def __init__(self, scales=3, scale_downsample_pooling="AvgPool1d",
+                 scale_downsample_pooling_params={"kernel_size": 4, "stride": 2, "padding": 2},
+                 scale_discriminator_params={"in_channels": 1, "out_channels": 1, "kernel_sizes": [15, 41, 5, 3],
+                                             "channels": 128, "max_downsample_channels": 1024, "max_groups": 16,
+                                             "bias": True, "downsample_scales": [2, 2, 4, 4, 1],
+                                             "nonlinear_activation": "LeakyReLU",
+                                             "nonlinear_activation_params": {"negative_slope": 0.1}},
+                 follow_official_norm=True, periods=[2, 3, 5, 7, 11],
+                 period_discriminator_params={"in_channels": 1, "out_channels": 1, "kernel_sizes": [5, 3],
+                                              "channels": 32, "downsample_scales": [3, 3, 3, 3, 1],
+                                              "max_downsample_channels": 1024, "bias": True,
+                                              "nonlinear_activation": "LeakyReLU",
+                                              "nonlinear_activation_params": {"negative_slope": 0.1},
+                                              "use_weight_norm": True, "use_spectral_norm": False}):
+        super().__init__()
+        self.msd = HiFiGANMultiScaleDiscriminator(scales=scales, downsample_pooling=scale_downsample_pooling,
+                                                  downsample_pooling_params=scale_downsample_pooling_params,
+                                                  discriminator_params=scale_discriminator_params,
+                                                  follow_official_norm=follow_official_norm)
+        self.mpd = HiFiGANMultiPeriodDiscriminator(periods=periods, discriminator_params=period_discriminator_params)
+
+    def forward(self, x):
+        """x (B, C, T) -> list of lists of each sub-discriminator's layer outputs
+        (MSD then MPD), HiFiGAN.py:380-395."""
+        batch, channel, time = x.size()
+        if channel != 1:
+            x = x.reshape(batch * channel, 1, time)
+        return self.msd(x) + self.mpd(x)

@@ -72,6 +72,19 @@ SIGNATURES = {
     "sel_shape_loss_workspace": (SZ, [I64, I64, I32]),
     "sel_shape_loss_fwd": (I32, [P, P, I64, I64, I32, P, P, P, P, SZ, P]),
     "sel_shape_loss_bwd": (I32, [P, I64, I64, I32, P, P, P, F32, P, P]),
+    "sel_dconv_uses_mfma": (I32, [P, I32]),
+    "sel_dconv_fwd": (I32, [P, I32, P, P, P, P, P, P, P]),
+    "sel_dconv_geometry": (I32, [I32, I32, I32, P, P]),
+    "sel_dconv_pack": (I32, [I32, P, P, I32, I32, I32, I32, I32, I32, I32, P, P]),
+    "sel_dconv_wgrad_workspace": (SZ, [P, I32]),
+    "sel_dconv_wgrad": (I32, [P, I32, P, P, I32, I32, I32, I32, I32, P, P, P, P, P, P, SZ, P]),
+    "sel_avgpool1d_fwd": (I32, [P, I32, I32, I32, I32, I32, I32, I32, I32, P, P]),
+    "sel_avgpool1d_bwd": (I32, [P, I32, I32, I32, I32, I32, I32, I32, I32, P, P]),
+    "sel_mpd_fold": (I32, [P, I32, I32, I32, I32, I32, P, P]),
+    "sel_mpd_unfold": (I32, [P, I32, I32, I32, I32, I32, P, P]),
+    "sel_gan_workspace": (SZ, []),
+    "sel_gan_reduce": (I32, [I32, I32, P, P, P, P, P, P, I32, F32, ctypes.c_double, I32, P, P, SZ, P]),
+    "sel_gan_grad": (I32, [I32, I32, P, P, P, P, P, P, I32, F32, P, F32, P, P, I32, P]),
 }
 
 _lock = threading.Lock()

@@ -1,0 +1,365 @@
+"""Autograd ops over the HiFi-GAN discriminator kernels of libsel.so (dconv.hip).
+
+A sub-discriminator (one HiFiGANScaleDiscriminator or HiFiGANPeriodDiscriminator,
+models/vocoder/modules/discriminator.py:26-372) is a chain of convs with
+LeakyReLU; it runs as ONE autograd Function whose forward keeps every layer's
+output in a channels-last buffer (B_seq, T_alloc, C) — T_alloc padded to the
+next layer's stride so its phase view is free — and returns the reference-layout
+views of them, and whose backward walks the chain with the adjoint primitive,
+adding the gradients that arrive on the feature maps (feature matching) before
+each LeakyReLU' multiply.
+
+Reference layouts returned (views, no copies):
+  scale discriminator:  (B, C, T)         <- buffer (B, T_alloc, C)
+  period discriminator: (B, C, T/p, p)    <- buffer (B*p, L_alloc, C)
+                        final (B, L*p)    (a copy, as torch.flatten in :134)
+"""
+import ctypes
+
+import torch
+
+from . import _lib as L
+from .convops import BF16, F32, _code, compute_dtype
+
+
+class DConvDesc(ctypes.Structure):
+    """include/sel.h sel_dconv_desc"""
+    _fields_ = [(n, ctypes.c_int32) for n in ("B", "Tv", "Tvs", "ldx", "Tvo", "Tvalid", "ldo", "K", "q0", "S", "Cs",
+                                               "Cg", "G", "So", "Ns", "Ng", "act")] + [("slope", ctypes.c_float)]
+
+
+def geometry(Kt, stride, pad):
+    K, q0 = ctypes.c_int(), ctypes.c_int()
+    L.check(L.load().sel_dconv_geometry(Kt, stride, pad, ctypes.byref(K), ctypes.byref(q0)), "sel_dconv_geometry")
+    return K.value, q0.value
+
+
+def _roundup(v, m):
+    return (v + m - 1) // m * m
+
+
+class LayerSpec:
+    """One conv of a sub-discriminator: torch Conv1d(cin, cout, Kt, stride,
+    padding=pad, groups) (or Conv2d (Kt, 1) on the period axis), LeakyReLU after
+    it when `leaky`."""
+
+    __slots__ = ("cin", "cout", "Kt", "stride", "pad", "groups", "leaky", "K", "q0")
+
+    def __init__(self, cin, cout, Kt, stride, pad, groups, leaky):
+        self.cin, self.cout, self.Kt, self.stride, self.pad = cin, cout, Kt, stride, pad
+        self.groups, self.leaky = groups, leaky
+        self.K, self.q0 = geometry(Kt, stride, pad)
+
+    def t_out(self, T):
+        return (T + 2 * self.pad - self.Kt) // self.stride + 1
+
+
+def _fwd_desc(sp, Bs, T_in, T_alloc_in, T_out, T_out_alloc, slope):
+    s = sp.stride
+    return DConvDesc(B=Bs, Tv=T_alloc_in // s, Tvs=T_alloc_in // s, ldx=s * sp.cin, Tvo=T_out_alloc, Tvalid=T_out,
+                     ldo=sp.cout, K=sp.K, q0=sp.q0, S=s, Cs=sp.cin, Cg=sp.cin // sp.groups, G=sp.groups, So=1,
+                     Ns=sp.cout, Ng=sp.cout // sp.groups, act=1 if sp.leaky else 0, slope=slope)
+
+
+def _dgrad_desc(sp, Bs, T_alloc_in, T_out, T_out_alloc, slope, prev_leaky):
+    """Adjoint of the forward layer: gout (Bs, T_out_alloc rows, T_out valid, N
+    channels) -> gin in the phase view of the layer input (Bs, T_alloc_in / s
+    rows, s * cin channels)."""
+    s = sp.stride
+    Tvo = T_alloc_in // s
+    return DConvDesc(B=Bs, Tv=T_out, Tvs=T_out_alloc, ldx=sp.cout, Tvo=Tvo, Tvalid=Tvo, ldo=s * sp.cin, K=sp.K,
+                     q0=-sp.q0 - (sp.K - 1), S=1, Cs=sp.cout, Cg=sp.cout // sp.groups, G=sp.groups, So=s,
+                     Ns=sp.cin, Ng=sp.cin // sp.groups, act=0, slope=slope)
+
+
+def pack(sp, w, wg, dtype, mode):
+    """torch weight (or weight_v with weight_g) -> packed forward (mode 0) /
+    adjoint (mode 1) form in `dtype`."""
+    N, Cg = sp.cout, sp.cin // sp.groups
+    nred = sp.stride * Cg
+    n = N * sp.K * nred
+    out = torch.empty(n, dtype=dtype, device=w.device)
+    wc = w.detach().contiguous().float()
+    gc = wg.detach().contiguous().float() if wg is not None else None
+    L.call("sel_dconv_pack", mode, L.ptr(wc), L.ptr(gc), N, Cg, sp.Kt, sp.stride, sp.pad, sp.groups, _code(dtype),
+           L.ptr(out), L.stream())
+    return out
+
+
+def prim(desc, x, wp, out, bias=None, aux=None, res=None, tag=""):
+    L.call("sel_dconv_fwd", ctypes.byref(desc), _code(x.dtype), L.ptr(x), L.ptr(wp), L.ptr(bias), L.ptr(aux),
+           L.ptr(res), L.ptr(out), L.stream(), meta=lambda: _meta(desc, x, out, tag))
+    return out
+
+
+def _meta(d, x, out, tag):
+    """(kernel tag, algorithmic bytes, flops) of one launch for the bench timer."""
+    es = x.element_size()
+    width = d.So * d.Ng
+    flops = 2.0 * d.B * d.Tvalid * d.G * width * d.K * d.S * d.Cg
+    nbytes = es * (d.B * d.Tvs * d.ldx + d.B * d.Tvo * d.ldo + d.G * width * d.K * d.S * d.Cg)
+    mf = L.lib().sel_dconv_uses_mfma(ctypes.byref(d), _code(x.dtype))
+    return (f"k_dconv_{'mfma' if mf else 'valu'}{tag}", nbytes, flops)
+
+
+def wgrad(sp, desc, gout, x, w_or_v, wg, want_w, want_b):
+    """(gw or gv, gg, gb) of one layer (fp32, torch layouts)."""
+    lib = L.lib()
+    ws = L.workspace(lib.sel_dconv_wgrad_workspace(ctypes.byref(desc), _code(x.dtype)), x.device)
+    gw = torch.empty(w_or_v.shape, dtype=torch.float32, device=x.device)
+    gg = torch.empty(wg.shape, dtype=torch.float32, device=x.device) if wg is not None else None
+    gb = torch.empty(sp.cout, dtype=torch.float32, device=x.device) if want_b else None
+    v = w_or_v.detach().contiguous().float() if wg is not None else None
+    g = wg.detach().contiguous().float() if wg is not None else None
+    L.call("sel_dconv_wgrad", ctypes.byref(desc), _code(x.dtype), L.ptr(gout), L.ptr(x), sp.cout,
+           sp.cin // sp.groups, sp.Kt, sp.stride, sp.pad, L.ptr(v), L.ptr(g), L.ptr(gw), L.ptr(gg), L.ptr(gb),
+           L.ptr(ws), ws.numel(), L.stream())
+    return (gw if want_w else None), gg, gb
+
+
+def _cast(x, dtype):
+    from .convops import _cast_raw
+    return x if x.dtype == dtype else _cast_raw(x.contiguous(), dtype)
+
+
+def _view(y, kind, B, T, p):
+    """Reference-layout view of a layer buffer (no copy)."""
+    if kind == "scale":  # (B, T_alloc, C) -> (B, C, T)
+        return y[:, :T, :].permute(0, 2, 1)
+    # period: (B*p, L_alloc, C) -> (B, C, L, p)
+    Bp, La, C = y.shape
+    return y.view(B, p, La, C)[:, :, :T, :].permute(0, 3, 2, 1)
+
+
+class ChainFn(torch.autograd.Function):
+    """One sub-discriminator: x0 (Bs, T0_alloc, 1) in the compute dtype with T0
+    valid rows -> the reference-layout views of every layer's output.
+
+    forward(ctx, x0, T0, specs, slope, wn, kind, B, p, *params): params per
+    layer are (w, bias) or, with weight norm (wn), (weight_v, weight_g, bias)."""
+
+    @staticmethod
+    def forward(ctx, x0, T0, specs, slope, wn, kind, B, p, *params):
+        L.need_device(x0)
+        ctx.set_materialize_grads(False)  # unused feature maps arrive as None
+        dtype = x0.dtype
+        Bs = x0.shape[0]
+        per = 3 if wn else 2
+        bufs, views, geo = [], [], []
+        T_in, T_alloc_in, x = T0, x0.shape[1], x0
+        for li, sp in enumerate(specs):
+            w, wg, b = _layer_params(params, li, wn)
+            T_out = sp.t_out(T_in)
+            nxt = specs[li + 1].stride if li + 1 < len(specs) else 1
+            T_out_alloc = _roundup(T_out, nxt)
+            d = _fwd_desc(sp, Bs, T_in, T_alloc_in, T_out, T_out_alloc, slope)
+            wp = pack(sp, w, wg, dtype, 0)
+            y = torch.empty(Bs, T_out_alloc, sp.cout, dtype=dtype, device=x0.device)
+            prim(d, x, wp, y, bias=b.detach().float().contiguous() if b is not None else None, tag=f"_fwd{li}")
+            bufs.append(y)
+            views.append(_view(y, kind, B, T_out, p))
+            geo.append((T_in, T_alloc_in, T_out, T_out_alloc))
+            x, T_in, T_alloc_in = y, T_out, T_out_alloc
+        ctx.save_for_backward(x0, *bufs, *params)
+        ctx.cfg = (specs, slope, wn, geo, len(bufs), kind, B, p, per)
+        return tuple(views)
+
+    @staticmethod
+    def backward(ctx, *gviews):
+        saved = ctx.saved_tensors
+        specs, slope, wn, geo, nl, kind, B, p, per = ctx.cfg
+        x0, bufs, params = saved[0], saved[1:1 + nl], saved[1 + nl:]
+        dtype = x0.dtype
+        Bs = x0.shape[0]
+        npre = 8  # leading non-param inputs of forward
+        pgrads = [None] * len(params)
+
+        def ext(li):
+            g = gviews[li]
+            return None if g is None else _as_buffer(g, bufs[li], kind, B, geo[li][2], p)
+
+        top = max((li for li in range(nl) if gviews[li] is not None), default=None)
+        if top is None:
+            return (None,) * (npre + len(params))
+        g = ext(top)
+        gpre = _lrelu_bwd(g, bufs[top], slope) if specs[top].leaky else g
+        gx0 = None
+        for li in range(top, -1, -1):
+            sp = specs[li]
+            T_in, T_alloc_in, T_out, T_out_alloc = geo[li]
+            w, wg, b = _layer_params(params, li, wn)
+            x_in = bufs[li - 1] if li > 0 else x0
+            base = npre + per * li
+            need_w = ctx.needs_input_grad[base]
+            need_g = wn and ctx.needs_input_grad[base + 1]
+            need_b = b is not None and ctx.needs_input_grad[base + per - 1]
+            if need_w or need_g or need_b:
+                d_f = _fwd_desc(sp, Bs, T_in, T_alloc_in, T_out, T_out_alloc, slope)
+                gw, gg, gb = wgrad(sp, d_f, gpre, x_in, w, wg, True, need_b)
+                pgrads[per * li] = gw if need_w else None
+                if wn:
+                    pgrads[per * li + 1] = gg if need_g else None
+                if need_b:
+                    pgrads[per * li + per - 1] = gb
+            if li == 0 and not ctx.needs_input_grad[0]:
+                break
+            # adjoint of this layer: the previous layer's feature-map gradient is
+            # added and its LeakyReLU' applied in the same epilogue
+            d_b = _dgrad_desc(sp, Bs, T_alloc_in, T_out, T_out_alloc, slope, li > 0)
+            wd = pack(sp, w, wg, dtype, 1)
+            gin = torch.empty(Bs, T_alloc_in, sp.cin, dtype=dtype, device=x0.device)
+            res = aux = None
+            if li > 0:
+                res = ext(li - 1)
+                if not specs[li - 1].leaky:
+                    raise NotImplementedError("inner discriminator layers are LeakyReLU layers")
+                aux = bufs[li - 1]
+            prim(d_b, gpre, wd, gin, aux=aux, res=res, tag=f"_dgrad{li}")
+            if li == 0:
+                gx0 = gin
+            gpre = gin
+        return (gx0, None, None, None, None, None, None, None, *pgrads)
+
+
+def _layer_params(params, li, wn):
+    if wn:
+        return params[3 * li], params[3 * li + 1], params[3 * li + 2]
+    return params[2 * li], None, params[2 * li + 1]
+
+
+def _lrelu_bwd(g, y, slope):
+    """g * LeakyReLU'(y) (the top layer's external gradient; elementwise)."""
+    return torch.where(y > 0, g, g * slope)
+
+
+def _as_buffer(g, y, kind, B, T, p):
+    """Gradient of a feature-map view -> y's (Bs, T_alloc, C) buffer layout
+    (rows past the valid length are never read).  A gradient written by the GAN
+    loss kernels into a same-strided buffer is used in place."""
+    v = _view(y, kind, B, T, p)
+    if (g.dtype == y.dtype and tuple(g.stride()) == tuple(v.stride()) and g.storage_offset() == 0
+            and g.untyped_storage().nbytes() >= y.numel() * y.element_size()):
+        return torch.as_strided(g, y.shape, y.stride(), 0)
+    buf = torch.empty_like(y)
+    _view(buf, kind, B, T, p).copy_(g)
+    return buf
+
+
+# ---------------------------------------------------------------------------
+# front-ends: MSD average pooling, MPD reflect-pad + period fold
+# ---------------------------------------------------------------------------
+class AvgPoolFn(torch.autograd.Function):
+    """AvgPool1d(kernel, stride, padding) over (B, T) fp32 rows (count_include_pad)."""
+
+    @staticmethod
+    def forward(ctx, x, kernel, stride, pad):
+        L.need_device(x)
+        B, T = x.shape
+        To = (T + 2 * pad - kernel) // stride + 1
+        y = torch.empty(B, To, dtype=torch.float32, device=x.device)
+        xc = x.contiguous()
+        L.call("sel_avgpool1d_fwd", L.ptr(xc), B, T, T, kernel, stride, pad, To, To, L.ptr(y), L.stream())
+        ctx.cfg = (B, T, kernel, stride, pad, To)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        B, T, kernel, stride, pad, To = ctx.cfg
+        gy = gy.contiguous()
+        gx = torch.empty(B, T, dtype=torch.float32, device=gy.device)
+        L.call("sel_avgpool1d_bwd", L.ptr(gy), B, T, T, kernel, stride, pad, To, To, L.ptr(gx), L.stream())
+        return gx, None, None, None
+
+
+class MpdFoldFn(torch.autograd.Function):
+    """(B, T) fp32 -> (B*p, L_alloc) sequences of the period grid (reflect pad)."""
+
+    @staticmethod
+    def forward(ctx, x, p, Lalloc):
+        L.need_device(x)
+        B, T = x.shape
+        y = torch.empty(B * p, Lalloc, dtype=torch.float32, device=x.device)
+        xc = x.contiguous()
+        L.call("sel_mpd_fold", L.ptr(xc), B, T, T, p, Lalloc, L.ptr(y), L.stream())
+        ctx.cfg = (B, T, p, Lalloc)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        B, T, p, Lalloc = ctx.cfg
+        gy = gy.contiguous()
+        gx = torch.empty(B, T, dtype=torch.float32, device=gy.device)
+        L.call("sel_mpd_unfold", L.ptr(gy), B, T, T, p, Lalloc, L.ptr(gx), L.stream())
+        return gx, None, None
+
+
+# ---------------------------------------------------------------------------
+# GAN losses (losses/adversarial_loss.py, losses/feat_match_loss.py)
+# ---------------------------------------------------------------------------
+L1, MSE, HINGE_REAL, HINGE_FAKE, SUM = 0, 1, 2, 3, 4
+
+
+def _view_args(t):
+    nd = t.dim()
+    size = (ctypes.c_int64 * nd)(*t.shape)
+    stride = (ctypes.c_int64 * nd)(*t.stride())
+    return size, stride, nd
+
+
+class GanReduceFn(torch.autograd.Function):
+    """scale * sum over elements of a (strided view) of |a - b| (kind L1),
+    (a - target)^2 (MSE) or the hinge terms; gradient w.r.t. a only (b is the
+    detached real-data feature map, feat_match_loss.py:47)."""
+
+    @staticmethod
+    def forward(ctx, a, b, kind, target, scale):
+        L.need_device(a)
+        if a.dim() > 4:
+            raise ValueError("GAN loss views have at most 4 dims")
+        sa, ta, nd = _view_args(a)
+        if b is not None:
+            if b.shape != a.shape or b.dtype != a.dtype:
+                raise ValueError(f"feature maps differ: {tuple(a.shape)}/{a.dtype} vs {tuple(b.shape)}/{b.dtype}")
+            sb, tb, _ = _view_args(b)
+        else:
+            sb = tb = None
+        out = torch.empty((), dtype=torch.float32, device=a.device)
+        ws = L.workspace(L.lib().sel_gan_workspace(), a.device)
+        L.call("sel_gan_reduce", kind, _code(a.dtype), L.ptr(a), sa, ta, L.ptr(b), sb, tb, nd, float(target),
+               float(scale), 0, L.ptr(out), L.ptr(ws), ws.numel(), L.stream())
+        ctx.save_for_backward(a, b)
+        ctx.cfg = (kind, target, scale)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        a, b = ctx.saved_tensors
+        kind, target, scale = ctx.cfg
+        sa, ta, nd = _view_args(a)
+        sb, tb = (None, None) if b is None else _view_args(b)[:2]
+        # same strides as the view, over a full copy of its base storage, so the
+        # discriminator backward can consume it in place (sel.dconvops._as_buffer)
+        base = a._base if a._base is not None else a
+        gbuf = torch.empty_like(base) if base is not a else torch.empty_like(a)
+        ga = torch.as_strided(gbuf, a.shape, a.stride(), a.storage_offset()) if base is not a else gbuf
+        gs = (ctypes.c_int64 * nd)(*ga.stride())
+        gc = (g.float() * scale).reshape(1).contiguous()
+        L.call("sel_gan_grad", kind, _code(a.dtype), L.ptr(a), sa, ta, L.ptr(b), sb, tb, nd, float(target),
+               L.ptr(gc), 1.0, L.ptr(ga), gs, 0, L.stream())
+        return ga, None, None, None, None
+
+
+def l1_mean(a, b):
+    return GanReduceFn.apply(a, b.detach(), L1, 0.0, 1.0 / a.numel())
+
+
+def mse_to(a, target):
+    return GanReduceFn.apply(a, None, MSE, float(target), 1.0 / a.numel())
+
+
+def hinge(a, real):
+    return GanReduceFn.apply(a, None, HINGE_REAL if real else HINGE_FAKE, 0.0, -1.0 / a.numel())
+
+
+def neg_mean(a):
+    return GanReduceFn.apply(a, None, SUM, 0.0, -1.0 / a.numel())

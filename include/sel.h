@@ -271,6 +271,78 @@ int sel_shape_loss_fwd(const float* y_hat, const float* y, int64_t rows, int64_t
 int sel_shape_loss_bwd(const float* y_hat, int64_t rows, int64_t T, int win, const int32_t* argidx,
                        const float* dsign, const float* g_out, float g_mul, float* g_yhat, sel_stream_t stream);
 
+/* ---- HiFi-GAN discriminator (GAN mode) ------------------
+ * models/vocoder/HiFiGAN.py:308-395 (Discriminator), models/vocoder/modules/
+ * discriminator.py:26-447 (HiFiGANPeriod/Scale discriminators and their multi-
+ * versions), losses/adversarial_loss.py:13-124, losses/feat_match_loss.py:13-55.
+ *
+ * One conv primitive over channels-last rows covers every layer and adjoint:
+ *   out[b, j, col(g,o)] = sum_{i<K, r<S, c<Cg} Wp[g][o][i][r][c] * x[b, j+q0+i, r*Cs + g*Cg + c]
+ * (input rows outside [0, Tv) read as 0), col(g, o) = (o / Ng)*Ns + g*Ng + o % Ng.
+ * Strided convs run on the phase view of their input (S = stride phases of C
+ * channels per row, Cs = C), their adjoints with So = stride output phases.
+ * Epilogue: + bias[col], then (+ res) * LeakyReLU'(aux) when aux != NULL, then
+ * LeakyReLU(slope) when act = 1; rows j in [Tvalid, Tvo) are written as 0. */
+typedef struct sel_dconv_desc {
+  int32_t B;       /* sequences */
+  int32_t Tv;      /* input rows per sequence read (rows >= Tv read as 0) */
+  int32_t Tvs;     /* input rows allocated per sequence (>= Tv) */
+  int32_t ldx;     /* input row pitch (elements) */
+  int32_t Tvo;     /* output rows per sequence (allocated) */
+  int32_t Tvalid;  /* computed output rows per sequence */
+  int32_t ldo;     /* output row pitch (elements) */
+  int32_t K;       /* taps */
+  int32_t q0;      /* row offset of tap 0 */
+  int32_t S, Cs, Cg; /* reduction: S phases (stride Cs columns) x Cg channels per group */
+  int32_t G;       /* groups */
+  int32_t So, Ns, Ng; /* outputs: So phases (stride Ns columns) x Ng channels per group */
+  int32_t act;     /* 0 none, 1 LeakyReLU */
+  float slope;     /* LeakyReLU negative slope (nonlinear_activation_params) */
+} sel_dconv_desc;
+/* 1 when a launch of this shape runs on the matrix cores (else the VALU kernel) */
+int sel_dconv_uses_mfma(const sel_dconv_desc* d, int dtype);
+int sel_dconv_fwd(const sel_dconv_desc* d, int dtype, const void* x, const void* wpack, const float* bias,
+                  const void* aux, const void* res, void* out, sel_stream_t stream);
+/* phase-view tap geometry of a torch conv (kernel Kt, stride, symmetric pad):
+ * K = floor((Kt-1-pad)/stride) - q0 + 1 taps from row offset q0 = floor(-pad/stride) */
+int sel_dconv_geometry(int Kt, int stride, int pad, int* K, int* q0);
+/* torch weight w[N][Cg][Kt] (Conv1d, groups G; or Conv2d (Kt,1)), optionally
+ * weight-normed (wg != NULL: w = wg[n] * v / ||v_n||, v = w), into the forward
+ * form Wp[g][n][i][r][c] (mode 0) or the adjoint form Wd[g][(r,c)][K-1-i][n] (mode 1). */
+int sel_dconv_pack(int mode, const float* w, const float* wg, int N, int Cg, int Kt, int stride, int pad, int G,
+                   int dtype, void* out, sel_stream_t stream);
+/* weight/bias gradient of a forward layer descriptor (So = 1): gw[N][Cg][Kt] fp32
+ * in the torch layout, or, with weight norm (v = the weight_v parameter, wg =
+ * weight_g): gw = dL/dv and gg[N] = dL/dg; gb[N] = sum of gout when non-NULL. */
+size_t sel_dconv_wgrad_workspace(const sel_dconv_desc* d, int dtype);
+int sel_dconv_wgrad(const sel_dconv_desc* d, int dtype, const void* gout, const void* x, int N, int Cg, int Kt,
+                    int stride, int pad, const float* v, const float* wg, float* gw, float* gg, float* gb, void* ws,
+                    size_t ws_bytes, sel_stream_t stream);
+/* AvgPool1d(kernel, stride, padding, count_include_pad) between MSD scales
+ * (discriminator.py:428-447): (B, T) rows of pitch ldx -> (B, To) rows of pitch ldo
+ * (positions >= To zero-filled); backward overwrites gx. */
+int sel_avgpool1d_fwd(const float* x, int B, int T, int ldx, int kernel, int stride, int pad, int To, int ldo,
+                      float* y, sel_stream_t stream);
+int sel_avgpool1d_bwd(const float* gy, int B, int T, int ldx, int kernel, int stride, int pad, int To, int ldo,
+                      float* gx, sel_stream_t stream);
+/* MPD front-end (discriminator.py:120-126): reflect-pad T to a multiple of the
+ * period, (B, 1, T/p, p) -> B*p sequences of L = ceil(T/p) rows (pitch Lalloc,
+ * rows >= L zero); unfold = the adjoint (folds the reflect pad), overwrites gx. */
+int sel_mpd_fold(const float* x, int B, int T, int ldx, int period, int Lalloc, float* y, sel_stream_t stream);
+int sel_mpd_unfold(const float* gy, int B, int T, int ldx, int period, int Lalloc, float* gx, sel_stream_t stream);
+/* GAN loss reductions over strided views (ndim <= 4, sizes/strides in elements,
+ * host arrays): kind 0 = sum|a-b| (feat_match_loss.py:46), 1 = sum (a-target)^2
+ * (adversarial_loss.py:57/115/118), 2 = sum min(a-1,0), 3 = sum min(-a-1,0)
+ * (hinge, :121/:124), 4 = sum a (generator hinge -mean, :60).  out[0] (+)= scale * sum.  grad (+)= gscale[0] * mult *
+ * d(term)/da elementwise (gscale: device scalar, the upstream gradient). */
+size_t sel_gan_workspace(void);
+int sel_gan_reduce(int kind, int dtype, const void* a, const int64_t* a_size, const int64_t* a_stride,
+                   const void* b, const int64_t* b_size, const int64_t* b_stride, int ndim, float target,
+                   double scale, int accumulate, float* out, void* ws, size_t ws_bytes, sel_stream_t stream);
+int sel_gan_grad(int kind, int dtype, const void* a, const int64_t* a_size, const int64_t* a_stride, const void* b,
+                 const int64_t* b_size, const int64_t* b_stride, int ndim, float target, const float* gscale,
+                 float mult, void* grad, const int64_t* g_stride, int accumulate, sel_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

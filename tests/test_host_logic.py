@@ -99,3 +99,38 @@ def test_set_epoch_reshuffles_distributed_shards():
     set_epoch((dl, plain), 1)
     e1 = list(iter(s))
     assert s.epoch == 1 and sorted(e0) != e0 and e0 != e1
+
+
+def test_discriminator_state_dict_matches_reference():
+    """models/vocoder/HiFiGAN.Discriminator builds its parameters exactly as the
+    reference (same modules, init order and weight_norm): the seeded state_dict
+    equals the reference's (tests/golden/discriminator.npz, seed 93) bit for bit,
+    keys included (weight_g / weight_v on the MPD convs, plain weights on the MSD)."""
+    import warnings
+    from conftest import golden
+    from test_gpu_gan import D_PARAMS
+    from models.vocoder.HiFiGAN import Discriminator
+    g = golden("discriminator")
+    torch.manual_seed(93)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        D = Discriminator(**D_PARAMS)
+    sd = D.state_dict()
+    ref = {k[3:]: v for k, v in g.items() if k.startswith("sd.")}
+    assert list(sd) == list(ref)
+    for k, v in sd.items():
+        assert torch.equal(v, torch.from_numpy(ref[k])), k
+
+
+def test_dconv_geometry_matches_torch_conv_lengths():
+    """Phase-view tap geometry (sel_dconv_geometry) covers exactly the taps of a
+    strided, symmetrically padded torch conv."""
+    from sel import dconvops as DC
+    for Kt, s, pad in ((41, 4, 20), (41, 2, 20), (41, 1, 20), (5, 3, 2), (15, 1, 7), (2, 1, 1), (3, 1, 1)):
+        K, q0 = DC.geometry(Kt, s, pad)
+        taps = [s * (q0 + i) + r + pad for i in range(K) for r in range(s)]
+        # every torch tap k is exactly one phase-view (i, r); the others are structural zeros
+        assert sorted(k for k in taps if 0 <= k < Kt) == list(range(Kt))
+        # and no phase-view tap is entirely padding (K is minimal)
+        assert any(0 <= s * q0 + r + pad < Kt for r in range(s))
+        assert any(0 <= s * (q0 + K - 1) + r + pad < Kt for r in range(s))
