@@ -204,6 +204,108 @@ def c3_cpu_baseline(B_sample=4, steps=20):
 
 
 # ---------------------------------------------------------------------------
+# c5: GAN-mode denoise step at 48 kHz (generator + HiFi-GAN MSD/MPD discriminator)
+# ---------------------------------------------------------------------------
+
+C5_CONFIG = "symAD_vctk_48000_hop300"
+SR48 = 48000
+
+
+def c5_setup(dev, B, world, local, dtype=torch.bfloat16):
+    """train_denoise.py model_step in GAN mode (:138-165, :213-263): generator
+    45*mel + adv + 2*feat-match, Adam; discriminator real/fake LSGAN, Adam."""
+    from sel import configs
+    from sel.convops import precision
+    from models.autoencoder_without_PQC.AudioDec import Generator
+    from models.vocoder.HiFiGAN import Discriminator
+    from train_denoise import DenoiseStep
+    from dataloader.data_utils import add_noise
+    cfg = configs.get(C5_CONFIG)
+    torch.manual_seed(93)
+    G = Generator(**cfg["generator_params"]).to(dev)
+    for mod in (G.projector, G.quantizer, G.decoder.conv1):  # unused by the without-PQC forward
+        for p in mod.parameters():
+            p.requires_grad_(False)
+    import warnings
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        D = Discriminator(**cfg["discriminator_params"]).to(dev)
+    st = DenoiseStep(cfg, dev, generator=G, discriminator=D)
+    if world > 1:
+        from sel.dist import wrap_ddp
+        st.model["generator"] = wrap_ddp(G, dev)
+        st.model["discriminator"] = wrap_ddp(D, dev)
+    st.discriminator_enabled = True
+    clean, noise = synthetic_batch(B, SR48, seed=93 + 2 * int(os.environ.get("RANK", "0")))
+    clean, noise = clean.to(dev), noise.to(dev)
+    if world > 1:
+        from sel.dist import add_noise_global
+        mixed = add_noise_global(clean, noise, 15)
+    else:
+        mixed = add_noise(clean, noise, 15)
+
+    def step():
+        with precision(dtype):
+            st.model_step(clean, mixed)
+    return step
+
+
+def c5_cpu_baseline(B_sample=1, steps=3):
+    """Oracle (op-for-op PyTorch-CPU restatement) of the same GAN step, fp32."""
+    from oracle import ref_ops as R
+    from oracle.melfilters import mel as melbank
+    from sel import configs
+    from models.autoencoder_without_PQC.AudioDec import Generator
+    from models.vocoder.HiFiGAN import Discriminator
+    import warnings
+    cfg = configs.get(C5_CONFIG)
+    mp = cfg["mel_loss_params"]
+    mm = torch.from_numpy(melbank(sr=mp["fs"], n_fft=2048, n_mels=80, fmin=mp["fmin"], fmax=mp["fmax"]).T.copy())
+    torch.manual_seed(93)
+    Gp = {k: v.clone() for k, v in Generator(**cfg["generator_params"]).state_dict().items()}
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        Dp = {k: v.clone() for k, v in Discriminator(**cfg["discriminator_params"]).state_dict().items()}
+    gtrain = [k for k in Gp if k.startswith(("encoder.", "decoder.conv_blocks", "decoder.conv2"))
+              and not k.endswith("pad_buffer")]
+    for k in gtrain:
+        Gp[k].requires_grad_(True)
+    for v in Dp.values():
+        v.requires_grad_(True)
+    og = torch.optim.Adam([Gp[k] for k in gtrain], **cfg["generator_optimizer_params"])
+    od = torch.optim.Adam(list(Dp.values()), **cfg["discriminator_optimizer_params"])
+    dkw = cfg["discriminator_params"]
+    geo = R.generator_geometry()
+    clean, noise = synthetic_batch(B_sample, SR48)
+    mixed = R.add_noise(clean, noise, 15)
+    win = R.hann(2048)
+
+    def step():
+        pred = R.generator_forward(Gp, mixed, geo, pqc=False)
+        mel = R.multi_mel_loss(pred, clean, [(2048, 300, 2048)], [win], [mm], 1e-10, None)
+        p_ = R.hifigan_discriminator(Dp, pred, **dkw)
+        with torch.no_grad():
+            p = R.hifigan_discriminator(Dp, clean, **dkw)
+        gen = cfg["lambda_mel_loss"] * mel + cfg["lambda_adv"] * R.generator_adv_loss(pred, False) + \
+            cfg["lambda_feat_match"] * R.feat_match_loss(p_, p)
+        og.zero_grad()
+        gen.backward()
+        og.step()
+        with torch.no_grad():
+            pred2 = R.generator_forward(Gp, mixed, geo, pqc=False)
+        rl, fl = R.discriminator_adv_loss(R.hifigan_discriminator(Dp, pred2, **dkw),
+                                          R.hifigan_discriminator(Dp, clean, **dkw), False)
+        od.zero_grad()
+        (rl + fl).backward()
+        od.step()
+    step()
+    dt = _median_time(step, steps)
+    return B_sample * SR48 / HOP / dt, (f"oracle (PyTorch-CPU op-for-op restatement) GAN-mode denoise step, "
+                                        f"without-PQC generator + HiFi-GAN MSD/MPD fp32, B={B_sample} x 1 s @ 48 kHz, "
+                                        f"median of {steps} timed steps after 1 warm-up, on {_cpu_model()}")
+
+
+# ---------------------------------------------------------------------------
 
 MFMA_BF16_PEAK_TFS = 2500.0  # MI355X dense bf16 (MI355X_MICROARCH.md)
 
@@ -371,7 +473,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default="c3", choices=["c2", "c3"])
+    ap.add_argument("--config", default="c3", choices=["c2", "c3", "c5"])
     ap.add_argument("--batch", type=int, default=0, help="per-GPU batch (default: config's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fp32-companion", action="store_true")
@@ -391,26 +493,35 @@ def main():
 
     from sel import _lib
     cfg = args.config
-    B = args.batch or (32 if cfg == "c2" else 64)
+    B = args.batch or {"c2": 32, "c3": 64, "c5": 16}[cfg]
+    sr = SR48 if cfg == "c5" else SR
     if cfg == "c2":
         step = c2_setup(dev, B)
         dom = "sel_stft_loss_fwd"
         workload = "configs[1]: MR-STFT(3 res) + mel(2048/300/80) loss fwd+bwd, fp32, 1 s @ 24 kHz"
         dtype = "fp32"
-    else:
+    elif cfg == "c3":
         step = c3_setup(dev, B, world, local)
         dom = "sel_conv_fwd"
         workload = (f"configs[2]/[3]: denoise-trainer step (trainer/denoise.py) on the PQC AudioDec generator, "
                     f"{C3_CONFIG} (derived), bf16 convs / fp32 losses, {B} x 1 s @ 24 kHz per GPU")
         dtype = "bf16"
+    else:
+        step = c5_setup(dev, B, world, local)
+        dom = "sel_conv_fwd"
+        workload = (f"configs[4]: GAN-mode denoise step (train_denoise.py model_step, discriminator enabled): "
+                    f"without-PQC AudioDec generator + HiFi-GAN MSD/MPD discriminator, {C5_CONFIG}, bf16 convs / "
+                    f"fp32 losses, {B} x 1 s @ 48 kHz per GPU")
+        dtype = "bf16"
 
     for _ in range(args.warmup):
         step()
-    timer = _lib.KernelTimer([dom] + (["sel_resunit_fwd"] if cfg == "c3" else []))
+    timer = _lib.KernelTimer([dom] + (["sel_resunit_fwd"] if cfg == "c3" else [])
+                             + (["sel_dconv_fwd"] if cfg == "c5" else []))
     elapsed, per_step = _timed_steps(step, args.steps, world, dev, timer)
 
     ms_per_step = 1e3 * elapsed / args.steps
-    frames_per_step = world * B * SR / HOP
+    frames_per_step = world * B * sr / HOP
     value = frames_per_step * args.steps / elapsed
     med_ms = float(np.median(per_step))
     roof = roofline(cfg, timer, dom, B, 1)  # the timer covered the last timed step
@@ -427,25 +538,26 @@ def main():
                 "median_ms_per_step": round(float(np.median(per32)), 3)}
         del step32
 
-    stft_roof = stft_kernel_roofline(dev) if world == 1 else None
+    stft_roof = stft_kernel_roofline(dev) if world == 1 and cfg != "c5" else None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         ncores = len(os.sched_getaffinity(0))
         ncores = min(ncores, int(os.environ.get("OMP_NUM_THREADS", ncores)))
         torch.set_num_threads(ncores)
-        v, sample = c2_cpu_baseline() if cfg == "c2" else c3_cpu_baseline()
+        v, sample = {"c2": c2_cpu_baseline, "c3": c3_cpu_baseline, "c5": c5_cpu_baseline}[cfg]()
         cpu = {"value": round(v, 1), "unit": "frames/s", "cores": ncores, "kind": "port", "sample": sample}
 
     if rank == 0:
         out = {
-            "metric": "denoise-train frames/sec (24 kHz, hop 300)",
+            "metric": ("denoise-train frames/sec (24 kHz, hop 300)" if cfg != "c5"
+                       else "GAN-mode denoise-train frames/sec (48 kHz, hop 300)"),
             "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
             "median_ms_per_step": round(med_ms, 3),
             "value_at_median": round(frames_per_step / (med_ms * 1e-3), 1),
             "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": dtype, "data": "synthetic",
-            "config": {"workload": workload, "global_batch": world * B, "seq_len": SR,
+            "config": {"workload": workload, "global_batch": world * B, "seq_len": sr,
                        "parallelism": f"dp{world}"},
             "roofline": roof, "cpu_baseline": cpu, "fp32_companion": fp32, "stft_kernel": stft_roof,
         }

@@ -14,6 +14,7 @@ Reference quirk kept: ``apply_weight_norm`` / ``apply_spectral_norm`` of the
 SCALE discriminator only match ``Conv2d`` (:354-372), so the MSD is never
 normalised — whatever ``follow_official_norm`` says.
 """
+import contextlib
 import copy
 import logging
 
@@ -28,6 +29,24 @@ def _slope(name, params):
     if name != "LeakyReLU":
         raise NotImplementedError(f"discriminator activation {name}: only LeakyReLU is lowered to the HIP path")
     return float(params.get("negative_slope", 0.01))
+
+
+@contextlib.contextmanager
+def frozen_parameters(module):
+    """Run a discriminator with its parameters as constants (no weight-gradient
+    kernels).  train_denoise.py's generator step back-propagates through D only
+    to reach the generator; the D gradients it also computes (:234-235) are
+    discarded by optimizer["discriminator"].zero_grad() before the D step
+    (:252), so skipping them changes no result."""
+    subs = [m for m in module.modules() if hasattr(m, "_params")]
+    prev = [getattr(m, "_frozen", False) for m in subs]
+    for m in subs:
+        m._frozen = True
+    try:
+        yield module
+    finally:
+        for m, p in zip(subs, prev):
+            m._frozen = p
 
 
 class HiFiGANPeriodDiscriminator(nn.Module):
@@ -78,7 +97,7 @@ class HiFiGANPeriodDiscriminator(nn.Module):
                 out += [m.weight_v, m.weight_g, m.bias]
             else:
                 out += [m.weight, m.bias]
-        return out
+        return [p.detach() for p in out] if getattr(self, "_frozen", False) else out
 
     def plan(self):
         if self._plan is None:
@@ -184,7 +203,7 @@ class HiFiGANScaleDiscriminator(nn.Module):
         out = []
         for m in self._convs():
             out += [m.weight, m.bias]
-        return out
+        return [p.detach() for p in out] if getattr(self, "_frozen", False) else out
 
     def plan(self):
         if self._plan is None:

@@ -15,8 +15,9 @@ Differences, all outside the numerics of a step:
     (sel.dist.add_noise_global) and the SNR term uses the global batch mean
     (see ``_global_snr_term``) — so a DDP step equals the single-device step on
     the global batch;
-  * the HiFiGAN discriminator is not built yet: a run whose
-    schedule would enable it raises instead of silently training without it.
+  * GAN mode (epoch >= epoch_to_enable_discriminator): the HiFi-GAN MSD + MPD
+    discriminator runs on the HIP discriminator kernels; the discriminator step
+    scores D(target) and D(pred) in one pass over the concatenated batch.
 
 Reference quirks reproduced on purpose: ``noise_dropout`` runs after mixing and
 never changes the model input (:313-319); validation also increments ``steps``
@@ -32,8 +33,11 @@ import torch
 from torch import nn
 
 from dataloader.data_utils import add_noise, set_epoch
-from losses import MultiMelSpectrogramLoss
+from losses import (DiscriminatorAdversarialLoss, FeatureMatchLoss, GeneratorAdversarialLoss,
+                    MultiMelSpectrogramLoss)
 from models.autoencoder_without_PQC.AudioDec import Generator as GeneratorAudioDec
+from models.vocoder.HiFiGAN import Discriminator as DiscriminatorHiFiGAN
+from models.vocoder.modules.discriminator import frozen_parameters
 from sel import configs as sel_configs
 from sel import dist as D
 from sel.metrics import SignalNoiseRatio
@@ -68,24 +72,41 @@ def _global_snr_term(snr_local, lam):
     return lam * (1 - s) + (-lam * s * (1 - s)) * (snr_local - snr_local.detach())
 
 
-class DenoiseStep:
-    """model_step + calculate_generator_loss of train_denoise.py:138-263."""
+def _unwrap(m):
+    return getattr(m, "module", m)
 
-    def __init__(self, config, device, generator=None, optimizer=None, discriminator=None):
+
+class DenoiseStep:
+    """model_step + calculate_generator_loss / calculate_discriminator_loss of
+    train_denoise.py:138-165, :213-263 (GAN mode once ``discriminator_enabled``)."""
+
+    def __init__(self, config, device, generator=None, optimizer=None, discriminator=None,
+                 disc_optimizer=None):
         self.config = config
         self.device = device
         self.model = {"generator": generator if generator is not None
                       else GeneratorAudioDec(**config["generator_params"]).to(device),
                       "discriminator": discriminator}
         gen = self.model["generator"]
+        on_gpu = next(gen.parameters()).is_cuda
         # on the GPU: torch's fused multi-tensor Adam (one launch per step, same update rule)
         opt_kw = dict(config["generator_optimizer_params"])
-        if next(gen.parameters()).is_cuda:
+        if on_gpu:
             opt_kw.setdefault("fused", True)
         self.optimizer = {"generator": optimizer if optimizer is not None
                           else torch.optim.Adam(gen.parameters(), **opt_kw)}
+        if discriminator is not None:
+            dkw = dict(config.get("discriminator_optimizer_params", {}))
+            if on_gpu:
+                dkw.setdefault("fused", True)
+            self.optimizer["discriminator"] = (disc_optimizer if disc_optimizer is not None
+                                               else torch.optim.Adam(discriminator.parameters(), **dkw))
         self.measures = {"MAE": nn.L1Loss(), "SNR": SignalNoiseRatio(),
                          "Mel-loss": MultiMelSpectrogramLoss(**config["mel_loss_params"]).to(device)}
+        # :123-131 (note: FeatureMatchLoss() with its DEFAULT averaging, as the reference builds it)
+        self.criterion = {"gen_adv": GeneratorAdversarialLoss(**config.get("generator_adv_loss_params", {})),
+                          "dis_adv": DiscriminatorAdversarialLoss(**config.get("discriminator_adv_loss_params", {})),
+                          "feat_match": FeatureMatchLoss()}
         self.discriminator_enabled = False
         self.last_grad_norm = None  # pre-clip total norm of the last train step (device tensor)
 
@@ -100,17 +121,40 @@ class DenoiseStep:
         else:
             # the reference evaluates the SNR term even at weight 0 (value 0 * ...)
             snr_loss = torch.zeros((), device=pred.device)
-        if self.discriminator_enabled:
-            raise NotImplementedError("HiFiGAN discriminator (SURVEY §8f, row f1) is not built yet")
         zero = torch.zeros((), device=pred.device)
-        return mel_loss + snr_loss, (("mel_loss", mel_loss), ("adv_loss", zero), ("feat_loss", zero),
-                                     ("snr_loss", snr_loss))
+        adv_loss = feat_loss = zero
+        if self.discriminator_enabled:
+            # D only carries the gradient to the generator here (its own grads
+            # are discarded by the D step's zero_grad): constant parameters, and
+            # the unwrapped module so no DDP reducer waits for them
+            with frozen_parameters(_unwrap(self.model["discriminator"])) as D:
+                p_ = D(pred)
+                with torch.no_grad():
+                    p = D(target)
+            adv_loss = c["lambda_adv"] * self.criterion["gen_adv"](pred)  # :147 passes the waveform (quirk)
+            feat_loss = c["lambda_feat_match"] * self.criterion["feat_match"](p_, p)
+        return mel_loss + adv_loss + feat_loss + snr_loss, (("mel_loss", mel_loss), ("adv_loss", adv_loss),
+                                                            ("feat_loss", feat_loss), ("snr_loss", snr_loss))
+
+    def calculate_discriminator_loss(self, pred, target):
+        """:157-165, with D(target) and D(pred) as ONE pass over the concatenated
+        batch (every clip is independent: identical outputs, one backward per
+        forward under DDP)."""
+        D = self.model["discriminator"]
+        B = target.shape[0]
+        outs = D(torch.cat([target, pred], 0))
+        p = [[t[:B] for t in o] for o in outs]
+        p_ = [[t[B:] for t in o] for o in outs]
+        real_loss, fake_loss = self.criterion["dis_adv"](p_, p)
+        return (real_loss + fake_loss) * self.config["lambda_adv"]
 
     def model_step(self, target, x, mode="train"):
         gen = self.model["generator"]
         x = x.to(self.device)
         target = target.to(self.device)
         gen.train(mode == "train")
+        if self.discriminator_enabled:
+            self.model["discriminator"].train(mode == "train")
         y_pred = gen(x)
         gen_loss, fragments = self.calculate_generator_loss(y_pred, target)
         if mode == "train":
@@ -121,7 +165,20 @@ class DenoiseStep:
                 self.last_grad_norm = torch.nn.utils.clip_grad_norm_(gen.parameters(),
                                                                      self.config["generator_grad_norm"])
             opt.step()
-        return gen_loss, torch.zeros((), device=self.device), fragments
+        dis_loss = torch.zeros((), device=self.device)
+        if self.discriminator_enabled:
+            with torch.no_grad():
+                y_pred = gen(x)
+            dis_loss = self.calculate_discriminator_loss(y_pred.detach(), target)
+            if mode == "train":
+                od = self.optimizer["discriminator"]
+                od.zero_grad()
+                dis_loss.backward()
+                if self.config["discriminator_grad_norm"] > 0:
+                    torch.nn.utils.clip_grad_norm_(self.model["discriminator"].parameters(),
+                                                   self.config["discriminator_grad_norm"])
+                od.step()
+        return gen_loss, dis_loss, fragments
 
 
 def noise_dropout(clean_sample_batch, noise_sample_batch, noise_dropout_rate):
@@ -139,6 +196,19 @@ def _synthetic_loaders(batch_size, batch_length, n_batches, seed):
         for _ in range(n_batches):
             yield torch.from_numpy((0.1 * rng.standard_normal((batch_size, 1, batch_length))).astype(np.float32))
     return (lambda: gen(seed)), (lambda: gen(seed + 1))
+
+
+# :47-67.  HPC corpus locations default to the reference's and can be moved
+# with SEL_HPC_CLEAN_PATH / SEL_HPC_NOISE_PATH (the roots are the directory names).
+ENV_PATHS = {
+    "LAPTOP": ("corpus/train/clean", "clean", "corpus/train/noise", "noise"),
+    "HPC": (os.environ.get("SEL_HPC_CLEAN_PATH", "/work3/s164396/data/DNS-Challenge-4/datasets_fullband/"
+                                                 "clean_fullband/vctk_wav48_silence_trimmed"),
+            "vctk_wav48_silence_trimmed",
+            os.environ.get("SEL_HPC_NOISE_PATH", "/work3/s164396/data/DNS-Challenge-4/datasets_fullband/"
+                                                 "noise_fullband"),
+            "noise_fullband"),
+}
 
 
 def main(argv=None):
@@ -161,14 +231,16 @@ def main(argv=None):
     SAMPLE_RATE = config["sample_rate"]
     NOISE_DROPOUT_RATE = config["noise_dropout_rate"]
     EPOCHS = args.epochs if args.epochs is not None else config["epochs"]
-    if EPOCHS > config["epoch_to_enable_discriminator"]:
-        raise NotImplementedError("this schedule enables the HiFiGAN discriminator (SURVEY §8f row f1), "
-                                  "not built yet; pass --epochs <= epoch_to_enable_discriminator")
+    if env not in ENV_PATHS and env != "SYNTH":
+        raise Exception("Illegal argument: " + env)
     torch.manual_seed(config["seed"])
     task_name = config.get("experiment_name", "denoise") if env == "HPC" else f"{env}-run"
     writer = ScalarWriter(os.path.join("job_out", task_name) if rank == 0 else None)
 
-    step = DenoiseStep(config, device)
+    disc = None
+    if config.get("discriminator_params") is not None:  # :97-98 (built always, enabled by the schedule)
+        disc = DiscriminatorHiFiGAN(**config["discriminator_params"]).to(device)
+    step = DenoiseStep(config, device, discriminator=disc)
     gen = step.model["generator"]
     if config.get("initial_model", ""):
         ckpt = os.path.join("job_out", config["initial_model"])
@@ -182,6 +254,8 @@ def main(argv=None):
             p.requires_grad_(False)
     if world > 1:
         step.model["generator"] = D.wrap_ddp(gen, device)
+        if disc is not None:
+            step.model["discriminator"] = D.wrap_ddp(disc, device)
 
     batch_length = 1 * SAMPLE_RATE
     batch_size = 4 if env == "LAPTOP" else int(config["batch_size"])
@@ -194,10 +268,7 @@ def main(argv=None):
     else:
         from dataloader.AudioDataset import AudioDataset
         from dataloader.data_utils import get_dataloaders
-        paths = {"LAPTOP": ("corpus/train/clean", "clean", "corpus/train/noise", "noise")}
-        if env not in paths:
-            raise Exception("Illegal argument: " + env)
-        cp, cr, npth, nr = paths[env]
+        cp, cr, npth, nr = ENV_PATHS[env]
         split = [0.7, 0.15, 0.15]
         tc, vc, _ = get_dataloaders(AudioDataset(cp, cr, SAMPLE_RATE), split, batch_size, batch_length,
                                     config["seed"], rank, world)
@@ -220,9 +291,11 @@ def main(argv=None):
     start = time.perf_counter()
     for epoch in range(EPOCHS):
         set_epoch(loaders, epoch)  # data parallel: new shard order every epoch
+        if disc is not None and epoch == config["epoch_to_enable_discriminator"]:  # :296-297
+            step.discriminator_enabled = True
         if epoch > config["epoch_to_enable_noise_dropout_decay"]:
             NOISE_DROPOUT_RATE -= config["noise_dropout_rate_decay"]
-        losses = []
+        losses, dlosses = [], []
         for i_batch, (clean_batch, noise_batch) in enumerate(train_pairs()):
             if env == "LAPTOP" and i_batch == 3:
                 break
@@ -233,26 +306,32 @@ def main(argv=None):
             steps += 1
             train_steps += 1
             losses.append(gen_loss.detach())
+            dlosses.append(dis_loss.detach())
             if steps % 100 == 0 or env in ("LAPTOP", "SYNTH"):
                 writer.add_scalar("Generator Batch Loss/Train", gen_loss.item(), train_steps)
+                writer.add_scalar("Discriminator Batch Loss/Train", dis_loss.item(), train_steps)
                 for name, v in fragments:
                     writer.add_scalar(f"Generator Batch Loss/{name}", float(v), train_steps)
         avg_train = torch.stack(losses).mean().item() if losses else math.nan
+        avg_dtrain = torch.stack(dlosses).mean().item() if dlosses else math.nan
         if env == "HPC" and rank == 0:
             os.makedirs("job_out", exist_ok=True)
             torch.save(gen.state_dict(), os.path.join("job_out", f"{task_name}checkpoint-{train_steps}.pkl"))
-        val, n = 0.0, 0
+        val, dval, n = 0.0, 0.0, 0
         for i_batch, (clean_batch, noise_batch) in enumerate(val_pairs()):
             if env == "LAPTOP" and i_batch == 3:
                 break
             target, mixed = mix(clean_batch, noise_batch)
             with torch.no_grad():
-                gl, _, _ = step.model_step(target, mixed, mode="eval")
+                gl, dl, _ = step.model_step(target, mixed, mode="eval")
             val += gl.item()
+            dval += dl.item()
             n += 1
             steps += 1
         writer.add_scalar("Generator Loss/Train", avg_train, epoch)
         writer.add_scalar("Generator Loss/Validation", val / max(n, 1), epoch)
+        writer.add_scalar("Discriminator Loss/Train", avg_dtrain, epoch)
+        writer.add_scalar("Discriminator Loss/Validation", dval / max(n, 1), epoch)
         if rank == 0:
             t = time.perf_counter() - start
             print(f"epoch {epoch}: train {avg_train:.4f} val {val / max(n, 1):.4f} step {train_steps} "

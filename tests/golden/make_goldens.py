@@ -251,6 +251,7 @@ def make_gan(ref, clean, noise, out):
     od = torch.optim.Adam(D.parameters(), lr=2e-4, betas=(0.5, 0.9), weight_decay=0.0)
     g = {"x_noisy": _np(x), "x_clean": _np(y)}
     lam_mel, lam_adv, lam_fm = 45.0, 1.0, 2.0
+    fm_step = fm.FeatureMatchLoss()
     for step in range(2):
         G.train()
         D.train()
@@ -260,7 +261,7 @@ def make_gan(ref, clean, noise, out):
         with torch.no_grad():
             p = D(y)
         adv_loss = lam_adv * gal(pred)  # reference quirk (:147): the waveform, not p_
-        feat_loss = lam_fm * fml(p_, p)
+        feat_loss = lam_fm * fm_step(p_, p)  # train_denoise.py:127 builds FeatureMatchLoss() (defaults)
         gen_loss = mel_loss + adv_loss + feat_loss
         og.zero_grad()
         gen_loss.backward()

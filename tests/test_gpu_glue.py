@@ -146,3 +146,93 @@ def test_steps_without_copy_use_updated_weights(gpu, bf16):
             y2 = G2(xn.to(gpu))
     assert not torch.equal(y0, y1), "the weights did not move"
     assert torch.equal(y1, y2), (y1 - y2).abs().max().item()
+
+
+def test_denoise_trainer_step_matches_reference_golden(gpu):
+    """trainer/denoise.Trainer._train_step (:52-84) against the reference CLASS
+    ITSELF run in the build container (tests/golden/trainer_step.npz,
+    make_goldens.py --only trainer): reduced-width PQC generator, codebook eval,
+    lambda_vq * sum(vqloss) + 45 * mel (libritts-24k mel), decoder/quantizer
+    frozen, Adam(1e-4, (0.5, 0.9)) — fused Adam here, two steps with nothing
+    touching the weights in between (so the packed-weight refresh is exercised).
+    Logged keys and values: mel/vq/generator loss 1e-5 (step 0) / 1e-4 (step 1),
+    perplexities 1e-5; updates as in test_train_step_matches_golden."""
+    from models.autoencoder.AudioDec import Generator
+    from losses import MultiMelSpectrogramLoss
+    from trainer.denoise import Trainer
+    g = golden("trainer_step")
+    gp = dict(encode_channels=4, decode_channels=4, code_dim=64, codebook_num=2, codebook_size=64)
+    G = Generator(**gp)
+    G.load_state_dict({k[4:]: torch.from_numpy(v) for k, v in g.items() if k.startswith("sd0.")})
+    G = G.to(gpu)
+    mel = MultiMelSpectrogramLoss(fs=24000, fft_sizes=[2048], hop_sizes=[300], win_lengths=[2048],
+                                  window="hann_window", num_mels=80, fmin=0, fmax=12000, log_base=None).to(gpu)
+    cfg = {"outdir": None, "train_max_steps": 10, "use_mel_loss": True, "use_stft_loss": False,
+           "use_shape_loss": False, "lambda_mel_loss": 45.0, "lambda_vq_loss": 1.0, "generator_grad_norm": -1}
+    opt = torch.optim.Adam(G.parameters(), lr=1e-4, betas=(0.5, 0.9), weight_decay=0.0, fused=True)
+    sched = torch.optim.lr_scheduler.StepLR(opt, step_size=200000, gamma=1.0)
+    tr = Trainer(steps=0, epochs=0, data_loader={}, model={"generator": G, "discriminator": None},
+                 criterion={"mel": mel}, optimizer={"generator": opt}, scheduler={"generator": sched},
+                 config=cfg, device=gpu)
+    xn, xc = torch.from_numpy(g["x_noisy"]), torch.from_numpy(g["x_clean"])
+    lr = 1e-4
+    trainable = [k for k, p in G.named_parameters() if p.requires_grad]
+    assert trainable and all(k.startswith(("encoder.", "projector.")) for k in trainable)
+    for s in range(2):
+        before = {k: p.detach().clone() for k, p in G.named_parameters()}
+        tr._train_step((xn, xc))
+        tol = 1e-5 if s == 0 else 1e-4
+        rec = {k: float(v) for k, v in tr.total_train_loss.items()}
+        ref = {k[len(f"rec.{s}."):]: float(v) for k, v in g.items() if k.startswith(f"rec.{s}.")}
+        assert set(rec) == set(ref), set(rec) ^ set(ref)
+        for k, v in ref.items():
+            assert abs(rec[k] - v) <= tol * abs(v) + 1e-7, (s, k, rec[k], v)
+        tr.total_train_loss.clear()
+        flips, tot, num, den = 0, 0, 0.0, 0.0
+        for k in trainable:
+            p = dict(G.named_parameters())[k]
+            refd = torch.from_numpy(g[f"sd{s + 1}.{k}"]).double() - (
+                torch.from_numpy(g[f"sd{s}.{k}"]).double() if s else before[k].double().cpu())
+            d = (p.detach() - before[k]).double().cpu()
+            flips += ((d - refd).abs() > 0.5 * lr).sum().item()
+            tot += d.numel()
+            num += ((d - refd) ** 2).sum().item()
+            den += (refd ** 2).sum().item()
+        assert flips <= 0.02 * tot, (s, flips, tot)
+        assert (num / den) ** 0.5 <= 0.10, (s, (num / den) ** 0.5)
+        if s == 0:  # continue from the reference's weights (no version bump: fused Adam + .data)
+            for k in trainable:
+                with torch.no_grad():
+                    dict(G.named_parameters())[k].copy_(torch.from_numpy(g[f"sd1.{k}"]).to(gpu))
+
+
+@pytest.mark.parametrize("gan", [False, True])
+def test_train_denoise_main_synthetic(gpu, tmp_path, monkeypatch, gan):
+    """train_denoise.main() end to end under -e SYNTH (synthetic 1 s clips): one
+    epoch of training + validation, losses finite and logged; with gan=True a
+    reduced config whose schedule enables the discriminator at epoch 0 (GAN step,
+    :296-297)."""
+    import json
+    import train_denoise
+    from sel import configs
+    monkeypatch.chdir(tmp_path)
+    name = "symAD_24Mel"
+    if gan:
+        c = configs.get("symAD_24Mel")
+        c.update(epoch_to_enable_discriminator=0, batch_size=2, lambda_feat_match=2.0,
+                 generator_params=dict(c["generator_params"], encode_channels=8, decode_channels=8))
+        dp = c["discriminator_params"]
+        dp["scale_discriminator_params"] = dict(dp["scale_discriminator_params"], channels=16,
+                                                max_downsample_channels=64)
+        dp["period_discriminator_params"] = dict(dp["period_discriminator_params"], channels=8,
+                                                 max_downsample_channels=64)
+        monkeypatch.setitem(configs.CONFIGS, "test_gan", c)
+        name = "test_gan"
+    step = train_denoise.main(["-e", "SYNTH", "-c", f"{name}.yaml", "--epochs", "1", "--synthetic-batches", "2"])
+    assert step.discriminator_enabled == gan
+    rows = [json.loads(l) for l in open(tmp_path / "job_out" / "SYNTH-run" / "scalars.jsonl")]
+    keys = {r["key"] for r in rows}
+    assert {"Generator Batch Loss/Train", "Generator Loss/Validation", "Discriminator Loss/Train"} <= keys
+    assert all(np.isfinite(r["value"]) for r in rows)
+    dis = [r["value"] for r in rows if r["key"] == "Discriminator Batch Loss/Train"]
+    assert (min(dis) > 0) == gan

@@ -134,3 +134,55 @@ def test_dconv_geometry_matches_torch_conv_lengths():
         # and no phase-view tap is entirely padding (K is minimal)
         assert any(0 <= s * q0 + r + pad < Kt for r in range(s))
         assert any(0 <= s * (q0 + K - 1) + r + pad < Kt for r in range(s))
+
+
+def test_trainer_checkpoint_roundtrip_with_reference_file(tmp_path):
+    """TrainerGAN.save_checkpoint / load_checkpoint (trainerGAN.py:95-149): our
+    trainer loads the checkpoint the REFERENCE trainer saved
+    (tests/golden/trainer_ckpt.pt: reduced PQC generator + HiFi-GAN discriminator,
+    Adam / StepLR / MultiStepLR states), with load_only_params both ways, and
+    writes back a dict of the identical structure and values."""
+    import warnings
+    from conftest import GOLDEN
+    from test_gpu_gan import D_PARAMS
+    from models.autoencoder.AudioDec import Generator
+    from models.vocoder.HiFiGAN import Discriminator
+    from trainer.denoise import Trainer
+    ref_path = os.path.join(GOLDEN, "trainer_ckpt.pt")
+    ref = torch.load(ref_path, map_location="cpu", weights_only=True)
+    gp = dict(encode_channels=4, decode_channels=4, code_dim=64, codebook_num=2, codebook_size=64)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        G, D = Generator(**gp), Discriminator(**D_PARAMS)
+    og = torch.optim.Adam(G.parameters(), lr=1e-4, betas=(0.5, 0.9))
+    od = torch.optim.Adam(D.parameters(), lr=2e-4, betas=(0.5, 0.9))
+    tr = Trainer(steps=0, epochs=0, data_loader={}, model={"generator": G, "discriminator": D}, criterion={},
+                 optimizer={"generator": og, "discriminator": od},
+                 scheduler={"generator": torch.optim.lr_scheduler.StepLR(og, 200000, 1.0),
+                            "discriminator": torch.optim.lr_scheduler.MultiStepLR(od, [200000, 400000], 0.5)},
+                 config={"outdir": None})
+    tr.load_checkpoint(ref_path, load_only_params=True)
+    assert tr.steps == 0
+    for k, v in ref["model"]["generator"].items():
+        assert torch.equal(G.state_dict()[k], v), k
+    tr.load_checkpoint(ref_path)
+    assert tr.steps == ref["steps"] == 2 and tr.epochs == ref["epochs"]
+    out = tmp_path / "ck" / "checkpoint-2steps.pkl"
+    tr.save_checkpoint(str(out))
+    mine = torch.load(out, map_location="cpu", weights_only=True)
+
+    def same(a, b, path=""):
+        assert type(a) == type(b) or (isinstance(a, (list, tuple)) and isinstance(b, (list, tuple))), path
+        if isinstance(a, dict):
+            assert list(a) == list(b), (path, set(a) ^ set(b))
+            for k in a:
+                same(a[k], b[k], f"{path}/{k}")
+        elif isinstance(a, (list, tuple)):
+            assert len(a) == len(b), path
+            for i, (x, y) in enumerate(zip(a, b)):
+                same(x, y, f"{path}[{i}]")
+        elif torch.is_tensor(a):
+            assert torch.equal(a, b), path
+        else:
+            assert a == b, path
+    same(mine, ref)

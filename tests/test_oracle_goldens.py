@@ -316,7 +316,7 @@ def test_gan_step():
         with torch.no_grad():
             p = R.hifigan_discriminator(Dp, y, **D_PARAMS)
         adv = R.generator_adv_loss(pred, False)
-        fm = 2.0 * R.feat_match_loss(p_, p, False, False, False)
+        fm = 2.0 * R.feat_match_loss(p_, p)  # train_denoise.py:127: FeatureMatchLoss() defaults
         gen = mel + adv + fm
         og.zero_grad()
         od.zero_grad()
