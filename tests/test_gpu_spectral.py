@@ -290,3 +290,42 @@ def test_stft_loss_full_size_properties(gpu):
     s2, m2 = mod(xg, y)
     (2.0 * s2 + 2.0 * m2).backward()
     spec_close(xg.grad, 2.0 * g1, rtol=1e-6, floor=0)
+
+
+def test_buffer_b64_loads_at_dword_offsets(gpu):
+    """Root cause of spectral.hip's frame-fetch rule (r1 workaround note): an
+    interior STFT frame starts at ANY dword of the batch (odd hop or odd T), so an
+    8-byte raw_buffer_load_b64 there is only correct if the hardware honours
+    4-byte-aligned offsets.  This probe records what gfx950 returns for every
+    dword offset through the kernels' own buffer resource; the 8-byte-aligned
+    offsets must be exact.  The frame fetch uses 8-B loads only when the frame
+    start is 8-byte aligned and per-dword loads otherwise, which is correct
+    whatever the misaligned result is (asserted by the odd-hop / odd-T STFT
+    parity test below)."""
+    from sel import _lib as L
+    n = 4097
+    x = torch.arange(n, dtype=torch.float32, device=gpu) + 0.5
+    out = torch.full((2 * n,), -1.0, device=gpu)
+    L.call("sel_probe_buffer_b64", L.ptr(x), n, L.ptr(out), L.stream())
+    got = out[: 2 * (n - 1)].view(n - 1, 2).cpu()
+    want = torch.stack([x[:-1], x[1:]], 1).cpu()
+    ok = (got == want).all(1)
+    assert ok[0::2].all(), "8-byte-aligned b64 buffer loads must be exact"
+    print(f"b64 buffer loads at 4-mod-8 byte offsets exact: {bool(ok[1::2].all())} "
+          f"(first misaligned pair returned {got[1].tolist()} for {want[1].tolist()})")
+
+
+@pytest.mark.parametrize("T,hop,n_fft,win", [(4801, 75, 1024, 600), (3333, 111, 512, 240), (2049, 33, 2048, 1200)])
+def test_stft_mag_odd_alignment_vs_oracle(gpu, T, hop, n_fft, win):
+    """Frames starting at odd sample offsets (odd hop, odd T: 4-byte-aligned
+    frame starts in every signal but the first) through the STFT |X| kernel vs
+    the oracle: the fetch must pick the per-dword path for them."""
+    from losses import stft
+    from oracle import ref_ops as R
+    torch.manual_seed(T + hop)
+    x = torch.randn(3, T)
+    w = torch.hann_window(win)
+    got = stft(x.to(gpu), n_fft, hop, win, w.to(gpu))
+    ref = R.stft_mag(x.double(), n_fft, hop, win, w.double())
+    e = ((got.double().cpu() - ref).norm() / ref.norm()).item()
+    assert e < 1e-5, e
