@@ -79,28 +79,39 @@ int sel_tune(int key, int value) {
 }  // extern "C"
 
 // ---------------------------------------------------------------------------
-// Hardware probe behind spectral.hip's frame loads (tests/test_gpu_spectral.py):
+// Probe behind spectral.hip's frame loads (tests/test_gpu_spectral.py):
 // out[2i], out[2i+1] = the pair a raw_buffer_load_b64 returns at byte offset 4i
 // of x, through the same buffer resource the STFT kernels build (num_records
-// n*4, word3 0x00020000 = CK's gfx9 value).  Interior STFT frames start at any
-// dword (hop and T odd), so whether an 8-byte buffer load honours a 4-byte-aligned
-// offset decides which load form the frame fetch may use.
+// n*4, word3 0x00020000 = CK's gfx9 value).  mode 0 takes the two dwords out of
+// the returned vector as scalars; mode 1 writes __builtin_bit_cast(float, v[1])
+// — the form round 1 used.  ROCm 7.2's clang lowers a bit_cast of an
+// ext_vector ELEMENT lvalue to a load from the vector's base address, so mode 1
+// returns element 0 twice (one buffer_load_dword + v_mov in the ISA): that, not
+// the hardware or the descriptor, was the "wrong pairs" of the r1 workaround.
 // ---------------------------------------------------------------------------
 namespace {
-__global__ void k_probe_buffer_b64(const float* __restrict__ x, int n, float* __restrict__ out) {
+typedef unsigned int probe_u2 __attribute__((ext_vector_type(2)));
+__global__ void k_probe_buffer_b64(const float* __restrict__ x, int n, int mode, float* __restrict__ out) {
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x), 0, n * 4, 0x00020000);
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i + 1 < n; i += gridDim.x * blockDim.x) {
     const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, i * 4, 0, 0);
-    out[2 * i] = __builtin_bit_cast(float, v[0]);
-    out[2 * i + 1] = __builtin_bit_cast(float, v[1]);
+    if (mode == 0) {
+      const probe_u2 u = v;
+      const unsigned e0 = u.x, e1 = u.y;
+      out[2 * i] = __builtin_bit_cast(float, e0);
+      out[2 * i + 1] = __builtin_bit_cast(float, e1);
+    } else {
+      out[2 * i] = __builtin_bit_cast(float, v[0]);
+      out[2 * i + 1] = __builtin_bit_cast(float, v[1]);
+    }
   }
 }
 }  // namespace
 
-extern "C" int sel_probe_buffer_b64(const float* x, int n, float* out, sel_stream_t stream) {
-  SEL_REQUIRE(x && out && n >= 2 && n < (1 << 28), SEL_ERR_ARG, "bad probe arguments");
+extern "C" int sel_probe_buffer_b64(const float* x, int n, int mode, float* out, sel_stream_t stream) {
+  SEL_REQUIRE(x && out && n >= 2 && n < (1 << 28) && (mode == 0 || mode == 1), SEL_ERR_ARG, "bad probe arguments");
   hipLaunchKernelGGL(k_probe_buffer_b64, dim3((n + 255) / 256), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
-                     x, n, out);
+                     x, n, mode, out);
   SEL_LAUNCH_CHECK();
   return SEL_OK;
 }

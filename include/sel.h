@@ -45,8 +45,10 @@ int sel_version(void);
  * 0 = built-in heuristic); returns the previous value. */
 int sel_tune(int key, int value);
 /* diagnostics: out[2i], out[2i+1] = raw_buffer_load_b64 of x at byte offset 4i
- * (i < n-1) through the STFT kernels' buffer resource (spectral.hip fetch_frame) */
-int sel_probe_buffer_b64(const float* x, int n, float* out, sel_stream_t stream);
+ * (i < n-1) through the STFT kernels' buffer resource (spectral.hip fetch_frame);
+ * mode 0: elements taken as scalars, mode 1: __builtin_bit_cast of the vector
+ * elements (miscompiled by ROCm 7.2 clang: element 0 twice) */
+int sel_probe_buffer_b64(const float* x, int n, int mode, float* out, sel_stream_t stream);
 
 /* ---- STFT magnitude: losses/stft_loss.py:19-35 (stft) ------------------
  * x (B,T) -> mag (B, F, K), F = 1 + T/hop, K = n_fft/2 + 1.
