@@ -238,6 +238,90 @@ __global__ __launch_bounds__(256) void k_dconv_valu(D d, const T* __restrict__ x
   }
 }
 
+// Short-reduction primitive (K * S * Cg <= 64, one group, single output phase,
+// Ng % 8 == 0): the 1-channel-input convs (MSD k15, MPD k5/s3 -> 2 taps x 3
+// phases) and the adjoints of the 1-channel-output convs.  One thread = one
+// output row x 8 consecutive channels: the row's input window in registers, the
+// weights in LDS (fp32), one 16-B (bf16) / 32-B (fp32) store.
+
+template <typename T, int KR>
+__global__ __launch_bounds__(256) void k_dconv_short(D d, const T* __restrict__ x, const T* __restrict__ wp,
+                                                     const float* __restrict__ bias, const T* __restrict__ aux,
+                                                     const T* __restrict__ res, T* __restrict__ out) {
+  constexpr int RW = 4;   // rows per thread: each weight read from LDS serves RW rows
+  extern __shared__ float wsh[];  // [K * nred][Ng] (transposed: a thread's 8 channels are 2 float4)
+  const int nred = d.S * d.Cg;
+  for (int e = threadIdx.x; e < d.Ng * KR; e += 256) {
+    const int n = e / KR, k = e - n * KR;
+    wsh[k * d.Ng + n] = to_f(wp[e]);
+  }
+  __syncthreads();
+  const int n8 = d.Ng / 8;
+  const int64_t rows = int64_t(d.B) * d.Tvo;
+  const int64_t total = (rows + RW - 1) / RW * n8;
+  for (int64_t idx = int64_t(blockIdx.x) * 256 + threadIdx.x; idx < total; idx += int64_t(gridDim.x) * 256) {
+    const int64_t rg = idx / n8;
+    const int n0 = int(idx - rg * n8) * 8;
+    float xw[RW][KR];
+    int64_t orow[RW];
+    bool valid[RW];
+#pragma unroll
+    for (int q = 0; q < RW; ++q) {
+      const int64_t row = rg * RW + q;
+      const int b = int(row / d.Tvo), j = int(row - int64_t(b) * d.Tvo);
+      orow[q] = row < rows ? row * d.ldo : -1;
+      valid[q] = row < rows && j < d.Tvalid;
+#pragma unroll
+      for (int e = 0; e < KR; ++e) {
+        const int i = e / nred, rc = e - i * nred;
+        const int r = rc / d.Cg, c = rc - r * d.Cg;
+        const int t = j + d.q0 + i;
+        xw[q][e] = (valid[q] && t >= 0 && t < d.Tv) ? to_f(x[(int64_t(b) * d.Tvs + t) * d.ldx + in_col(d, 0, r, c)])
+                                                    : 0.f;
+      }
+    }
+    float acc[RW][8];
+#pragma unroll
+    for (int q = 0; q < RW; ++q)
+#pragma unroll
+      for (int c = 0; c < 8; ++c) acc[q][c] = 0.f;
+#pragma unroll
+    for (int e = 0; e < KR; ++e) {
+      const float4 w0 = *reinterpret_cast<const float4*>(wsh + e * d.Ng + n0);
+      const float4 w1 = *reinterpret_cast<const float4*>(wsh + e * d.Ng + n0 + 4);
+      const float w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+      for (int q = 0; q < RW; ++q)
+#pragma unroll
+        for (int c = 0; c < 8; ++c) acc[q][c] = fmaf(w[c], xw[q][e], acc[q][c]);
+    }
+#pragma unroll
+    for (int q = 0; q < RW; ++q) {
+      if (orow[q] < 0) continue;
+      T ov[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        float a = 0.f;
+        if (valid[q]) {
+          const int64_t col = n0 + c;
+          a = acc[q][c];
+          if (bias) a += bias[col];
+          if (res) a += to_f(res[orow[q] + col]);
+          if (aux) a *= leaky_grad(to_f(aux[orow[q] + col]), d.slope);
+          if (d.act) a = leaky(a, d.slope);
+        }
+        ov[c] = from_f<T>(a);
+      }
+      if constexpr (sizeof(T) == 2) {
+        *reinterpret_cast<uint4*>(out + orow[q] + n0) = *reinterpret_cast<uint4*>(ov);
+      } else {
+        *reinterpret_cast<uint4*>(out + orow[q] + n0) = *reinterpret_cast<uint4*>(ov);
+        *reinterpret_cast<uint4*>(out + orow[q] + n0 + 4) = *reinterpret_cast<uint4*>(ov + 4);
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Weight gradient partials.  gW[g][o][i][r][c] = sum over rows (b, j < Tvalid)
 // of gout[b, j, col(g, o)] * x[b, j + q0 + i, r*Cs + g*Cg + c]; bias partials
@@ -264,20 +348,22 @@ __global__ __launch_bounds__(256) void k_dwgrad_valu(D d, const T* __restrict__ 
       const int g = int(go / no_per_g), o = int(go - int64_t(g) * no_per_g);
       const int rph = rc / d.Cg, c = rc - rph * d.Cg;
       const int64_t oc = out_col(d, g, o), ic = in_col(d, g, rph, c);
+      int b = int(r0 / d.Tvalid), j = int(r0 - int64_t(b) * d.Tvalid);  // one division, then a row walk
       for (int64_t rr = r0; rr < r1; ++rr) {
-        const int b = int(rr / d.Tvalid), j = int(rr - int64_t(b) * d.Tvalid);
         const int t = j + d.q0 + i;
-        if (t < 0 || t >= d.Tv) continue;
-        acc += to_f(gout[(int64_t(b) * d.Tvo + j) * d.ldo + oc]) * to_f(x[(int64_t(b) * d.Tvs + t) * d.ldx + ic]);
+        if (t >= 0 && t < d.Tv)
+          acc += to_f(gout[(int64_t(b) * d.Tvo + j) * d.ldo + oc]) * to_f(x[(int64_t(b) * d.Tvs + t) * d.ldx + ic]);
+        if (++j == d.Tvalid) j = 0, ++b;
       }
       part[int64_t(blockIdx.y) * nw + idx] = acc;
     } else {
       const int64_t go = idx - nw;
       const int g = int(go / no_per_g), o = int(go - int64_t(g) * no_per_g);
       const int64_t oc = out_col(d, g, o);
+      int b = int(r0 / d.Tvalid), j = int(r0 - int64_t(b) * d.Tvalid);
       for (int64_t rr = r0; rr < r1; ++rr) {
-        const int b = int(rr / d.Tvalid), j = int(rr - int64_t(b) * d.Tvalid);
         acc += to_f(gout[(int64_t(b) * d.Tvo + j) * d.ldo + oc]);
+        if (++j == d.Tvalid) j = 0, ++b;
       }
       bpart[int64_t(blockIdx.y) * nb + go] = acc;
     }
@@ -394,24 +480,105 @@ __global__ __launch_bounds__(256) void k_dwgrad_mfma(D d, const __bf16* __restri
   }
 }
 
-// bias partials for the MFMA wgrad path: gb[col] over a split of rows
+// bias partials for the MFMA wgrad path: gb[col] over a split of rows.  Block =
+// 64 output columns x 4 row lanes (a row's 64 columns are one coalesced read),
+// row walk without divisions, the 4 lanes summed in LDS.
 template <typename T>
 __global__ __launch_bounds__(256) void k_dbias_part(D d, const T* __restrict__ gout, int rows_per_split,
                                                     float* __restrict__ bpart) {
+  __shared__ float red[4][64];
   const int no_per_g = d.So * d.Ng;
   const int64_t nb = int64_t(d.G) * no_per_g;
   const int64_t total_rows = int64_t(d.B) * d.Tvalid;
   const int64_t r0 = int64_t(blockIdx.y) * rows_per_split;
   const int64_t r1 = r0 + rows_per_split < total_rows ? r0 + rows_per_split : total_rows;
-  for (int64_t go = int64_t(blockIdx.x) * 256 + threadIdx.x; go < nb; go += int64_t(gridDim.x) * 256) {
+  const int cl = threadIdx.x & 63, ly = threadIdx.x >> 6;
+  const int64_t go = int64_t(blockIdx.x) * 64 + cl;
+  float acc = 0.f;
+  if (go < nb) {
     const int g = int(go / no_per_g), o = int(go - int64_t(g) * no_per_g);
     const int64_t oc = out_col(d, g, o);
-    float acc = 0.f;
-    for (int64_t rr = r0; rr < r1; ++rr) {
-      const int b = int(rr / d.Tvalid), j = int(rr - int64_t(b) * d.Tvalid);
+    int64_t rr = r0 + ly;
+    int b = int(rr / d.Tvalid), j = int(rr - int64_t(b) * d.Tvalid);
+    for (; rr < r1; rr += 4) {
       acc += to_f(gout[(int64_t(b) * d.Tvo + j) * d.ldo + oc]);
+      j += 4;
+      while (j >= d.Tvalid) j -= d.Tvalid, ++b;
     }
-    bpart[int64_t(blockIdx.y) * nb + go] = acc;
+  }
+  red[ly][cl] = acc;
+  __syncthreads();
+  if (ly == 0 && go < nb) bpart[int64_t(blockIdx.y) * nb + go] = (red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]);
+}
+
+// Partial sums over groups of PRESUM splits (coalesced over the weights), so the
+// final per-output reduction reads at most PRESUM partials.
+constexpr int PRESUM = 16;
+__global__ __launch_bounds__(256) void k_presum(const float* __restrict__ part, int nsplit, int64_t n,
+                                                float* __restrict__ out) {
+  const int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int s0 = blockIdx.y * PRESUM, s1 = s0 + PRESUM < nsplit ? s0 + PRESUM : nsplit;
+  float acc = 0.f;
+  int sp = s0;
+  for (; sp + 4 <= s1; sp += 4) {
+    const float a0 = part[int64_t(sp) * n + i], a1 = part[int64_t(sp + 1) * n + i], a2 = part[int64_t(sp + 2) * n + i],
+                a3 = part[int64_t(sp + 3) * n + i];
+    acc += (a0 + a1) + (a2 + a3);
+  }
+  for (; sp < s1; ++sp) acc += part[int64_t(sp) * n + i];
+  out[int64_t(blockIdx.y) * n + i] = acc;
+}
+
+// Weight gradient of the short-reduction layers (K * S * Cg = KR in {2, 3, 6, 15},
+// one group, one output phase): block = a row range; thread = one output channel
+// n x one row lane, KR + 1 accumulators (weights and bias) over its rows; the row
+// lanes summed in LDS; one partial per block.
+template <typename T, int KR>
+__global__ __launch_bounds__(256) void k_dwgrad_short(D d, const T* __restrict__ gout, const T* __restrict__ x,
+                                                      int rows_per_split, float* __restrict__ part,
+                                                      float* __restrict__ bpart) {
+  __shared__ float red[256 * (KR + 1) <= 4096 ? 256 * (KR + 1) : 4096];
+  const int N = d.Ng;
+  const int nl = N < 256 ? N : 256;  // lanes over n (N <= 256 here)
+  const int RL = 256 / nl;
+  const int n = threadIdx.x % nl, rl = threadIdx.x / nl;
+  const int nred = d.S * d.Cg;
+  const int64_t total_rows = int64_t(d.B) * d.Tvalid;
+  const int64_t r0 = int64_t(blockIdx.x) * rows_per_split;
+  const int64_t r1 = r0 + rows_per_split < total_rows ? r0 + rows_per_split : total_rows;
+  float acc[KR + 1];
+#pragma unroll
+  for (int e = 0; e <= KR; ++e) acc[e] = 0.f;
+  int64_t rr = r0 + rl;
+  if (rr < r1 && threadIdx.x < nl * RL) {
+    int b = int(rr / d.Tvalid), j = int(rr - int64_t(b) * d.Tvalid);
+    for (; rr < r1; rr += RL) {
+      const float gv = to_f(gout[(int64_t(b) * d.Tvo + j) * d.ldo + n]);
+#pragma unroll
+      for (int e = 0; e < KR; ++e) {
+        const int i = e / nred, rc = e - i * nred;
+        const int r = rc / d.Cg, c = rc - r * d.Cg;
+        const int t = j + d.q0 + i;
+        if (t >= 0 && t < d.Tv) acc[e] = fmaf(gv, to_f(x[(int64_t(b) * d.Tvs + t) * d.ldx + in_col(d, 0, r, c)]), acc[e]);
+      }
+      acc[KR] += gv;
+      j += RL;
+      while (j >= d.Tvalid) j -= d.Tvalid, ++b;
+    }
+  }
+  // reduce the RL row lanes: red[rl][n][e]
+#pragma unroll
+  for (int e = 0; e <= KR; ++e) {
+    if (threadIdx.x < nl * RL) red[(rl * nl + n) * (KR + 1) + e] = acc[e];
+  }
+  __syncthreads();
+  for (int o = threadIdx.x; o < nl * (KR + 1); o += 256) {
+    float sum = 0.f;
+    for (int l = 0; l < RL; ++l) sum += red[l * nl * (KR + 1) + o];
+    const int nn = o / (KR + 1), e = o - nn * (KR + 1);
+    if (e < KR) part[int64_t(blockIdx.x) * N * KR + int64_t(nn) * KR + e] = sum;
+    else if (bpart) bpart[int64_t(blockIdx.x) * N + nn] = sum;
   }
 }
 
@@ -472,7 +639,9 @@ __global__ __launch_bounds__(256) void k_dpack(PackGeo pg, int mode, const float
 
 // Final wgrad reduction: sum the split partials, unpack to the torch layout,
 // and (weight norm) gv = (g/||v||) (gw - w_hat (w_hat . gw)), gg = w_hat . gw.
-// One block per output channel n.
+// One block per output channel n; the partials are walked in their packed
+// (tap, phase, channel) order, so each split's slice is one coalesced read, and
+// scattered once into the torch (channel, tap) positions.
 __global__ __launch_bounds__(256) void k_dwgrad_finish(PackGeo pg, const float* __restrict__ part, int nsplit,
                                                        const float* __restrict__ bpart, int bsplit,
                                                        const float* __restrict__ v, const float* __restrict__ wg,
@@ -485,27 +654,34 @@ __global__ __launch_bounds__(256) void k_dwgrad_finish(PackGeo pg, const float* 
   const int Ng = pg.N / pg.G, g = n / Ng, nl = n - g * Ng;
   const int nred = pg.s * pg.Cg;
   const int64_t nw = int64_t(pg.N) * pg.K * nred;
-  // pass 1: the reduced gradient of the effective weight, kept in gw
+  const int64_t base = (int64_t(g) * Ng + nl) * pg.K * nred;
   float dot = 0.f, vv = 0.f;
-  for (int e = threadIdx.x; e < per; e += 256) {
-    const int c = e / pg.Kt, k = e - c * pg.Kt;
-    // k = s*(q0+i) + r + pad
-    const int kk = k - pg.pad - pg.s * pg.q0;
-    const int i = kk / pg.s, r = kk - i * pg.s;
-    const int64_t src = ((int64_t(g) * Ng + nl) * pg.K + i) * nred + r * pg.Cg + c;
+  for (int e = threadIdx.x; e < pg.K * nred; e += 256) {
+    const int i = e / nred, rc = e - i * nred;
+    const int r = rc / pg.Cg, c = rc - r * pg.Cg;
+    const int k = pg.s * (pg.q0 + i) + r + pg.pad;
+    if (k < 0 || k >= pg.Kt) continue;  // structural zero of the phase view
     float acc = 0.f;
-    for (int sp = 0; sp < nsplit; ++sp) acc += part[int64_t(sp) * nw + src];
-    gw[int64_t(n) * per + e] = acc;
+    int sp = 0;
+    for (; sp + 4 <= nsplit; sp += 4) {  // 4 loads in flight, fixed order
+      const float a0 = part[int64_t(sp) * nw + base + e], a1 = part[int64_t(sp + 1) * nw + base + e],
+                  a2 = part[int64_t(sp + 2) * nw + base + e], a3 = part[int64_t(sp + 3) * nw + base + e];
+      acc += (a0 + a1) + (a2 + a3);
+    }
+    for (; sp < nsplit; ++sp) acc += part[int64_t(sp) * nw + base + e];
+    const int64_t o = int64_t(n) * per + c * pg.Kt + k;
+    gw[o] = acc;
     if (v) {
-      const float vv_ = v[int64_t(n) * per + e];
+      const float vv_ = v[o];
       dot += vv_ * acc;
       vv += vv_ * vv_;
     }
   }
-  if (gb && threadIdx.x == 0) {
+  if (gb) {  // the bias partials of this n, spread over the block (fixed order per thread)
     float acc = 0.f;
-    for (int sp = 0; sp < bsplit; ++sp) acc += bpart[int64_t(sp) * pg.N + n];
-    gb[n] = acc;
+    for (int sp = threadIdx.x; sp < bsplit; sp += 256) acc += bpart[int64_t(sp) * pg.N + n];
+    acc = block_sum(acc, red);
+    if (threadIdx.x == 0) gb[n] = acc;
   }
   if (!v) return;
   dot = block_sum(dot, red);
@@ -518,6 +694,7 @@ __global__ __launch_bounds__(256) void k_dwgrad_finish(PackGeo pg, const float* 
   // w = gn * v / nv ; dL/dgn = (v . gw) / nv ; dL/dv = gn/nv * (gw - v (v . gw) / nv^2)
   if (threadIdx.x == 0) gg[n] = bc[0] / nv;
   const float a = gn / nv, bcoef = gn * bc[0] / (nv * nv * nv);
+  __syncthreads();  // every gw[o] of this n written before the in-place update
   for (int e = threadIdx.x; e < per; e += 256) {
     const int64_t o = int64_t(n) * per + e;
     gw[o] = a * gw[o] - bcoef * v[o];
@@ -607,15 +784,25 @@ struct View4 {
   int64_t stride[4];
 };
 
-__device__ __forceinline__ int64_t view_off(const View4& v, int64_t i) {
-  int64_t off = 0;
-#pragma unroll
-  for (int d = 3; d >= 0; --d) {
-    const int64_t q = i / v.size[d];
-    off += (i - q * v.size[d]) * v.stride[d];
-    i = q;
-  }
-  return off;
+// 4-D index of flat element i (last dim fastest) with 32-bit divisions (the host
+// permutes the views to memory order, so the last dim is the contiguous one)
+struct Idx4 {
+  uint32_t i0, i1, i2, i3;
+};
+__device__ __forceinline__ Idx4 unflat(const View4& v, uint32_t i) {
+  Idx4 r;
+  const uint32_t s3 = uint32_t(v.size[3]), s2 = uint32_t(v.size[2]), s1 = uint32_t(v.size[1]);
+  uint32_t q = i / s3;
+  r.i3 = i - q * s3;
+  uint32_t q2 = q / s2;
+  r.i2 = q - q2 * s2;
+  r.i0 = q2 / s1;
+  r.i1 = q2 - r.i0 * s1;
+  return r;
+}
+__device__ __forceinline__ int64_t off4(const View4& v, const Idx4& x) {
+  return int64_t(x.i0) * v.stride[0] + int64_t(x.i1) * v.stride[1] + int64_t(x.i2) * v.stride[2] +
+         int64_t(x.i3) * v.stride[3];
 }
 
 template <typename T>
@@ -623,19 +810,20 @@ __global__ __launch_bounds__(256) void k_gan_reduce(int kind, const T* __restric
                                                     const T* __restrict__ b, View4 vb, float target, int64_t n,
                                                     double* __restrict__ partials) {
   __shared__ double red[16];
-  double s = 0.0;
+  float s = 0.f;  // per-thread partial (<= a few hundred terms), fp64 across threads and blocks
   for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256) {
-    const float x = to_f(a[view_off(va, i)]);
+    const Idx4 ix = unflat(va, uint32_t(i));
+    const float x = to_f(a[off4(va, ix)]);
     float v;
-    if (kind == 0) v = fabsf(x - to_f(b[view_off(vb, i)]));  // L1
-    else if (kind == 1) v = (x - target) * (x - target);     // MSE to target
-    else if (kind == 2) v = fminf(x - 1.f, 0.f);             // hinge real: min(x - 1, 0)
-    else if (kind == 3) v = fminf(-x - 1.f, 0.f);            // hinge fake: min(-x - 1, 0)
-    else v = x;                                              // plain sum (generator hinge: -mean)
-    s += double(v);
+    if (kind == 0) v = fabsf(x - to_f(b[off4(vb, ix)]));  // L1
+    else if (kind == 1) v = (x - target) * (x - target);  // MSE to target
+    else if (kind == 2) v = fminf(x - 1.f, 0.f);          // hinge real: min(x - 1, 0)
+    else if (kind == 3) v = fminf(-x - 1.f, 0.f);         // hinge fake: min(-x - 1, 0)
+    else v = x;                                           // plain sum (generator hinge: -mean)
+    s += v;
   }
-  s = block_sum(s, red);
-  if (threadIdx.x == 0) partials[blockIdx.x] = s;
+  const double t = block_sum(double(s), red);
+  if (threadIdx.x == 0) partials[blockIdx.x] = t;
 }
 
 __global__ void k_gan_finish(const double* __restrict__ partials, int nblocks, double scale, float* __restrict__ out,
@@ -655,10 +843,11 @@ __global__ __launch_bounds__(256) void k_gan_grad(int kind, const T* __restrict_
                                                   T* __restrict__ grad, View4 vg, int accumulate) {
   const float c = gscale[0] * mult;
   for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256) {
-    const float x = to_f(a[view_off(va, i)]);
+    const Idx4 ix = unflat(va, uint32_t(i));
+    const float x = to_f(a[off4(va, ix)]);
     float gv;
     if (kind == 0) {
-      const float dlt = x - to_f(b[view_off(vb, i)]);
+      const float dlt = x - to_f(b[off4(vb, ix)]);
       gv = dlt > 0.f ? c : (dlt < 0.f ? -c : 0.f);
     } else if (kind == 1) {
       gv = 2.f * (x - target) * c;
@@ -669,7 +858,7 @@ __global__ __launch_bounds__(256) void k_gan_grad(int kind, const T* __restrict_
     } else {
       gv = c;
     }
-    const int64_t o = view_off(vg, i);
+    const int64_t o = off4(vg, ix);
     grad[o] = from_f<T>(accumulate ? to_f(grad[o]) + gv : gv);
   }
 }
@@ -701,9 +890,14 @@ int check(const sel_dconv_desc* d) {
 bool mfma_ok(const sel_dconv_desc* d, int dtype) {
   const int vec = dtype == SEL_BF16 ? 8 : 4;
   // 8-channel (bf16) / 4-channel (fp32) vectors may not straddle a phase or a
-  // group, and the group's output width must fill at least half a 32-wide tile
-  return d->Cg % vec == 0 && d->Cs % vec == 0 && d->ldx % vec == 0 && (d->S * d->Cg) % 8 == 0 &&
-         d->So * d->Ng >= 16 && d->K <= 64;
+  // group.  A group narrower than the 32-wide MFMA tile still runs on the
+  // matrix cores when its reduction is long (the 1-channel-output convs and the
+  // adjoints of the 1-channel-input convs: K * S * Cg >= 256 products per output,
+  // where the VALU kernel's per-thread strided row walk is far slower than a
+  // 1/32-filled MFMA tile fed from LDS)
+  const int width = d->So * d->Ng;
+  return d->Cg % vec == 0 && d->Cs % vec == 0 && d->ldx % vec == 0 && (d->S * d->Cg) % 8 == 0 && d->K <= 64 &&
+         (width >= 16 || d->K * d->S * d->Cg >= 256);
 }
 
 template <typename T, int BM, int BN>
@@ -736,10 +930,38 @@ int launch_valu(const sel_dconv_desc* d, const void* x, const void* wp, const fl
   return SEL_OK;
 }
 
+// instantiated reductions: MSD first conv (15 taps), MPD first conv (2 taps x 3
+// phases), the adjoints of the 1-channel output convs (3 / 2 taps)
+bool short_kr_ok(int kr) { return kr == 2 || kr == 3 || kr == 6 || kr == 15; }
+
+bool short_ok(const sel_dconv_desc* d) {
+  return d->G == 1 && d->So == 1 && d->Ng % 8 == 0 && d->ldo % 8 == 0 && short_kr_ok(d->K * d->S * d->Cg) &&
+         size_t(d->Ng) * d->K * d->S * d->Cg * sizeof(float) <= 64 * 1024;
+}
+
+template <typename T>
+int launch_short(const sel_dconv_desc* d, const void* x, const void* wp, const float* bias, const void* aux,
+                 const void* res, void* out, hipStream_t s) {
+  const int64_t total = (int64_t(d->B) * d->Tvo + 3) / 4 * (d->Ng / 8);
+  const unsigned blocks = unsigned(std::min<int64_t>((total + 255) / 256, 16384));
+  const int kr = d->K * d->S * d->Cg;
+  const size_t lds = size_t(d->Ng) * kr * sizeof(float);
+  auto kern = kr == 2 ? k_dconv_short<T, 2> : kr == 3 ? k_dconv_short<T, 3> : kr == 6 ? k_dconv_short<T, 6>
+                                                                                    : k_dconv_short<T, 15>;
+  hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), lds, s, *d, static_cast<const T*>(x), static_cast<const T*>(wp),
+                     bias, static_cast<const T*>(aux), static_cast<const T*>(res), static_cast<T*>(out));
+  SEL_LAUNCH_CHECK();
+  return SEL_OK;
+}
+
 template <typename T>
 int dispatch_fwd(const sel_dconv_desc* d, const void* x, const void* wp, const float* bias, const void* aux,
                  const void* res, void* out, hipStream_t s, int dtype) {
-  if (!mfma_ok(d, dtype) || tune(9) == 1) return launch_valu<T>(d, x, wp, bias, aux, res, out, s);
+  if (tune(9) == 1) return launch_valu<T>(d, x, wp, bias, aux, res, out, s);
+  if (!mfma_ok(d, dtype)) {
+    if (short_ok(d)) return launch_short<T>(d, x, wp, bias, aux, res, out, s);
+    return launch_valu<T>(d, x, wp, bias, aux, res, out, s);
+  }
   const int width = d->So * d->Ng;
   const int64_t rows = int64_t(d->B) * d->Tvo;
   // narrow groups: 32-wide tiles; short sequences / few rows: 64-row tiles
@@ -752,7 +974,7 @@ int dispatch_fwd(const sel_dconv_desc* d, const void* x, const void* wp, const f
 }
 
 struct WgPlanD {
-  bool mfma;
+  bool mfma, shortk;
   int nsplit, bsplit;
   int rows_per_split, brows_per_split;
   int tiles_per_seq, tiles_per_split, ntg, nt;
@@ -766,6 +988,15 @@ WgPlanD wg_plan(const sel_dconv_desc* d, int dtype) {
            width % 16 == 0 && tune(9) != 1;
   const int64_t rows = int64_t(d->B) * d->Tvalid;
   const int64_t nw = int64_t(d->G) * width * d->K * nred;
+  p.shortk = !p.mfma && tune(9) != 1 && d->G == 1 && d->So == 1 && d->Ng <= 256 && (256 % d->Ng) == 0 &&
+             short_kr_ok(d->K * nred);
+  if (p.shortk) {
+    const int64_t want = std::max<int64_t>(1, std::min<int64_t>(2048, rows / 64));
+    p.rows_per_split = int((rows + want - 1) / want);
+    p.nsplit = int((rows + p.rows_per_split - 1) / p.rows_per_split);
+    p.bsplit = p.nsplit;
+    return p;
+  }
   if (p.mfma) {
     p.nt = width % 32 == 0 ? 2 : 1;
     p.ntg = (d->K + WG_TAPS - 1) / WG_TAPS;
@@ -796,13 +1027,27 @@ size_t wg_bytes(const sel_dconv_desc* d, const WgPlanD& p) {
   const int64_t width = int64_t(d->So) * d->Ng;
   const int64_t nw = int64_t(d->G) * width * d->K * d->S * d->Cg;
   const int64_t nb = int64_t(d->G) * width;
-  return size_t(int64_t(p.nsplit) * nw + int64_t(std::max(p.bsplit, p.nsplit)) * nb) * sizeof(float) + 256;
+  const int64_t ng = (p.nsplit + PRESUM - 1) / PRESUM;
+  return size_t(int64_t(p.nsplit) * nw + int64_t(std::max(p.bsplit, p.nsplit)) * nb + (ng + 1) * nw) * sizeof(float) +
+         256;
 }
 
 hipError_t wgrad_fill(const sel_dconv_desc* d, int dtype, const WgPlanD& p, const void* gout, const void* x,
                       float* part, float* bpart, hipStream_t s) {
   const int width = d->So * d->Ng;
   const int nred = d->S * d->Cg;
+  if (p.shortk) {
+    const int kr = d->K * nred;
+#define SEL_DWS(TT, KR)                                                                                     \
+  hipLaunchKernelGGL((k_dwgrad_short<TT, KR>), dim3(p.nsplit), dim3(256), 0, s, *d, static_cast<const TT*>(gout), \
+                     static_cast<const TT*>(x), p.rows_per_split, part, bpart)
+#define SEL_DWS_T(TT) \
+  if (kr == 2) SEL_DWS(TT, 2); else if (kr == 3) SEL_DWS(TT, 3); else if (kr == 6) SEL_DWS(TT, 6); else SEL_DWS(TT, 15);
+    if (dtype == SEL_BF16) { SEL_DWS_T(__bf16) } else { SEL_DWS_T(float) }
+#undef SEL_DWS_T
+#undef SEL_DWS
+    return hipGetLastError();
+  }
   if (p.mfma) {
     const int bn = 16 * p.nt;
     dim3 grid(unsigned(d->G * ((width + bn - 1) / bn)), unsigned((nred + 31) / 32), unsigned(p.nsplit * p.ntg));
@@ -815,7 +1060,7 @@ hipError_t wgrad_fill(const sel_dconv_desc* d, int dtype, const WgPlanD& p, cons
                          static_cast<const __bf16*>(x), p.tiles_per_seq, p.tiles_per_split, p.ntg, part);
     if (bpart) {
       const int64_t nb = int64_t(d->G) * width;
-      dim3 bg(unsigned((nb + 255) / 256), unsigned(p.bsplit));
+      dim3 bg(unsigned((nb + 63) / 64), unsigned(p.bsplit));
       hipLaunchKernelGGL(k_dbias_part<__bf16>, bg, dim3(256), 0, s, *d, static_cast<const __bf16*>(gout),
                          p.brows_per_split, bpart);
     }
@@ -862,7 +1107,10 @@ int sel_dconv_fwd(const sel_dconv_desc* d, int dtype, const void* x, const void*
   return SEL_ERR_UNSUPPORTED;
 }
 
-int sel_dconv_uses_mfma(const sel_dconv_desc* d, int dtype) { return d && mfma_ok(d, dtype) && tune(9) != 1; }
+int sel_dconv_uses_mfma(const sel_dconv_desc* d, int dtype) {
+  if (!d || tune(9) == 1) return 0;
+  return mfma_ok(d, dtype) ? 1 : (short_ok(d) ? 2 : 0);
+}
 
 size_t sel_dconv_wgrad_workspace(const sel_dconv_desc* d, int dtype) {
   if (!d || check(d) != SEL_OK) return 16;
@@ -887,8 +1135,22 @@ int sel_dconv_wgrad(const sel_dconv_desc* d, int dtype, const void* gout, const 
   const int64_t nw = int64_t(N) * d->K * d->S * d->Cg;
   float* bpart = gb ? part + int64_t(p.nsplit) * nw : nullptr;
   SEL_HIP(wgrad_fill(d, dtype, p, gout, x, part, bpart, s));
-  const int bsplit = p.mfma ? p.bsplit : p.nsplit;
-  hipLaunchKernelGGL(k_dwgrad_finish, dim3(N), dim3(256), 0, s, pg, part, p.nsplit, bpart, bsplit, v, wg, gw, gg,
+  const int bsplit = (p.mfma || p.shortk) ? p.bsplit : p.nsplit;
+  int nsplit = p.nsplit;
+  if (nsplit > PRESUM) {  // fold the partials to <= PRESUM per weight before the per-output pass
+    float* tmp = part + int64_t(p.nsplit) * nw + int64_t(std::max(p.bsplit, p.nsplit)) * N;
+    float* src = part;
+    while (nsplit > PRESUM) {
+      const int ng = (nsplit + PRESUM - 1) / PRESUM;
+      float* dst = src == part ? tmp : part;
+      hipLaunchKernelGGL(k_presum, dim3(unsigned((nw + 255) / 256), unsigned(ng)), dim3(256), 0, s, src, nsplit, nw,
+                         dst);
+      src = dst;
+      nsplit = ng;
+    }
+    part = src;
+  }
+  hipLaunchKernelGGL(k_dwgrad_finish, dim3(N), dim3(256), 0, s, pg, part, nsplit, bpart, bsplit, v, wg, gw, gg,
                      gb);
   SEL_LAUNCH_CHECK();
   return SEL_OK;
@@ -979,6 +1241,7 @@ int sel_gan_reduce(int kind, int dtype, const void* a, const int64_t* a_size, co
     n *= a_size[i];
     if (kind == 0) SEL_REQUIRE(b_size[i] == a_size[i], SEL_ERR_ARG, "shape mismatch");
   }
+  SEL_REQUIRE(n < (int64_t(1) << 32), SEL_ERR_ARG, "view too large (%lld elements)", (long long)n);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const View4 va = to_view(a_size, a_stride, ndim);
   const View4 vb = kind == 0 ? to_view(b_size, b_stride, ndim) : va;
@@ -1004,6 +1267,7 @@ int sel_gan_grad(int kind, int dtype, const void* a, const int64_t* a_size, cons
   SEL_REQUIRE(kind != 0 || (b && view_ok(b_size, b_stride)), SEL_ERR_ARG, "L1 needs b");
   int64_t n = 1;
   for (int i = 0; i < ndim; ++i) n *= a_size[i];
+  SEL_REQUIRE(n < (int64_t(1) << 32), SEL_ERR_ARG, "view too large (%lld elements)", (long long)n);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const View4 va = to_view(a_size, a_stride, ndim);
   const View4 vb = kind == 0 ? to_view(b_size, b_stride, ndim) : va;

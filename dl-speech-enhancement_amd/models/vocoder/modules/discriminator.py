@@ -34,7 +34,7 @@ def _slope(name, params):
 @contextlib.contextmanager
 def frozen_parameters(module):
     """Run a discriminator with its parameters as constants (no weight-gradient
-    kernels).  train_denoise.py's generator step back-propagates through D only
+    kernels; the parameters receive no gradient and fire no DDP hook).  train_denoise.py's generator step back-propagates through D only
     to reach the generator; the D gradients it also computes (:234-235) are
     discarded by optimizer["discriminator"].zero_grad() before the D step
     (:252), so skipping them changes no result."""
@@ -97,7 +97,7 @@ class HiFiGANPeriodDiscriminator(nn.Module):
                 out += [m.weight_v, m.weight_g, m.bias]
             else:
                 out += [m.weight, m.bias]
-        return [p.detach() for p in out] if getattr(self, "_frozen", False) else out
+        return out
 
     def plan(self):
         if self._plan is None:
@@ -117,7 +117,7 @@ class HiFiGANPeriodDiscriminator(nn.Module):
         seqs = DC.MpdFoldFn.apply(x2, p, DC._roundup(Lv, specs[0].stride))
         x0 = CO.cast(seqs, CO.compute_dtype()).unsqueeze(-1)
         outs = list(DC.ChainFn.apply(x0, Lv, specs, self.slope, self.use_weight_norm, "period", b, p,
-                                     *self._params()))
+                                     getattr(self, "_frozen", False), *self._params()))
         outs[-1] = torch.flatten(outs[-1], 1, -1)
         return outs
 
@@ -203,7 +203,7 @@ class HiFiGANScaleDiscriminator(nn.Module):
         out = []
         for m in self._convs():
             out += [m.weight, m.bias]
-        return [p.detach() for p in out] if getattr(self, "_frozen", False) else out
+        return out
 
     def plan(self):
         if self._plan is None:
@@ -216,7 +216,8 @@ class HiFiGANScaleDiscriminator(nn.Module):
         if c != 1:
             raise NotImplementedError("the HIP scale discriminator takes 1-channel input (in_channels=1)")
         x0 = CO.cast(x.reshape(b, t, 1).float(), CO.compute_dtype())
-        return list(DC.ChainFn.apply(x0, t, self.plan(), self.slope, False, "scale", b, 1, *self._params()))
+        return list(DC.ChainFn.apply(x0, t, self.plan(), self.slope, False, "scale", b, 1,
+                                     getattr(self, "_frozen", False), *self._params()))
 
     def apply_weight_norm(self):
         pass  # reference :354-362 matches Conv2d only

@@ -15,8 +15,10 @@ Reference layouts returned (views, no copies):
                         final (B, L*p)    (a copy, as torch.flatten in :134)
 """
 import ctypes
+import weakref
 
 import torch
+from torch.optim.optimizer import register_optimizer_step_post_hook as _register_optimizer_step_post_hook
 
 from . import _lib as L
 from .convops import BF16, F32, _code, compute_dtype
@@ -72,7 +74,53 @@ def _dgrad_desc(sp, Bs, T_alloc_in, T_out, T_out_alloc, slope, prev_leaky):
                      Ns=sp.cin, Ng=sp.cin // sp.groups, act=0, slope=slope)
 
 
+class _DPackCache:
+    """Packed forms of the discriminator weights, reused until the parameter
+    changes: the version counter (copy_, load_state_dict, foreach Adam) or an
+    optimizer step on it (torch's fused Adam does not bump the version; same
+    global post-step hook as sel.convops.PackCache).  A D forward + adjoint
+    otherwise repacks every layer at every call (3 D passes per GAN step)."""
+
+    def __init__(self):
+        self._e = {}
+
+    def get(self, sp, w, wg, dtype, mode):
+        key = (id(w), mode, dtype, sp.Kt, sp.stride, sp.pad, sp.groups)
+        ver = (w._version, wg._version if wg is not None else None)
+        hit = self._e.get(key)
+        if hit is not None and hit[0]() is w and hit[1] == ver:
+            return hit[2]
+        out = _pack(sp, w, wg, dtype, mode)
+        self._e[key] = (weakref.ref(w), ver, out)
+        return out
+
+    def mark_stale(self, params):
+        ids = {id(p) for p in params}
+        for k in [k for k in self._e if k[0] in ids]:
+            del self._e[k]
+
+    def prune(self):
+        for k in [k for k, v in self._e.items() if v[0]() is None]:
+            del self._e[k]
+
+
+DPACKS = _DPackCache()
+
+
+def _optimizer_stepped(optimizer, args, kwargs):
+    DPACKS.mark_stale([p for g in optimizer.param_groups for p in g["params"]])
+    DPACKS.prune()
+
+
+_register_optimizer_step_post_hook(_optimizer_stepped)
+
+
 def pack(sp, w, wg, dtype, mode):
+    """Cached packed form (see _DPackCache); weight_v's entry also tracks weight_g."""
+    return DPACKS.get(sp, w, wg, dtype, mode)
+
+
+def _pack(sp, w, wg, dtype, mode):
     """torch weight (or weight_v with weight_g) -> packed forward (mode 0) /
     adjoint (mode 1) form in `dtype`."""
     N, Cg = sp.cout, sp.cin // sp.groups
@@ -99,7 +147,7 @@ def _meta(d, x, out, tag):
     flops = 2.0 * d.B * d.Tvalid * d.G * width * d.K * d.S * d.Cg
     nbytes = es * (d.B * d.Tvs * d.ldx + d.B * d.Tvo * d.ldo + d.G * width * d.K * d.S * d.Cg)
     mf = L.lib().sel_dconv_uses_mfma(ctypes.byref(d), _code(x.dtype))
-    return (f"k_dconv_{'mfma' if mf else 'valu'}{tag}", nbytes, flops)
+    return (f"k_dconv_{('valu', 'mfma', 'short')[mf]}{tag}", nbytes, flops)
 
 
 def wgrad(sp, desc, gout, x, w_or_v, wg, want_w, want_b):
@@ -135,11 +183,13 @@ class ChainFn(torch.autograd.Function):
     """One sub-discriminator: x0 (Bs, T0_alloc, 1) in the compute dtype with T0
     valid rows -> the reference-layout views of every layer's output.
 
-    forward(ctx, x0, T0, specs, slope, wn, kind, B, p, *params): params per
-    layer are (w, bias) or, with weight norm (wn), (weight_v, weight_g, bias)."""
+    forward(ctx, x0, T0, specs, slope, wn, kind, B, p, frozen, *params): params
+    per layer are (w, bias) or, with weight norm (wn), (weight_v, weight_g, bias);
+    frozen = the parameters are constants here (no weight-gradient kernels, no
+    gradient returned for them)."""
 
     @staticmethod
-    def forward(ctx, x0, T0, specs, slope, wn, kind, B, p, *params):
+    def forward(ctx, x0, T0, specs, slope, wn, kind, B, p, frozen, *params):
         L.need_device(x0)
         ctx.set_materialize_grads(False)  # unused feature maps arrive as None
         dtype = x0.dtype
@@ -161,17 +211,17 @@ class ChainFn(torch.autograd.Function):
             geo.append((T_in, T_alloc_in, T_out, T_out_alloc))
             x, T_in, T_alloc_in = y, T_out, T_out_alloc
         ctx.save_for_backward(x0, *bufs, *params)
-        ctx.cfg = (specs, slope, wn, geo, len(bufs), kind, B, p, per)
+        ctx.cfg = (specs, slope, wn, geo, len(bufs), kind, B, p, per, frozen)
         return tuple(views)
 
     @staticmethod
     def backward(ctx, *gviews):
         saved = ctx.saved_tensors
-        specs, slope, wn, geo, nl, kind, B, p, per = ctx.cfg
+        specs, slope, wn, geo, nl, kind, B, p, per, frozen = ctx.cfg
         x0, bufs, params = saved[0], saved[1:1 + nl], saved[1 + nl:]
         dtype = x0.dtype
         Bs = x0.shape[0]
-        npre = 8  # leading non-param inputs of forward
+        npre = 9  # leading non-param inputs of forward
         pgrads = [None] * len(params)
 
         def ext(li):
@@ -190,9 +240,9 @@ class ChainFn(torch.autograd.Function):
             w, wg, b = _layer_params(params, li, wn)
             x_in = bufs[li - 1] if li > 0 else x0
             base = npre + per * li
-            need_w = ctx.needs_input_grad[base]
-            need_g = wn and ctx.needs_input_grad[base + 1]
-            need_b = b is not None and ctx.needs_input_grad[base + per - 1]
+            need_w = ctx.needs_input_grad[base] and not frozen
+            need_g = wn and ctx.needs_input_grad[base + 1] and not frozen
+            need_b = b is not None and ctx.needs_input_grad[base + per - 1] and not frozen
             if need_w or need_g or need_b:
                 d_f = _fwd_desc(sp, Bs, T_in, T_alloc_in, T_out, T_out_alloc, slope)
                 gw, gg, gb = wgrad(sp, d_f, gpre, x_in, w, wg, True, need_b)
@@ -218,7 +268,7 @@ class ChainFn(torch.autograd.Function):
             if li == 0:
                 gx0 = gin
             gpre = gin
-        return (gx0, None, None, None, None, None, None, None, *pgrads)
+        return (gx0, None, None, None, None, None, None, None, None, *pgrads)
 
 
 def _layer_params(params, li, wn):
@@ -306,6 +356,13 @@ def _view_args(t):
     return size, stride, nd
 
 
+def _memory_order(t):
+    """Dim permutation that walks `t` in memory order (largest stride outermost):
+    the kernels iterate the LAST dim fastest, so a (B, C, T) view of a
+    channels-last buffer is read row by row, coalesced."""
+    return sorted(range(t.dim()), key=lambda d: (-t.stride(d), -t.shape[d]))
+
+
 class GanReduceFn(torch.autograd.Function):
     """scale * sum over elements of a (strided view) of |a - b| (kind L1),
     (a - target)^2 (MSE) or the hinge terms; gradient w.r.t. a only (b is the
@@ -316,11 +373,12 @@ class GanReduceFn(torch.autograd.Function):
         L.need_device(a)
         if a.dim() > 4:
             raise ValueError("GAN loss views have at most 4 dims")
-        sa, ta, nd = _view_args(a)
+        perm = _memory_order(a)
+        sa, ta, nd = _view_args(a.permute(perm))
         if b is not None:
             if b.shape != a.shape or b.dtype != a.dtype:
                 raise ValueError(f"feature maps differ: {tuple(a.shape)}/{a.dtype} vs {tuple(b.shape)}/{b.dtype}")
-            sb, tb, _ = _view_args(b)
+            sb, tb, _ = _view_args(b.permute(perm))
         else:
             sb = tb = None
         out = torch.empty((), dtype=torch.float32, device=a.device)
@@ -335,14 +393,15 @@ class GanReduceFn(torch.autograd.Function):
     def backward(ctx, g):
         a, b = ctx.saved_tensors
         kind, target, scale = ctx.cfg
-        sa, ta, nd = _view_args(a)
-        sb, tb = (None, None) if b is None else _view_args(b)[:2]
+        perm = _memory_order(a)
+        sa, ta, nd = _view_args(a.permute(perm))
+        sb, tb = (None, None) if b is None else _view_args(b.permute(perm))[:2]
         # same strides as the view, over a full copy of its base storage, so the
         # discriminator backward can consume it in place (sel.dconvops._as_buffer)
         base = a._base if a._base is not None else a
         gbuf = torch.empty_like(base) if base is not a else torch.empty_like(a)
         ga = torch.as_strided(gbuf, a.shape, a.stride(), a.storage_offset()) if base is not a else gbuf
-        gs = (ctypes.c_int64 * nd)(*ga.stride())
+        gs = (ctypes.c_int64 * nd)(*ga.permute(perm).stride())
         gc = (g.float() * scale).reshape(1).contiguous()
         L.call("sel_gan_grad", kind, _code(a.dtype), L.ptr(a), sa, ta, L.ptr(b), sb, tb, nd, float(target),
                L.ptr(gc), 1.0, L.ptr(ga), gs, 0, L.stream())
