@@ -493,6 +493,340 @@ __global__ __launch_bounds__(256) void k_conv_fwd_bf16(Args a, const __bf16* __r
 }
 
 // ---------------------------------------------------------------------------
+// Warp-specialised bf16 forward for the wide layers at few rows (256 output
+// channels at T = 400 x 64 clips: the RU256 k7 forwards and dgrads, the
+// 640 -> 256 phase-view strided conv).  The tiled kernel above runs those at
+// 2 waves per SIMD with staging (ELU + LDS stores) and MFMAs in separate
+// barrier phases: SQ counters show the matrix pipe busy 28% of the kernel and
+// ~3,700 VALU instructions per wave, as many issue cycles as its MFMAs
+// (profiles/r2_ws_conv.md).  Here one 256 x 128 tile per CU, 12 waves:
+//   waves 0-7  consumers: 4 x 2 grid of 64 x 64 wave tiles; per 16-channel
+//              chunk K taps x 4 MFMAs, the next tap's fragments read while the
+//              current tap's MFMAs run;
+//   waves 8-11 producers: global -> LDS DMA (global_load_lds_dwordx4) of the
+//              input span and the K weight slices three chunks ahead into a
+//              4-slot LDS ring, then the input ELU in place one chunk ahead;
+//   all 12:    the epilogue, through an fp32 LDS tile with row-contiguous 16-B
+//              global accesses.
+// One barrier per chunk.  LDS rows are 32 B (16 channels) with the 16-B slot
+// XOR-swizzled by row bit 3 (conflict-free ds_read_b128 for both MFMA operands);
+// the DMA destination is lane-linear, so the swizzle is applied to the SOURCE
+// address.  Padding rows are DMA'd from a zero buffer.
+// Measured limits (block stamps, tools/ws_probe.py): consumers alone run the
+// main loop at ~75% of the MFMA pipe (2.1 GHz); the producers' DMA into LDS
+// costs the consumers ~900 cycles per chunk and lowers the clock to ~1.87 GHz,
+// the in-place ELU ~3 us per launch; one wave of 256 tiles leaves the prologue
+// and the epilogue (~2 us fwd, ~4 us with aux + res) exposed.
+// ---------------------------------------------------------------------------
+constexpr int WS_BM = 256, WS_BN = 128, WS_CK = 16, WS_NBUF = 4;
+constexpr int WS_RPI = 1024 / (WS_CK * 2);    // LDS rows per 1-KB DMA piece
+constexpr int WS_SPR = WS_CK / 8;             // 16-B slots per LDS row
+constexpr int WS_XROWS = WS_BM + F4_HALOMAX;  // staged input rows per chunk (multiple of WS_RPI)
+constexpr int WS_CMAX = 4096;                 // input channels the zero source covers
+constexpr int WS_EP = WS_BN + 4;              // fp32 epilogue tile pitch (conflict-free 16-B writes)
+
+__device__ __attribute__((aligned(64))) __bf16 g_ws_zero[WS_CMAX];
+
+// XOR pattern of LDS row `row`'s 16-B slots: conflict-free ds_read_b128 of 16
+// consecutive rows per lane group for both row widths (brute-force checked)
+__device__ __forceinline__ int ws_swzbits(int row) { return WS_CK == 16 ? (row >> 3) & 1 : (row >> 2) & 3; }
+// element offset of 16-B slot `slot` of LDS row `row` (WS_CK channels)
+__device__ __forceinline__ int ws_swz(int row, int slot) { return row * WS_CK + ((slot ^ ws_swzbits(row)) << 3); }
+
+inline size_t ws_buf_bytes(int K) { return (size_t(WS_XROWS) + size_t(K) * WS_BN) * WS_CK * 2; }
+inline size_t ws_lds_bytes(int K) {
+  return std::max(WS_NBUF * ws_buf_bytes(K), size_t(WS_BM) * WS_EP * sizeof(float));
+}
+
+// s_waitcnt vmcnt(N) alone (expcnt / lgkmcnt left at their no-wait maxima)
+template <int N>
+__device__ __forceinline__ void ws_wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+// DMA piece of producer wave pw's u-th slot: q = 4u + pw, clamped to the last piece
+template <int TI>
+__device__ __forceinline__ int ws_piece(int u, int pw) {
+  return u * 4 + pw < TI ? u * 4 + pw : TI - 1;
+}
+
+// In-place input ELU of producer wave pw's input pieces (q = 4u + pw < XI) of
+// one ring slot: each lane rewrites exactly the 16 B its own DMA wrote, so this
+// wave's vmcnt wait alone orders it (elementwise, so the swizzle does not
+// matter).  Inline-asm LDS access: hipcc would put vmcnt(0) before a plain LDS
+// read while DMAs are in flight, draining the next chunk's prefetch too.
+template <int PW>
+__device__ __forceinline__ void ws_elu_pieces(unsigned char* lane_base, int pw, int xi) {
+#pragma unroll
+  for (int u = 0; u < PW; ++u) {
+    const int q = u * 4 + pw;
+    if (q >= xi) break;
+    const unsigned addr = unsigned(reinterpret_cast<uintptr_t>(lane_base + q * 1024));
+    bf16x8 val;
+    asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(val) : "v"(addr) : "memory");
+#pragma unroll
+    for (int e = 0; e < 8; ++e) val[e] = __bf16(elu_fast(float(val[e])));
+    asm volatile("ds_write_b128 %0, %1" : : "v"(addr), "v"(val) : "memory");
+  }
+}
+
+template <int KT, typename TO>
+__global__ __launch_bounds__(768) void k_conv_ws_bf16(Args a, const __bf16* __restrict__ in,
+                                                      const __bf16* __restrict__ wp,
+                                                      const float* __restrict__ bias, const TO* __restrict__ aux,
+                                                      const TO* __restrict__ res, TO* __restrict__ out, int ncol,
+                                                      int dbg) {
+  constexpr int BM = WS_BM, BN = WS_BN;
+  constexpr int TM = 2, TN = 2, WTM = 64, WTN = 64;
+  constexpr int XI = WS_XROWS / WS_RPI;  // DMA pieces (1 KB) per chunk: input span
+  constexpr int WI = KT * BN / WS_RPI;   // weight slices
+  constexpr int TI = XI + WI;
+  constexpr int PW = (TI + 3) / 4;   // per producer wave (the last one repeats its final piece)
+  constexpr int BUF = (WS_XROWS + KT * BN) * WS_CK;  // bf16 elements per ring slot
+  extern __shared__ __align__(16) unsigned char smem[];
+  __bf16* const lds = reinterpret_cast<__bf16*>(smem);
+  const int halo = (KT - 1) * a.dil;
+  const int span = BM + halo;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // diagnostic (tune key 13 bit 3): per-block start / end stamps (100 MHz
+  // realtime) and hardware ids into the output buffer instead of results
+  const uint64_t t_start = (dbg & 8) ? __builtin_amdgcn_s_memrealtime() : 0;
+  const uint64_t c_start = (dbg & 8) ? __builtin_amdgcn_s_memtime() : 0;
+  uint64_t t_loop = 0;
+  const int tps = (a.T + BM - 1) / BM;
+  int64_t mt;
+  int nt;
+  xcd_tile(ncol, mt, nt);
+  const int64_t b = mt / tps;
+  const int t0 = int(mt % tps) * BM;
+  const int64_t m0 = b * a.T + t0;
+  const int mrows = a.T - t0 < BM ? a.T - t0 : BM;
+  const int n0 = nt * BN;
+  const int nchunk = a.C / WS_CK;
+
+  if (wave >= 8) {
+    // ---------------- producers ----------------
+    const int pw = wave - 8;
+    // DMA piece q (1 KB) goes to producer wave q % 4 (the input pieces, which
+    // get the ELU pass, spread over all four); a wave short of PW repeats its last
+    const __bf16* src[PW];
+#pragma unroll
+    for (int u = 0; u < PW; ++u) {
+      const int q = ws_piece<TI>(u, pw);
+      if (q < XI) {
+        const int R = q * WS_RPI + lane / WS_SPR, ls = (lane % WS_SPR) ^ ws_swzbits(R);
+        int ti = t0 - a.pad + R;
+        const bool valid = R < span && ((ti >= 0 && ti < a.T) || a.pad_mode == SEL_PAD_REPLICATE);
+        ti = ti < 0 ? 0 : (ti >= a.T ? a.T - 1 : ti);
+        src[u] = valid ? in + (b * a.T + ti) * a.C + 8 * ls : g_ws_zero + 8 * ls;
+      } else {
+        const int R = (q - XI) * WS_RPI + lane / WS_SPR, ls = (lane % WS_SPR) ^ ws_swzbits(R);
+        const int k = R / BN, n = R % BN;
+        src[u] = wp + (int64_t(n0 + n) * KT + k) * a.C + 8 * ls;
+      }
+    }
+    auto issue = [&](int ch) {
+      unsigned char* const base = smem + (ch % WS_NBUF) * (BUF * 2);
+#pragma unroll
+      for (int u = 0; u < PW; ++u) {
+        const int q = ws_piece<TI>(u, pw);
+        if ((dbg & 32) && q < XI) continue;   // diagnostic: no input DMA (tune key 13 bit 5)
+        if ((dbg & 64) && q >= XI) continue;  // diagnostic: no weight DMA (tune key 13 bit 6)
+        const int off = q < XI ? q * 1024 : WS_XROWS * WS_CK * 2 + (q - XI) * 1024;
+        __builtin_amdgcn_global_load_lds((const void*)(src[u] + ch * WS_CK), (lds_ptr_t)(base + off), 16, 0, 0);
+      }
+    };
+      const int xi_used = (span + WS_RPI - 1) / WS_RPI;  // input pieces holding rows < span (the rest stay zero)
+    auto elu_pass = [&](int ch) __attribute__((always_inline)) {
+      ws_elu_pieces<PW>(smem + (ch % WS_NBUF) * (BUF * 2) + lane * 16, pw, xi_used);
+    };
+    if (dbg & 1) {  // diagnostic: consumers alone (tune key 13 bit 0)
+      for (int ch = 0; ch <= nchunk; ++ch) __syncthreads();
+    } else {
+    // prefetch distance D = WS_NBUF - 1 chunks; wait_chunk(n): chunk landed
+    // with n younger chunks still allowed in flight
+    constexpr int D = WS_NBUF - 1;
+    static_assert(D >= 1 && D <= 3, "ring depth");
+    auto wait_chunk = [&](int younger) __attribute__((always_inline)) {
+      if (younger >= 2) ws_wait_vm<(D >= 3 ? 2 * PW : 0)>();
+      else if (younger == 1) ws_wait_vm<(D >= 2 ? PW : 0)>();
+      else ws_wait_vm<0>();
+    };
+    for (int c = 0; c < D && c < nchunk; ++c) issue(c);
+    wait_chunk(std::min(D, nchunk) - 1);
+    if (a.in_elu && !(dbg & 16)) elu_pass(0);  // bit 4: diagnostic without the ELU pass
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    for (int ch = 0; ch < nchunk; ++ch) {
+      if (ch + 1 < nchunk) {
+        // chunk ch+1 landed (later ones may still be in flight), then its ELU
+        wait_chunk(std::min(D - 1, nchunk - 2 - ch));
+        if (a.in_elu && !(dbg & 16)) elu_pass(ch + 1);
+      }
+      if (ch + D < nchunk) issue(ch + D);  // slot (ch+D)%NBUF = (ch-1)%NBUF, released by the last barrier
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+    }
+  } else {
+  // ---------------- consumers ----------------
+  const int wm = wave >> 1, wn = wave & 1;
+  const int hl = lane >> 5;
+  int arow[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) arow[i] = wm * WTM + i * 32 + (lane & 31);
+  int boff[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) boff[j] = WS_XROWS * WS_CK + ws_swz(wn * WTN + j * 32 + (lane & 31), hl);
+
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  __syncthreads();
+  // consumers outrank the producers in the SIMD's issue arbitration (tune key
+  // 13 bit 7 = diagnostic without)
+  if (!(dbg & 128)) __builtin_amdgcn_s_setprio(2);
+  for (int ch = 0; ch < nchunk; ++ch) {
+    if (dbg & 2) {  // diagnostic: producers alone (tune key 13 bit 1)
+      __syncthreads();
+      continue;
+    }
+    const __bf16* const xb = lds + (ch % WS_NBUF) * BUF;
+    bf16x8 fa[2][TM], fb[2][TN];
+    constexpr int NS = KT * (WS_CK / 16);  // (tap, 16-channel half) steps
+    // slot bit 1 <-> element offset bit 4 (row * 32 keeps bits 0-4 clear)
+    auto fetch = [&](int st, int q) {
+      const int k = st / (WS_CK / 16), h = st % (WS_CK / 16);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        fb[q][j] = *reinterpret_cast<const bf16x8*>(xb + ((boff[j] + k * BN * WS_CK) ^ (16 * h)));
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        fa[q][i] = *reinterpret_cast<const bf16x8*>(xb + ws_swz(arow[i] + k * a.dil, 2 * h + hl));
+    };
+    for (int rep = 0; rep < ((dbg & 256) ? 2 : 1); ++rep) {  // bit 8: diagnostic double MFMA work
+    fetch(0, 0);
+#pragma unroll
+    for (int st = 0; st < NS; ++st) {
+      // pin the order: the next step's fragment reads go out before this step's MFMAs
+      if (st + 1 < NS) fetch(st + 1, (st + 1) & 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[st & 1][j], fa[st & 1][i], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    }
+    __syncthreads();
+  }
+
+  __builtin_amdgcn_s_setprio(0);
+  if (dbg & 8) {
+    if (tid == 0) t_loop = __builtin_amdgcn_s_memrealtime();
+  }
+  if (!(dbg & 4)) {
+    // accumulators -> fp32 tile [BM][BN + 4] over the (drained) ring: lane ->
+    // row lane & 31 of its 32-row tile, element r -> column (r & 3) + 8 (r >> 2)
+    // + 4 (lane >> 5), i.e. four 16-B runs per accumulator
+    float* const tile = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int r = wm * WTM + i * 32 + (lane & 31);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          floatx4 v4;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v4[e] = acc[i][j][4 * g + e];
+          *reinterpret_cast<floatx4*>(tile + r * WS_EP + wn * WTN + j * 32 + 8 * g + 4 * hl) = v4;
+        }
+    }
+  }
+  }
+  if (dbg & 4) return;  // diagnostic: no epilogue (tune key 13 bit 2)
+  __syncthreads();
+
+  // epilogue by all 12 waves: 8 consecutive channels per thread, row-contiguous
+  // 16-B global accesses (aux / res fetched for every vector first)
+  struct alignas(16) V8 { TO v[8]; };
+  constexpr int EV = (BM * BN / 8 + 767) / 768;
+  const float* const tile = reinterpret_cast<const float*>(smem);
+  const int nvec = mrows * (BN / 8);
+  V8 av[EV], rv[EV];
+#pragma unroll
+  for (int u = 0; u < EV; ++u) {
+    const int v = tid + u * 768;
+    if (v >= nvec) break;
+    const int64_t o = (m0 + (v >> 4)) * a.N + n0 + (v & 15) * 8;
+    if (aux) av[u] = *reinterpret_cast<const V8*>(aux + o);
+    if (res) rv[u] = *reinterpret_cast<const V8*>(res + o);
+  }
+#pragma unroll
+  for (int u = 0; u < EV; ++u) {
+    const int v = tid + u * 768;
+    if (v >= nvec) break;
+    const int row = v >> 4, c8 = (v & 15) * 8;
+    const int64_t o = (m0 + row) * a.N + n0 + c8;
+    const floatx4 lo = *reinterpret_cast<const floatx4*>(tile + row * WS_EP + c8);
+    const floatx4 hi = *reinterpret_cast<const floatx4*>(tile + row * WS_EP + c8 + 4);
+    float x[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    if (bias && a.bias_period) {
+      if (a.bias_period % 8 == 0) {
+        const float* const bp = bias + (n0 + c8) % a.bias_period;
+        const floatx4 b0 = *reinterpret_cast<const floatx4*>(bp), b1 = *reinterpret_cast<const floatx4*>(bp + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[e] += b0[e], x[e + 4] += b1[e];
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x[e] += bias[(n0 + c8 + e) % a.bias_period];
+      }
+    }
+    if (aux) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] *= elu_grad_fast(to_f(av[u].v[e]));
+    }
+    if (res) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] += to_f(rv[u].v[e]);
+    }
+    V8 ov;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) ov.v[e] = from_f<TO>(x[e]);
+    *reinterpret_cast<V8*>(out + o) = ov;
+  }
+  if ((dbg & 8) && bias && !a.bias_period) {
+    // diagnostic (tune key 13 bit 3): per-block stamps into a scratch "bias"
+    // buffer: realtime (100 MHz) start / main-loop end / block end, shader
+    // clock start / end, HW_ID, XCC_ID
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      uint64_t* st = reinterpret_cast<uint64_t*>(const_cast<float*>(bias)) +
+                     8 * (int64_t(blockIdx.y) * gridDim.x + blockIdx.x);
+      st[0] = t_start;
+      st[1] = t_loop;
+      st[2] = __builtin_amdgcn_s_memrealtime();
+      st[3] = c_start;
+      st[4] = __builtin_amdgcn_s_memtime();
+      st[5] = uint64_t(__builtin_amdgcn_s_getreg(4 | (31 << 11)));   // HW_ID
+      st[6] = uint64_t(__builtin_amdgcn_s_getreg(20 | (31 << 11)));  // XCC_ID
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Weight-stationary streaming conv for the thin layers (32/64/96 input and
 // 32/64 output channels: the residual-unit convs at T = 24000 / 8000, their
 // dgrads, the first strided layer and the last transposed layer's dgrad).
@@ -2018,15 +2352,41 @@ int launch_fwd4(const Args& a, const void* in, const void* wp, const float* bias
   return SEL_OK;
 }
 
+template <int KT, typename TO>
+int launch_ws(const Args& a, const void* in, const void* wp, const float* bias, const void* aux, const void* res,
+              void* out, hipStream_t s) {
+  const size_t lds = ws_lds_bytes(KT);
+  const int64_t tiles = (a.rows / a.T) * ((a.T + WS_BM - 1) / WS_BM);
+  const int ncol = a.N / WS_BN;
+  if (tiles == 0) return SEL_OK;
+  const bool xcd = ncol > 1 && tune(8) == 0 && tiles * ncol < (int64_t(1) << 31);
+  const dim3 grid = xcd ? dim3(unsigned(tiles * ncol)) : dim3(unsigned(tiles), unsigned(ncol));
+  auto kern = k_conv_ws_bf16<KT, TO>;
+  SEL_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
+  hipLaunchKernelGGL(kern, grid, dim3(768), lds, s, a, static_cast<const __bf16*>(in),
+                     static_cast<const __bf16*>(wp), bias, static_cast<const TO*>(aux), static_cast<const TO*>(res),
+                     static_cast<TO*>(out), xcd ? ncol : 0, tune(13));
+  SEL_LAUNCH_CHECK();
+  return SEL_OK;
+}
+
+// the warp-specialised kernel's legal shapes: K in {3, 7}, 128-multiple N,
+// 16-multiple C within the zero source, halo within the staged span, the
+// 4-slot ring within 160 KB
+bool ws_ok(const Args& a) {
+  return (a.K == 3 || a.K == 7) && a.N % WS_BN == 0 && a.C % WS_CK == 0 && a.C <= WS_CMAX &&
+         (a.K - 1) * a.dil <= F4_HALOMAX && ws_lds_bytes(a.K) <= 160 * 1024;
+}
+
 // Variant the dispatcher picks for a bf16 forward launch (see fwd4_variant);
 // -1 when the generic (non-pipelined) kernel is used.
 int fwd4_choice(const Args& a) {
   const int v = tune(0);
   if (!((a.C % CK) == 0 && (a.K - 1) * a.dil <= F4_HALOMAX && a.K <= 8 && (v == 0 || v > 20))) return -1;
-  if (v > 20) return v;
+  if (v > 20 && (v != 27 || ws_ok(a))) return v;
   if (a.N <= 32 || (a.N % 64) != 0 || a.rows < 8192) return 22;
   if (a.N >= 256 && a.K == 1) return 26;
-  if (a.N >= 256 && a.rows >= 16384) return 24;
+  if (a.N >= 256 && a.rows >= 16384) return ws_ok(a) ? 27 : 24;
   if (a.N <= 64 || a.rows < 65536) return 23;
   if (a.N == 128 && a.K > 1 && a.pad == 0 && !a.in_elu) return 22;
   return 24;
@@ -2042,6 +2402,10 @@ int fwd4_variant(int v, const Args& a, const void* in, const void* wp, const flo
     case 24: return launch_fwd4<256, 64, 4, KMAX, TO>(a, in, wp, bias, aux, res, out, s);
     case 25: return launch_fwd4<128, 128, 2, KMAX, TO>(a, in, wp, bias, aux, res, out, s);
     case 26: return launch_fwd4<64, 128, 1, KMAX, TO>(a, in, wp, bias, aux, res, out, s);
+    case 27:
+      if (!ws_ok(a)) break;
+      return a.K == 7 ? launch_ws<7, TO>(a, in, wp, bias, aux, res, out, s)
+                      : launch_ws<3, TO>(a, in, wp, bias, aux, res, out, s);
     default: break;
   }
   // heuristic from tools/conv_bench.py on the C3 layer shapes (profiles/r1_conv_bench.md):
@@ -2051,9 +2415,16 @@ int fwd4_variant(int v, const Args& a, const void* in, const void* wp, const flo
     return launch_fwd4<128, 32, 4, KMAX, TO>(a, in, wp, bias, aux, res, out, s);
   // 256-wide 1x1 (RU256 1x1 fwd 27.5 -> 20.9 us, dgrad 22.5 -> 19.2): 64x128 tiles
   if (a.N >= 256 && a.K == 1) return launch_fwd4<64, 128, 1, KMAX, TO>(a, in, wp, bias, aux, res, out, s);
-  // 256-wide layers at 400 samples x 64 clips (25.6k rows): 256x64 tiles
+  // 256-wide layers at 400 samples x 64 clips (25.6k rows): the warp-specialised
+  // 256x128 kernel where legal (rocprofv3 kernel trace, profiles/r2_ws_conv.md:
+  // RU256 k7 fwd+dgrad 43.5 -> 38.4 us, down2 46.6 -> 41.8), else 256x64 tiles
   // (RU256 k7 fwd 50.7 -> 36.2 us, dgrad 54.2 -> 43.0, down2 51.2 -> 43.1)
-  if (a.N >= 256 && a.rows >= 16384) return launch_fwd4<256, 64, 4, KMAX, TO>(a, in, wp, bias, aux, res, out, s);
+  if (a.N >= 256 && a.rows >= 16384) {
+    if (ws_ok(a) && (a.K == 7 || a.K == 3))
+      return a.K == 7 ? launch_ws<7, TO>(a, in, wp, bias, aux, res, out, s)
+                      : launch_ws<3, TO>(a, in, wp, bias, aux, res, out, s);
+    return launch_fwd4<256, 64, 4, KMAX, TO>(a, in, wp, bias, aux, res, out, s);
+  }
   if (a.N <= 64 || a.rows < 65536) return launch_fwd4<128, 64, 2, KMAX, TO>(a, in, wp, bias, aux, res, out, s);
   // 128-wide k7 dgrad at 2000 samples (pad 0, no input ELU): 128x32 tiles (76.5 -> 62.6 us)
   if (a.N == 128 && a.K > 1 && a.pad == 0 && !a.in_elu)
@@ -2336,6 +2707,7 @@ int sel_conv_fwd_kernel_id(const sel_conv_desc* d, int in_dtype, int out_dtype) 
     return 1000000000 + ((thin_rows(a) / 32 * 1000 + a.C) * 1000 + a.N) * 10 + a.K;
   const int v = fwd4_choice(a);
   if (v < 0) return -1;
+  if (v == 27) return 900000000 + a.K;  // warp-specialised kernel: 9e8 + K
   const int kmax = a.K == 1 ? 1 : (a.K <= 3 ? 3 : 8);
   static const int bm[] = {256, 128, 128, 256, 128, 64}, bn[] = {32, 32, 64, 64, 128, 128}, wm[] = {4, 4, 2, 4, 2, 1};
   const int i = v - 21;

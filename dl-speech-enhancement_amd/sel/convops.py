@@ -274,10 +274,12 @@ def fwd_kernel_name(desc, in_dtype, out_dtype):
         kid -= 10 ** 9
         k, n, c, r = kid % 10, (kid // 10) % 1000, (kid // 10000) % 1000, 32 * (kid // 10000000)
         return f"k_conv_thin_bf16<{c}, {n}, {k}, {r}>"
+    to = "bf16" if out_dtype == torch.bfloat16 else "float"
+    if kid >= 9 * 10 ** 8:  # warp-specialised double-buffered kernel: 9e8 + K
+        return f"k_conv_ws_bf16<{kid - 9 * 10 ** 8}, {to}>"
     kmax, kid = kid % 10, kid // 10
     wm, kid = kid % 10, kid // 10
     bm, bn = kid // 1000, kid % 1000
-    to = "bf16" if out_dtype == torch.bfloat16 else "float"
     return f"k_conv_fwd_bf16<{bm}, {bn}, {wm}, {kmax}, {to}>"
 
 

@@ -1,7 +1,7 @@
 """Parity of the C3 (BASELINE configs[2]) bf16 path at the bench's own size.
 
-1. Every bf16 tile variant of the MFMA conv primitive (tune key 0 = 21..26,
-   conv.hip fwd4_variant) on the real C3 layer shapes in primitive form,
+1. Every bf16 tile variant of the MFMA conv primitive (tune key 0 = 21..27,
+   conv.hip fwd4_variant; 27 = the warp-specialised k_conv_ws_bf16) on the real C3 layer shapes in primitive form,
    forward and dgrad (adjoint) forms, against an fp64 reference computed from
    the SAME bf16 operands.  Both accumulate exact bf16 products (fp32 vs fp64
    sums) and the kernel rounds once to bf16, so the bound is bf16 output
@@ -105,11 +105,11 @@ def test_fwd4_tile_variants_on_c3_shapes(gpu, shape, form):
     p4 = lib.sel_tune(4, 1)  # the weight-stationary thin kernel would pre-empt the tiled one
     try:
         default_name = CO.fwd_kernel_name(d, torch.bfloat16, torch.bfloat16)
-        assert default_name.startswith("k_conv_fwd_bf16"), default_name
+        assert default_name.startswith(("k_conv_fwd_bf16", "k_conv_ws_bf16")), default_name
         default = CO.prim(d, x, wp, bias=b, aux=a_, res=r_).clone()
         _check(default, ref, (form, "default", default_name))
         matched = False
-        for v in range(21, 27):
+        for v in range(21, 28):
             p0 = lib.sel_tune(0, v)
             try:
                 name = CO.fwd_kernel_name(d, torch.bfloat16, torch.bfloat16)
