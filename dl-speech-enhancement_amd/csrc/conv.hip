@@ -42,7 +42,29 @@ __device__ __forceinline__ float elu_grad(float v) { return v > 0.f ? 1.f : expf
 // bf16 path: the result is rounded to bf16 (8-bit mantissa), so the hardware
 // exp (v_exp_f32, a few ulp of fp32) replaces the libm expm1/exp range reduction.
 __device__ __forceinline__ float elu_fast(float v) { return v > 0.f ? v : __expf(v) - 1.f; }
-__device__ __forceinline__ float elu_grad_fast(float v) { return v > 0.f ? 1.f : __expf(v); }
+// v > 0 ? 1 : exp(v) as one min: exp(v) >= 1 exactly when v >= 0 (monotone
+// hardware exp, exp(0) = 1), so the result is bit-identical to the select
+__device__ __forceinline__ float elu_grad_fast(float v) { return fminf(__expf(v), 1.f); }
+
+// elu_fast over 8 bf16 (round-to-nearest back to bf16), with the log2(e) scale
+// and the -1 as packed fp32 ops: per element the same arithmetic as elu_fast
+// (exp(v) = v_exp_f32(v * log2 e), as __expf lowers), so bit-identical
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint4 elu8(uint4 w) {
+  const unsigned in[4] = {w.x, w.y, w.z, w.w};
+  unsigned o[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const f32x2 f = {__uint_as_float(in[q] << 16), __uint_as_float(in[q] & 0xffff0000u)};
+    const f32x2 t = f * 1.44269502f;
+    f32x2 e = {__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};
+    e = e - 1.f;
+    const f32x2 r = {f.x > 0.f ? f.x : e.x, f.y > 0.f ? f.y : e.y};
+    o[q] = __builtin_bit_cast(unsigned, __builtin_convertvector(r, bf16x2));  // v_cvt_pk_bf16_f32
+  }
+  return make_uint4(o[0], o[1], o[2], o[3]);
+}
 
 struct Args {
   int64_t rows;
@@ -377,9 +399,7 @@ __global__ __launch_bounds__(256) void k_conv_fwd_bf16(Args a, const __bf16* __r
       // on the load there (vmcnt(0)) and serialise the register prefetch
       uint4 val = xok[u] ? xr[u] : make_uint4(0, 0, 0, 0);
       if (a.in_elu) {
-        __bf16* t = reinterpret_cast<__bf16*>(&val);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) t[e] = __bf16(elu_fast(float(t[e])));
+        val = elu8(val);
       }
       *reinterpret_cast<uint4*>(xs + (v >> 2) * P + (v & 3) * 8) = val;
     }
@@ -567,8 +587,7 @@ __device__ __forceinline__ void ws_elu_pieces(unsigned char* lane_base, int pw, 
     const unsigned addr = unsigned(reinterpret_cast<uintptr_t>(lane_base + q * 1024));
     bf16x8 val;
     asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(val) : "v"(addr) : "memory");
-#pragma unroll
-    for (int e = 0; e < 8; ++e) val[e] = __bf16(elu_fast(float(val[e])));
+    val = __builtin_bit_cast(bf16x8, elu8(__builtin_bit_cast(uint4, val)));
     asm volatile("ds_write_b128 %0, %1" : : "v"(addr), "v"(val) : "memory");
   }
 }
@@ -935,9 +954,7 @@ __global__ __launch_bounds__(256) void k_conv_thin_bf16(Args a, const __bf16* __
       if (r >= span) continue;
       uint4 val = xok[u] ? xr[u] : make_uint4(0, 0, 0, 0);
       if (a.in_elu) {
-        __bf16* t = reinterpret_cast<__bf16*>(&val);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) t[e] = __bf16(elu_fast(float(t[e])));
+        val = elu8(val);
       }
       *reinterpret_cast<uint4*>(xs + ((c >> 5) * G::SPAN + r) * P + (c & 31)) = val;
     }
@@ -1036,17 +1053,19 @@ __global__ __launch_bounds__(256) void k_conv_thin_bf16(Args a, const __bf16* __
         for (int e = 0; e < 8; ++e) v[e] += bias[(n + e) % a.bias_period];
       }
       const int64_t o = obase + int64_t(r) * N + n;
+      // explicit roundings (no FMA contraction): every instance, and the fused
+      // residual-unit kernels, produce the same bits
       if (aux) {
         uint4 raw = apv ? *apv : *reinterpret_cast<const uint4*>(aux + o);
         const __bf16* av = reinterpret_cast<const __bf16*>(&raw);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] *= elu_grad_fast(float(av[e]));
+        for (int e = 0; e < 8; ++e) v[e] = __fmul_rn(v[e], elu_grad_fast(float(av[e])));
       }
       if (res) {
         uint4 raw = rpv ? *rpv : *reinterpret_cast<const uint4*>(res + o);
         const __bf16* rv = reinterpret_cast<const __bf16*>(&raw);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] += float(rv[e]);
+        for (int e = 0; e < 8; ++e) v[e] = __fadd_rn(v[e], float(rv[e]));
       }
       uint4 ov;
       __bf16* op = reinterpret_cast<__bf16*>(&ov);
@@ -1144,9 +1163,7 @@ __global__ __launch_bounds__(256) void k_ru_thin_bf16(Args a, const __bf16* __re
       const int r = v / CV, c = (v % CV) * 8;
       if (r >= span) continue;
       uint4 val = xok[u] ? xr[u] : make_uint4(0, 0, 0, 0);
-      __bf16* t = reinterpret_cast<__bf16*>(&val);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) t[e] = __bf16(elu_fast(float(t[e])));
+      val = elu8(val);
       *reinterpret_cast<uint4*>(xs + ((c >> 5) * G::SPAN + r) * P + (c & 31)) = val;
     }
   };
@@ -1255,6 +1272,332 @@ __global__ __launch_bounds__(256) void k_ru_thin_bf16(Args a, const __bf16* __re
 #pragma unroll
       for (int e = 0; e < 8; ++e) op[e] = __bf16(v[e] + float(rv[e]));
       *reinterpret_cast<uint4*>(out + o) = ov;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Residual unit at 32 channels, forward and backward in ONE launch each, with
+// the 1x1 conv done in registers (residual_unit.py:43-46; conv1 = causal k7
+// dilated 32 -> 32, conv2 = 1x1 32 -> 32, both with bias in AudioDec).
+//
+// A wave owns 32-row sub-tiles of a sample-aligned R-row tile and all 32
+// channels of them.  conv1's accumulators (lane -> row, element e -> channel
+// (e & 3) + 8 (e >> 2) + 4 (lane >> 5)) are packed to bf16 and re-laid out with
+// two v_permlane32_swap per channel-group pair into 8-consecutive-channel
+// vectors: exactly the B operand of the next 32x32x16 MFMA AND one 16-B
+// store.  So h goes to HBM (saved for the backward) and ELU(h) straight into
+// conv2's MFMAs without an LDS round trip or a block barrier; the only shared
+// stage is the input tile with its causal halo.  HBM per row: forward reads x
+// and writes h, out (3 tensors instead of 5 over two launches); backward
+// reads g (grad of out), h, x and writes gx (+ gh for the weight gradient):
+// 4-5 tensors instead of 7 over two launches.
+//
+// Same MFMA order, same bf16 rounding points and the same epilogue arithmetic
+// as the two-launch primitive path, so the results are bit-identical to it
+// (test_gpu_conv.py::test_resunit32_*).
+// ---------------------------------------------------------------------------
+constexpr int RU_C = 32, RU_K = 7;
+
+// acc (one 32x32 MFMA result) -> bf16, re-laid out: frag[kc] = channels
+// 16 kc + 8 (lane >> 5) .. +8 of this lane's row (T21 of the HIP guide)
+__device__ __forceinline__ void ru_acc_to_frags(const float (&v)[16], bf16x8 (&frag)[2]) {
+  unsigned pk[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q)
+    pk[q] = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2{v[2 * q], v[2 * q + 1]}), bf16x2));
+  // group g = elements 4g..4g+3 = pk[2g], pk[2g+1]; swap pairs (0,1) and (2,3)
+#pragma unroll
+  for (int pr = 0; pr < 2; ++pr) {
+    unsigned a0 = pk[4 * pr], a1 = pk[4 * pr + 1], b0 = pk[4 * pr + 2], b1 = pk[4 * pr + 3];
+    const auto r0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
+    const auto r1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 w = {r0[0], r1[0], r0[1], r1[1]};
+    frag[pr] = __builtin_bit_cast(bf16x8, w);
+  }
+}
+
+template <int R>
+struct Ru32 {
+  static constexpr int P = F4_P;
+  static constexpr int SPAN = R + F4_HALOMAX;   // staged rows (tile + max halo)
+  static constexpr int XV = (SPAN * 4 + 255) / 256;
+  static constexpr int TM = R / 128;            // 32-row sub-tiles per wave
+  static constexpr size_t LDS_FWD = size_t(SPAN + R) * P * 2;  // ELU(x) span + raw tile rows
+  static constexpr size_t LDS_BWD = 2 * size_t(SPAN) * P * 2;  // g tile + gh tile
+  static_assert(R % 128 == 0, "ru32 tile rows");
+};
+
+// stage `span` rows of a 32-channel tensor starting at sample row t0 + off
+// (rows outside [0, T) -> zero) into registers / LDS (optionally ELU'd)
+template <int R>
+struct Ru32Stage {
+  uint4 r[Ru32<R>::XV];
+  bool ok[Ru32<R>::XV];
+  __device__ __forceinline__ void load(const Args& a, const __bf16* __restrict__ src, int64_t b, int t0, int off,
+                                       int span) {
+#pragma unroll
+    for (int u = 0; u < Ru32<R>::XV; ++u) {
+      const int v = threadIdx.x + u * 256;
+      const int row = v >> 2, c = (v & 3) * 8;
+      int ti = t0 + off + row;
+      ok[u] = row < span && ti >= 0 && ti < a.T;
+      ti = ti < 0 ? 0 : (ti >= a.T ? a.T - 1 : ti);
+      if ((u * 256) / 4 < span) r[u] = *reinterpret_cast<const uint4*>(src + (b * a.T + ti) * RU_C + c);
+    }
+  }
+  // raw != nullptr: rows [raw_off, raw_off + R) are also stored un-ELU'd into raw
+  __device__ __forceinline__ void store(__bf16* xs, int span, bool elu, __bf16* raw = nullptr, int raw_off = 0) {
+#pragma unroll
+    for (int u = 0; u < Ru32<R>::XV; ++u) {
+      const int v = threadIdx.x + u * 256;
+      const int row = v >> 2, c = (v & 3) * 8;
+      if (row >= span) continue;
+      uint4 val = ok[u] ? r[u] : make_uint4(0, 0, 0, 0);
+      if (raw && row >= raw_off && row < raw_off + R) *reinterpret_cast<uint4*>(raw + (row - raw_off) * F4_P + c) = val;
+      if (elu) {
+        val = elu8(val);
+      }
+      *reinterpret_cast<uint4*>(xs + row * F4_P + c) = val;
+    }
+  }
+};
+
+// XCD-contiguous tile range of this block (as k_conv_thin_bf16)
+__device__ __forceinline__ bool ru_tiles(int64_t ntiles, int tiles_per_block, int64_t& t_begin, int64_t& t_end) {
+  const int64_t vb = int64_t(blockIdx.x % 8) * (gridDim.x / 8) + blockIdx.x / 8;
+  t_begin = vb * tiles_per_block;
+  t_end = t_begin + tiles_per_block < ntiles ? t_begin + tiles_per_block : ntiles;
+  return t_begin < t_end;
+}
+
+// A fragments of a packed [32][K][32] weight (row n = lane & 31, channels 16 g + 8 (lane >> 5))
+template <int K>
+__device__ __forceinline__ void ru_wfrags(const __bf16* __restrict__ wp, bf16x8 (&wf)[K][2]) {
+  const int lane = threadIdx.x & 63;
+  const __bf16* wrow = wp + int64_t(lane & 31) * K * RU_C + 8 * (lane >> 5);
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+#pragma unroll
+    for (int g = 0; g < 2; ++g) wf[k][g] = *reinterpret_cast<const bf16x8*>(wrow + k * RU_C + 16 * g);
+}
+
+template <int R>
+__global__ __launch_bounds__(256) void k_ru32_fwd(Args a, const __bf16* __restrict__ x,
+                                                  const __bf16* __restrict__ w1p, const float* __restrict__ b1,
+                                                  const __bf16* __restrict__ w2p, const float* __restrict__ b2,
+                                                  __bf16* __restrict__ hout, __bf16* __restrict__ out,
+                                                  int tiles_per_block, int dbg) {
+  using G = Ru32<R>;
+  constexpr int P = G::P;
+  extern __shared__ __align__(16) unsigned char smem[];
+  __bf16* const xs = reinterpret_cast<__bf16*>(smem);  // [SPAN][P]: ELU(x) rows t0 - pad ..
+  __bf16* const xr = xs + G::SPAN * P;                 // [R][P]: raw x rows t0 .. (the residual)
+  const int lane = threadIdx.x & 63, hl = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int span = R + a.pad;
+  const int tps = (a.T + R - 1) / R;
+  int64_t tile0, tile_end;
+  if (!ru_tiles((a.rows / a.T) * tps, tiles_per_block, tile0, tile_end)) return;
+
+  bf16x8 wf[RU_K][2], w2f[1][2];
+  ru_wfrags<RU_K>(w1p, wf);
+  ru_wfrags<1>(w2p, w2f);
+
+  Ru32Stage<R> st;
+  st.load(a, x, tile0 / tps, int(tile0 % tps) * R, -a.pad, span);
+  for (int64_t tile = tile0; tile < tile_end; ++tile) {
+    const int64_t b = tile / tps;
+    const int t0 = int(tile % tps) * R;
+    const int mrows = a.T - t0 < R ? a.T - t0 : R;
+    __syncthreads();  // every wave is done with the previous tile's rows
+    st.store(xs, span, true, xr, a.pad);
+    __syncthreads();
+    if (tile + 1 < tile_end) st.load(a, x, (tile + 1) / tps, int((tile + 1) % tps) * R, -a.pad, span);
+#pragma unroll
+    for (int i = 0; i < G::TM; ++i) {
+      const int lr = wave * (R / 4) + i * 32 + (lane & 31);  // this lane's row in the tile
+      if (__builtin_amdgcn_readfirstlane(wave * (R / 4) + i * 32) >= mrows) break;  // wave-uniform
+      const bool valid = lr < mrows;
+      const int64_t orow = (b * a.T + t0 + lr) * RU_C;
+      floatx16 acc;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+      const __bf16* xw = xs + lr * P + 8 * hl;
+#pragma unroll
+      for (int k = 0; k < RU_K; ++k)
+#pragma unroll
+        for (int g = 0; g < 2; ++g)
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[k][g], *reinterpret_cast<const bf16x8*>(xw + k * a.dil * P + 16 * g),
+                                                        acc, 0, 0, 0);
+      // h = conv1 + b1 -> bf16 -> HBM, ELU(h) -> conv2
+      // bias in accumulator order: element group q = channels 8 q + 4 hl .. +4
+      float v[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const floatx4 bq = b1 ? *reinterpret_cast<const floatx4*>(b1 + 8 * q + 4 * hl) : floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[4 * q + e] = acc[4 * q + e] + bq[e];
+      }
+      bf16x8 hf[2];
+      ru_acc_to_frags(v, hf);
+      if (valid && !(dbg & 1)) {  // tune key 15 bit 0: diagnostic without the h store
+        *reinterpret_cast<bf16x8*>(hout + orow + 8 * hl) = hf[0];
+        *reinterpret_cast<bf16x8*>(hout + orow + 16 + 8 * hl) = hf[1];
+      }
+      floatx16 acc2;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc2[e] = 0.f;
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        const bf16x8 ef = __builtin_bit_cast(bf16x8, elu8(__builtin_bit_cast(uint4, hf[g])));
+        acc2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w2f[0][g], ef, acc2, 0, 0, 0);
+      }
+      // out = conv2 + b2 + x (the residual in accumulator order: 4 runs of 4 channels)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint2 xres = *reinterpret_cast<const uint2*>(xr + lr * P + 8 * q + 4 * hl);
+        const __bf16* rv = reinterpret_cast<const __bf16*>(&xres);
+        const floatx4 bq = b2 ? *reinterpret_cast<const floatx4*>(b2 + 8 * q + 4 * hl) : floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[4 * q + e] = acc2[4 * q + e] + bq[e] + float(rv[e]);
+      }
+      bf16x8 of[2];
+      ru_acc_to_frags(v, of);
+      if (valid && !(dbg & 2)) {  // bit 1: diagnostic without the out store
+        *reinterpret_cast<bf16x8*>(out + orow + 8 * hl) = of[0];
+        *reinterpret_cast<bf16x8*>(out + orow + 16 + 8 * hl) = of[1];
+      }
+    }
+  }
+}
+
+// Backward: gh = (W2^T g) * ELU'(h) over the tile + its anti-causal halo (the
+// adjoint of the causal conv reads rows t .. t + 6 dil), in registers -> LDS
+// (and HBM when the weight gradient needs it); gx = conv1^T(gh) * ELU'(x) + g.
+// wd1 / wd2 are the dgrad-packed weights of the primitive path.
+template <int R>
+__global__ __launch_bounds__(256) void k_ru32_bwd(Args a, const __bf16* __restrict__ g,
+                                                  const __bf16* __restrict__ h, const __bf16* __restrict__ x,
+                                                  const __bf16* __restrict__ wd1, const __bf16* __restrict__ wd2,
+                                                  __bf16* __restrict__ ghout, __bf16* __restrict__ gx,
+                                                  int tiles_per_block) {
+  using G = Ru32<R>;
+  constexpr int P = G::P;
+  extern __shared__ __align__(16) unsigned char smem[];
+  __bf16* const gs = reinterpret_cast<__bf16*>(smem);  // [SPAN][P]: g rows t0 ..
+  __bf16* const ghs = gs + G::SPAN * P;                // [SPAN][P]: gh rows t0 ..
+  const int lane = threadIdx.x & 63, hl = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int halo = (RU_K - 1) * a.dil;
+  const int span = R + halo;
+  const int nsub = (span + 31) / 32;  // gh sub-tiles (tile + halo)
+  const int tps = (a.T + R - 1) / R;
+  int64_t tile0, tile_end;
+  if (!ru_tiles((a.rows / a.T) * tps, tiles_per_block, tile0, tile_end)) return;
+
+  bf16x8 wf[RU_K][2], w2f[1][2];
+  ru_wfrags<RU_K>(wd1, wf);
+  ru_wfrags<1>(wd2, w2f);
+
+  Ru32Stage<R> st;
+  st.load(a, g, tile0 / tps, int(tile0 % tps) * R, 0, span);
+  for (int64_t tile = tile0; tile < tile_end; ++tile) {
+    const int64_t b = tile / tps;
+    const int t0 = int(tile % tps) * R;
+    const int mrows = a.T - t0 < R ? a.T - t0 : R;
+    __syncthreads();  // every wave is done with the previous tile's g / gh rows
+    st.store(gs, span, false);
+    __syncthreads();
+    if (tile + 1 < tile_end) st.load(a, g, (tile + 1) / tps, int((tile + 1) % tps) * R, 0, span);
+    // every global operand of this tile's MFMA phases is requested up front (L2-hot:
+    // h and x rows of the tile): ELU'(h) for this wave's gh sub-tiles, ELU'(x) for its gx sub-tiles
+    constexpr int NSUB_W = (G::SPAN / 32 + 3) / 4;  // gh sub-tiles per wave (max)
+    uint2 hpre[NSUB_W][4], xpre[G::TM][4];
+#pragma unroll
+    for (int j = 0; j < NSUB_W; ++j) {
+      const int ti = t0 + (wave + 4 * j) * 32 + (lane & 31);
+      const bool in = wave + 4 * j < nsub && ti < a.T;
+      const int64_t orow = (b * a.T + (in ? ti : 0)) * RU_C;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) hpre[j][q] = in ? *reinterpret_cast<const uint2*>(h + orow + 8 * q + 4 * hl) : make_uint2(0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < G::TM; ++i) {
+      const int lr = wave * (R / 4) + i * 32 + (lane & 31);
+      const bool in = lr < mrows;
+      const int64_t orow = (b * a.T + t0 + (in ? lr : 0)) * RU_C;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) xpre[i][q] = in ? *reinterpret_cast<const uint2*>(x + orow + 8 * q + 4 * hl) : make_uint2(0, 0);
+    }
+    // gh for rows t0 .. t0 + span (rows >= T: g staged as zero -> gh = 0)
+#pragma unroll
+    for (int j = 0; j < NSUB_W; ++j) {
+      const int sb = wave + 4 * j;
+      if (sb >= nsub) break;
+      const int lr = sb * 32 + (lane & 31);
+      floatx16 acc;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+      const __bf16* gw = gs + lr * P + 8 * hl;
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w2f[0][c], *reinterpret_cast<const bf16x8*>(gw + 16 * c), acc, 0, 0, 0);
+      const int ti = t0 + lr;
+      const bool inside = ti < a.T;
+      const int64_t orow = (b * a.T + (inside ? ti : 0)) * RU_C;
+      float v[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const __bf16* hv = reinterpret_cast<const __bf16*>(&hpre[j][q]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[4 * q + e] = acc[4 * q + e] * elu_grad_fast(float(hv[e]));
+      }
+      bf16x8 ghf[2];
+      ru_acc_to_frags(v, ghf);
+      if (lr < span) {
+        *reinterpret_cast<bf16x8*>(ghs + lr * P + 8 * hl) = ghf[0];
+        *reinterpret_cast<bf16x8*>(ghs + lr * P + 16 + 8 * hl) = ghf[1];
+      }
+      if (ghout && lr < mrows) {
+        *reinterpret_cast<bf16x8*>(ghout + orow + 8 * hl) = ghf[0];
+        *reinterpret_cast<bf16x8*>(ghout + orow + 16 + 8 * hl) = ghf[1];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < G::TM; ++i) {
+      const int lr = wave * (R / 4) + i * 32 + (lane & 31);
+      if (__builtin_amdgcn_readfirstlane(wave * (R / 4) + i * 32) >= mrows) break;
+      floatx16 acc;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+      const __bf16* hw = ghs + lr * P + 8 * hl;
+#pragma unroll
+      for (int k = 0; k < RU_K; ++k)
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[k][c], *reinterpret_cast<const bf16x8*>(hw + k * a.dil * P + 16 * c),
+                                                        acc, 0, 0, 0);
+      const bool valid = lr < mrows;
+      const int64_t orow = (b * a.T + t0 + (valid ? lr : 0)) * RU_C;
+      float v[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint2 graw = *reinterpret_cast<const uint2*>(gs + lr * P + 8 * q + 4 * hl);
+        const __bf16* xv = reinterpret_cast<const __bf16*>(&xpre[i][q]);
+        const __bf16* gv = reinterpret_cast<const __bf16*>(&graw);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          v[4 * q + e] = __fadd_rn(__fmul_rn(acc[4 * q + e], elu_grad_fast(float(xv[e]))), float(gv[e]));
+      }
+      bf16x8 of[2];
+      ru_acc_to_frags(v, of);
+      if (valid) {
+        *reinterpret_cast<bf16x8*>(gx + orow + 8 * hl) = of[0];
+        *reinterpret_cast<bf16x8*>(gx + orow + 16 + 8 * hl) = of[1];
+      }
     }
   }
 }
@@ -1724,9 +2067,7 @@ __global__ __launch_bounds__(256) void k_wgrad2_bf16(Args a, const __bf16* __res
       if ((v >> 2) >= W2_BM + W2_HALO) continue;
       uint4 val = xr[u];
       if (a.in_elu) {
-        __bf16* t = reinterpret_cast<__bf16*>(&val);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) t[e] = __bf16(elu_fast(float(t[e])));
+        val = elu8(val);
       }
       *reinterpret_cast<uint4*>(x + (v >> 2) * 32 + (v & 3) * 8) = val;
     }
@@ -1899,9 +2240,7 @@ __global__ __launch_bounds__(256) void k_wgrad3_bf16(Args a, const __bf16* __res
       const int r = v / (CB / 8), c8 = v % (CB / 8);
       uint4 val = xok[u] ? xr[u] : make_uint4(0, 0, 0, 0);
       if (a.in_elu) {
-        __bf16* t = reinterpret_cast<__bf16*>(&val);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) t[e] = __bf16(elu_fast(float(t[e])));
+        val = elu8(val);
       }
       *reinterpret_cast<uint4*>(x + (c8 >> 2) * (XROWS * 32) + r * 32 + (c8 & 3) * 8) = val;
     }
@@ -2540,6 +2879,52 @@ int launch_ru_thin(const Args& a, const void* in, const void* w1p, const float* 
   return SEL_OK;
 }
 
+// fused 32-channel residual unit: one round of resident workgroups, each
+// walking an XCD-contiguous range of sample-aligned tiles
+template <int R, bool BWD>
+int64_t ru32_tiles_per_block(int64_t ntiles) {
+  static const int64_t slots = [] {
+    int dev = 0, cus = 0, per_cu = 0;
+    const size_t lds = BWD ? Ru32<R>::LDS_BWD : Ru32<R>::LDS_FWD;
+    const void* kern = BWD ? (const void*)k_ru32_bwd<R> : (const void*)k_ru32_fwd<R>;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, lds) != hipSuccess)
+      return int64_t(0);
+    return int64_t(cus) * per_cu / 8 * 8;
+  }();
+  const int64_t target = slots > 0 ? slots : 1024;
+  return std::max<int64_t>(1, (ntiles + target - 1) / target);
+}
+
+template <int R>
+int launch_ru32_fwd(const Args& a, const void* x, const void* w1p, const float* b1, const void* w2p,
+                    const float* b2, void* h, void* out, hipStream_t s) {
+  const int64_t ntiles = (a.rows / a.T) * ((a.T + R - 1) / R);
+  if (ntiles == 0) return SEL_OK;
+  const int64_t tpb = ru32_tiles_per_block<R, false>(ntiles);
+  const unsigned nb = unsigned(((ntiles + tpb - 1) / tpb + 7) / 8 * 8);
+  hipLaunchKernelGGL(k_ru32_fwd<R>, dim3(nb), dim3(256), Ru32<R>::LDS_FWD, s, a, static_cast<const __bf16*>(x),
+                     static_cast<const __bf16*>(w1p), b1, static_cast<const __bf16*>(w2p), b2,
+                     static_cast<__bf16*>(h), static_cast<__bf16*>(out), int(tpb), tune(15));
+  SEL_LAUNCH_CHECK();
+  return SEL_OK;
+}
+
+template <int R>
+int launch_ru32_bwd(const Args& a, const void* g, const void* h, const void* x, const void* wd1, const void* wd2,
+                    void* gh, void* gx, hipStream_t s) {
+  const int64_t ntiles = (a.rows / a.T) * ((a.T + R - 1) / R);
+  if (ntiles == 0) return SEL_OK;
+  const int64_t tpb = ru32_tiles_per_block<R, true>(ntiles);
+  const unsigned nb = unsigned(((ntiles + tpb - 1) / tpb + 7) / 8 * 8);
+  hipLaunchKernelGGL(k_ru32_bwd<R>, dim3(nb), dim3(256), Ru32<R>::LDS_BWD, s, a, static_cast<const __bf16*>(g),
+                     static_cast<const __bf16*>(h), static_cast<const __bf16*>(x), static_cast<const __bf16*>(wd1),
+                     static_cast<const __bf16*>(wd2), static_cast<__bf16*>(gh), static_cast<__bf16*>(gx), int(tpb));
+  SEL_LAUNCH_CHECK();
+  return SEL_OK;
+}
+
 bool ru_fused_ok(const Args& a) {
   return (a.C == 32 || a.C == 64) && a.N == a.C && a.K == 7 && a.pad == (a.K - 1) * a.dil &&
          a.pad_mode == SEL_PAD_ZERO && a.in_elu == 1 && (a.K - 1) * a.dil <= F4_HALOMAX &&
@@ -2740,8 +3125,22 @@ int sel_resunit_fwd(const sel_conv_desc* d1, int dtype, const void* x, const voi
   SEL_REQUIRE(dtype == SEL_BF16 && ru_fused_ok(a), SEL_ERR_UNSUPPORTED,
               "sel_resunit_fwd: fused path needs bf16, C = N in {32, 64}, K = 7, causal zero pad, ELU prologue");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (a.C == 32) return launch_ru_thin<32, 7, 128>(a, x, w1pack, b1, w2pack, b2, h, out, s);
+  if (a.C == 32) return launch_ru32_fwd<256>(a, x, w1pack, b1, w2pack, b2, h, out, s);
   return launch_ru_thin<64, 7, 64>(a, x, w1pack, b1, w2pack, b2, h, out, s);
+}
+
+/* Fused residual unit backward at 32 channels (residual_unit.py:43-46 adjoint):
+ * gh = (W2^T g) * ELU'(h), gx = conv1^T(gh) * ELU'(x) + g in one launch.  d1 is
+ * the forward conv1 descriptor; wd1 / wd2 the dgrad-packed weights; gh may be
+ * null (only the weight gradient of conv1 needs it). */
+int sel_resunit_bwd(const sel_conv_desc* d1, int dtype, const void* g, const void* h, const void* x,
+                    const void* wd1pack, const void* wd2pack, void* gh, void* gx, sel_stream_t stream) {
+  if (int rc = check_desc(d1)) return rc;
+  const Args a = to_args(d1);
+  SEL_REQUIRE(dtype == SEL_BF16 && ru_fused_ok(a) && a.C == 32, SEL_ERR_UNSUPPORTED,
+              "sel_resunit_bwd: fused path needs bf16, C = N = 32, K = 7, causal zero pad, ELU prologue");
+  SEL_REQUIRE(g && h && x && wd1pack && wd2pack && gx, SEL_ERR_ARG, "null pointer");
+  return launch_ru32_bwd<128>(a, g, h, x, wd1pack, wd2pack, gh, gx, reinterpret_cast<hipStream_t>(stream));
 }
 
 size_t sel_conv_wgrad_workspace(const sel_conv_desc* d) {

@@ -46,6 +46,7 @@ SIGNATURES = {
     "sel_conv_fwd_kernel_id": (I32, [P, I32, I32]),
     "sel_conv_fwd": (I32, [P, I32, I32, P, P, P, P, P, P, P]),
     "sel_resunit_fwd": (I32, [P, I32, P, P, P, P, P, P, P, P]),
+    "sel_resunit_bwd": (I32, [P, I32, P, P, P, P, P, P, P, P]),
     "sel_conv_wgrad_workspace": (SZ, [P]),
     "sel_conv_wgrad": (I32, [P, I32, P, P, P, P, P, SZ, P]),
     "sel_pack_weight": (I32, [I32, P, I32, I32, I32, I32, I32, P, P]),

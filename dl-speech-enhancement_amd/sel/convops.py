@@ -394,16 +394,48 @@ class ConvLayerFn(torch.autograd.Function):
         return gx, gw, gb, None, None, None
 
 
-# fused residual-unit forward (sel_resunit_fwd) for the 32/64-channel units; the
-# fusion is OFF by default: measured slower than the two calls
-RU_FUSED = os.environ.get("SEL_RU_FUSED", "0") == "1"
+# fused residual unit (sel_resunit_fwd / sel_resunit_bwd): ON by default at 32
+# channels (register-resident 1x1, k_ru32_fwd / k_ru32_bwd); the 64-channel
+# forward (k_ru_thin_bf16) measured slower than the two calls and is only used
+# with SEL_RU_FUSED=1; SEL_RU_FUSED=0 turns every fused path off
+RU_FUSED = os.environ.get("SEL_RU_FUSED", "")
+
+
+def _ru_shape_ok(d1, dtype):
+    """Mirror of the C side's eligibility (conv.hip ru_fused_ok)."""
+    return (dtype == torch.bfloat16 and d1.C == d1.N and d1.C in (32, 64) and d1.K == 7
+            and d1.pad == 6 * d1.dil and d1.pad_mode == PAD_ZERO and d1.in_elu == 1 and 6 * d1.dil <= 64
+            and d1.bias_period in (0, d1.N))
 
 
 def ru_fused_ok(d1, dtype):
-    """Mirror of the C side's eligibility (conv.hip ru_fused_ok)."""
-    return (RU_FUSED and dtype == torch.bfloat16 and d1.C == d1.N and d1.C in (32, 64) and d1.K == 7
-            and d1.pad == 6 * d1.dil and d1.pad_mode == PAD_ZERO and d1.in_elu == 1 and 6 * d1.dil <= 64
-            and d1.bias_period in (0, d1.N))
+    """Fused residual-unit forward for this conv1 descriptor?"""
+    if RU_FUSED == "0" or not _ru_shape_ok(d1, dtype):
+        return False
+    return d1.C == 32 or RU_FUSED == "1"
+
+
+def ru_bwd_fused_ok(d1, dtype):
+    """Fused residual-unit backward (32 channels only)?"""
+    return RU_FUSED != "0" and _ru_shape_ok(d1, dtype) and d1.C == 32
+
+
+def resunit_bwd(d1, gf, h, xf, wd1, wd2, want_gh):
+    """gx (and gh = (W2^T g) * ELU'(h) when want_gh) of a 32-channel residual unit
+    in one launch; all (rows, 32) bf16."""
+    gx = torch.empty_like(xf)
+    gh = torch.empty_like(xf) if want_gh else None
+    L.call("sel_resunit_bwd", ctypes.byref(d1), _code(xf.dtype), L.ptr(gf), L.ptr(h), L.ptr(xf), L.ptr(wd1),
+           L.ptr(wd2), L.ptr(gh), L.ptr(gx), L.stream(), meta=lambda: _ru_bwd_meta(d1, xf, want_gh))
+    return gx, gh
+
+
+def _ru_bwd_meta(d1, xf, want_gh):
+    """Algorithmic bytes: read g, h, x once, write gx (and gh)."""
+    es = xf.element_size()
+    nbytes = (4 + int(want_gh)) * d1.rows * d1.C * es
+    flops = 2.0 * d1.rows * d1.N * d1.C * (d1.K + 1)
+    return "k_ru32_bwd<128>", nbytes, flops
 
 
 def resunit_fwd(d1, xf, wp1, b1, wp2, b2):
@@ -420,7 +452,7 @@ def _ru_meta(d1, xf, wp1, wp2):
     es = xf.element_size()
     nbytes = 3 * d1.rows * d1.C * es + (wp1.numel() + wp2.numel()) * es
     flops = 2.0 * d1.rows * d1.N * d1.C * (d1.K + 1)
-    return f"k_ru_thin_bf16<{d1.C}, 7, {128 if d1.C == 32 else 64}>", nbytes, flops
+    return ("k_ru32_fwd<256>" if d1.C == 32 else "k_ru_thin_bf16<64, 7, 64>"), nbytes, flops
 
 
 class ResidualUnitFn(torch.autograd.Function):
@@ -461,17 +493,23 @@ class ResidualUnitFn(torch.autograd.Function):
             g = cast(g, x.dtype)
         gf = g.view(B * T, C)
         xf = x.view(B * T, C)
-        # dL/dh = (W2^T g) * ELU'(h)
-        gh = prim(d2.adjoint(), gf, wd2, aux=h)
+        need_w1 = ctx.needs_input_grad[1] or ctx.needs_input_grad[2]
+        gx = None
+        if ctx.needs_input_grad[0] and ru_bwd_fused_ok(d1, x.dtype):
+            # one launch: gh = (W2^T g) * ELU'(h) and gx = g + conv_adjoint(gh) * ELU'(x)
+            gx, gh = resunit_bwd(d1, gf, h, xf, wd1, wd2, need_w1)
+            gx = gx.view(B, T, C)
+        else:
+            # dL/dh = (W2^T g) * ELU'(h)
+            gh = prim(d2.adjoint(), gf, wd2, aux=h)
         gw1 = gb1 = gw2 = gb2 = None
         if ctx.needs_input_grad[3] or ctx.needs_input_grad[4]:
             gw2, gb2 = wgrad_torch(d2, gf, h, PACK_FWD, s2, 1, d2.bias_period > 0 and ctx.needs_input_grad[4])
             gw2 = gw2 if ctx.needs_input_grad[3] else None
-        gx = None
-        if ctx.needs_input_grad[0]:
+        if ctx.needs_input_grad[0] and gx is None:
             # dL/dx = g + (conv_adjoint(gh)) * ELU'(x)
             gx = prim(d1.adjoint(), gh, wd1, aux=xf, res=gf).view(B, T, C)
-        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+        if need_w1:
             gw1, gb1 = wgrad_torch(d1, gh, xf, PACK_FWD, s1, 1, d1.bias_period > 0 and ctx.needs_input_grad[2])
             gw1 = gw1 if ctx.needs_input_grad[1] else None
         return gx, gw1, gb1, gw2, gb2, None

@@ -173,6 +173,12 @@ int sel_conv_fwd(const sel_conv_desc* d, int in_dtype, int out_dtype, const void
  * Returns SEL_ERR_UNSUPPORTED for any other shape. */
 int sel_resunit_fwd(const sel_conv_desc* d1, int dtype, const void* x, const void* w1pack, const float* b1,
                     const void* w2pack, const float* b2, void* h, void* out, sel_stream_t stream);
+/* Fused residual-unit backward at 32 channels (replaces the two adjoint
+ * primitive calls of residual_unit.py:43-46's backward): gh = (W2^T g) * ELU'(h),
+ * gx = conv1^T(gh) * ELU'(x) + g; d1 is conv1's forward descriptor, wd1/wd2 the
+ * dgrad-packed weights (sel_pack_dgrad); gh may be NULL. */
+int sel_resunit_bwd(const sel_conv_desc* d1, int dtype, const void* g, const void* h, const void* x,
+                    const void* wd1pack, const void* wd2pack, void* gh, void* gx, sel_stream_t stream);
 /* weight/bias gradient of the same primitive: gwpack[N][K][C] (fp32) and, when
  * gbias != NULL, gbias[bias_period] = sum over rows and phases of gout. */
 size_t sel_conv_wgrad_workspace(const sel_conv_desc* d);

@@ -358,7 +358,7 @@ def test_fused_residual_unit_matches_two_calls(gpu, shape, monkeypatch):
     d2 = CO.ConvDesc(B * T, T, C, C, 1, 1, 0, CO.PAD_ZERO, 1, C if bias else 0)
     wp1 = CO.pack(CO.PACK_FWD, w1, 1, torch.bfloat16)
     wp2 = CO.pack(CO.PACK_FWD, w2, 1, torch.bfloat16)
-    monkeypatch.setattr(CO, "RU_FUSED", True)  # off by default in the product path
+    monkeypatch.setattr(CO, "RU_FUSED", "1")  # the 64-channel instance is off by default
     assert CO.ru_fused_ok(d1, torch.bfloat16)
     h, out = CO.resunit_fwd(d1, x, wp1, b1, wp2, b2)
     h_ref = CO.prim(d1, x, wp1, bias=b1)
@@ -366,6 +366,9 @@ def test_fused_residual_unit_matches_two_calls(gpu, shape, monkeypatch):
     for a_, b_ in ((h, h_ref), (out, out_ref)):
         e = ((a_.float() - b_.float()).norm() / b_.float().norm()).item()
         assert e < 4e-3, e
+    if C == 32:
+        # k_ru32_fwd: same MFMA order and rounding points as the two calls
+        assert torch.equal(h, h_ref) and torch.equal(out, out_ref)
     # fp64 reference of the same bf16 operands
     elu = lambda v: torch.where(v > 0, v, torch.expm1(v))
     xa = elu(x.double()).to(torch.bfloat16).double().view(B, T, C)
@@ -386,3 +389,76 @@ def test_fused_residual_unit_matches_two_calls(gpu, shape, monkeypatch):
     for a_, b_ in ((h, hr), (out, outr)):
         e = ((a_.double().view(B, T, C) - b_).norm() / b_.norm()).item()
         assert e < 1e-2, e
+
+
+RU32_BWD_SHAPES = [(1, 0, 2, 1000), (3, 1, 3, 777), (9, 1, 2, 1000), (9, 0, 2, 40), (9, 1, 4, 24000)]
+
+
+@pytest.mark.parametrize("shape", RU32_BWD_SHAPES, ids=lambda s: "d{}b{}B{}T{}".format(*s))
+def test_resunit32_bwd_matches_two_calls(gpu, shape):
+    """sel_resunit_bwd (one launch, k_ru32_bwd) against the two adjoint primitive
+    calls of ResidualUnitFn's unfused backward on the same bf16 operands: gh
+    and gx bit-identical (same MFMA order, same rounding points), ragged tails,
+    T < halo and the C3 size (T = 24000)."""
+    from sel import convops as CO
+    dil, bias, B, T = shape
+    C = 32
+    torch.manual_seed(dil + T)
+    x = (0.5 * torch.randn(B * T, C, device=gpu)).to(torch.bfloat16)
+    h = (0.5 * torch.randn(B * T, C, device=gpu)).to(torch.bfloat16)
+    g = (0.5 * torch.randn(B * T, C, device=gpu)).to(torch.bfloat16)
+    w1 = 0.1 * torch.randn(C, C, 7, device=gpu)
+    w2 = 0.2 * torch.randn(C, C, 1, device=gpu)
+    d1 = CO.ConvDesc(B * T, T, C, C, 7, dil, 6 * dil, CO.PAD_ZERO, 1, C if bias else 0)
+    d2 = CO.ConvDesc(B * T, T, C, C, 1, 1, 0, CO.PAD_ZERO, 1, C if bias else 0)
+    wp1, wd1 = CO.PACKS.get(CO.PACK_FWD, w1, 1, torch.bfloat16)
+    wp2, wd2 = CO.PACKS.get(CO.PACK_FWD, w2, 1, torch.bfloat16)
+    assert CO.ru_bwd_fused_ok(d1, torch.bfloat16)
+    gx, gh = CO.resunit_bwd(d1, g, h, x, wd1, wd2, True)
+    gh_ref = CO.prim(d2.adjoint(), g, wd2, aux=h)
+    gx_ref = CO.prim(d1.adjoint(), gh_ref, wd1, aux=x, res=g)
+    assert torch.equal(gh, gh_ref), ((gh.float() - gh_ref.float()).abs().max().item())
+    _ulp_close(gx, gx_ref)
+    gx2, gh2 = CO.resunit_bwd(d1, g, h, x, wd1, wd2, False)
+    assert gh2 is None and torch.equal(gx2, gx)
+
+
+def _ulp_close(a, b, frac=1e-3):
+    """bf16 tensors equal up to one ulp on at most `frac` of the elements: the
+    ELU'(x) factor's hardware exp rounds differently in the fused kernel on a
+    few ties (measured at T = 24000: 47 of 96000 rows, equally close to fp64)."""
+    af, bf = a.double(), b.double()
+    m = torch.maximum(af.abs(), bf.abs())
+    _, ex = torch.frexp(m)
+    ulp = torch.ldexp(torch.ones_like(m), ex - 8)  # bf16: 8 significant bits
+    d = (af - bf).abs()
+    tiny = 1e-6 * bf.abs().max()
+    assert bool((d <= ulp + tiny).all()), float((d - ulp).max())
+    assert float((d > 0).float().mean()) <= frac, float((d > 0).float().mean())
+
+
+def test_resunit32_autograd_fused_vs_unfused(gpu, monkeypatch):
+    """ResidualUnitFn at 32 channels: forward and all five gradients with the
+    fused launches (default) equal the unfused primitive path (SEL_RU_FUSED=0)."""
+    from sel import convops as CO
+    torch.manual_seed(5)
+    B, T, C, dil = 2, 3000, 32, 3
+    x0 = (0.5 * torch.randn(B, T, C, device=gpu)).to(torch.bfloat16)
+    w1 = (0.1 * torch.randn(C, C, 7, device=gpu)).requires_grad_(True)
+    b1 = torch.randn(C, device=gpu).requires_grad_(True)
+    w2 = (0.2 * torch.randn(C, C, 1, device=gpu)).requires_grad_(True)
+    b2 = torch.randn(C, device=gpu).requires_grad_(True)
+    gy = (0.5 * torch.randn(B, T, C, device=gpu)).to(torch.bfloat16)
+    res = {}
+    for mode in ("", "0"):
+        monkeypatch.setattr(CO, "RU_FUSED", mode)
+        x = x0.clone().requires_grad_(True)
+        for p_ in (w1, b1, w2, b2):
+            p_.grad = None
+        y = CO.ResidualUnitFn.apply(x, w1, b1, w2, b2, dil)
+        y.backward(gy)
+        res[mode] = [y.detach().clone(), x.grad.clone()] + [p_.grad.clone() for p_ in (w1, b1, w2, b2)]
+    assert torch.equal(res[""][0], res["0"][0])  # forward: bit-identical
+    _ulp_close(res[""][1], res["0"][1])          # gx
+    for a_, b_ in zip(res[""][2:], res["0"][2:]):  # weight / bias grads (fp32) through the same gh
+        assert ((a_ - b_).norm() / b_.norm()).item() < 1e-3
