@@ -310,7 +310,10 @@ def c5_cpu_baseline(B_sample=1, steps=3):
 MFMA_BF16_PEAK_TFS = 2500.0  # MI355X dense bf16 (MI355X_MICROARCH.md)
 
 
-PMC_FILE = os.path.join(REPO, "profiles", "r1_c3_pmc_traffic.json")
+# newest committed PMC traffic table of the C3 bench (tools/pmc_round.sh)
+PMC_FILE = next((f for f in (os.path.join(REPO, "profiles", n) for n in ("r2_c3_pmc_traffic.json",
+                                                                          "r1_c3_pmc_traffic.json"))
+                 if os.path.exists(f)), "")
 
 
 def _mangled_fragment(tag):
@@ -329,7 +332,7 @@ def pmc_traffic(tag, B, steps_cfg="c3"):
     """HBM bytes per launch of kernel `tag` from the committed rocprofv3 PMC passes
     (tools/pmc_traffic.py over FETCH_SIZE / WRITE_SIZE runs of this same bench
     command, gfx950 corrections applied there), or None if not measured."""
-    if steps_cfg != "c3" or B != 64 or not os.path.exists(PMC_FILE):
+    if steps_cfg != "c3" or B != 64 or not PMC_FILE:
         return None
     frag = _mangled_fragment(tag)
     with open(PMC_FILE) as f:
@@ -516,7 +519,7 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    timer = _lib.KernelTimer([dom] + (["sel_resunit_fwd"] if cfg == "c3" else [])
+    timer = _lib.KernelTimer([dom] + (["sel_resunit_fwd", "sel_resunit_bwd"] if cfg == "c3" else [])
                              + (["sel_dconv_fwd"] if cfg == "c5" else []))
     elapsed, per_step = _timed_steps(step, args.steps, world, dev, timer)
 

@@ -2462,37 +2462,44 @@ __global__ void k_pack_many(const sel_pack_job* __restrict__ jobs, int njobs, in
       else hi = mid - 1;
     }
     const sel_pack_job& J = jobs[lo];
-    const int64_t li = i - J.offset;
-    const int s = J.stride, cin = J.cin, cout = J.cout, K = J.k;
+    // a layer's packed index fits 32 bits (host-checked): unsigned 32-bit
+    // division instead of the 64-bit sequences (the per-step pack of the C3
+    // weights took 105 us with them)
+    const unsigned li = unsigned(i - J.offset);
+    const unsigned s = unsigned(J.stride), cin = unsigned(J.cin), cout = unsigned(J.cout), K = unsigned(J.k);
     float v = 0.f;
-    int N, KP, CP, n, kp, cp;
+    unsigned N, KP, n, kp, cp;
     if (J.kind == SEL_PACK_FWD) {
-      N = cout, KP = K, CP = cin;
-      cp = int(li % cin);
-      kp = int((li / cin) % K);
-      n = int(li / (int64_t(cin) * K));
-      v = J.w[(int64_t(n) * cin + cp) * K + kp];
+      N = cout, KP = K;
+      const unsigned q = li / cin;
+      cp = li - q * cin;
+      n = q / K;
+      kp = q - n * K;
+      v = J.w[(n * cin + cp) * K + kp];
     } else if (J.kind == SEL_PACK_FWD_STRIDED) {
-      N = cout, KP = 3, CP = s * cin;
-      cp = int(li % CP);
-      kp = int((li / CP) % 3);
-      n = int(li / (int64_t(CP) * 3));
-      const int ph = cp / cin, ci = cp % cin;
-      const int k = strided_k(kp, ph, s);
-      v = k >= 0 ? J.w[(int64_t(n) * cin + ci) * (2 * s) + k] : 0.f;
+      N = cout, KP = 3;
+      const unsigned CP = s * cin;
+      const unsigned q = li / CP;
+      cp = li - q * CP;
+      n = q / 3u;
+      kp = q - n * 3u;
+      const unsigned ph = cp / cin, ci = cp - ph * cin;
+      const int k = strided_k(int(kp), int(ph), int(s));
+      v = k >= 0 ? J.w[(n * cin + ci) * (2 * s) + unsigned(k)] : 0.f;
     } else {
-      N = s * cout, KP = 2, CP = cin;
-      cp = int(li % cin);
-      kp = int((li / cin) % 2);
-      n = int(li / (int64_t(cin) * 2));
-      const int ph = n / cout, co = n % cout;
-      const int k = kp == 0 ? ph + s : ph;
-      v = J.w[(int64_t(cp) * cout + co) * (2 * s) + k];
+      N = s * cout, KP = 2;
+      const unsigned q = li / cin;
+      cp = li - q * cin;
+      n = q >> 1;
+      kp = q & 1u;
+      const unsigned ph = n / cout, co = n - ph * cout;
+      const unsigned k = kp == 0 ? ph + s : ph;
+      v = J.w[(cp * cout + co) * (2 * s) + k];
     }
     const TO tv = from_f<TO>(v);
     static_cast<TO*>(J.wpack)[li] = tv;
     // Wd[c][j][n] = Wp[n][KP-1-j][c]
-    if (J.wdgrad) static_cast<TO*>(J.wdgrad)[(int64_t(cp) * KP + (KP - 1 - kp)) * N + n] = tv;
+    if (J.wdgrad) static_cast<TO*>(J.wdgrad)[(cp * KP + (KP - 1 - kp)) * N + n] = tv;
   }
 }
 
@@ -3320,6 +3327,8 @@ int sel_pack_weight(int kind, const float* w, int cout, int cin, int k, int stri
 
 int sel_pack_many(const sel_pack_job* jobs, int njobs, int64_t total, int dtype, sel_stream_t stream) {
   SEL_REQUIRE(jobs && njobs > 0 && total > 0, SEL_ERR_ARG, "empty pack job table");
+  // (the job table is device memory: each job's element count is checked < 2^31
+  // by the host binding, sel/convops.py PackCache._refresh)
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   dim3 grid(unsigned(std::min<int64_t>(8192, (total + 255) / 256)));
   if (dtype == SEL_F32)

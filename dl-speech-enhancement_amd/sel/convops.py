@@ -221,6 +221,8 @@ class PackCache:
         for e, w in stale:
             shp, cout, cin, k = _packed_shape(e.kind, w, e.stride)
             n = shp[0] * shp[1] * shp[2]
+            if n >= 1 << 31 or w.numel() >= 1 << 31:
+                raise L.SelError("sel: a packed conv weight must stay below 2^31 elements")
             shapes.append((shp, cout, cin, k, total, n))
             total += n
         flat = torch.empty(2 * total, dtype=dtype, device=device)
@@ -242,10 +244,12 @@ PACKS = PackCache()
 
 
 def _optimizer_stepped(optimizer, args, kwargs):
-    """Global torch.optim post-step hook: every conv weight the optimizer owns
-    is repacked before its next use (see PackCache: fused Adam does not bump
-    the parameters' version counters)."""
-    PACKS.mark_stale(p for g in optimizer.param_groups for p in g["params"])
+    """Global torch.optim post-step hook: every conv weight the optimizer
+    updated is repacked before its next use (see PackCache: fused Adam does not
+    bump the parameters' version counters).  torch's optimizers skip parameters
+    whose .grad is None (the frozen decoder and quantizer of the denoise
+    trainer), so those keep their packs."""
+    PACKS.mark_stale(p for g in optimizer.param_groups for p in g["params"] if p.grad is not None)
 
 
 _register_optimizer_step_post_hook(_optimizer_stepped)

@@ -108,7 +108,8 @@ DPACKS = _DPackCache()
 
 
 def _optimizer_stepped(optimizer, args, kwargs):
-    DPACKS.mark_stale([p for g in optimizer.param_groups for p in g["params"]])
+    # (parameters without a gradient were not updated: torch's optimizers skip them)
+    DPACKS.mark_stale([p for g in optimizer.param_groups for p in g["params"] if p.grad is not None])
     DPACKS.prune()
 
 
