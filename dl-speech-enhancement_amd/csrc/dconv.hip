@@ -201,6 +201,147 @@ __global__ __launch_bounds__(256) void k_dconv_mfma(D d, const T* __restrict__ x
 }
 
 // ---------------------------------------------------------------------------
+// Register-prefetched MFMA primitive for one group with a contiguous reduction
+// row (G == 1, S == 1 or Cs == Cg: every MPD layer and the MSD's dense ones)
+// and K <= 8 taps: the next 32-channel chunk's input span and ALL K weight
+// slices are fetched into registers while the current chunk's MFMAs run (the
+// tap-grouped kernel above stages each chunk synchronously: ~5% of the bf16
+// peak on the MPD's 512/1024-wide layers, profiles/r2_c5_kernel_stats.md).
+// ---------------------------------------------------------------------------
+constexpr int PF_KMAX = 8;
+
+template <int BM, int BN>
+__global__ __launch_bounds__(256) void k_dconv_pf(D d, const __bf16* __restrict__ x, const __bf16* __restrict__ wp,
+                                                  const float* __restrict__ bias, const __bf16* __restrict__ aux,
+                                                  const __bf16* __restrict__ res, __bf16* __restrict__ out) {
+  constexpr int P = Elt<__bf16>::P;
+  constexpr int WAVES_N = BN / 32, WAVES_M = 4 / WAVES_N;
+  constexpr int TM = BM / (32 * WAVES_M);
+  constexpr int XV = ((BM + PF_KMAX - 1) * 4 + 255) / 256;
+  constexpr int WV = (PF_KMAX * BN * 4 + 255) / 256;
+  static_assert(TM >= 1 && WAVES_N * WAVES_M == 4, "tile");
+  extern __shared__ __align__(16) unsigned char smem[];
+  __bf16* const xs = reinterpret_cast<__bf16*>(smem);
+  const int span = BM + d.K - 1;
+  __bf16* const ws = xs + span * P;  // [K][BN][P]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+  const int hl = lane >> 5;
+  const int tps = (d.Tvo + BM - 1) / BM;
+  const int b = blockIdx.x / tps;
+  const int j0 = (blockIdx.x % tps) * BM;
+  const int no_per_g = d.So * d.Ng;
+  const int o0 = blockIdx.y * BN;
+  const int nred = d.S * d.Cg;
+  const int nchunk = (nred + CH - 1) / CH;
+
+  const __bf16* xsrc[XV];
+  bool xok[XV];
+  int xsub[XV];
+#pragma unroll
+  for (int u = 0; u < XV; ++u) {
+    const int v = tid + u * 256, rr = v >> 2;
+    const int t = j0 + d.q0 + rr;
+    xok[u] = rr < span && t >= 0 && t < d.Tv;
+    xsub[u] = (v & 3) * 8;
+    xsrc[u] = x + (int64_t(b) * d.Tvs + (xok[u] ? t : 0)) * d.ldx + xsub[u];
+  }
+  const __bf16* wsrc[WV];
+  bool wok[WV];
+#pragma unroll
+  for (int u = 0; u < WV; ++u) {
+    const int v = tid + u * 256;
+    const int k = v / (BN * 4), n = (v >> 2) % BN;
+    wok[u] = k < d.K && o0 + n < no_per_g;
+    wsrc[u] = wp + (int64_t(wok[u] ? o0 + n : 0) * d.K + (wok[u] ? k : 0)) * nred + (v & 3) * 8;
+  }
+  uint4 xr[XV], wr[WV];
+  auto load = [&](int cc) {
+#pragma unroll
+    for (int u = 0; u < XV; ++u)
+      if ((u * 256) / 4 < span) xr[u] = *reinterpret_cast<const uint4*>(xsrc[u] + (cc + xsub[u] < nred ? cc : 0));
+#pragma unroll
+    for (int u = 0; u < WV; ++u)
+      if ((u * 256) / (BN * 4) < d.K) wr[u] = *reinterpret_cast<const uint4*>(wsrc[u] + (cc + (((tid + u * 256) & 3) * 8) < nred ? cc : 0));
+  };
+  auto store = [&](int cc) {
+#pragma unroll
+    for (int u = 0; u < XV; ++u) {
+      const int v = tid + u * 256;
+      if ((v >> 2) >= span) continue;
+      const uint4 val = (xok[u] && cc + xsub[u] < nred) ? xr[u] : make_uint4(0, 0, 0, 0);
+      *reinterpret_cast<uint4*>(xs + (v >> 2) * P + xsub[u]) = val;
+    }
+#pragma unroll
+    for (int u = 0; u < WV; ++u) {
+      const int v = tid + u * 256;
+      const int k = v / (BN * 4), n = (v >> 2) % BN;
+      if (k >= d.K) continue;
+      const uint4 val = (wok[u] && cc + (v & 3) * 8 < nred) ? wr[u] : make_uint4(0, 0, 0, 0);
+      *reinterpret_cast<uint4*>(ws + (k * BN + n) * P + (v & 3) * 8) = val;
+    }
+  };
+
+  floatx16 acc[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
+  int lrow[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) lrow[i] = wm * (BM / WAVES_M) + i * 32 + (lane & 31);
+  const int nw_ = wn * 32 + (lane & 31);
+
+  load(0);
+  for (int ch = 0; ch < nchunk; ++ch) {
+    const int cc = ch * CH;
+    if (ch) __syncthreads();
+    store(cc);
+    __syncthreads();
+    if (ch + 1 < nchunk) load(cc + CH);
+    const int chn = nred - cc < CH ? nred - cc : CH;
+    for (int k = 0; k < d.K; ++k) {
+#pragma unroll
+      for (int h = 0; h < CH / 16; ++h) {
+        if (h * 16 >= chn) break;
+        const int co = 16 * h + 8 * hl;
+        const bf16x8 bw = *reinterpret_cast<const bf16x8*>(ws + (k * BN + nw_) * P + co);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const bf16x8 af = *reinterpret_cast<const bf16x8*>(xs + (lrow[i] + k) * P + co);
+          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bw, af, acc[i], 0, 0, 0);
+        }
+      }
+    }
+  }
+
+  // epilogue as k_dconv_mfma
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int j = j0 + lrow[i];
+    if (j >= d.Tvo) continue;
+    const int64_t orow = (int64_t(b) * d.Tvo + j) * d.ldo;
+    const bool valid = j < d.Tvalid;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int o = o0 + wn * 32 + (e & 3) + 8 * (e >> 2) + 4 * hl;
+      if (o >= no_per_g) continue;
+      const int64_t col = out_col(d, 0, o);
+      float v = 0.f;
+      if (valid) {
+        v = acc[i][e];
+        if (bias) v += bias[col];
+        if (res) v += to_f(res[orow + col]);
+        if (aux) v *= leaky_grad(to_f(aux[orow + col]), d.slope);
+        if (d.act) v = leaky(v, d.slope);
+      }
+      out[orow + col] = from_f<__bf16>(v);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // VALU primitive (any Cg; used when S*Cg*K or the group output width is tiny).
 // One thread per (row, output channel); the reduction walks (i, r, c).
 // ---------------------------------------------------------------------------
@@ -476,6 +617,164 @@ __global__ __launch_bounds__(256) void k_dwgrad_mfma(D d, const __bf16* __restri
     for (int e = 0; e < 4; ++e) {
       const int o = o0 + nt * 16 + 4 * (lane >> 4) + e;
       if (o < no_per_g && ch < nred) pdst[((int64_t(g) * no_per_g + o) * d.K + k) * nred + ch] = acc[j][e];
+    }
+  }
+}
+
+// Weight gradient for one group with a contiguous reduction row and K <= 8
+// taps (every MPD layer, the MSD's dense ones): the generator's k_wgrad3_bf16
+// scheme on the dconv descriptor.  A block owns 32*NT output x 32*CT reduction
+// channels x ALL taps over a contiguous range of 128-row tiles of one
+// sequence: gout and x are read once per block (the 16-wide per-tap-group
+// kernel above re-read them (N/32)*(nred/32) times, ~5% of the bf16 peak),
+// double-buffered in LDS with a register prefetch of the next tile, operands
+// through transposing reads, 32x32x16 MFMA.
+constexpr int W3_BM = 128, W3_HALO = 64;
+
+template <int NT, int CT, int MAXT>
+__global__ __launch_bounds__(256) void k_dwgrad_w3(D d, const __bf16* __restrict__ gout, const __bf16* __restrict__ x,
+                                                   int tiles_per_seq, int64_t n_tiles, int tiles_per_split,
+                                                   float* __restrict__ part) {
+  constexpr int NB = 32 * NT, CB = 32 * CT;
+  constexpr int XROWS = W3_BM + W3_HALO;
+  constexpr int GV = W3_BM * NB / 8 / 256;
+  constexpr int XV = XROWS * CB / 8 / 256;
+  constexpr int GS = NT * W3_BM * 32, XS = CT * XROWS * 32;
+  constexpr int WPN = 4 / NT;
+  extern __shared__ __align__(16) unsigned char smem[];
+  __bf16* const base = reinterpret_cast<__bf16*>(smem);  // [buf]{G[NT][128][32], X[CT][192][32]}
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t split = blockIdx.x;
+  const int n0 = blockIdx.y * NB, c0 = blockIdx.z * CB;
+  const int nred = d.S * d.Cg;
+  const int64_t tb = split * tiles_per_split;
+  const int64_t te = tb + tiles_per_split < n_tiles ? tb + tiles_per_split : n_tiles;
+  const int span = W3_BM + d.K - 1;
+  const int P = CT * d.K;
+  const int RG = P >= WPN ? 1 : WPN / P;
+  const int WPP = WPN / RG;
+  const int nt = wave / WPN, wsub = wave % WPN;
+  const int rg = wsub / WPP, pw = wsub % WPP;
+  const int RROWS = W3_BM / RG;
+
+  uint4 gr[GV], xr[XV];
+  bool gok[GV], xok[XV];
+  auto load = [&](int64_t tile) {
+    const int b = int(tile / tiles_per_seq);
+    const int j0 = int(tile % tiles_per_seq) * W3_BM;
+#pragma unroll
+    for (int u = 0; u < GV; ++u) {
+      const int v = tid + u * 256;
+      const int j = j0 + v / (NB / 8);
+      gok[u] = j < d.Tvalid;
+      gr[u] = *reinterpret_cast<const uint4*>(gout + (int64_t(b) * d.Tvo + (gok[u] ? j : 0)) * d.ldo + n0 +
+                                              (v % (NB / 8)) * 8);
+    }
+#pragma unroll
+    for (int u = 0; u < XV; ++u) {
+      const int v = tid + u * 256;
+      const int r = v / (CB / 8);
+      const int t = j0 + d.q0 + r;
+      xok[u] = r < span && t >= 0 && t < d.Tv;
+      if (u * 256 / (CB / 8) < span)
+        xr[u] = *reinterpret_cast<const uint4*>(x + (int64_t(b) * d.Tvs + (xok[u] ? t : 0)) * d.ldx + c0 +
+                                                (v % (CB / 8)) * 8);
+    }
+  };
+  auto store = [&](int buf) {
+    __bf16* g = base + buf * (GS + XS);
+    __bf16* xx = g + GS;
+#pragma unroll
+    for (int u = 0; u < GV; ++u) {
+      const int v = tid + u * 256;
+      const int r = v / (NB / 8), c8 = v % (NB / 8);
+      *reinterpret_cast<uint4*>(g + (c8 >> 2) * (W3_BM * 32) + r * 32 + (c8 & 3) * 8) =
+          gok[u] ? gr[u] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < XV; ++u) {
+      if (u * 256 / (CB / 8) >= span) continue;
+      const int v = tid + u * 256;
+      const int r = v / (CB / 8), c8 = v % (CB / 8);
+      *reinterpret_cast<uint4*>(xx + (c8 >> 2) * (XROWS * 32) + r * 32 + (c8 & 3) * 8) =
+          xok[u] ? xr[u] : make_uint4(0, 0, 0, 0);
+    }
+  };
+
+  int xoff[MAXT];
+#pragma unroll
+  for (int j = 0; j < MAXT; ++j) {
+    int p = pw + WPP * j;
+    p = p < P ? p : P - 1;
+    xoff[j] = (p / d.K) * (XROWS * 32) + (p % d.K) * 32;
+  }
+  floatx16 acc[MAXT];
+#pragma unroll
+  for (int j = 0; j < MAXT; ++j)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
+
+  const int h = lane >> 5;
+  const int col = ((lane >> 4) & 1) * 16 + 4 * (lane & 3);
+  const int q = (lane & 15) >> 2;
+  const int lrow = (4 * h + q) * 32 + col;
+
+  if (tb < te) load(tb);
+  int buf = 0;
+  for (int64_t tile = tb; tile < te; ++tile, buf ^= 1) {
+    store(buf);
+    __syncthreads();
+    if (tile + 1 < te) load(tile + 1);
+    const __bf16* g = base + buf * (GS + XS) + nt * (W3_BM * 32);
+    const __bf16* xx = base + buf * (GS + XS) + GS;
+    for (int kh = 0; kh < RROWS / 16; ++kh) {
+      const int R = (rg * RROWS + kh * 16) * 32 + lrow;
+      const v4i16 a0 = tr_read(g + R);
+      const v4i16 a1 = tr_read(g + R + 8 * 32);
+      const bf16x8 A = __builtin_bit_cast(bf16x8, __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+      for (int j = 0; j < MAXT; ++j) {
+        const v4i16 b0 = tr_read(xx + xoff[j] + R);
+        const v4i16 b1 = tr_read(xx + xoff[j] + R + 8 * 32);
+        const bf16x8 Bf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7));
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, Bf, acc[j], 0, 0, 0);
+      }
+    }
+  }
+
+  const int64_t nw = int64_t(d.Ng) * d.K * nred;
+  float* pdst = part + split * nw;
+  if (RG == 1) {
+#pragma unroll
+    for (int j = 0; j < MAXT; ++j) {
+      const int p = pw + WPP * j;
+      if (p >= P) break;
+      const int ct = p / d.K, k = p % d.K;
+      const int c = c0 + ct * 32 + (lane & 31);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int n = n0 + nt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        pdst[(int64_t(n) * d.K + k) * nred + c] = acc[j][r];
+      }
+    }
+  } else {
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);  // [wave][32*32]
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      red[wave * 1024 + row * 32 + (lane & 31)] = acc[0][r];
+    }
+    __syncthreads();
+    for (int i = tid; i < NT * P * 1024; i += 256) {
+      const int e = i & 1023, pi = (i >> 10) % P, ni = (i >> 10) / P;
+      float v = 0.f;
+      for (int r = 0; r < RG; ++r) v += red[(ni * WPN + r * WPP + pi) * 1024 + e];
+      const int ct = pi / d.K, k = pi % d.K;
+      const int n = n0 + ni * 32 + (e >> 5), c = c0 + ct * 32 + (e & 31);
+      pdst[(int64_t(n) * d.K + k) * nred + c] = v;
     }
   }
 }
@@ -954,6 +1253,28 @@ int launch_short(const sel_dconv_desc* d, const void* x, const void* wp, const f
   return SEL_OK;
 }
 
+template <int BM, int BN>
+int launch_pf(const sel_dconv_desc* d, const void* x, const void* wp, const float* bias, const void* aux,
+              const void* res, void* out, hipStream_t s) {
+  constexpr int P = Elt<__bf16>::P;
+  const size_t lds = (size_t(BM + d->K - 1) + size_t(d->K) * BN) * P * sizeof(__bf16);
+  const int tps = (d->Tvo + BM - 1) / BM;
+  const int ntg = (d->So * d->Ng + BN - 1) / BN;
+  dim3 grid(unsigned(int64_t(d->B) * tps), unsigned(ntg));
+  auto kern = k_dconv_pf<BM, BN>;
+  if (lds > 64 * 1024)
+    SEL_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
+  hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, *d, static_cast<const __bf16*>(x), static_cast<const __bf16*>(wp),
+                     bias, static_cast<const __bf16*>(aux), static_cast<const __bf16*>(res), static_cast<__bf16*>(out));
+  SEL_LAUNCH_CHECK();
+  return SEL_OK;
+}
+
+// the prefetching kernel's shapes: bf16, one group, contiguous reduction rows, K <= 8
+bool pf_ok(const sel_dconv_desc* d, int dtype) {
+  return dtype == SEL_BF16 && d->G == 1 && (d->S == 1 || d->Cs == d->Cg) && d->K <= PF_KMAX && tune(16) != 1;
+}
+
 template <typename T>
 int dispatch_fwd(const sel_dconv_desc* d, const void* x, const void* wp, const float* bias, const void* aux,
                  const void* res, void* out, hipStream_t s, int dtype) {
@@ -964,6 +1285,12 @@ int dispatch_fwd(const sel_dconv_desc* d, const void* x, const void* wp, const f
   }
   const int width = d->So * d->Ng;
   const int64_t rows = int64_t(d->B) * d->Tvo;
+  if constexpr (sizeof(T) == 2) {
+    if (width > 32 && pf_ok(d, dtype)) {
+      if (rows * (width / 64) < 65536) return launch_pf<64, 64>(d, x, wp, bias, aux, res, out, s);
+      return launch_pf<128, 64>(d, x, wp, bias, aux, res, out, s);
+    }
+  }
   // narrow groups: 32-wide tiles; short sequences / few rows: 64-row tiles
   if (width <= 32) {
     if (rows * d->G < 131072) return launch_mfma<T, 128, 32>(d, x, wp, bias, aux, res, out, s);
@@ -974,7 +1301,8 @@ int dispatch_fwd(const sel_dconv_desc* d, const void* x, const void* wp, const f
 }
 
 struct WgPlanD {
-  bool mfma, shortk;
+  bool mfma, shortk, w3;
+  int w3_nt, w3_ct, w3_maxt;
   int nsplit, bsplit;
   int rows_per_split, brows_per_split;
   int tiles_per_seq, tiles_per_split, ntg, nt;
@@ -997,7 +1325,24 @@ WgPlanD wg_plan(const sel_dconv_desc* d, int dtype) {
     p.bsplit = p.nsplit;
     return p;
   }
-  if (p.mfma) {
+  p.w3 = p.mfma && d->G == 1 && d->So == 1 && (d->S == 1 || d->Cs == d->Cg) && d->K <= 8 && width % 32 == 0 &&
+         nred % 32 == 0 && d->ldo % 8 == 0 && tune(16) != 1;
+  if (p.w3) {
+    p.w3_nt = width % 64 == 0 ? 2 : 1;
+    p.w3_ct = nred % 64 == 0 ? 2 : 1;
+    const int P = p.w3_ct * d->K, WPN = 4 / p.w3_nt;
+    const int RG = P >= WPN ? 1 : WPN / P, WPP = WPN / RG;
+    const int need = (P + WPP - 1) / WPP;
+    p.w3_maxt = need <= 1 ? 1 : need <= 2 ? 2 : need <= 4 ? 4 : 8;
+    p.tiles_per_seq = (d->Tvalid + W3_BM - 1) / W3_BM;
+    const int64_t ntiles = int64_t(d->B) * p.tiles_per_seq;
+    const int64_t blocks = int64_t(width / (32 * p.w3_nt)) * (nred / (32 * p.w3_ct));
+    int64_t want = std::max<int64_t>(1, (512 + blocks - 1) / blocks);
+    want = std::min<int64_t>(want, std::max<int64_t>(1, (int64_t(64) << 20) / (nw * 4)));
+    want = std::min<int64_t>(want, std::max<int64_t>(1, ntiles));
+    p.tiles_per_split = int((ntiles + want - 1) / want);
+    p.nsplit = int((ntiles + p.tiles_per_split - 1) / p.tiles_per_split);
+  } else if (p.mfma) {
     p.nt = width % 32 == 0 ? 2 : 1;
     p.ntg = (d->K + WG_TAPS - 1) / WG_TAPS;
     p.tiles_per_seq = (d->Tvalid + WG_BM - 1) / WG_BM;
@@ -1046,6 +1391,24 @@ hipError_t wgrad_fill(const sel_dconv_desc* d, int dtype, const WgPlanD& p, cons
     if (dtype == SEL_BF16) { SEL_DWS_T(__bf16) } else { SEL_DWS_T(float) }
 #undef SEL_DWS_T
 #undef SEL_DWS
+    return hipGetLastError();
+  }
+  if (p.w3) {
+    const int NB = 32 * p.w3_nt, CB = 32 * p.w3_ct;
+    const size_t lds = 2 * (size_t(p.w3_nt) * W3_BM * 32 + size_t(p.w3_ct) * (W3_BM + W3_HALO) * 32) * sizeof(__bf16);
+    const int64_t ntiles = int64_t(d->B) * p.tiles_per_seq;
+    dim3 grid(unsigned(p.nsplit), unsigned(width / NB), unsigned(nred / CB));
+#define SEL_W3(NT_, CT_, MT_)                                                                                    if (p.w3_nt == NT_ && p.w3_ct == CT_ && p.w3_maxt == MT_) {                                                      auto kern = k_dwgrad_w3<NT_, CT_, MT_>;                                                                        if (lds > 64 * 1024) {                                                                                           const hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,                                                int(lds));                                                            if (e != hipSuccess) return e;                                                                               }                                                                                                              hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, *d, static_cast<const __bf16*>(gout),                                            static_cast<const __bf16*>(x), p.tiles_per_seq, ntiles, p.tiles_per_split, part);         } else
+    SEL_W3(1, 1, 1) SEL_W3(1, 1, 2) SEL_W3(1, 1, 4) SEL_W3(1, 2, 1) SEL_W3(1, 2, 2) SEL_W3(1, 2, 4)
+    SEL_W3(2, 1, 1) SEL_W3(2, 1, 2) SEL_W3(2, 1, 4) SEL_W3(2, 1, 8) SEL_W3(2, 2, 1) SEL_W3(2, 2, 2)
+    SEL_W3(2, 2, 4) SEL_W3(2, 2, 8) { return hipErrorInvalidValue; }
+#undef SEL_W3
+    if (bpart) {
+      const int64_t nb = int64_t(d->G) * width;
+      dim3 bg(unsigned((nb + 63) / 64), unsigned(p.bsplit));
+      hipLaunchKernelGGL(k_dbias_part<__bf16>, bg, dim3(256), 0, s, *d, static_cast<const __bf16*>(gout),
+                         p.brows_per_split, bpart);
+    }
     return hipGetLastError();
   }
   if (p.mfma) {
@@ -1109,7 +1472,8 @@ int sel_dconv_fwd(const sel_dconv_desc* d, int dtype, const void* x, const void*
 
 int sel_dconv_uses_mfma(const sel_dconv_desc* d, int dtype) {
   if (!d || tune(9) == 1) return 0;
-  return mfma_ok(d, dtype) ? 1 : (short_ok(d) ? 2 : 0);
+  if (mfma_ok(d, dtype)) return (d->So * d->Ng > 32 && pf_ok(d, dtype)) ? 3 : 1;
+  return short_ok(d) ? 2 : 0;
 }
 
 size_t sel_dconv_wgrad_workspace(const sel_dconv_desc* d, int dtype) {

@@ -148,7 +148,7 @@ def _meta(d, x, out, tag):
     flops = 2.0 * d.B * d.Tvalid * d.G * width * d.K * d.S * d.Cg
     nbytes = es * (d.B * d.Tvs * d.ldx + d.B * d.Tvo * d.ldo + d.G * width * d.K * d.S * d.Cg)
     mf = L.lib().sel_dconv_uses_mfma(ctypes.byref(d), _code(x.dtype))
-    return (f"k_dconv_{('valu', 'mfma', 'short')[mf]}{tag}", nbytes, flops)
+    return (f"k_dconv_{('valu', 'mfma', 'short', 'pf')[mf]}{tag}", nbytes, flops)
 
 
 def wgrad(sp, desc, gout, x, w_or_v, wg, want_w, want_b):

@@ -310,8 +310,9 @@ typedef struct sel_dconv_desc {
   int32_t act;     /* 0 none, 1 LeakyReLU */
   float slope;     /* LeakyReLU negative slope (nonlinear_activation_params) */
 } sel_dconv_desc;
-/* kernel a launch of this shape uses: 1 matrix cores, 2 short-reduction VALU
- * kernel (1-channel convs), 0 generic VALU kernel */
+/* kernel a launch of this shape uses: 1 matrix cores, 3 matrix cores with the
+ * register prefetch (one group, K <= 8), 2 short-reduction VALU kernel
+ * (1-channel convs), 0 generic VALU kernel */
 int sel_dconv_uses_mfma(const sel_dconv_desc* d, int dtype);
 int sel_dconv_fwd(const sel_dconv_desc* d, int dtype, const void* x, const void* wpack, const float* bias,
                   const void* aux, const void* res, void* out, sel_stream_t stream);
