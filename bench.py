@@ -404,8 +404,23 @@ def stft_kernel_roofline(dev):
 
     t_copy = timed(lambda: dst.copy_(src))
     copy_gbs = 2 * src.numel() * 4 / t_copy / 1e9
-    t = timed(lambda: L.call("sel_stft_mag_fwd", L.ptr(x), B, T, n, h, w, L.ptr(win), 1e-7, L.ptr(mag),
-                             L.stream()))
+
+    def launch():
+        L.call("sel_stft_mag_fwd", L.ptr(x), B, T, n, h, w, L.ptr(win), 1e-7, L.ptr(mag), L.stream())
+
+    # ten launches replayed from one captured graph: back-to-back Python
+    # launches leave ~10 us host gaps between these ~80 us kernels
+    launch()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        launch()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(10):
+            launch()
+    t = timed(g.replay, iters=3) / 10
     nbytes = 4 * B * (T + F * K)
     gbs = nbytes / t / 1e9
     return {"kernel": "k_stft_mag_fwd<10>", "shape": f"B={B} x {T}, n_fft/hop/win {n}/{h}/{w}",

@@ -201,9 +201,13 @@ struct LaneTw {
   float2 nq[NQ ? G::PPL : 1];
   const float2* g1;
   const float2* g2;
+  // table offsets as constants (the recursive constexpr helpers are otherwise
+  // emitted as device calls in the prologue)
+  static constexpr int OFF1 = twp_off(LOGN, 1), OFF2 = twp_off(LOGN, 2), OFF3 = twp_off(LOGN, 3),
+                       OFFN = tw_off(LOGN) + G::M;
   __device__ __forceinline__ void load(int l) {
-    g1 = g_tw + twp_off(LOGN, 1) + (l & (G::NS1 - 1)) * (G::R1 - 1);
-    g2 = g_tw + twp_off(LOGN, 2) + (l & (G::NS2 - 1)) * (G::R2 - 1);
+    g1 = g_tw + OFF1 + (l & (G::NS1 - 1)) * (G::R1 - 1);
+    g2 = g_tw + OFF2 + (l & (G::NS2 - 1)) * (G::R2 - 1);
     if constexpr (RES) {
 #pragma unroll
       for (int r = 1; r < G::R1; ++r) p1[r - 1] = g1[r - 1];
@@ -212,12 +216,12 @@ struct LaneTw {
     }
     if constexpr (G::R3 > 1) {
 #pragma unroll
-      for (int r = 1; r < G::R3; ++r) p3[r - 1] = g_tw[twp_off(LOGN, 3) + (l & (G::NS3 - 1)) * (G::R3 - 1) + r - 1];
+      for (int r = 1; r < G::R3; ++r) p3[r - 1] = g_tw[OFF3 + (l & (G::NS3 - 1)) * (G::R3 - 1) + r - 1];
     }
-    n = g_tw[tw_off(LOGN) + G::M + l];
+    n = g_tw[OFFN + l];
     if constexpr (NQ) {
 #pragma unroll
-      for (int q = 0; q < G::PPL; ++q) nq[q] = g_tw[tw_off(LOGN) + G::M + l + G::LPF * q];
+      for (int q = 0; q < G::PPL; ++q) nq[q] = g_tw[OFFN + l + G::LPF * q];
     }
   }
   __device__ __forceinline__ const float2* t1() const {
@@ -261,7 +265,8 @@ __device__ __forceinline__ void fft_pass_store(float2 (&v)[Geo<LOGN>::PPL], floa
 #pragma unroll
       for (int r = 1; r < R; ++r) {
         float2 t = twb[r - 1];
-        if (NS > G::LPF && u > 0) t = cmul(t, g_tw[twp_off(LOGN, PASS) + kf * (R - 1) + r - 1]);
+        constexpr int OFFP = twp_off(LOGN, PASS);
+        if (NS > G::LPF && u > 0) t = cmul(t, g_tw[OFFP + kf * (R - 1) + r - 1]);
         a[r] = cmul(a[r], t);
       }
     }
@@ -511,13 +516,15 @@ __device__ __forceinline__ float pw(float2 z) { return z.x * z.x + z.y * z.y; }
 
 // Frame ownership: block b, iteration it -> frames (b*iters + it)*FPB + slot;
 // the next frame's samples are fetched before the current one is transformed.
-#define FRAME_PROLOGUE(LOGN, EXTRA_FLOATS)                                          \
+#define FRAME_PROLOGUE(LOGN, EXTRA_FLOATS) FRAME_PROLOGUE_X(LOGN, EXTRA_FLOATS, Geo<LOGN>::FPB)
+// FPBV = frames per block iteration (block size / lanes per frame)
+#define FRAME_PROLOGUE_X(LOGN, EXTRA_FLOATS, FPBV)                                  \
   using G = Geo<LOGN>;                                                              \
   extern __shared__ __align__(16) float2 lds_dyn[];                                 \
   const int slot = threadIdx.x / G::LPF, l = threadIdx.x % G::LPF;                  \
   float2* z = lds_dyn + slot * (G::PADN + (EXTRA_FLOATS) / 2);                      \
   const int nframes = int(a.B * a.F);                                               \
-  const int fr0 = int(blockIdx.x) * iters * G::FPB + slot;                          \
+  const int fr0 = int(blockIdx.x) * iters * (FPBV) + slot;                          \
   Win<LOGN> wn;                                                                     \
   wn.init(window, a, l);                                                            \
   LaneTw<LOGN> tw;                                                                  \
@@ -577,27 +584,229 @@ struct FramePos {
 
 #define FRAME_LOOP_END }
 
+// ---- hand-counted prefetch (|X| kernel) ----------------------------------
+// Loads and stores share vmcnt on gfx950 and retire in issue order
+// (MI355X_MICROARCH §vmcnt), but hipcc treats a counter with both pending as
+// out of order and waits for vmcnt(0) before the prefetched samples are used:
+// every frame then also waits for the previous frame's |X| stores to reach
+// memory.  The prefetch is issued through inline asm (invisible to hipcc's
+// counter model) and waited for by hand with vmcnt(kVmStores): in each
+// iteration the stores of an active frame follow the next frame's loads.
+#ifndef SEL_STFT_VMA
+#define SEL_STFT_VMA 1
+#endif
+typedef float v2f_t __attribute__((ext_vector_type(2)));
+// |X| stores issued after the prefetch by any wave whose frame is active
+constexpr int kVmStores = 8;
+// timing ablations of the |X| kernel: 1 no |X| stores, 2 no FFT,
+// 4 no sample loads, 8 per-wave clock stamps over the first rows; 0 in every build
+#ifndef SEL_STFT_ABL
+#define SEL_STFT_ABL 0
+#endif
+
 template <int LOGN>
-__global__ __launch_bounds__(256) SEL_FFT_OCC void k_stft_mag_fwd(const float* __restrict__ x, FrameArgs a,
-                                                      const float* __restrict__ window, float floor_,
-                                                      float* __restrict__ mag, int iters) {
-  FRAME_PROLOGUE(LOGN, 0)
-  FRAME_LOOP_BEGIN(x, raw, SEL_PF)
-  (void)f;
-  fft_half<LOGN>(v, z, l, tw);
-  float pwr[G::PPL], pmid;
-  split_pairs<LOGN>(z, l, tw, pwr, pmid);
-  if (active) {
-    constexpr int K = G::M + 1, H = G::PPL / 2;
-    float* out = mag + fr * K;
+__device__ __forceinline__ void fetch_frame_vm(const float* __restrict__ x, __amdgpu_buffer_rsrc_t xr,
+                                               const FrameArgs& a, int b, int f, int l, bool active,
+                                               v2f_t (&raw)[8]) {
+  using G = Geo<LOGN>;
+  static_assert(G::PPL == 8 && G::LPF * 8 * 7 < 4096, "immediate offsets");
+  constexpr int S = G::LPF * 8;  // bytes between a lane's consecutive points
+  const int T = int(a.T);
+  const int base = f * a.hop - a.P;
+  const int sig = b * T;
+  const float* xs = x + sig + base;
+  if (active && base >= 0 && base + G::N <= T && (reinterpret_cast<uintptr_t>(xs) & 7) == 0) {
+    const float2* p = reinterpret_cast<const float2*>(xs) + l;
+    asm volatile(
+        "global_load_dwordx2 %0, %8, off\n\t"
+        "global_load_dwordx2 %1, %8, off offset:%9\n\t"
+        "global_load_dwordx2 %2, %8, off offset:%10\n\t"
+        "global_load_dwordx2 %3, %8, off offset:%11\n\t"
+        "global_load_dwordx2 %4, %8, off offset:%12\n\t"
+        "global_load_dwordx2 %5, %8, off offset:%13\n\t"
+        "global_load_dwordx2 %6, %8, off offset:%14\n\t"
+        "global_load_dwordx2 %7, %8, off offset:%15"
+        : "=&v"(raw[0]), "=&v"(raw[1]), "=&v"(raw[2]), "=&v"(raw[3]), "=&v"(raw[4]), "=&v"(raw[5]),
+          "=&v"(raw[6]), "=&v"(raw[7])
+        : "v"(p), "i"(S), "i"(2 * S), "i"(3 * S), "i"(4 * S), "i"(5 * S), "i"(6 * S), "i"(7 * S)
+        : "memory");
+  } else if (active) {
+    unsigned o[16];
 #pragma unroll
-    for (int q = 0; q < H; ++q) {
-      out[l + G::LPF * q] = clamp_sqrt(pwr[q], floor_);
-      out[G::M - l - G::LPF * q] = clamp_sqrt(pwr[H + q], floor_);
+    for (int q = 0; q < 8; ++q) {
+      int n0 = abs(base + 2 * (l + G::LPF * q)), n1 = abs(base + 2 * (l + G::LPF * q) + 1);
+      n0 = min(n0, 2 * (T - 1) - n0);
+      n1 = min(n1, 2 * (T - 1) - n1);
+      o[2 * q] = unsigned(sig + n0) * 4u;
+      o[2 * q + 1] = unsigned(sig + n1) * 4u;
     }
-    if (l == 0) out[G::M / 2] = clamp_sqrt(pmid, floor_);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      float r[8];
+      asm volatile(
+          "buffer_load_dword %0, %8, %16, 0 offen\n\t"
+          "buffer_load_dword %1, %9, %16, 0 offen\n\t"
+          "buffer_load_dword %2, %10, %16, 0 offen\n\t"
+          "buffer_load_dword %3, %11, %16, 0 offen\n\t"
+          "buffer_load_dword %4, %12, %16, 0 offen\n\t"
+          "buffer_load_dword %5, %13, %16, 0 offen\n\t"
+          "buffer_load_dword %6, %14, %16, 0 offen\n\t"
+          "buffer_load_dword %7, %15, %16, 0 offen"
+          : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]), "=&v"(r[5]), "=&v"(r[6]),
+            "=&v"(r[7])
+          : "v"(o[8 * h]), "v"(o[8 * h + 1]), "v"(o[8 * h + 2]), "v"(o[8 * h + 3]), "v"(o[8 * h + 4]),
+            "v"(o[8 * h + 5]), "v"(o[8 * h + 6]), "v"(o[8 * h + 7]), "s"(xr)
+          : "memory");
+#pragma unroll
+      for (int q = 0; q < 4; ++q) raw[4 * h + q] = v2f_t{r[2 * q], r[2 * q + 1]};
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) raw[q] = v2f_t{0.f, 0.f};
   }
-  FRAME_LOOP_END
+}
+
+// the prefetched samples are in registers once at most N younger vector-memory
+// operations are pending; the "+v" ties keep every use of raw[] below this point
+template <int N>
+__device__ __forceinline__ void vm_wait_raw(v2f_t (&raw)[8]) {
+  asm volatile("s_waitcnt vmcnt(%8)"
+               : "+v"(raw[0]), "+v"(raw[1]), "+v"(raw[2]), "+v"(raw[3]), "+v"(raw[4]), "+v"(raw[5]), "+v"(raw[6]),
+                 "+v"(raw[7])
+               : "i"(N)
+               : "memory");
+}
+
+// Frames of wave unit u (FPW consecutive frames, lane slot sw): the unit index
+// is wave-uniform, so the division by F runs on the scalar unit.
+__device__ __forceinline__ FramePos unit_pos(int u, int FPW, int sw, int nframes, int F) {
+  FramePos p;
+  const int base = u * FPW, b0 = base / F;
+  p.fr = base + sw;
+  p.active = p.fr < nframes;
+  p.b = b0;
+  p.f = base - b0 * F + sw;
+  while (p.f >= F) {  // sw < FPW <= 4: at most a few rounds
+    p.f -= F;
+    ++p.b;
+  }
+  if (!p.active) p.b = p.f = 0;
+  return p;
+}
+
+// Block size of the |X| kernel where a frame fits one wave: one 1024-lane block
+// per CU.  The SQ arbitrates issue by priority, then age, so with a static
+// frame split the first-dispatched waves of a SIMD finish early and the CU ends
+// on one or two latency-bound waves (per-wave stamps at B = 512, 1024/120/600:
+// blocks of 4 waves took 51.7 / 57.1 / 65.5 / 73.2 us by dispatch rank on their
+// CU); in one block the CU's 16 waves draw frames from one LDS counter and
+// finish together.
+#ifndef SEL_STFT_BS
+#define SEL_STFT_BS 1024
+#endif
+template <int LOGN>
+constexpr int mag_block() {
+  return (SEL_STFT_VMA && Geo<LOGN>::LPF <= 64) ? SEL_STFT_BS : 256;
+}
+
+template <int LOGN, int BS = mag_block<LOGN>()>
+__global__ __launch_bounds__(BS) SEL_FFT_OCC void k_stft_mag_fwd(const float* __restrict__ x, FrameArgs a,
+                                                     const float* __restrict__ window, float floor_,
+                                                     float* __restrict__ mag, int iters) {
+  constexpr int FPBB = BS / Geo<LOGN>::LPF;
+  FRAME_PROLOGUE_X(LOGN, 0, FPBB)
+  constexpr int K = G::M + 1, H = G::PPL / 2;
+  if constexpr (SEL_STFT_VMA && G::PPL == 8 && G::LPF <= 64) {
+    // wave units of FPW frames; the block owns units [ub, ue) and its waves
+    // take them in turn from an LDS counter (first one each by wave index)
+    constexpr int FPW = 64 / G::LPF, WPB = BS / 64;
+    __shared__ unsigned s_next;
+    if (threadIdx.x == 0) s_next = 0;
+    __syncthreads();
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / 64), sw = (threadIdx.x % 64) / G::LPF;
+    const int ub = int(blockIdx.x) * iters * WPB;
+    const int ue = min(ub + iters * WPB, (nframes + FPW - 1) / FPW);
+    v2f_t raw[8];
+    const __amdgpu_buffer_rsrc_t xr = signal_rsrc(x, a);
+    int u = ub + wid;
+    FramePos P = unit_pos(u, FPW, sw, nframes, a.F);
+    if (u < ue) fetch_frame_vm<LOGN>(x, xr, a, P.b, P.f, l, P.active && !(SEL_STFT_ABL & 4), raw);
+    vm_wait_raw<0>(raw);
+    [[maybe_unused]] uint64_t t0 = 0, r0 = 0;
+    if constexpr ((SEL_STFT_ABL & 8) != 0) {
+      t0 = __builtin_amdgcn_s_memtime();
+      r0 = __builtin_amdgcn_s_memrealtime();
+    }
+    while (u < ue) {
+      float2 v[G::PPL];
+#pragma unroll
+      for (int q = 0; q < G::PPL; ++q) {
+        const float2 w = wn.get(q);
+        v[q] = make_float2(raw[q].x * w.x, raw[q].y * w.y);
+      }
+      unsigned tk = 0;
+      if (threadIdx.x % 64 == 0) tk = atomicAdd(&s_next, 1u);
+      const int un = ub + WPB + __builtin_amdgcn_readlane(int(tk), 0);
+      const bool pf = un < ue;
+      const FramePos cur = P;
+      if (pf) {
+        P = unit_pos(un, FPW, sw, nframes, a.F);
+        fetch_frame_vm<LOGN>(x, xr, a, P.b, P.f, l, P.active && !(SEL_STFT_ABL & 4), raw);
+      }
+      float pwr[G::PPL], pmid;
+      if constexpr ((SEL_STFT_ABL & 2) != 0) {
+#pragma unroll
+        for (int q = 0; q < G::PPL; ++q) pwr[q] = v[q].x * v[q].x + v[q].y * v[q].y;
+        pmid = pwr[0];
+      } else {
+        fft_half<LOGN>(v, z, l, tw);
+        split_pairs<LOGN>(z, l, tw, pwr, pmid);
+      }
+      if (cur.active && !(SEL_STFT_ABL & 1)) {
+        float* out = mag + int64_t(cur.fr) * K;
+#pragma unroll
+        for (int q = 0; q < H; ++q) {
+          out[l + G::LPF * q] = clamp_sqrt(pwr[q], floor_);
+          out[G::M - l - G::LPF * q] = clamp_sqrt(pwr[H + q], floor_);
+        }
+        if (l == 0) out[G::M / 2] = clamp_sqrt(pmid, floor_);
+      }
+      if (pf) vm_wait_raw<(SEL_STFT_ABL & 1) ? 0 : kVmStores>(raw);
+      u = un;
+    }
+    if constexpr ((SEL_STFT_ABL & 8) != 0) {  // per-wave shader-clock / 100 MHz stamps over the frame loop
+      const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+      __syncthreads();
+      if (threadIdx.x % 64 == 0) {
+        uint64_t* st = reinterpret_cast<uint64_t*>(mag) + (size_t(blockIdx.x) * (BS / 64) + threadIdx.x / 64) * 8;
+        st[0] = t0;
+        st[1] = t1;
+        st[2] = r0;
+        st[3] = r1;
+        st[4] = __builtin_amdgcn_s_getreg(0xF804);  // HW_ID: simd [5:4], cu [11:8], sh [12], se [15:13]
+        st[5] = __builtin_amdgcn_s_getreg((15 << 11) | 20);  // XCC_ID
+        st[6] = blockIdx.x;
+        st[7] = 0x5354465453544654ull;  // record marker
+      }
+    }
+  } else {
+    static_assert(BS == 256, "FRAME_LOOP_BEGIN advances by Geo::FPB");
+    FRAME_LOOP_BEGIN(x, raw, SEL_PF)
+    (void)f;
+    fft_half<LOGN>(v, z, l, tw);
+    float pwr[G::PPL], pmid;
+    split_pairs<LOGN>(z, l, tw, pwr, pmid);
+    if (active) {
+      float* out = mag + fr * K;
+#pragma unroll
+      for (int q = 0; q < H; ++q) {
+        out[l + G::LPF * q] = clamp_sqrt(pwr[q], floor_);
+        out[G::M - l - G::LPF * q] = clamp_sqrt(pwr[H + q], floor_);
+      }
+      if (l == 0) out[G::M / 2] = clamp_sqrt(pmid, floor_);
+    }
+    FRAME_LOOP_END
+  }
 }
 
 template <int LOGN>
@@ -1008,9 +1217,8 @@ FrameArgs frame_args(int64_t B, int64_t T, int n_fft, int hop, int win) {
 // B = 512, 1024/120/600: 117 us at 8 iters -> 98-100 us).  tune key 14: -1 = the
 // earlier rule (<= 8 iters, >= 2048 groups per iter), > 0 = fixed iters.
 template <int LOGN>
-unsigned frame_grid(int64_t nframes, int& iters, int64_t slots = 0) {
-  using G = Geo<LOGN>;
-  const int64_t groups = (nframes + G::FPB - 1) / G::FPB;
+unsigned frame_grid(int64_t nframes, int& iters, int64_t slots = 0, int fpb = Geo<LOGN>::FPB) {
+  const int64_t groups = (nframes + fpb - 1) / fpb;
   if (tune(14) > 0) {
     iters = tune(14);
   } else if (tune(14) == -1 || slots <= 0) {
@@ -1027,11 +1235,11 @@ thread_local unsigned t_last_frame_grid = 0;
 // resident-block capacity of a frame kernel at `lds` bytes per block (cached
 // per call site by the dispatch macro)
 template <typename KerT>
-int64_t frame_slots(KerT ker, size_t lds) {
+int64_t frame_slots(KerT ker, size_t lds, int block = 256) {
   int dev = 0, cus = 0, per_cu = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ker, 256, lds) != hipSuccess)
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ker, block, lds) != hipSuccess)
     return 0;
   return int64_t(cus) * per_cu;
 }
@@ -1104,7 +1312,27 @@ int sel_stft_mag_fwd(const float* x, int64_t B, int64_t T, int n_fft, int hop, i
   const FrameArgs a = frame_args(B, T, n_fft, hop, win_length);
   const int64_t nf = B * a.F;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  SEL_FRAME_DISPATCH(logn, nf, s, k_stft_mag_fwd, x, a, window, pow_floor, mag);
+  switch (logn) {
+#define SEL_MAG_CASE(L)                                                                                   \
+    case L: {                                                                                             \
+      constexpr int BS = mag_block<L>(), FPBB = BS / Geo<L>::LPF;                                         \
+      int iters;                                                                                          \
+      const size_t lds = size_t(FPBB) * Geo<L>::PADN * sizeof(float2);                                    \
+      static const int64_t slots = frame_slots(k_stft_mag_fwd<L, BS>, lds, BS);                           \
+      const unsigned grid = frame_grid<L>(nf, iters, slots, FPBB);                                        \
+      if (grid) hipLaunchKernelGGL((k_stft_mag_fwd<L, BS>), dim3(grid), dim3(BS), lds, s, x, a, window, pow_floor, \
+                                   mag, iters);                                                           \
+    } break;
+    SEL_MAG_CASE(8)
+    SEL_MAG_CASE(9)
+    SEL_MAG_CASE(10)
+    SEL_MAG_CASE(11)
+#undef SEL_MAG_CASE
+    default:
+      ::sel::set_error("unsupported log2(n_fft)=%d", logn);
+      return SEL_ERR_UNSUPPORTED;
+  }
+  SEL_LAUNCH_CHECK();
   return SEL_OK;
 }
 
