@@ -408,19 +408,18 @@ def stft_kernel_roofline(dev):
     def launch():
         L.call("sel_stft_mag_fwd", L.ptr(x), B, T, n, h, w, L.ptr(win), 1e-7, L.ptr(mag), L.stream())
 
-    # ten launches replayed from one captured graph: back-to-back Python
-    # launches leave ~10 us host gaps between these ~80 us kernels
-    launch()
-    s = torch.cuda.Stream()
-    s.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(s):
+    # average launch duration: a HIP event pair around each of ten launches
+    # (back-to-back Python launches leave host gaps between these ~80 us kernels,
+    # which an event pair around the whole loop would count)
+    for _ in range(2):
         launch()
-    torch.cuda.current_stream().wait_stream(s)
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
-        for _ in range(10):
-            launch()
-    t = timed(g.replay, iters=3) / 10
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(10)]
+    for e0, e1 in ev:
+        e0.record()
+        launch()
+        e1.record()
+    torch.cuda.synchronize()
+    t = sum(e0.elapsed_time(e1) for e0, e1 in ev) / len(ev) * 1e-3
     nbytes = 4 * B * (T + F * K)
     gbs = nbytes / t / 1e9
     return {"kernel": "k_stft_mag_fwd<10>", "shape": f"B={B} x {T}, n_fft/hop/win {n}/{h}/{w}",

@@ -419,6 +419,16 @@ __device__ __forceinline__ void real_split(const float2* z, int l, const LaneTw<
 // X_{M-k} = conj(e_k - W^k o_k) while X_k = e_k + W^k o_k; p[q] <- |X_k|^2,
 // p[PPL/2 + q] <- |X_{M-k}|^2 (k = 0 pairs with the Nyquist bin M), and pmid <-
 // |X_{M/2}|^2 = |Z_{M/2}|^2 (valid on l == 0).
+// |X_k|^2 and |X_{M-k}|^2 of one bin pair from Z_k, Z_{M-k} and W_N^k
+__device__ __forceinline__ void pair_power(float2 zk, float2 zm, float2 w, float& pk, float& pm) {
+  const float ex = zk.x + zm.x, ey = zk.y - zm.y;  // 2 e_k
+  const float ox = zk.y + zm.y, oy = zm.x - zk.x;  // 2 o_k
+  const float wox = w.x * ox - w.y * oy, woy = w.x * oy + w.y * ox;
+  const float ax = ex + wox, ay = ey + woy, bx = ex - wox, by = ey - woy;
+  pk = 0.25f * (ax * ax + ay * ay);
+  pm = 0.25f * (bx * bx + by * by);
+}
+
 template <int LOGN>
 __device__ __forceinline__ void split_pairs(const float2* z, int l, const LaneTw<LOGN>& tw,
                                             float (&p)[Geo<LOGN>::PPL], float& pmid) {
@@ -428,18 +438,83 @@ __device__ __forceinline__ void split_pairs(const float2* z, int l, const LaneTw
 #pragma unroll
   for (int q = 0; q < H; ++q) {
     const int im = q == 0 ? (l == 0 ? 0 : padd(pn, -l, M)) : padd(pn, -l, M - G::LPF * q);
-    const float2 zk = z[padd(pl, l, G::LPF * q)], zm = z[im];
-    const float ex = zk.x + zm.x, ey = zk.y - zm.y;  // 2 e_k
-    const float ox = zk.y + zm.y, oy = zm.x - zk.x;  // 2 o_k
-    const float2 w = split_tw<LOGN>(tw, q);
-    const float wox = w.x * ox - w.y * oy, woy = w.x * oy + w.y * ox;
-    const float ax = ex + wox, ay = ey + woy, bx = ex - wox, by = ey - woy;
-    p[q] = 0.25f * (ax * ax + ay * ay);
-    p[H + q] = 0.25f * (bx * bx + by * by);
+    pair_power(z[padd(pl, l, G::LPF * q)], z[im], split_tw<LOGN>(tw, q), p[q], p[H + q]);
   }
   const float2 zc = z[pidx(M / 2)];
   pmid = zc.x * zc.x + zc.y * zc.y;
   frame_fence<LOGN>();
+}
+
+// The last Stockham pass in registers: the same butterflies as
+// fft_pass_store, written back to v in place (the pass's input point q = u +
+// r*NB and output r of butterfly u share a register), so for the final pass
+// (NS = M/R, j < NS) v[m] = Z[l + LPF*m].
+template <int LOGN, int R, int NS, int PASS>
+__device__ __forceinline__ void fft_pass_reg(float2 (&v)[Geo<LOGN>::PPL], int l, const float2* twb) {
+  using G = Geo<LOGN>;
+  constexpr int NB = G::PPL / R;
+  static_assert(NS * R == G::M && NS >= G::LPF * NB, "final pass: j < NS");
+#pragma unroll
+  for (int u = 0; u < NB; ++u) {
+    float2 a[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) a[r] = v[u + r * NB];
+    const int kf = (G::LPF * u) & (NS - 1);
+#pragma unroll
+    for (int r = 1; r < R; ++r) {
+      float2 t = twb[r - 1];
+      constexpr int OFFP = twp_off(LOGN, PASS);
+      if (NS > G::LPF && u > 0) t = cmul(t, g_tw[OFFP + kf * (R - 1) + r - 1]);
+      a[r] = cmul(a[r], t);
+    }
+    dft<R>(a);
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[u + r * NB] = a[r];
+  }
+}
+
+__device__ __forceinline__ float2 bpermute2(int addr, float2 x) {
+  return make_float2(__builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(addr, __builtin_bit_cast(int, x.x))),
+                     __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(addr, __builtin_bit_cast(int, x.y))));
+}
+
+// FFT + bin-pair powers (split_pairs' outputs).  Where a frame fits one wave the
+// last pass stays in registers: lane l's Z_{l+LPF m} pairs with Z_{M-l-LPF m},
+// register 7 - m of lane LPF - l (lane 0: its own register (8 - m) mod 8), so 8
+// ds_bpermute replace the last pass's LDS store and the pair reads.
+#ifndef SEL_FFT_REGPAIRS
+#define SEL_FFT_REGPAIRS 1
+#endif
+// REG = false keeps the LDS form (the fused loss forward: +16 VGPRs past the
+// 4-wave budget with two spectra live, measured 195 -> 203 us at B = 512)
+template <int LOGN, bool REG = true>
+__device__ __forceinline__ void fft_pairs(float2 (&v)[Geo<LOGN>::PPL], float2* z, int l, const LaneTw<LOGN>& tw,
+                                          float (&p)[Geo<LOGN>::PPL], float& pmid) {
+  using G = Geo<LOGN>;
+  if constexpr (SEL_FFT_REGPAIRS && REG && G::LPF <= 64 && G::NP == 3 && G::PPL == 8) {
+    constexpr int H = G::PPL / 2;
+    fft_pass_store<LOGN, G::R0, 1, 0>(v, z, l, nullptr);
+    frame_fence<LOGN>();
+    fft_pass_load<LOGN, G::R1>(v, z, l);
+    frame_fence<LOGN>();
+    fft_pass_store<LOGN, G::R1, G::NS1, 1>(v, z, l, tw.t1());
+    frame_fence<LOGN>();
+    fft_pass_load<LOGN, G::R2>(v, z, l);
+    frame_fence<LOGN>();
+    fft_pass_reg<LOGN, G::R2, G::NS2, 2>(v, l, tw.t2());
+    const int lane = int(threadIdx.x % 64);
+    const int addr = 4 * (lane - l + ((G::LPF - l) & (G::LPF - 1)));
+#pragma unroll
+    for (int q = 0; q < H; ++q) {
+      const float2 pm = bpermute2(addr, v[7 - q]);
+      const float2 zm = l == 0 ? v[(8 - q) & 7] : pm;
+      pair_power(v[q], zm, split_tw<LOGN>(tw, q), p[q], p[H + q]);
+    }
+    pmid = v[4].x * v[4].x + v[4].y * v[4].y;
+  } else {
+    fft_half<LOGN>(v, z, l, tw);
+    split_pairs<LOGN>(z, l, tw, p, pmid);
+  }
 }
 
 // Gradient through real_split + FFT: given G_k for this lane's bins (Gq[q],
@@ -759,8 +834,7 @@ __global__ __launch_bounds__(BS) SEL_FFT_OCC void k_stft_mag_fwd(const float* __
         for (int q = 0; q < G::PPL; ++q) pwr[q] = v[q].x * v[q].x + v[q].y * v[q].y;
         pmid = pwr[0];
       } else {
-        fft_half<LOGN>(v, z, l, tw);
-        split_pairs<LOGN>(z, l, tw, pwr, pmid);
+        fft_pairs<LOGN>(v, z, l, tw, pwr, pmid);
       }
       if (cur.active && !(SEL_STFT_ABL & 1)) {
         float* out = mag + int64_t(cur.fr) * K;
@@ -844,14 +918,14 @@ template <int LOGN, bool PAIRED>
 __device__ __forceinline__ void ref_mag(float2 (&v)[Geo<LOGN>::PPL], int l, float2* z, const LaneTw<LOGN>& tw,
                                         float floor_, float (&ym)[Geo<LOGN>::PPL + 1]) {
   using G = Geo<LOGN>;
-  fft_half<LOGN>(v, z, l, tw);
   if constexpr (PAIRED) {  // split_pairs' bins (the fused forward)
     float pwr[G::PPL], pmid;
-    split_pairs<LOGN>(z, l, tw, pwr, pmid);
+    fft_pairs<LOGN, false>(v, z, l, tw, pwr, pmid);
 #pragma unroll
     for (int q = 0; q < G::PPL; ++q) ym[q] = clamp_sqrt(pwr[q], floor_);
     ym[G::PPL] = clamp_sqrt(pmid, floor_);
   } else {  // real_split's bins k = l + LPF*q, then M (the backward)
+    fft_half<LOGN>(v, z, l, tw);
     float2 X[G::PPL], XM;
     real_split<LOGN>(z, l, tw, X, XM);
 #pragma unroll
@@ -885,9 +959,8 @@ __global__ __launch_bounds__(256) SEL_FFT_OCC void k_stft_loss_fwd(const float* 
   Y_FRAME(vy)
   float ym[G::PPL + 1];
   ref_mag<LOGN, true>(vy, l, z, tw, floor_, ym);
-  fft_half<LOGN>(v, z, l, tw);
   float pwr[G::PPL], pmid;
-  split_pairs<LOGN>(z, l, tw, pwr, pmid);  // same bin pairing as ref_mag's ym
+  fft_pairs<LOGN, false>(v, z, l, tw, pwr, pmid);  // same bin pairing as ref_mag's ym
   if (active) {
 #pragma unroll
     for (int q = 0; q <= G::PPL; ++q) {
@@ -966,9 +1039,8 @@ __global__ __launch_bounds__(256) SEL_FFT_OCC void k_logmel_fwd(const float* __r
   float* magb = reinterpret_cast<float*>(z);
   FRAME_LOOP_BEGIN(x, raw, SEL_PF)
   (void)fr;
-  fft_half<LOGN>(v, z, l, tw);
   float pwr[G::PPL], pmid;
-  split_pairs<LOGN>(z, l, tw, pwr, pmid);
+  fft_pairs<LOGN>(v, z, l, tw, pwr, pmid);
 #pragma unroll
   for (int q = 0; q < G::PPL / 2; ++q) {
     magb[l + G::LPF * q] = clamp_sqrt(pwr[q], ma.eps);
