@@ -1104,6 +1104,25 @@ __device__ __forceinline__ int64_t off4(const View4& v, const Idx4& x) {
          int64_t(x.i3) * v.stride[3];
 }
 
+// per-element loss term and its derivative (times coef c)
+__device__ __forceinline__ float gan_val(int kind, float x, float y, float target) {
+  if (kind == 0) return fabsf(x - y);                  // L1
+  if (kind == 1) return (x - target) * (x - target);   // MSE to target
+  if (kind == 2) return fminf(x - 1.f, 0.f);           // hinge real: min(x - 1, 0)
+  if (kind == 3) return fminf(-x - 1.f, 0.f);          // hinge fake: min(-x - 1, 0)
+  return x;                                            // plain sum (generator hinge: -mean)
+}
+__device__ __forceinline__ float gan_dval(int kind, float x, float y, float target, float c) {
+  if (kind == 0) {
+    const float dlt = x - y;
+    return dlt > 0.f ? c : (dlt < 0.f ? -c : 0.f);
+  }
+  if (kind == 1) return 2.f * (x - target) * c;
+  if (kind == 2) return x - 1.f < 0.f ? c : 0.f;
+  if (kind == 3) return -x - 1.f < 0.f ? -c : 0.f;
+  return c;
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void k_gan_reduce(int kind, const T* __restrict__ a, View4 va,
                                                     const T* __restrict__ b, View4 vb, float target, int64_t n,
@@ -1113,13 +1132,36 @@ __global__ __launch_bounds__(256) void k_gan_reduce(int kind, const T* __restric
   for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256) {
     const Idx4 ix = unflat(va, uint32_t(i));
     const float x = to_f(a[off4(va, ix)]);
-    float v;
-    if (kind == 0) v = fabsf(x - to_f(b[off4(vb, ix)]));  // L1
-    else if (kind == 1) v = (x - target) * (x - target);  // MSE to target
-    else if (kind == 2) v = fminf(x - 1.f, 0.f);          // hinge real: min(x - 1, 0)
-    else if (kind == 3) v = fminf(-x - 1.f, 0.f);         // hinge fake: min(-x - 1, 0)
-    else v = x;                                           // plain sum (generator hinge: -mean)
-    s += v;
+    s += gan_val(kind, x, kind == 0 ? to_f(b[off4(vb, ix)]) : 0.f, target);
+  }
+  const double t = block_sum(double(s), red);
+  if (threadIdx.x == 0) partials[blockIdx.x] = t;
+}
+
+// 16-B vector forms: every view's last dim contiguous with a multiple of V = 16 /
+// sizeof(T) elements, the other strides multiples of V and the bases 16-B
+// aligned (the channels-last feature maps): one index decomposition and one
+// 16-B load per V elements instead of per element
+template <typename T>
+struct Vec16 {
+  static constexpr int V = 16 / sizeof(T);
+  T v[V];
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_gan_reduce_v(int kind, const T* __restrict__ a, View4 va,
+                                                      const T* __restrict__ b, View4 vb, float target, uint32_t nv,
+                                                      double* __restrict__ partials) {
+  constexpr int V = Vec16<T>::V;
+  __shared__ double red[16];
+  float s = 0.f;
+  for (uint32_t iv = blockIdx.x * 256u + threadIdx.x; iv < nv; iv += gridDim.x * 256u) {
+    const Idx4 ix = unflat(va, iv * V);
+    const Vec16<T> xa = *reinterpret_cast<const Vec16<T>*>(a + off4(va, ix));
+    Vec16<T> xb;
+    if (kind == 0) xb = *reinterpret_cast<const Vec16<T>*>(b + off4(vb, ix));
+#pragma unroll
+    for (int e = 0; e < V; ++e) s += gan_val(kind, to_f(xa.v[e]), kind == 0 ? to_f(xb.v[e]) : 0.f, target);
   }
   const double t = block_sum(double(s), red);
   if (threadIdx.x == 0) partials[blockIdx.x] = t;
@@ -1144,22 +1186,41 @@ __global__ __launch_bounds__(256) void k_gan_grad(int kind, const T* __restrict_
   for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256) {
     const Idx4 ix = unflat(va, uint32_t(i));
     const float x = to_f(a[off4(va, ix)]);
-    float gv;
-    if (kind == 0) {
-      const float dlt = x - to_f(b[off4(vb, ix)]);
-      gv = dlt > 0.f ? c : (dlt < 0.f ? -c : 0.f);
-    } else if (kind == 1) {
-      gv = 2.f * (x - target) * c;
-    } else if (kind == 2) {
-      gv = x - 1.f < 0.f ? c : 0.f;
-    } else if (kind == 3) {
-      gv = -x - 1.f < 0.f ? -c : 0.f;
-    } else {
-      gv = c;
-    }
+    const float gv = gan_dval(kind, x, kind == 0 ? to_f(b[off4(vb, ix)]) : 0.f, target, c);
     const int64_t o = off4(vg, ix);
     grad[o] = from_f<T>(accumulate ? to_f(grad[o]) + gv : gv);
   }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_gan_grad_v(int kind, const T* __restrict__ a, View4 va,
+                                                    const T* __restrict__ b, View4 vb, float target, uint32_t nv,
+                                                    const float* __restrict__ gscale, float mult,
+                                                    T* __restrict__ grad, View4 vg, int accumulate) {
+  constexpr int V = Vec16<T>::V;
+  const float c = gscale[0] * mult;
+  for (uint32_t iv = blockIdx.x * 256u + threadIdx.x; iv < nv; iv += gridDim.x * 256u) {
+    const Idx4 ix = unflat(va, iv * V);
+    const Vec16<T> xa = *reinterpret_cast<const Vec16<T>*>(a + off4(va, ix));
+    Vec16<T> xb, go;
+    if (kind == 0) xb = *reinterpret_cast<const Vec16<T>*>(b + off4(vb, ix));
+    Vec16<T>* gp = reinterpret_cast<Vec16<T>*>(grad + off4(vg, ix));
+    if (accumulate) go = *gp;
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      const float gv = gan_dval(kind, to_f(xa.v[e]), kind == 0 ? to_f(xb.v[e]) : 0.f, target, c);
+      go.v[e] = from_f<T>(accumulate ? to_f(go.v[e]) + gv : gv);
+    }
+    *gp = go;
+  }
+}
+
+// the 16-B vector kernels apply to this view (see Vec16)
+template <typename T>
+bool vec_view(const void* base, const View4& v) {
+  constexpr int V = 16 / sizeof(T);
+  return (reinterpret_cast<uintptr_t>(base) & 15) == 0 && v.stride[3] == 1 && v.size[3] % V == 0 &&
+         v.stride[0] % V == 0 && v.stride[1] % V == 0 && v.stride[2] % V == 0;
 }
 
 }  // namespace dconv
@@ -1609,14 +1670,25 @@ int sel_gan_reduce(int kind, int dtype, const void* a, const int64_t* a_size, co
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const View4 va = to_view(a_size, a_stride, ndim);
   const View4 vb = kind == 0 ? to_view(b_size, b_stride, ndim) : va;
-  const int nb = int(std::min<int64_t>(1024, std::max<int64_t>(1, (n + 255) / 256)));
   double* part = static_cast<double*>(ws);
-  if (dtype == SEL_BF16)
+  const void* bb = b ? b : a;
+  const bool vec = dtype == SEL_BF16 ? vec_view<__bf16>(a, va) && (kind != 0 || vec_view<__bf16>(bb, vb))
+                                     : vec_view<float>(a, va) && (kind != 0 || vec_view<float>(bb, vb));
+  const int vw = dtype == SEL_BF16 ? 8 : 4;
+  const int64_t nt = vec ? n / vw : n;  // threads' work items
+  const int nb = int(std::min<int64_t>(1024, std::max<int64_t>(1, (nt + 255) / 256)));
+  if (dtype == SEL_BF16 && vec)
+    hipLaunchKernelGGL(k_gan_reduce_v<__bf16>, dim3(nb), dim3(256), 0, s, kind, static_cast<const __bf16*>(a), va,
+                       static_cast<const __bf16*>(bb), vb, target, uint32_t(nt), part);
+  else if (dtype == SEL_BF16)
     hipLaunchKernelGGL(k_gan_reduce<__bf16>, dim3(nb), dim3(256), 0, s, kind, static_cast<const __bf16*>(a), va,
-                       static_cast<const __bf16*>(b ? b : a), vb, target, n, part);
+                       static_cast<const __bf16*>(bb), vb, target, n, part);
+  else if (vec)
+    hipLaunchKernelGGL(k_gan_reduce_v<float>, dim3(nb), dim3(256), 0, s, kind, static_cast<const float*>(a), va,
+                       static_cast<const float*>(bb), vb, target, uint32_t(nt), part);
   else
     hipLaunchKernelGGL(k_gan_reduce<float>, dim3(nb), dim3(256), 0, s, kind, static_cast<const float*>(a), va,
-                       static_cast<const float*>(b ? b : a), vb, target, n, part);
+                       static_cast<const float*>(bb), vb, target, n, part);
   hipLaunchKernelGGL(k_gan_finish, dim3(1), dim3(256), 0, s, part, nb, scale, out, accumulate);
   SEL_LAUNCH_CHECK();
   return SEL_OK;
@@ -1636,8 +1708,22 @@ int sel_gan_grad(int kind, int dtype, const void* a, const int64_t* a_size, cons
   const View4 va = to_view(a_size, a_stride, ndim);
   const View4 vb = kind == 0 ? to_view(b_size, b_stride, ndim) : va;
   const View4 vg = to_view(a_size, g_stride, ndim);
-  const unsigned nb = unsigned(launch_blocks(n));
-  if (dtype == SEL_BF16)
+  const void* bb = b ? b : a;
+  const bool vec = dtype == SEL_BF16 ? vec_view<__bf16>(a, va) && vec_view<__bf16>(grad, vg) &&
+                                           (kind != 0 || vec_view<__bf16>(bb, vb))
+                                     : vec_view<float>(a, va) && vec_view<float>(grad, vg) &&
+                                           (kind != 0 || vec_view<float>(bb, vb));
+  const int64_t nt = vec ? n / (dtype == SEL_BF16 ? 8 : 4) : n;
+  const unsigned nb = unsigned(launch_blocks(nt));
+  if (dtype == SEL_BF16 && vec)
+    hipLaunchKernelGGL(k_gan_grad_v<__bf16>, dim3(nb), dim3(256), 0, s, kind, static_cast<const __bf16*>(a), va,
+                       static_cast<const __bf16*>(bb), vb, target, uint32_t(nt), gscale, mult,
+                       static_cast<__bf16*>(grad), vg, accumulate);
+  else if (vec)
+    hipLaunchKernelGGL(k_gan_grad_v<float>, dim3(nb), dim3(256), 0, s, kind, static_cast<const float*>(a), va,
+                       static_cast<const float*>(bb), vb, target, uint32_t(nt), gscale, mult,
+                       static_cast<float*>(grad), vg, accumulate);
+  else if (dtype == SEL_BF16)
     hipLaunchKernelGGL(k_gan_grad<__bf16>, dim3(nb), dim3(256), 0, s, kind, static_cast<const __bf16*>(a), va,
                        static_cast<const __bf16*>(b ? b : a), vb, target, n, gscale, mult,
                        static_cast<__bf16*>(grad), vg, accumulate);
