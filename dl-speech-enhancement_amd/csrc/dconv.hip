@@ -397,29 +397,38 @@ __global__ __launch_bounds__(256) void k_dconv_short(D d, const T* __restrict__ 
     wsh[k * d.Ng + n] = to_f(wp[e]);
   }
   __syncthreads();
+  // tap offset and input column of reduction element e (kernel-uniform: hoisted
+  // out of the row loop, where the runtime divisions cost ~60 VALU per element)
+  int tap[KR], col[KR];
+#pragma unroll
+  for (int e = 0; e < KR; ++e) {
+    const int i = e / nred, rc = e - i * nred;
+    const int r = rc / d.Cg, c = rc - r * d.Cg;
+    tap[e] = d.q0 + i;
+    col[e] = int(in_col(d, 0, r, c));
+  }
   const int n8 = d.Ng / 8;
-  const int64_t rows = int64_t(d.B) * d.Tvo;
-  const int64_t total = (rows + RW - 1) / RW * n8;
-  for (int64_t idx = int64_t(blockIdx.x) * 256 + threadIdx.x; idx < total; idx += int64_t(gridDim.x) * 256) {
-    const int64_t rg = idx / n8;
-    const int n0 = int(idx - rg * n8) * 8;
+  const int rows = d.B * d.Tvo;  // < 2^31 (host check)
+  const int total = (rows + RW - 1) / RW * n8;
+  for (int idx = int(blockIdx.x) * 256 + threadIdx.x; idx < total; idx += int(gridDim.x) * 256) {
+    const int rg = idx / n8;
+    const int n0 = (idx - rg * n8) * 8;
     float xw[RW][KR];
     int64_t orow[RW];
     bool valid[RW];
+    int row = rg * RW, b = row / d.Tvo, j = row - b * d.Tvo;
 #pragma unroll
     for (int q = 0; q < RW; ++q) {
-      const int64_t row = rg * RW + q;
-      const int b = int(row / d.Tvo), j = int(row - int64_t(b) * d.Tvo);
-      orow[q] = row < rows ? row * d.ldo : -1;
+      orow[q] = row < rows ? int64_t(row) * d.ldo : -1;
       valid[q] = row < rows && j < d.Tvalid;
+      const T* xb = x + int64_t(b) * d.Tvs * d.ldx;
 #pragma unroll
       for (int e = 0; e < KR; ++e) {
-        const int i = e / nred, rc = e - i * nred;
-        const int r = rc / d.Cg, c = rc - r * d.Cg;
-        const int t = j + d.q0 + i;
-        xw[q][e] = (valid[q] && t >= 0 && t < d.Tv) ? to_f(x[(int64_t(b) * d.Tvs + t) * d.ldx + in_col(d, 0, r, c)])
-                                                    : 0.f;
+        const int t = j + tap[e];
+        xw[q][e] = (valid[q] && t >= 0 && t < d.Tv) ? to_f(xb[int64_t(t) * d.ldx + col[e]]) : 0.f;
       }
+      ++row;
+      if (++j == d.Tvo) j = 0, ++b;
     }
     float acc[RW][8];
 #pragma unroll
@@ -458,6 +467,86 @@ __global__ __launch_bounds__(256) void k_dconv_short(D d, const T* __restrict__ 
       } else {
         *reinterpret_cast<uint4*>(out + orow[q] + n0) = *reinterpret_cast<uint4*>(ov);
         *reinterpret_cast<uint4*>(out + orow[q] + n0 + 4) = *reinterpret_cast<uint4*>(ov + 4);
+      }
+    }
+  }
+}
+
+// Staged form of the short-reduction forward for a contiguous phase view (G = 1,
+// Cs = Cg, ldx = S*Cg = NR: the 1-channel-input convs): reduction element
+// e = i*NR + rc of output row j reads x[j + q0 + i][rc], i.e. the flat window
+// xs[(j - j0)*NR + e] of a tile staged once in LDS.  k_dconv_short issues KR
+// per-lane global loads per row (the MSD's k15 1 -> 128 conv: 60 loads per
+// thread, bound by the texture unit's address rate at 645 us for 393 MB of
+// output); here a thread's RW rows read one (RW + K - 1)*NR-float window from LDS.
+template <typename T, int K, int NR>
+__global__ __launch_bounds__(256) void k_dconv_shortx(D d, const T* __restrict__ x, const T* __restrict__ wp,
+                                                      const float* __restrict__ bias, const T* __restrict__ aux,
+                                                      const T* __restrict__ res, T* __restrict__ out) {
+  constexpr int KR = K * NR, RW = 8, XW = (RW + K - 1) * NR;
+  extern __shared__ float sh[];
+  float* const wsh = sh;            // [KR][Ng]
+  float* const xs = sh + KR * d.Ng;  // [(RB + K - 1) * NR]
+  for (int e = threadIdx.x; e < d.Ng * KR; e += 256) {
+    const int n = e / KR, k = e - n * KR;
+    wsh[k * d.Ng + n] = to_f(wp[e]);
+  }
+  const int n8 = d.Ng / 8, RL = 256 / n8, RB = RL * RW;
+  const int rl = threadIdx.x / n8, n0 = (threadIdx.x - rl * n8) * 8;
+  const int tps = (d.Tvo + RB - 1) / RB, ntiles = d.B * tps;
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int b = tile / tps, j0 = (tile - b * tps) * RB;
+    __syncthreads();  // the previous tile's window reads are done (and the weights are in)
+    for (int p = threadIdx.x; p < (RB + K - 1) * NR; p += 256) {
+      const int t = j0 + d.q0 + p / NR;
+      xs[p] = (t >= 0 && t < d.Tv) ? to_f(x[(int64_t(b) * d.Tvs + t) * NR + p % NR]) : 0.f;
+    }
+    __syncthreads();
+    const int jr = rl * RW;
+    if (j0 + jr >= d.Tvo) continue;
+    float xw[XW];
+#pragma unroll
+    for (int u = 0; u < XW; ++u) xw[u] = xs[jr * NR + u];
+    float acc[RW][8];
+#pragma unroll
+    for (int q = 0; q < RW; ++q)
+#pragma unroll
+      for (int c = 0; c < 8; ++c) acc[q][c] = 0.f;
+#pragma unroll
+    for (int e = 0; e < KR; ++e) {
+      const float4 w0 = *reinterpret_cast<const float4*>(wsh + e * d.Ng + n0);
+      const float4 w1 = *reinterpret_cast<const float4*>(wsh + e * d.Ng + n0 + 4);
+      const float w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+      for (int q = 0; q < RW; ++q)
+#pragma unroll
+        for (int c = 0; c < 8; ++c) acc[q][c] = fmaf(w[c], xw[q * NR + e], acc[q][c]);
+    }
+#pragma unroll
+    for (int q = 0; q < RW; ++q) {
+      const int j = j0 + jr + q;
+      if (j >= d.Tvo) break;
+      const int64_t orow = (int64_t(b) * d.Tvo + j) * d.ldo;
+      const bool valid = j < d.Tvalid;
+      T ov[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        float a = 0.f;
+        if (valid) {
+          const int64_t col = n0 + c;
+          a = acc[q][c];
+          if (bias) a += bias[col];
+          if (res) a += to_f(res[orow + col]);
+          if (aux) a *= leaky_grad(to_f(aux[orow + col]), d.slope);
+          if (d.act) a = leaky(a, d.slope);
+        }
+        ov[c] = from_f<T>(a);
+      }
+      if constexpr (sizeof(T) == 2) {
+        *reinterpret_cast<uint4*>(out + orow + n0) = *reinterpret_cast<uint4*>(ov);
+      } else {
+        *reinterpret_cast<uint4*>(out + orow + n0) = *reinterpret_cast<uint4*>(ov);
+        *reinterpret_cast<uint4*>(out + orow + n0 + 4) = *reinterpret_cast<uint4*>(ov + 4);
       }
     }
   }
@@ -849,17 +938,24 @@ __global__ __launch_bounds__(256) void k_dwgrad_short(D d, const T* __restrict__
   float acc[KR + 1];
 #pragma unroll
   for (int e = 0; e <= KR; ++e) acc[e] = 0.f;
+  int tap[KR], col[KR];  // hoisted as in k_dconv_short
+#pragma unroll
+  for (int e = 0; e < KR; ++e) {
+    const int i = e / nred, rc = e - i * nred;
+    const int r = rc / d.Cg, c = rc - r * d.Cg;
+    tap[e] = d.q0 + i;
+    col[e] = int(in_col(d, 0, r, c));
+  }
   int64_t rr = r0 + rl;
   if (rr < r1 && threadIdx.x < nl * RL) {
     int b = int(rr / d.Tvalid), j = int(rr - int64_t(b) * d.Tvalid);
     for (; rr < r1; rr += RL) {
       const float gv = to_f(gout[(int64_t(b) * d.Tvo + j) * d.ldo + n]);
+      const T* xb = x + int64_t(b) * d.Tvs * d.ldx;
 #pragma unroll
       for (int e = 0; e < KR; ++e) {
-        const int i = e / nred, rc = e - i * nred;
-        const int r = rc / d.Cg, c = rc - r * d.Cg;
-        const int t = j + d.q0 + i;
-        if (t >= 0 && t < d.Tv) acc[e] = fmaf(gv, to_f(x[(int64_t(b) * d.Tvs + t) * d.ldx + in_col(d, 0, r, c)]), acc[e]);
+        const int t = j + tap[e];
+        if (t >= 0 && t < d.Tv) acc[e] = fmaf(gv, to_f(xb[int64_t(t) * d.ldx + col[e]]), acc[e]);
       }
       acc[KR] += gv;
       j += RL;
@@ -875,6 +971,78 @@ __global__ __launch_bounds__(256) void k_dwgrad_short(D d, const T* __restrict__
   for (int o = threadIdx.x; o < nl * (KR + 1); o += 256) {
     float sum = 0.f;
     for (int l = 0; l < RL; ++l) sum += red[l * nl * (KR + 1) + o];
+    const int nn = o / (KR + 1), e = o - nn * (KR + 1);
+    if (e < KR) part[int64_t(blockIdx.x) * N * KR + int64_t(nn) * KR + e] = sum;
+    else if (bpart) bpart[int64_t(blockIdx.x) * N + nn] = sum;
+  }
+}
+
+// Staged weight gradient of the same layers (contiguous phase view, see
+// k_dconv_shortx): a thread owns 2 output channels (one 4-B gout load per row)
+// and 16 consecutive rows of each tile, whose x windows come from the tile staged
+// in LDS, 4 rows per register window; blocks accumulate over their tiles and
+// reduce their row lanes into one partial.  k_dwgrad_short's per-row global x
+// loads ran the MSD's k15 1 -> 128 layer at 2.6 ms for 393 MB of gout.
+template <typename T, int K, int NR>
+__global__ __launch_bounds__(256) void k_dwgrad_shortx(D d, const T* __restrict__ gout, const T* __restrict__ x,
+                                                       float* __restrict__ part, float* __restrict__ bpart) {
+  constexpr int KR = K * NR, RR = 16, XW = (4 + K - 1) * NR;
+  extern __shared__ float sh[];  // x window [(RB + K - 1) * NR], then the row-lane reduction [RL][Ng][KR + 1]
+  const int N = d.Ng, NL = N / 2, RL = 256 / NL, RB = RL * RR;
+  const int rl = threadIdx.x / NL, n = (threadIdx.x - rl * NL) * 2;
+  float a0[KR + 1], a1[KR + 1];
+#pragma unroll
+  for (int e = 0; e <= KR; ++e) a0[e] = a1[e] = 0.f;
+  const int tps = (d.Tvalid + RB - 1) / RB, ntiles = d.B * tps;
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int b = tile / tps, j0 = (tile - b * tps) * RB;
+    __syncthreads();
+    for (int p = threadIdx.x; p < (RB + K - 1) * NR; p += 256) {
+      const int t = j0 + d.q0 + p / NR;
+      sh[p] = (t >= 0 && t < d.Tv) ? to_f(x[(int64_t(b) * d.Tvs + t) * NR + p % NR]) : 0.f;
+    }
+    __syncthreads();
+    const T* grow = gout + int64_t(b) * d.Tvo * d.ldo + n;
+#pragma unroll 1
+    for (int q4 = 0; q4 < RR; q4 += 4) {
+      const int jl = rl * RR + q4;
+      if (j0 + jl >= d.Tvalid) break;
+      float gx[4], gy[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = j0 + jl + r;
+        gx[r] = gy[r] = 0.f;
+        if (j < d.Tvalid) {
+          const T* gp = grow + int64_t(j) * d.ldo;
+          gx[r] = to_f(gp[0]);
+          gy[r] = to_f(gp[1]);
+        }
+      }
+      float xw[XW];
+#pragma unroll
+      for (int u = 0; u < XW; ++u) xw[u] = sh[jl * NR + u];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+#pragma unroll
+        for (int e = 0; e < KR; ++e) {
+          a0[e] = fmaf(gx[r], xw[r * NR + e], a0[e]);
+          a1[e] = fmaf(gy[r], xw[r * NR + e], a1[e]);
+        }
+        a0[KR] += gx[r];
+        a1[KR] += gy[r];
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e <= KR; ++e) {
+    sh[(rl * N + n) * (KR + 1) + e] = a0[e];
+    sh[(rl * N + n + 1) * (KR + 1) + e] = a1[e];
+  }
+  __syncthreads();
+  for (int o = threadIdx.x; o < N * (KR + 1); o += 256) {
+    float sum = 0.f;
+    for (int l = 0; l < RL; ++l) sum += sh[l * N * (KR + 1) + o];
     const int nn = o / (KR + 1), e = o - nn * (KR + 1);
     if (e < KR) part[int64_t(blockIdx.x) * N * KR + int64_t(nn) * KR + e] = sum;
     else if (bpart) bpart[int64_t(blockIdx.x) * N + nn] = sum;
@@ -1296,12 +1464,44 @@ bool short_kr_ok(int kr) { return kr == 2 || kr == 3 || kr == 6 || kr == 15; }
 
 bool short_ok(const sel_dconv_desc* d) {
   return d->G == 1 && d->So == 1 && d->Ng % 8 == 0 && d->ldo % 8 == 0 && short_kr_ok(d->K * d->S * d->Cg) &&
+         int64_t(d->B) * d->Tvo + 4 < (int64_t(1) << 31) &&
          size_t(d->Ng) * d->K * d->S * d->Cg * sizeof(float) <= 64 * 1024;
+}
+
+// the staged kernel's (K, NR) instances; nullptr: use k_dconv_short
+template <typename T>
+decltype(&k_dconv_shortx<T, 15, 1>) shortx_kernel(const sel_dconv_desc* d) {
+  const int nr = d->S * d->Cg, n8 = d->Ng / 8;
+  if (tune(18) == 1 || d->G != 1 || d->So != 1 || d->Cs != d->Cg || d->ldx != nr || d->Ng % 8 != 0 || n8 > 256 ||
+      256 % n8 != 0)
+    return nullptr;
+  const int K = d->K;
+  if (K == 15 && nr == 1) return k_dconv_shortx<T, 15, 1>;
+  if (K == 2 && nr == 3) return k_dconv_shortx<T, 2, 3>;
+  if (K == 3 && nr == 1) return k_dconv_shortx<T, 3, 1>;
+  if (K == 2 && nr == 1) return k_dconv_shortx<T, 2, 1>;
+  if (K == 6 && nr == 1) return k_dconv_shortx<T, 6, 1>;
+  if (K == 1 && nr == 2) return k_dconv_shortx<T, 1, 2>;
+  if (K == 1 && nr == 3) return k_dconv_shortx<T, 1, 3>;
+  return nullptr;
 }
 
 template <typename T>
 int launch_short(const sel_dconv_desc* d, const void* x, const void* wp, const float* bias, const void* aux,
                  const void* res, void* out, hipStream_t s) {
+  if (auto kx = shortx_kernel<T>(d)) {
+    // tune key 18: 1 = the unstaged kernel
+    const int kr = d->K * d->S * d->Cg, rb = 256 / (d->Ng / 8) * 8;
+    const size_t lds = (size_t(d->Ng) * kr + size_t(rb + d->K - 1) * d->S * d->Cg) * sizeof(float);
+    const int64_t ntiles = int64_t(d->B) * ((d->Tvo + rb - 1) / rb);
+    const unsigned blocks = unsigned(std::min<int64_t>(ntiles, 2048));
+    if (lds > 64 * 1024)
+      SEL_HIP(hipFuncSetAttribute((const void*)kx, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
+    hipLaunchKernelGGL(kx, dim3(blocks), dim3(256), lds, s, *d, static_cast<const T*>(x), static_cast<const T*>(wp),
+                       bias, static_cast<const T*>(aux), static_cast<const T*>(res), static_cast<T*>(out));
+    SEL_LAUNCH_CHECK();
+    return SEL_OK;
+  }
   const int64_t total = (int64_t(d->B) * d->Tvo + 3) / 4 * (d->Ng / 8);
   const unsigned blocks = unsigned(std::min<int64_t>((total + 255) / 256, 16384));
   const int kr = d->K * d->S * d->Cg;
@@ -1444,6 +1644,35 @@ hipError_t wgrad_fill(const sel_dconv_desc* d, int dtype, const WgPlanD& p, cons
   const int nred = d->S * d->Cg;
   if (p.shortk) {
     const int kr = d->K * nred;
+    // staged kernel (tune key 18: 1 = off) where the phase view is contiguous
+    if (tune(18) != 1 && d->Cs == d->Cg && d->ldx == nred && d->Ng % 2 == 0 && d->ldo % 2 == 0 &&
+        int64_t(d->B) * d->Tvo < (int64_t(1) << 31)) {
+      const int rl = 256 / (d->Ng / 2), rb = rl * 16;
+      const size_t lds = std::max<size_t>(size_t(rb + d->K - 1) * nred, size_t(rl) * d->Ng * (kr + 1)) * sizeof(float);
+      void (*kx)(D, const __bf16*, const __bf16*, float*, float*) = nullptr;
+      void (*kf)(D, const float*, const float*, float*, float*) = nullptr;
+#define SEL_DWSX(K_, NR_)                                                       \
+  if (d->K == K_ && nred == NR_) {                                              \
+    kx = k_dwgrad_shortx<__bf16, K_, NR_>;                                      \
+    kf = k_dwgrad_shortx<float, K_, NR_>;                                       \
+  }
+      SEL_DWSX(15, 1) SEL_DWSX(2, 3) SEL_DWSX(3, 1) SEL_DWSX(2, 1) SEL_DWSX(6, 1) SEL_DWSX(1, 2) SEL_DWSX(1, 3)
+#undef SEL_DWSX
+      if (kx) {
+        const void* kern = dtype == SEL_BF16 ? (const void*)kx : (const void*)kf;
+        if (lds > 64 * 1024) {
+          const hipError_t e = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+          if (e != hipSuccess) return e;
+        }
+        if (dtype == SEL_BF16)
+          hipLaunchKernelGGL(kx, dim3(p.nsplit), dim3(256), lds, s, *d, static_cast<const __bf16*>(gout),
+                             static_cast<const __bf16*>(x), part, bpart);
+        else
+          hipLaunchKernelGGL(kf, dim3(p.nsplit), dim3(256), lds, s, *d, static_cast<const float*>(gout),
+                             static_cast<const float*>(x), part, bpart);
+        return hipGetLastError();
+      }
+    }
 #define SEL_DWS(TT, KR)                                                                                     \
   hipLaunchKernelGGL((k_dwgrad_short<TT, KR>), dim3(p.nsplit), dim3(256), 0, s, *d, static_cast<const TT*>(gout), \
                      static_cast<const TT*>(x), p.rows_per_split, part, bpart)
