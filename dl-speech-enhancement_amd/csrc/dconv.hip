@@ -1548,6 +1548,13 @@ int dispatch_fwd(const sel_dconv_desc* d, const void* x, const void* wp, const f
   const int64_t rows = int64_t(d->B) * d->Tvo;
   if constexpr (sizeof(T) == 2) {
     if (width > 32 && pf_ok(d, dtype)) {
+      // tune key 19: tile A/B (1: 256x64, 2: 128x128, 3: 256x128, 4: the <= 64-wide tiles below)
+      if (tune(19) == 1) return launch_pf<256, 64>(d, x, wp, bias, aux, res, out, s);
+      if (tune(19) == 3 && width % 128 == 0) return launch_pf<256, 128>(d, x, wp, bias, aux, res, out, s);
+      // 128-column tiles halve the input re-staging per output (MPD 512 -> 1024 k5 s3: 8.4 -> 5.5 ms,
+      // 1024 -> 1024 k5: 1.22 -> 0.80 ms at the probe's sizes, tools/dconv_probe.py, bit-identical)
+      if (width % 128 == 0 && (tune(19) == 2 || (tune(19) == 0 && rows * (width / 128) >= 65536)))
+        return launch_pf<128, 128>(d, x, wp, bias, aux, res, out, s);
       if (rows * (width / 64) < 65536) return launch_pf<64, 64>(d, x, wp, bias, aux, res, out, s);
       return launch_pf<128, 64>(d, x, wp, bias, aux, res, out, s);
     }

@@ -52,6 +52,18 @@ def timed(fn, iters=10):
     return sum(e0.elapsed_time(e1) for e0, e1 in ev) / iters * 1e3
 
 
+if os.environ.get("PF_AB"):  # forward tile A/B of the register-prefetched MFMA kernel (tune key 19)
+    lib.sel_tune(19, 0)
+    fwd()
+    ref = out.clone()
+    for v in (0, 1, 2, 3, 0):
+        lib.sel_tune(19, v)
+        fwd()
+        torch.cuda.synchronize()
+        print(f"layer {a} pf tile variant {v}: fwd {timed(fwd):.1f} us  same as default: {bool(torch.equal(out, ref))}",
+              flush=True)
+    lib.sel_tune(19, 0)
+    sys.exit(0)
 lib.sel_tune(18, 1)
 fwd()
 ref = out.clone()
