@@ -2347,15 +2347,10 @@ __global__ __launch_bounds__(256) void k_wgrad3_bf16(Args a, const __bf16* __res
 //   pass 2: out[j] = sum_g sum_{i % period == j} part2[g][i]
 constexpr int SPLIT_GROUP = 32;
 
-__global__ __launch_bounds__(256) void k_split_sum1(const float* __restrict__ part, int nsplit, int64_t n,
-                                                    float* __restrict__ part2) {
-  const int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x;
-  if (i >= n) return;
-  const int s0 = blockIdx.y * SPLIT_GROUP;
-  const int s1 = s0 + SPLIT_GROUP < nsplit ? s0 + SPLIT_GROUP : nsplit;
-  const float* p = part + int64_t(s0) * n + i;
+// sum of the partials p[0], p[n], ... p[(cnt - 1) n] of one split group (cnt <= 32)
+__device__ __forceinline__ float split_group_sum(const float* __restrict__ p, int cnt, int64_t n) {
   float acc = 0.f;
-  if (s1 - s0 == SPLIT_GROUP) {
+  if (cnt == SPLIT_GROUP) {
     // a full group: all 32 loads in flight at once (a serial chain of dependent
     // adds made the compiler issue them a few at a time: latency-bound), then a
     // fixed pairwise tree (deterministic)
@@ -2369,14 +2364,23 @@ __global__ __launch_bounds__(256) void k_split_sum1(const float* __restrict__ pa
     acc = v[0];
   } else {
     int u = 0;
-    for (; u + 4 <= s1 - s0; u += 4) {
+    for (; u + 4 <= cnt; u += 4) {
       const float a0 = p[int64_t(u) * n], a1 = p[int64_t(u + 1) * n], a2 = p[int64_t(u + 2) * n],
                   a3 = p[int64_t(u + 3) * n];
       acc += (a0 + a1) + (a2 + a3);
     }
-    for (; u < s1 - s0; ++u) acc += p[int64_t(u) * n];
+    for (; u < cnt; ++u) acc += p[int64_t(u) * n];
   }
-  part2[int64_t(blockIdx.y) * n + i] = acc;
+  return acc;
+}
+
+__global__ __launch_bounds__(256) void k_split_sum1(const float* __restrict__ part, int nsplit, int64_t n,
+                                                    float* __restrict__ part2) {
+  const int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int s0 = blockIdx.y * SPLIT_GROUP;
+  const int s1 = s0 + SPLIT_GROUP < nsplit ? s0 + SPLIT_GROUP : nsplit;
+  part2[int64_t(blockIdx.y) * n + i] = split_group_sum(part + int64_t(s0) * n + i, s1 - s0, n);
 }
 
 __global__ __launch_bounds__(256) void k_split_sum2(const float* __restrict__ part2, int ngroups, int64_t n,
@@ -2547,6 +2551,27 @@ __global__ __launch_bounds__(256) void k_split_sum2_unpack(const float* __restri
   }
   for (; g < ngroups; ++g) acc += p[int64_t(g) * n];
   gw[i] = acc;
+}
+
+// One split group (nsplit <= 32): both reduction passes, the unpack and the bias
+// fold in one launch, with the arithmetic of k_split_sum1 + k_split_sum2(_unpack)
+// (the second pass adds one group sum to 0, exactly): threads [0, nt) write the
+// weight gradient (torch layout when kind >= 0, else the packed one), threads
+// [nt, nt + period) the bias.
+__global__ __launch_bounds__(256) void k_split_finish1(const float* __restrict__ part, int nsplit, int64_t nw,
+                                                       int64_t nt, int kind, int cout, int cin, int K, int s,
+                                                       float* __restrict__ gw, const float* __restrict__ bpart,
+                                                       int64_t nb, int period, float* __restrict__ gb) {
+  const int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (i < nt) {
+    const int64_t j = kind >= 0 ? unpack_src(kind, i, cout, cin, K, s) : i;
+    gw[i] = 0.f + split_group_sum(part + j, nsplit, nw);
+  } else if (gb && i < nt + period) {
+    const int64_t jb = i - nt;
+    float acc = 0.f;
+    for (int64_t q = jb; q < nb; q += period) acc += split_group_sum(bpart + q, nsplit, nb);
+    gb[jb] = acc;
+  }
 }
 
 __global__ void k_unpack(int kind, const float* __restrict__ gp, int cout, int cin, int K, int s,
@@ -3281,6 +3306,17 @@ int wgrad_impl(const sel_conv_desc* d, int dtype, const void* gout, const void* 
   // two-pass split reduction; the second-level partials live after the first-level ones
   const int64_t nw = int64_t(d->N) * d->K * d->C;
   const int ng = (p.nsplit + SPLIT_GROUP - 1) / SPLIT_GROUP;
+  if (ng == 1 && tune(20) != 1) {  // one launch for both passes, the unpack and the bias (tune key 20: 1 = off)
+    const int64_t nt = up ? (up->kind == SEL_PACK_CONVT ? int64_t(up->cin) * up->cout * 2 * up->stride
+                             : int64_t(up->cout) * up->cin * (up->kind == SEL_PACK_FWD ? up->k : 2 * up->stride))
+                          : nw;
+    const int64_t nthreads = nt + (gbias ? d->bias_period : 0);
+    hipLaunchKernelGGL(k_split_finish1, dim3(unsigned((nthreads + 255) / 256)), dim3(256), 0, s, part, p.nsplit, nw, nt,
+                       up ? up->kind : -1, up ? up->cout : 0, up ? up->cin : 0, up ? up->k : 0, up ? up->stride : 0,
+                       gwpack, bpart, int64_t(d->N), gbias ? d->bias_period : 0, gbias);
+    SEL_LAUNCH_CHECK();
+    return SEL_OK;
+  }
   float* part2 = part + size_t(p.nsplit) * (size_t(d->N) * d->K * d->C + d->N);
   hipLaunchKernelGGL(k_split_sum1, dim3(unsigned((nw + 255) / 256), unsigned(ng)), dim3(256), 0, s, part, p.nsplit,
                      nw, part2);
