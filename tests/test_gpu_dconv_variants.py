@@ -1,0 +1,125 @@
+"""Kernel variants of the discriminator path agree with each other (round-2
+kernels; the default path of each shape is checked against fp64 torch in
+test_gpu_gan.py):
+
+* k_dconv_pf tiles (tune key 19: 128x64 / 64x64 by size, 256x64, 128x128,
+  256x128) run the same MFMA order, so every tile gives the same bits;
+* the LDS-staged short-reduction kernels (tune key 18: 1 = the unstaged ones):
+  the forward is bit-identical, the weight gradient sums rows in another order;
+* the GAN loss terms' 16-B vector path (contiguous last dim, multiple of 8) and
+  the per-element path, both against fp64 torch.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+# (tag, cin, cout, Kt, stride, pad, groups, Bs, T): one-group layers of C5 (48 kHz)
+PF_LAYERS = [
+    ("mpd1_s3", 32, 128, 5, 3, 2, 1, 6, 2001),
+    ("mpd2_s3", 128, 512, 5, 3, 2, 1, 6, 667),
+    ("mpd4_s1", 1024, 1024, 5, 1, 2, 1, 6, 25),
+    ("msd6_k5", 1024, 1024, 5, 1, 2, 1, 2, 48),
+]
+SHORT_LAYERS = [
+    ("msd0_k15", 1, 128, 15, 1, 7, 1, 2, 3000),
+    ("mpd0_s3", 1, 32, 5, 3, 2, 1, 6, 6001),
+]
+
+
+def _setup(gpu, shape, dt):
+    from sel import dconvops as DC
+    tag, cin, cout, Kt, s, pad, G, Bs, T = shape
+    sp = DC.LayerSpec(cin, cout, Kt, s, pad, G, True)
+    torch.manual_seed(Kt * 13 + cout)
+    T_out = sp.t_out(T)
+    Ta = DC._roundup(T, s)
+    x = torch.zeros(Bs, Ta, cin, device=gpu)
+    x[:, :T] = torch.randn(Bs, T, cin, device=gpu)
+    w = torch.randn(cout, cin // G, Kt, device=gpu) / (cin // G * Kt) ** 0.5
+    b = torch.randn(cout, device=gpu)
+    g = torch.randn(Bs, T_out, cout, device=gpu).to(dt).contiguous()
+    return sp, x.to(dt), w, b, g, (Bs, T, Ta, T_out)
+
+
+def _run(sp, x, w, b, g, geo, dt, want_wgrad=False):
+    from sel import dconvops as DC
+    Bs, T, Ta, T_out = geo
+    d = DC._fwd_desc(sp, Bs, T, Ta, T_out, T_out, 0.1)
+    y = torch.empty(Bs, T_out, sp.cout, dtype=dt, device=x.device)
+    DC.prim(d, x, DC.pack(sp, w, None, dt, 0), y, bias=b)
+    db = DC._dgrad_desc(sp, Bs, Ta, T_out, T_out, 0.1, False)
+    gin = torch.empty(Bs, Ta, sp.cin, dtype=dt, device=x.device)
+    DC.prim(db, g, DC.pack(sp, w, None, dt, 1), gin)
+    out = [y, gin]
+    if want_wgrad:
+        gw, _, gb = DC.wgrad(sp, d, g, x, w, None, True, True)
+        out += [gw, gb]
+    torch.cuda.synchronize()
+    return out
+
+
+@pytest.mark.parametrize("shape", PF_LAYERS, ids=[s[0] for s in PF_LAYERS])
+def test_pf_tiles_bit_identical(gpu, shape):
+    from sel import _lib as Lb
+    lib = Lb.lib()
+    dt = torch.bfloat16
+    sp, x, w, b, g, geo = _setup(gpu, shape, dt)
+    prev = lib.sel_tune(19, 0)
+    try:
+        ref = _run(sp, x, w, b, g, geo, dt)
+        for v in (1, 2, 3):
+            lib.sel_tune(19, v)
+            got = _run(sp, x, w, b, g, geo, dt)
+            for name, r, o in zip(("fwd", "adjoint"), ref, got):
+                assert torch.equal(r, o), (shape[0], v, name, float((r.float() - o.float()).abs().max()))
+    finally:
+        lib.sel_tune(19, prev)
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("shape", SHORT_LAYERS, ids=[s[0] for s in SHORT_LAYERS])
+def test_short_staged_matches_unstaged(gpu, shape, dtype):
+    from sel import _lib as Lb
+    lib = Lb.lib()
+    dt = torch.float32 if dtype == "fp32" else torch.bfloat16
+    sp, x, w, b, g, geo = _setup(gpu, shape, dt)
+    prev = lib.sel_tune(18, 1)
+    try:
+        y0, gi0, gw0, gb0 = _run(sp, x, w, b, g, geo, dt, want_wgrad=True)
+        lib.sel_tune(18, 0)
+        y1, gi1, gw1, gb1 = _run(sp, x, w, b, g, geo, dt, want_wgrad=True)
+    finally:
+        lib.sel_tune(18, prev)
+    assert torch.equal(y0, y1), float((y0.float() - y1.float()).abs().max())
+    assert torch.equal(gi0, gi1)  # the adjoint does not take the short path: same kernel
+    # fp32 partial sums over the rows in a different order: ~1e-7 relative
+    for a, c in ((gw0, gw1), (gb0, gb1)):
+        assert ((a - c).norm() / a.norm()).item() <= 1e-5
+
+
+@pytest.mark.parametrize("C", [64, 60], ids=["vector", "per_element"])
+def test_gan_terms_vector_and_scalar(gpu, C):
+    """(B, C, T) views of channels-last (B, T, C) feature maps: C % 8 == 0 takes
+    the 16-B vector kernels, C = 60 the per-element ones; fp64 torch reference."""
+    from sel import dconvops as DC
+    torch.manual_seed(C)
+    B, T = 3, 517
+    for dt, tol in ((torch.float32, 1e-6), (torch.bfloat16, 1e-6)):
+        fa = torch.randn(B, T, C, device=gpu).to(dt)
+        fb = torch.randn(B, T, C, device=gpu).to(dt)
+        a = fa.permute(0, 2, 1).detach().requires_grad_(True)
+        bv = fb.permute(0, 2, 1)
+        l1 = DC.l1_mean(a, bv)
+        ref = (a.double() - bv.double()).abs().mean()
+        assert abs(l1.item() - ref.item()) <= tol * max(1.0, abs(ref.item())), (C, dt, l1.item(), ref.item())
+        l1.backward()
+        gref = torch.sign(a.double() - bv.double()) / a.numel()
+        assert ((a.grad.double() - gref).abs().max() <= 1e-2 * gref.abs().max()).item()
+        a2 = fa.permute(0, 2, 1).detach().requires_grad_(True)
+        m = DC.mse_to(a2, 1.0)
+        mref = ((a2.double() - 1.0) ** 2).mean()
+        assert abs(m.item() - mref.item()) <= tol * max(1.0, abs(mref.item()))
+        m.backward()
+        g2 = 2.0 * (a2.double() - 1.0) / a2.numel()
+        assert ((a2.grad.double() - g2).norm() / g2.norm()).item() <= (1e-6 if dt == torch.float32 else 1e-2)
