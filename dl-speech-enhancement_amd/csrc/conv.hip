@@ -2759,7 +2759,9 @@ int fwd4_choice(const Args& a) {
   if (a.N >= 256 && a.K == 1) return 26;
   if (a.N >= 256 && a.rows >= 16384) return ws_ok(a) ? 27 : 24;
   if (a.N <= 64 || a.rows < 65536) return 23;
-  if (a.N == 128 && tune(17) == 1 && ws_ok(a)) return 27;
+  if (a.N == 128 && ws_ok(a) && tune(17) != 2 &&
+      (tune(17) == 1 || a.K == 3 || (a.K == 7 && a.pad == 0 && !a.in_elu)))
+    return 27;
   if (a.N == 128 && a.K > 1 && a.pad == 0 && !a.in_elu) return 22;
   return 24;
 }
@@ -2798,9 +2800,13 @@ int fwd4_variant(int v, const Args& a, const void* in, const void* wp, const flo
     return launch_fwd4<256, 64, 4, KMAX, TO>(a, in, wp, bias, aux, res, out, s);
   }
   if (a.N <= 64 || a.rows < 65536) return launch_fwd4<128, 64, 2, KMAX, TO>(a, in, wp, bias, aux, res, out, s);
-  // 128-wide k3/k7 layers at >= 64 k rows on the warp-specialised kernel (one
-  // 128-column tile: no input re-read across column tiles); tune key 17: 1 = on
-  if (a.N == 128 && tune(17) == 1 && ws_ok(a))
+  // 128-wide layers at >= 64 k rows on the warp-specialised kernel (one
+  // 128-column tile: no input re-read across column tiles) for the k7 dgrads
+  // (RU128 d9: 63.6 -> 53.2 us) and the k3 convs (down1: 49.3 -> 44.1 us), not
+  // the k7 forwards with their ELU'd 54-row halo (48.6 -> 52.9 us);
+  // tools/conv_bench.py.  Tune key 17: 1 = every 128-wide layer, 2 = none.
+  if (a.N == 128 && ws_ok(a) && tune(17) != 2 &&
+      (tune(17) == 1 || a.K == 3 || (a.K == 7 && a.pad == 0 && !a.in_elu)))
     return a.K == 7 ? launch_ws<7, TO>(a, in, wp, bias, aux, res, out, s)
                     : launch_ws<3, TO>(a, in, wp, bias, aux, res, out, s);
   // 128-wide k7 dgrad at 2000 samples (pad 0, no input ELU): 128x32 tiles (76.5 -> 62.6 us)
