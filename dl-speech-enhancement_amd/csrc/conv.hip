@@ -69,6 +69,17 @@ __device__ __forceinline__ uint4 elu8(uint4 w) {
 struct Args {
   int64_t rows;
   int T, C, N, K, dil, pad, pad_mode, in_elu, bias_period;
+  // discriminator layers on the warp-specialised kernel (sel_dconv_desc; the
+  // generator's own descriptors set tin_valid = tin_pitch = tout_valid = T,
+  // ldx = C, ldo = N, epi = 0): input rows valid / allocated per sequence and
+  // row pitches, output rows computed per sequence (later rows written as
+  // zeros), epilogue 1 = (v + bias + res) * LeakyReLU'(aux), LeakyReLU if act
+  int tin_valid, tin_pitch, ldx, ldo, tout_valid, epi, act;
+  float slope;
+  // > 0: flat tiling of all sequences' rows as one row space (equal input and
+  // output pitch seq_pitch, zero gaps between sequences): input rows valid where
+  // row % seq_pitch < tin_valid, outputs where row % seq_pitch < tout_valid
+  int seq_pitch;
 };
 
 // Flat input row for (output row m, tap k) or -1 (zero).
@@ -639,9 +650,11 @@ __global__ __launch_bounds__(768) void k_conv_ws_bf16(Args a, const __bf16* __re
       if (q < XI) {
         const int R = q * WS_RPI + lane / WS_SPR, ls = (lane % WS_SPR) ^ ws_swzbits(R);
         int ti = t0 - a.pad + R;
-        const bool valid = R < span && ((ti >= 0 && ti < a.T) || a.pad_mode == SEL_PAD_REPLICATE);
-        ti = ti < 0 ? 0 : (ti >= a.T ? a.T - 1 : ti);
-        src[u] = valid ? in + (b * a.T + ti) * a.C + 8 * ls : g_ws_zero + 8 * ls;
+        const bool valid =
+            R < span && (a.seq_pitch > 0 ? ti >= 0 && ti < a.T && ti % a.seq_pitch < a.tin_valid
+                                         : (ti >= 0 && ti < a.tin_valid) || a.pad_mode == SEL_PAD_REPLICATE);
+        ti = ti < 0 ? 0 : (ti >= a.tin_valid ? a.tin_valid - 1 : ti);
+        src[u] = valid ? in + (b * a.tin_pitch + ti) * a.ldx + 8 * ls : g_ws_zero + 8 * ls;
       } else {
         const int R = (q - XI) * WS_RPI + lane / WS_SPR, ls = (lane % WS_SPR) ^ ws_swzbits(R);
         const int k = R / BN, n = R % BN;
@@ -788,7 +801,7 @@ __global__ __launch_bounds__(768) void k_conv_ws_bf16(Args a, const __bf16* __re
   for (int u = 0; u < EV; ++u) {
     const int v = tid + u * 768;
     if (v >= nvec) break;
-    const int64_t o = (m0 + (v >> 4)) * a.N + n0 + (v & 15) * 8;
+    const int64_t o = (m0 + (v >> 4)) * a.ldo + n0 + (v & 15) * 8;
     if (aux) av[u] = *reinterpret_cast<const V8*>(aux + o);
     if (res) rv[u] = *reinterpret_cast<const V8*>(res + o);
   }
@@ -797,10 +810,27 @@ __global__ __launch_bounds__(768) void k_conv_ws_bf16(Args a, const __bf16* __re
     const int v = tid + u * 768;
     if (v >= nvec) break;
     const int row = v >> 4, c8 = (v & 15) * 8;
-    const int64_t o = (m0 + row) * a.N + n0 + c8;
+    const int64_t o = (m0 + row) * a.ldo + n0 + c8;
     const floatx4 lo = *reinterpret_cast<const floatx4*>(tile + row * WS_EP + c8);
     const floatx4 hi = *reinterpret_cast<const floatx4*>(tile + row * WS_EP + c8 + 4);
     float x[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    if (a.epi) {
+      // discriminator epilogue (k_dconv_mfma order): + bias, + res, * LeakyReLU'(aux),
+      // LeakyReLU; rows past the computed ones are the next layer's zero padding
+      const bool valid = (a.seq_pitch > 0 ? (t0 + row) % a.seq_pitch : t0 + row) < a.tout_valid;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float y = 0.f;
+        if (valid) {
+          y = x[e];
+          if (bias) y += bias[n0 + c8 + e];
+          if (res) y += to_f(rv[u].v[e]);
+          if (aux) y *= to_f(av[u].v[e]) > 0.f ? 1.f : a.slope;
+          if (a.act) y = y > 0.f ? y : y * a.slope;
+        }
+        x[e] = y;
+      }
+    } else {
     if (bias && a.bias_period) {
       if (a.bias_period % 8 == 0) {
         const float* const bp = bias + (n0 + c8) % a.bias_period;
@@ -819,6 +849,7 @@ __global__ __launch_bounds__(768) void k_conv_ws_bf16(Args a, const __bf16* __re
     if (res) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) x[e] += to_f(rv[u].v[e]);
+    }
     }
     V8 ov;
 #pragma unroll
@@ -1651,12 +1682,33 @@ __global__ __launch_bounds__(256) void k_conv_c1_bf16(Args a, const __bf16* __re
   }
   const int tps = (a.T + C1_TR - 1) / C1_TR;
   const int64_t ntiles = (a.rows / a.T) * tps;
+  // the next tile's samples are fetched into registers while this tile is
+  // computed and stored (one resident round of workgroups walks the tiles)
+  const int span = C1_TR + (a.K - 1) * a.dil;
+  float pre[2];
+  auto fetch = [&](int64_t tile) {
+    const int64_t b = tile / tps;
+    const int t0 = int(tile % tps) * C1_TR;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int r = threadIdx.x + 256 * u;
+      int ti = t0 - a.pad + r;
+      const bool ok = r < span && ((ti >= 0 && ti < a.T) || a.pad_mode == SEL_PAD_REPLICATE);
+      ti = ti < 0 ? 0 : (ti >= a.T ? a.T - 1 : ti);
+      const float v = ok ? float(in[b * a.T + ti]) : 0.f;
+      pre[u] = ok && a.in_elu ? elu_fast(v) : v;
+    }
+  };
+  if (int64_t(blockIdx.x) < ntiles) fetch(blockIdx.x);
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int64_t b = tile / tps;
     const int t0 = int(tile % tps) * C1_TR;
     __syncthreads();
-    c1_stage(a, in, b, t0, xs);
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      if (threadIdx.x + 256 * u < span) xs[threadIdx.x + 256 * u] = pre[u];
     __syncthreads();
+    if (tile + gridDim.x < ntiles) fetch(tile + gridDim.x);
     const int rows = a.T - t0 < C1_TR ? a.T - t0 : C1_TR;
     for (int r = rl; r < rows; r += nrl) {
       float v[V];
@@ -2620,8 +2672,21 @@ __global__ __launch_bounds__(1024) void k_replicate_fix(Args a, const T* __restr
   const int64_t row = int64_t(blockIdx.x) * a.T;
   const int c = blockIdx.y * 64 + lane;
   float s = 0.f;
-  if (c < a.C)
-    for (int n = wave; n < a.N; n += 16) s += to_f(gout[row * a.N + n]) * to_f(wp[(int64_t(n) * a.K + 0) * a.C + c]);
+  if (c < a.C) {
+    // 8 (gout, weight) pairs in flight per step, summed in the same n order
+    int n = wave;
+    for (; n + 16 * 7 < a.N; n += 16 * 8) {
+      float gv[8], wv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        gv[u] = to_f(gout[row * a.N + n + 16 * u]);
+        wv[u] = to_f(wp[(int64_t(n + 16 * u) * a.K + 0) * a.C + c]);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += gv[u] * wv[u];
+    }
+    for (; n < a.N; n += 16) s += to_f(gout[row * a.N + n]) * to_f(wp[(int64_t(n) * a.K + 0) * a.C + c]);
+  }
   red[wave][lane] = s;
   __syncthreads();
   if (wave == 0 && c < a.C) {
@@ -2675,6 +2740,12 @@ Args to_args(const sel_conv_desc* d) {
   a.pad_mode = d->pad_mode;
   a.in_elu = d->in_elu;
   a.bias_period = d->bias_period;
+  a.tin_valid = a.tin_pitch = a.tout_valid = d->T;
+  a.ldx = d->C;
+  a.ldo = d->N;
+  a.epi = a.act = 0;
+  a.slope = 0.f;
+  a.seq_pitch = 0;
   return a;
 }
 
@@ -2884,15 +2955,27 @@ int thin_rows(const Args& a) {
 constexpr int kThinEpfDefault = 0b101;  // instances 0 and 2
 constexpr int kThinEpfAlt = 0b100;      // instance 2 on its 64-row tiles
 
+// epilogue prefetch + split loop: only for launches with epilogue operands
+// (aux and/or res), per instance by kThinEpfDefault (key 12 bit i flips
+// instance i, key 11 bit 0 forces it off); kThinEpfAlt instances run it on
+// their alternative tile rows.  Returns the E flag, sets the tile rows.
+bool thin_variant(const Args& a, bool has_epilogue, int& rows) {
+  const int i = thin_index(a);
+  const bool epf = has_epilogue && ((kThinEpfDefault ^ tune(12)) >> i & 1) && !(tune(11) & 1);
+  const bool alt = (((tune(6) >> i) & 1) != 0) != (epf && ((kThinEpfAlt >> i) & 1));
+  rows = 0;
+#define SEL_THIN_RV(I_, C_, N_, K_, R_, R2_) if (i == I_) rows = alt ? R2_ : R_;
+  SEL_THIN_SHAPES(SEL_THIN_RV)
+#undef SEL_THIN_RV
+  return epf;
+}
+
 int dispatch_thin(const Args& a, const void* in, const void* wp, const float* bias, const void* aux,
                   const void* res, void* out, hipStream_t s) {
   const int i = thin_index(a);
   if (i < 0) return kNotThin;
-  // epilogue prefetch + split loop: only for launches with epilogue operands
-  // (aux and/or res), per instance by kThinEpfDefault (key 12 bit i flips
-  // instance i, key 11 bit 0 forces it off); kThinEpfAlt instances run it on
-  // their alternative tile rows
-  const bool epf = (aux || res) && ((kThinEpfDefault ^ tune(12)) >> i & 1) && !(tune(11) & 1);
+  int rows_unused;
+  const bool epf = thin_variant(a, aux || res, rows_unused);
   const bool alt = (((tune(6) >> i) & 1) != 0) != (epf && ((kThinEpfAlt >> i) & 1));
 #define SEL_THIN_LAUNCH(I_, C_, N_, K_, R_, R2_)                                             \
   if (i == I_)                                                                               \
@@ -2985,7 +3068,16 @@ int dispatch_fwd(const Args& a, const void* in, const void* wp, const float* bia
   if constexpr (sizeof(TI) == 2) {
     if (a.C == 1 && a.N % 8 == 0 && a.N <= C1_NMAX && a.K <= C1_KMAX && (a.K - 1) * a.dil <= C1_HALO &&
         tune(3) == 0) {
-      const int64_t blocks = std::min<int64_t>((a.rows / a.T) * ((a.T + C1_TR - 1) / C1_TR), 4096);
+      // one round of resident workgroups (they prefetch their next tile)
+      static const int64_t slots = [] {
+        int dev = 0, cus = 0, per_cu = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_conv_c1_bf16<TO>, 256, 0) != hipSuccess)
+          return int64_t(4096);
+        return std::max<int64_t>(256, int64_t(cus) * per_cu);
+      }();
+      const int64_t blocks = std::min<int64_t>((a.rows / a.T) * ((a.T + C1_TR - 1) / C1_TR), tune(23) > 0 ? tune(23) : slots);
       hipLaunchKernelGGL(k_conv_c1_bf16<TO>, dim3(unsigned(blocks)), dim3(256), 0, s, a,
                          static_cast<const __bf16*>(in), static_cast<const __bf16*>(wp), bias,
                          static_cast<const TO*>(aux), static_cast<const TO*>(res), static_cast<TO*>(out));
@@ -3127,13 +3219,72 @@ hipError_t launch_wgrad3(const WgPlan& p, const Args& a, const __bf16* gout, con
 
 }  // namespace
 
+// Discriminator layers (dconv.hip, sel_dconv_desc) on the warp-specialised
+// 256 x 128 kernel: one group, a contiguous reduction row (S == 1 or Cs == Cg:
+// the phase view of a strided layer is S * Cg contiguous channels), contiguous
+// output columns, K in {2, 3, 5, 7}.  The MPD's (5,1) convs are K = 5 (stride 1)
+// or K = 2 taps over 3 * Cin channels (stride 3, phase view); their adjoints the
+// same K over gout with So = 3 output phases.  Returns SEL_ERR_UNSUPPORTED for
+// any other shape (the caller keeps its own kernels).
+namespace sel {
+namespace conv {
+int dconv_ws_fwd(const sel_dconv_desc* d, const void* x, const void* wp, const float* bias, const void* aux,
+                 const void* res, void* out, hipStream_t s) {
+  const int width = d->So * d->Ng, nred = d->S * d->Cg;
+  const bool ok = d->G == 1 && (d->S == 1 || d->Cs == d->Cg) && (d->So == 1 || d->Ns == d->Ng) &&
+                  (d->K == 2 || d->K == 3 || d->K == 5 || d->K == 7) && width % WS_BN == 0 &&
+                  nred % WS_CK == 0 && nred <= WS_CMAX && d->ldx % 8 == 0 && d->ldo % 8 == 0 &&
+                  d->ldx >= nred && d->ldo >= width && d->Tvo > 0 && d->B > 0 && d->Tv <= d->Tvs &&
+                  d->K - 1 <= F4_HALOMAX && -d->q0 <= F4_HALOMAX && ws_lds_bytes(d->K) <= 160 * 1024;
+  if (!ok) return SEL_ERR_UNSUPPORTED;
+  // flat tiling (tune key 22: 1 = off) where the layout leaves zero gaps
+  // between sequences (sel.dconvops allocates the MPD chain so; its deep layers
+  // have 54-300 rows per period column, a 256-row sample-aligned tile wastes up
+  // to 80% there): every row a tap may read across a sequence boundary lies in a gap
+  // (input row >= Tv) or feeds an output row that is written as zero (>= Tvalid)
+  const int P = d->Tvo;
+  const bool flat = tune(22) != 1 && d->Tvs == P && P - d->Tv >= -d->q0 && P - d->Tvalid >= d->q0 + d->K - 1 &&
+                    int64_t(d->B) * P < (int64_t(1) << 31);
+  Args a;
+  a.rows = int64_t(d->B) * d->Tvo;
+  a.T = flat ? int(a.rows) : d->Tvo;
+  a.seq_pitch = flat ? P : 0;
+  a.C = nred;
+  a.N = width;
+  a.K = d->K;
+  a.dil = 1;
+  a.pad = -d->q0;
+  a.pad_mode = SEL_PAD_ZERO;
+  a.in_elu = 0;
+  a.bias_period = 0;
+  a.tin_valid = d->Tv;
+  a.tin_pitch = d->Tvs;
+  a.ldx = d->ldx;
+  a.ldo = d->ldo;
+  a.tout_valid = d->Tvalid;
+  a.epi = 1;
+  a.act = d->act;
+  a.slope = d->slope;
+  switch (d->K) {
+    case 2: return launch_ws<2, __bf16>(a, x, wp, bias, aux, res, out, s);
+    case 3: return launch_ws<3, __bf16>(a, x, wp, bias, aux, res, out, s);
+    case 5: return launch_ws<5, __bf16>(a, x, wp, bias, aux, res, out, s);
+    default: return launch_ws<7, __bf16>(a, x, wp, bias, aux, res, out, s);
+  }
+}
+}  // namespace conv
+}  // namespace sel
+
 extern "C" {
 
-int sel_conv_fwd_kernel_id(const sel_conv_desc* d, int in_dtype, int out_dtype) {
+int sel_conv_fwd_kernel_id(const sel_conv_desc* d, int in_dtype, int out_dtype, int has_epilogue) {
   if (!d || in_dtype != SEL_BF16) return -1;
   const Args a = to_args(d);
-  if (out_dtype == SEL_BF16 && thin_ok(a))  // thin: 1e9 + ((R/32*1000 + C)*1000 + N)*10 + K
-    return 1000000000 + ((thin_rows(a) / 32 * 1000 + a.C) * 1000 + a.N) * 10 + a.K;
+  if (out_dtype == SEL_BF16 && thin_ok(a)) {  // thin: 1e9 + E*5e8 + ((R/32*1000 + C)*1000 + N)*10 + K
+    int r = 0;
+    const bool e = thin_variant(a, has_epilogue != 0, r);
+    return 1000000000 + (e ? 500000000 : 0) + ((r / 32 * 1000 + a.C) * 1000 + a.N) * 10 + a.K;
+  }
   const int v = fwd4_choice(a);
   if (v < 0) return -1;
   if (v == 27) return 900000000 + a.K;  // warp-specialised kernel: 9e8 + K

@@ -38,6 +38,11 @@
 #include "sel_common.h"
 
 namespace sel {
+namespace conv {
+// conv.hip: discriminator layers on the generator's warp-specialised kernel
+int dconv_ws_fwd(const sel_dconv_desc* d, const void* x, const void* wp, const float* bias, const void* aux,
+                 const void* res, void* out, hipStream_t s);
+}  // namespace conv
 namespace dconv {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -1547,6 +1552,12 @@ int dispatch_fwd(const sel_dconv_desc* d, const void* x, const void* wp, const f
   const int width = d->So * d->Ng;
   const int64_t rows = int64_t(d->B) * d->Tvo;
   if constexpr (sizeof(T) == 2) {
+    // the MPD's >= 128-wide one-group layers and adjoints: warp-specialised
+    // 256 x 128 tiles (conv.hip k_conv_ws_bf16; tune key 21: 1 = off)
+    if (tune(21) != 1 && width % 128 == 0 && d->S * d->Cg >= 64 && rows * (width / 128) >= 65536) {
+      const int rc = sel::conv::dconv_ws_fwd(d, x, wp, bias, aux, res, out, s);
+      if (rc != SEL_ERR_UNSUPPORTED) return rc;
+    }
     if (width > 32 && pf_ok(d, dtype)) {
       // tune key 19: tile A/B (1: 256x64, 2: 128x128, 3: 256x128, 4: the <= 64-wide tiles below)
       if (tune(19) == 1) return launch_pf<256, 64>(d, x, wp, bias, aux, res, out, s);

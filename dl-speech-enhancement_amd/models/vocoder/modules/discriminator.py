@@ -114,7 +114,7 @@ class HiFiGANPeriodDiscriminator(nn.Module):
         p = self.period
         Lv = (t + p - 1) // p
         x2 = x.reshape(b, t).float()
-        seqs = DC.MpdFoldFn.apply(x2, p, DC._roundup(Lv, specs[0].stride))
+        seqs = DC.MpdFoldFn.apply(x2, p, DC.period_alloc(Lv, specs))
         x0 = CO.cast(seqs, CO.compute_dtype()).unsqueeze(-1)
         outs = list(DC.ChainFn.apply(x0, Lv, specs, self.slope, self.use_weight_norm, "period", b, p,
                                      getattr(self, "_frozen", False), *self._params()))

@@ -43,7 +43,7 @@ SIGNATURES = {
     "sel_logmel_bwd_workspace": (SZ, [I64, I64, I32, I32, I32]),
     "sel_logmel_bwd": (I32, [P, I64, I64, I32, I32, I32, P, P, P, P, I32, F32, I32,
                              P, P, P, F32, P, P, SZ, P]),
-    "sel_conv_fwd_kernel_id": (I32, [P, I32, I32]),
+    "sel_conv_fwd_kernel_id": (I32, [P, I32, I32, I32]),
     "sel_conv_fwd": (I32, [P, I32, I32, P, P, P, P, P, P, P]),
     "sel_resunit_fwd": (I32, [P, I32, P, P, P, P, P, P, P, P]),
     "sel_resunit_bwd": (I32, [P, I32, P, P, P, P, P, P, P, P]),

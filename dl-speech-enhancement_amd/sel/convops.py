@@ -269,15 +269,16 @@ def prim(desc, x, wp, bias=None, aux=None, res=None, out_dtype=None):
     return out
 
 
-def fwd_kernel_name(desc, in_dtype, out_dtype):
+def fwd_kernel_name(desc, in_dtype, out_dtype, has_epilogue=False):
     """rocprof name fragment of the kernel instance a launch uses."""
-    kid = L.lib().sel_conv_fwd_kernel_id(ctypes.byref(desc), _code(in_dtype), _code(out_dtype))
+    kid = L.lib().sel_conv_fwd_kernel_id(ctypes.byref(desc), _code(in_dtype), _code(out_dtype), int(has_epilogue))
     if kid < 0:
         return f"k_conv_fwd<{in_dtype}>"
-    if kid >= 10 ** 9:  # weight-stationary thin kernel: 1e9 + ((R/32*1000 + C)*1000 + N)*10 + K
+    if kid >= 10 ** 9:  # weight-stationary thin kernel: 1e9 + E*5e8 + ((R/32*1000 + C)*1000 + N)*10 + K
         kid -= 10 ** 9
+        e, kid = kid >= 5 * 10 ** 8, kid % (5 * 10 ** 8)
         k, n, c, r = kid % 10, (kid // 10) % 1000, (kid // 10000) % 1000, 32 * (kid // 10000000)
-        return f"k_conv_thin_bf16<{c}, {n}, {k}, {r}>"
+        return f"k_conv_thin_bf16<{c}, {n}, {k}, {r}, {'true' if e else 'false'}>"
     to = "bf16" if out_dtype == torch.bfloat16 else "float"
     if kid >= 9 * 10 ** 8:  # warp-specialised double-buffered kernel: 9e8 + K
         return f"k_conv_ws_bf16<{kid - 9 * 10 ** 8}, {to}>"
@@ -296,7 +297,7 @@ def _fwd_meta(desc, x, out, wp, aux, res):
         if t is not None:
             nbytes += t.numel() * t.element_size()
     flops = 2.0 * desc.rows * desc.N * desc.K * desc.C
-    return fwd_kernel_name(desc, x.dtype, out.dtype), nbytes, flops
+    return fwd_kernel_name(desc, x.dtype, out.dtype, aux is not None or res is not None), nbytes, flops
 
 
 def wgrad(desc, gout, x, want_bias):

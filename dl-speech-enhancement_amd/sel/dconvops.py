@@ -40,6 +40,24 @@ def _roundup(v, m):
     return (v + m - 1) // m * m
 
 
+# zero rows per sequence the period chain's layouts keep after the valid ones
+# (>= the widest tap reach across a sequence boundary of its convs: k5, pad 2)
+FLAT_GAP = 2
+
+
+def period_alloc(Lv, specs, gap=FLAT_GAP):
+    """Rows per folded sequence for an MPD chain on Lv valid rows such that every
+    layer's phase-view input and output share one row pitch with >= gap zero
+    rows after each sequence (the layout the warp-specialised kernel tiles
+    across sequences: conv.hip dconv_ws_fwd).  Falls back to the plain
+    roundup when the chain has a non-integer stride product."""
+    T, prod = Lv, 1
+    for sp in specs:
+        T = sp.t_out(T)
+        prod *= sp.stride
+    return max(_roundup(Lv, specs[0].stride), prod * (T + gap))
+
+
 class LayerSpec:
     """One conv of a sub-discriminator: torch Conv1d(cin, cout, Kt, stride,
     padding=pad, groups) (or Conv2d (Kt, 1) on the period axis), LeakyReLU after
@@ -57,19 +75,25 @@ class LayerSpec:
 
 
 def _fwd_desc(sp, Bs, T_in, T_alloc_in, T_out, T_out_alloc, slope):
+    """Forward layer: x (Bs, T_alloc_in rows, T_in valid; rows past T_in are
+    zero) in its phase view (T_alloc_in / s rows of s * cin channels, the first
+    ceil(T_in / s) of them holding samples) -> y (Bs, T_out_alloc rows, T_out
+    computed, the rest written as zeros)."""
     s = sp.stride
-    return DConvDesc(B=Bs, Tv=T_alloc_in // s, Tvs=T_alloc_in // s, ldx=s * sp.cin, Tvo=T_out_alloc, Tvalid=T_out,
+    return DConvDesc(B=Bs, Tv=(T_in + s - 1) // s, Tvs=T_alloc_in // s, ldx=s * sp.cin, Tvo=T_out_alloc, Tvalid=T_out,
                      ldo=sp.cout, K=sp.K, q0=sp.q0, S=s, Cs=sp.cin, Cg=sp.cin // sp.groups, G=sp.groups, So=1,
                      Ns=sp.cout, Ng=sp.cout // sp.groups, act=1 if sp.leaky else 0, slope=slope)
 
 
-def _dgrad_desc(sp, Bs, T_alloc_in, T_out, T_out_alloc, slope, prev_leaky):
+def _dgrad_desc(sp, Bs, T_alloc_in, T_out, T_out_alloc, slope, prev_leaky, T_in=None):
     """Adjoint of the forward layer: gout (Bs, T_out_alloc rows, T_out valid, N
     channels) -> gin in the phase view of the layer input (Bs, T_alloc_in / s
-    rows, s * cin channels)."""
+    rows, s * cin channels); with T_in, phase rows past ceil(T_in / s) (no input
+    sample there) are written as zeros instead of computed."""
     s = sp.stride
     Tvo = T_alloc_in // s
-    return DConvDesc(B=Bs, Tv=T_out, Tvs=T_out_alloc, ldx=sp.cout, Tvo=Tvo, Tvalid=Tvo, ldo=s * sp.cin, K=sp.K,
+    Tval = Tvo if T_in is None else (T_in + s - 1) // s
+    return DConvDesc(B=Bs, Tv=T_out, Tvs=T_out_alloc, ldx=sp.cout, Tvo=Tvo, Tvalid=Tval, ldo=s * sp.cin, K=sp.K,
                      q0=-sp.q0 - (sp.K - 1), S=1, Cs=sp.cout, Cg=sp.cout // sp.groups, G=sp.groups, So=s,
                      Ns=sp.cin, Ng=sp.cin // sp.groups, act=0, slope=slope)
 
@@ -203,6 +227,11 @@ class ChainFn(torch.autograd.Function):
             T_out = sp.t_out(T_in)
             nxt = specs[li + 1].stride if li + 1 < len(specs) else 1
             T_out_alloc = _roundup(T_out, nxt)
+            if T_alloc_in % sp.stride == 0 and (T_alloc_in // sp.stride) % nxt == 0 and \
+                    T_alloc_in // sp.stride - T_out >= FLAT_GAP:
+                # input pitch / s: one row pitch for the layer's phase-view input and its
+                # output, with >= FLAT_GAP zero rows per sequence (period_alloc)
+                T_out_alloc = T_alloc_in // sp.stride
             d = _fwd_desc(sp, Bs, T_in, T_alloc_in, T_out, T_out_alloc, slope)
             wp = pack(sp, w, wg, dtype, 0)
             y = torch.empty(Bs, T_out_alloc, sp.cout, dtype=dtype, device=x0.device)
@@ -256,7 +285,7 @@ class ChainFn(torch.autograd.Function):
                 break
             # adjoint of this layer: the previous layer's feature-map gradient is
             # added and its LeakyReLU' applied in the same epilogue
-            d_b = _dgrad_desc(sp, Bs, T_alloc_in, T_out, T_out_alloc, slope, li > 0)
+            d_b = _dgrad_desc(sp, Bs, T_alloc_in, T_out, T_out_alloc, slope, li > 0, T_in=T_in)
             wd = pack(sp, w, wg, dtype, 1)
             gin = torch.empty(Bs, T_alloc_in, sp.cin, dtype=dtype, device=x0.device)
             res = aux = None

@@ -158,11 +158,14 @@ typedef struct sel_conv_desc {
   int32_t bias_period;/* 0: no bias */
 } sel_conv_desc;
 
-/* which kernel instance a bf16 launch uses (for profiling tags):
+/* which kernel instance a bf16 launch uses (for profiling tags); has_epilogue:
+ * the launch passes aux and/or res (the thin kernel's epilogue-prefetch variant):
  * ((BM*1000 + BN)*10 + WAVES_M)*10 + KMAX for the tiled kernel,
- * 1000000000 + ((R/32*1000 + C)*1000 + N)*10 + K for the weight-stationary thin kernel,
+ * 900000000 + K for the warp-specialised kernel,
+ * 1000000000 + E*500000000 + ((R/32*1000 + C)*1000 + N)*10 + K for the
+ * weight-stationary thin kernel (E = epilogue-prefetch instance),
  * or -1 for the generic kernel */
-int sel_conv_fwd_kernel_id(const sel_conv_desc* d, int in_dtype, int out_dtype);
+int sel_conv_fwd_kernel_id(const sel_conv_desc* d, int in_dtype, int out_dtype, int has_epilogue);
 int sel_conv_fwd(const sel_conv_desc* d, int in_dtype, int out_dtype, const void* in,
                  const void* wpack, const float* bias, const void* aux, const void* res,
                  void* out, sel_stream_t stream);

@@ -123,3 +123,74 @@ def test_gan_terms_vector_and_scalar(gpu, C):
         m.backward()
         g2 = 2.0 * (a2.double() - 1.0) / a2.numel()
         assert ((a2.grad.double() - g2).norm() / g2.norm()).item() <= (1e-6 if dt == torch.float32 else 1e-2)
+
+
+# (tag, cin, cout, Kt, stride, pad, groups, Bs, T): MPD layers at sizes that take
+# the warp-specialised kernel (rows x width / 128 >= 65536; Bs = clips x period columns)
+WS_LAYERS = [
+    ("mpd1_s3", 32, 128, 5, 3, 2, 1, 32, 6150),
+    ("mpd2_s3", 128, 512, 5, 3, 2, 1, 32, 1602),
+    ("mpd3_s3", 512, 1024, 5, 3, 2, 1, 48, 600),
+    ("mpd4_s1", 1024, 1024, 5, 1, 2, 1, 48, 200),
+]
+
+
+@pytest.mark.parametrize("shape", WS_LAYERS, ids=[s[0] for s in WS_LAYERS])
+def test_ws_tiles_match_fp64_and_pf(gpu, shape):
+    """The MPD's wide layers on conv.hip's warp-specialised 256 x 128 kernel
+    (dconv_ws_fwd; tune key 21 = 1 keeps them on k_dconv_pf): forward with
+    bias + LeakyReLU and 3 zero rows past the computed ones, adjoint with the
+    (+ res) * LeakyReLU'(aux) epilogue, both against fp64 torch of the same bf16
+    operands (bound 1e-2 norm-wise: output rounding only) and against the pf
+    kernel (another fp32 summation order: <= 5e-3)."""
+    from sel import _lib as Lb
+    from sel import dconvops as DC
+    lib = Lb.lib()
+    dt = torch.bfloat16
+    tag, cin, cout, Kt, s, pad, G, Bs, T = shape
+    sp = DC.LayerSpec(cin, cout, Kt, s, pad, G, True)
+    slope = 0.1
+    torch.manual_seed(Kt * 31 + cout)
+    T_out = sp.t_out(T)
+    Ta = DC._roundup(T, s)
+    x = torch.zeros(Bs, Ta, cin, device=gpu)
+    x[:, :T] = torch.randn(Bs, T, cin, device=gpu)
+    x = x.to(dt)
+    w = torch.randn(cout, cin, Kt, device=gpu) / (cin * Kt) ** 0.5
+    b = torch.randn(cout, device=gpu)
+    wq = w.to(dt).double()
+    pre = torch.nn.functional.conv1d(x[:, :T].double().permute(0, 2, 1), wq, b.double(), stride=s,
+                                     padding=pad).permute(0, 2, 1)
+    ref_y = torch.nn.functional.leaky_relu(pre, slope)
+    g = torch.randn(Bs, T_out, cout, device=gpu).to(dt)
+    aux = torch.randn(Bs, Ta, cin, device=gpu).to(dt)
+    res = torch.randn(Bs, Ta, cin, device=gpu).to(dt)
+    xr = x[:, :T].double().clone().requires_grad_(True)
+    torch.nn.functional.conv1d(xr.permute(0, 2, 1), wq, None, stride=s, padding=pad).permute(0, 2, 1).backward(
+        g.double())
+    ref_gin = (xr.grad + res[:, :T].double()) * torch.where(aux[:, :T].double() > 0, 1.0, slope)
+
+    def run():
+        Tva = T_out + 3
+        d = DC._fwd_desc(sp, Bs, T, Ta, T_out, Tva, slope)
+        y = torch.full((Bs, Tva, cout), 7.0, dtype=dt, device=gpu)
+        DC.prim(d, x, DC.pack(sp, w, None, dt, 0), y, bias=b)
+        db = DC._dgrad_desc(sp, Bs, Ta, T_out, T_out, slope, False)
+        gin = torch.empty(Bs, Ta, cin, dtype=dt, device=gpu)
+        DC.prim(db, g, DC.pack(sp, w, None, dt, 1), gin, aux=aux, res=res)
+        torch.cuda.synchronize()
+        return y, gin
+
+    prev = lib.sel_tune(21, 0)
+    try:
+        y, gin = run()
+        lib.sel_tune(21, 1)
+        y_pf, gin_pf = run()
+    finally:
+        lib.sel_tune(21, prev)
+    assert torch.count_nonzero(y[:, T_out:]).item() == 0
+    rel = lambda a, r: ((a.double() - r).norm() / r.norm()).item()  # noqa: E731
+    assert rel(y[:, :T_out], ref_y) <= 1e-2, (tag, "fwd", rel(y[:, :T_out], ref_y))
+    assert rel(gin[:, :T], ref_gin) <= 1e-2, (tag, "adjoint", rel(gin[:, :T], ref_gin))
+    assert rel(y, y_pf.double()) <= 5e-3, (tag, "fwd vs pf", rel(y, y_pf.double()))
+    assert rel(gin, gin_pf.double()) <= 5e-3, (tag, "adjoint vs pf", rel(gin, gin_pf.double()))
