@@ -1504,6 +1504,184 @@ __global__ __launch_bounds__(256) void k_ru32_fwd(Args a, const __bf16* __restri
   }
 }
 
+// Residual unit at 64 channels, forward in ONE launch (round 3): the 32-channel
+// scheme with the 1x1 still fed from registers, but a wave computes conv1 for
+// one 32-channel output slice only (all 64 x 7 input fragments of its slice in
+// VGPRs, as k_conv_thin_bf16), so the 1x1 (all 64 h channels of a row) needs
+// the partner wave's slice: each wave writes ELU(bf16(h)) of its rows and slice
+// to a [2][R][P] LDS tile in the 1x1's B-fragment order, one block barrier, and
+// every wave reads its four fragments back.  Waves = 2 row groups x 2 slices.
+// h and out leave from the re-laid-out fragments as 16-B stores; the residual
+// rows (raw x) are requested before conv1 (L2-hot: the tile was just staged).
+// Same MFMA order, rounding points and epilogue arithmetic as the two thin
+// launches (k7 then 1x1), so the results are bit-identical to them.
+template <int R>
+struct Ru64 {
+  static constexpr int C = 64, K = 7, P = F4_P;
+  static constexpr int SPAN = R + F4_HALOMAX;
+  static constexpr int CV = C / 8;
+  static constexpr int XV = (SPAN * CV + 255) / 256;
+  static constexpr int WR = R / 2;  // rows per row group
+  static constexpr int TM = WR / 32;
+  static constexpr size_t LDS = size_t(2) * (SPAN + R) * P * 2;  // ELU(x) span planes + ELU(h) planes
+  static_assert(R % 64 == 0, "ru64 tile rows");
+};
+
+template <int R>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_ru64_fwd(Args a, const __bf16* __restrict__ x,
+                                                  const __bf16* __restrict__ w1p, const float* __restrict__ b1,
+                                                  const __bf16* __restrict__ w2p, const float* __restrict__ b2,
+                                                  __bf16* __restrict__ hout, __bf16* __restrict__ out,
+                                                  int tiles_per_block) {
+  using G = Ru64<R>;
+  constexpr int P = G::P, C = G::C, K = G::K, CV = G::CV;
+  extern __shared__ __align__(16) unsigned char smem[];
+  __bf16* const xs = reinterpret_cast<__bf16*>(smem);  // [2][SPAN][P]: ELU(x) rows t0 - pad ..
+  __bf16* const hs = xs + 2 * G::SPAN * P;             // [2][R][P]: ELU(h) rows t0 ..
+  const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ns = wave & 1, rg = wave >> 1;
+  const int span = R + a.pad;
+  const int tps = (a.T + R - 1) / R;
+  int64_t tile0, tile_end;
+  if (!ru_tiles((a.rows / a.T) * tps, tiles_per_block, tile0, tile_end)) return;
+
+  bf16x8 wf[K][C / 16], wf2[C / 16];
+  {
+    const __bf16* wrow = w1p + int64_t(ns * 32 + (lane & 31)) * K * C + 8 * hl;
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+#pragma unroll
+      for (int g = 0; g < C / 16; ++g) wf[k][g] = *reinterpret_cast<const bf16x8*>(wrow + k * C + 16 * g);
+    const __bf16* wrow2 = w2p + int64_t(ns * 32 + (lane & 31)) * C + 8 * hl;
+#pragma unroll
+    for (int g = 0; g < C / 16; ++g) wf2[g] = *reinterpret_cast<const bf16x8*>(wrow2 + 16 * g);
+  }
+  // biases in accumulator order (element group q = channels ns*32 + 8q + 4hl .. +4),
+  // read where used (L1-hot; registers are what bounds this kernel's occupancy)
+  auto bias_q = [&](const float* bp, int q) {
+    return bp ? *reinterpret_cast<const floatx4*>(bp + ns * 32 + 8 * q + 4 * hl) : floatx4{0.f, 0.f, 0.f, 0.f};
+  };
+
+  uint4 xr[G::XV];
+  bool xok[G::XV];
+  auto load = [&](int64_t tile) {
+    const int64_t b = tile / tps;
+    const int t0 = int(tile % tps) * R;
+#pragma unroll
+    for (int u = 0; u < G::XV; ++u) {
+      const int v = tid + u * 256;
+      const int r = v / CV, c = (v % CV) * 8;
+      int ti = t0 - a.pad + r;
+      xok[u] = r < span && ti >= 0 && ti < a.T;
+      ti = ti < 0 ? 0 : (ti >= a.T ? a.T - 1 : ti);
+      if ((u * 256) / CV < span) xr[u] = *reinterpret_cast<const uint4*>(x + (b * a.T + ti) * C + c);
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int u = 0; u < G::XV; ++u) {
+      const int v = tid + u * 256;
+      const int r = v / CV, c = (v % CV) * 8;
+      if (r >= span) continue;
+      const uint4 val = elu8(xok[u] ? xr[u] : make_uint4(0, 0, 0, 0));
+      *reinterpret_cast<uint4*>(xs + ((c >> 5) * G::SPAN + r) * P + (c & 31)) = val;
+    }
+  };
+
+  load(tile0);
+  for (int64_t tile = tile0; tile < tile_end; ++tile) {
+    const int64_t b = tile / tps;
+    const int t0 = int(tile % tps) * R;
+    const int mrows = a.T - t0 < R ? a.T - t0 : R;
+    __syncthreads();  // every wave is done with the previous tile's xs / hs
+    store();
+    __syncthreads();
+    if (tile + 1 < tile_end) load(tile + 1);
+
+    // conv1 (k_conv_thin_bf16 order: taps, 16-channel chunks, sub-tiles)
+    floatx16 acc[G::TM];
+#pragma unroll
+    for (int i = 0; i < G::TM; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
+    const __bf16* xw = xs + (rg * G::WR + (lane & 31)) * P + 8 * hl;
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+#pragma unroll
+      for (int g = 0; g < C / 16; ++g) {
+        const __bf16* xb = xw + ((g >> 1) * G::SPAN + k * a.dil) * P + 16 * (g & 1);
+#pragma unroll
+        for (int i = 0; i < G::TM; ++i)
+          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[k][g], *reinterpret_cast<const bf16x8*>(xb + i * 32 * P),
+                                                           acc[i], 0, 0, 0);
+      }
+    // residual rows of this wave's sub-tiles and slice in accumulator order
+    // (L2-hot), requested before the h epilogue and the barrier
+    uint2 xres[G::TM][4];
+#pragma unroll
+    for (int i = 0; i < G::TM; ++i) {
+      const int lr = rg * G::WR + i * 32 + (lane & 31);
+      const bool in = lr < mrows;
+      const int64_t orow = (b * a.T + t0 + (in ? lr : 0)) * C + ns * 32 + 4 * hl;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) xres[i][q] = in ? *reinterpret_cast<const uint2*>(x + orow + 8 * q) : make_uint2(0, 0);
+    }
+    // h = conv1 + b1 -> bf16 -> HBM; ELU(h) -> the 1x1's LDS tile (plane ns)
+#pragma unroll
+    for (int i = 0; i < G::TM; ++i) {
+      const int lr = rg * G::WR + i * 32 + (lane & 31);
+      float v[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const floatx4 bq = bias_q(b1, q);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[4 * q + e] = acc[i][4 * q + e] + bq[e];
+      }
+      bf16x8 hf[2];
+      ru_acc_to_frags(v, hf);
+      if (lr < mrows) {
+        const int64_t orow = (b * a.T + t0 + lr) * C + ns * 32 + 8 * hl;
+        *reinterpret_cast<bf16x8*>(hout + orow) = hf[0];
+        *reinterpret_cast<bf16x8*>(hout + orow + 16) = hf[1];
+      }
+#pragma unroll
+      for (int g = 0; g < 2; ++g)
+        *reinterpret_cast<uint4*>(hs + (ns * R + lr) * P + 16 * g + 8 * hl) = elu8(__builtin_bit_cast(uint4, hf[g]));
+    }
+    __syncthreads();
+    // out = x + conv2(ELU(h)) + b2 (k_conv_thin_bf16 epilogue order: + bias, then the residual)
+#pragma unroll
+    for (int i = 0; i < G::TM; ++i) {
+      const int lr = rg * G::WR + i * 32 + (lane & 31);
+      if (__builtin_amdgcn_readfirstlane(rg * G::WR + i * 32) >= mrows) break;  // wave-uniform
+      floatx16 acc2;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc2[e] = 0.f;
+      const __bf16* hw = hs + lr * P + 8 * hl;
+#pragma unroll
+      for (int g = 0; g < C / 16; ++g)
+        acc2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf2[g], *reinterpret_cast<const bf16x8*>(hw + (g >> 1) * R * P + 16 * (g & 1)),
+                                                       acc2, 0, 0, 0);
+      float v[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const __bf16* rv = reinterpret_cast<const __bf16*>(&xres[i][q]);
+        const floatx4 bq = bias_q(b2, q);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[4 * q + e] = __fadd_rn(acc2[4 * q + e] + bq[e], float(rv[e]));
+      }
+      bf16x8 of[2];
+      ru_acc_to_frags(v, of);
+      if (lr < mrows) {
+        const int64_t orow = (b * a.T + t0 + lr) * C + ns * 32 + 8 * hl;
+        *reinterpret_cast<bf16x8*>(out + orow) = of[0];
+        *reinterpret_cast<bf16x8*>(out + orow + 16) = of[1];
+      }
+    }
+  }
+}
+
 // Backward: gh = (W2^T g) * ELU'(h) over the tile + its anti-causal halo (the
 // adjoint of the causal conv reads rows t .. t + 6 dil), in registers -> LDS
 // (and HBM when the weight gradient needs it); gx = conv1^T(gh) * ELU'(x) + g.
@@ -1766,16 +1944,48 @@ __global__ __launch_bounds__(256) void k_wgrad_c1_bf16(Args a, const __bf16* __r
 #pragma unroll
     for (int k = 0; k < C1_KMAX; ++k) acc[e][k] = 0.f;
   }
+  // the next tile's samples are fetched into registers while this tile is
+  // reduced; this tile's gout rows are requested together before the FMAs
+  const int span = C1_TR + (a.K - 1) * a.dil;
+  float pre[2];
+  auto fetch = [&](int64_t tile) {
+    const int64_t b = tile / tps;
+    const int t0 = int(tile % tps) * C1_TR;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int r = threadIdx.x + 256 * u;
+      int ti = t0 - a.pad + r;
+      const bool ok = r < span && ((ti >= 0 && ti < a.T) || a.pad_mode == SEL_PAD_REPLICATE);
+      ti = ti < 0 ? 0 : (ti >= a.T ? a.T - 1 : ti);
+      const float v = ok ? float(in[b * a.T + ti]) : 0.f;
+      pre[u] = ok && a.in_elu ? elu_fast(v) : v;
+    }
+  };
+  if (tb < te) fetch(tb);
+  constexpr int MAXR = C1_TR / 32;  // rows per thread at NG = 8
   for (int64_t tile = tb; tile < te; ++tile) {
     const int64_t b = tile / tps;
     const int t0 = int(tile % tps) * C1_TR;
     __syncthreads();
-    c1_stage(a, in, b, t0, xs);
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      if (threadIdx.x + 256 * u < span) xs[threadIdx.x + 256 * u] = pre[u];
     __syncthreads();
+    if (tile + 1 < te) fetch(tile + 1);
     const int rows = a.T - t0 < C1_TR ? a.T - t0 : C1_TR;
-    for (int r = rl; r < rows; r += nrl) {
+    uint4 gq[MAXR];
+#pragma unroll
+    for (int j = 0; j < MAXR; ++j) {
+      const int r = rl + j * nrl;
+      if (j * nrl < C1_TR && r < rows)
+        gq[j] = *reinterpret_cast<const uint4*>(gout + (b * a.T + t0 + r) * a.N + grp * 8);
+    }
+#pragma unroll
+    for (int j = 0; j < MAXR; ++j) {
+      const int r = rl + j * nrl;
+      if (j * nrl >= C1_TR || r >= rows) break;
       __bf16 gv[8];
-      *reinterpret_cast<uint4*>(gv) = *reinterpret_cast<const uint4*>(gout + (b * a.T + t0 + r) * a.N + grp * 8);
+      *reinterpret_cast<uint4*>(gv) = gq[j];
       float xv[C1_KMAX];
 #pragma unroll
       for (int k = 0; k < C1_KMAX; ++k) xv[k] = k < a.K ? xs[r + k * a.dil] : 0.f;
@@ -3039,6 +3249,29 @@ int launch_ru32_fwd(const Args& a, const void* x, const void* w1p, const float* 
 }
 
 template <int R>
+int launch_ru64_fwd(const Args& a, const void* x, const void* w1p, const float* b1, const void* w2p,
+                    const float* b2, void* h, void* out, hipStream_t s) {
+  const int64_t ntiles = (a.rows / a.T) * ((a.T + R - 1) / R);
+  if (ntiles == 0) return SEL_OK;
+  static const int64_t slots = [] {
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_ru64_fwd<R>, 256, Ru64<R>::LDS) != hipSuccess)
+      return int64_t(0);
+    return int64_t(cus) * per_cu / 8 * 8;
+  }();
+  const int64_t target = tune(24) > 0 ? tune(24) : (slots > 0 ? slots : 1024);
+  const int64_t tpb = std::max<int64_t>(1, (ntiles + target - 1) / target);
+  const unsigned nb = unsigned(((ntiles + tpb - 1) / tpb + 7) / 8 * 8);
+  hipLaunchKernelGGL(k_ru64_fwd<R>, dim3(nb), dim3(256), Ru64<R>::LDS, s, a, static_cast<const __bf16*>(x),
+                     static_cast<const __bf16*>(w1p), b1, static_cast<const __bf16*>(w2p), b2,
+                     static_cast<__bf16*>(h), static_cast<__bf16*>(out), int(tpb));
+  SEL_LAUNCH_CHECK();
+  return SEL_OK;
+}
+
+template <int R>
 int launch_ru32_bwd(const Args& a, const void* g, const void* h, const void* x, const void* wd1, const void* wd2,
                     void* gh, void* gx, hipStream_t s) {
   const int64_t ntiles = (a.rows / a.T) * ((a.T + R - 1) / R);
@@ -3321,7 +3554,9 @@ int sel_resunit_fwd(const sel_conv_desc* d1, int dtype, const void* x, const voi
               "sel_resunit_fwd: fused path needs bf16, C = N in {32, 64}, K = 7, causal zero pad, ELU prologue");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (a.C == 32) return launch_ru32_fwd<256>(a, x, w1pack, b1, w2pack, b2, h, out, s);
-  return launch_ru_thin<64, 7, 64>(a, x, w1pack, b1, w2pack, b2, h, out, s);
+  // tune key 24 < 0: the LDS-staged k_ru_thin_bf16 (round 2) instead of k_ru64_fwd
+  if (tune(24) < 0) return launch_ru_thin<64, 7, 64>(a, x, w1pack, b1, w2pack, b2, h, out, s);
+  return launch_ru64_fwd<128>(a, x, w1pack, b1, w2pack, b2, h, out, s);
 }
 
 /* Fused residual unit backward at 32 channels (residual_unit.py:43-46 adjoint):

@@ -400,9 +400,9 @@ class ConvLayerFn(torch.autograd.Function):
 
 
 # fused residual unit (sel_resunit_fwd / sel_resunit_bwd): ON by default at 32
-# channels (register-resident 1x1, k_ru32_fwd / k_ru32_bwd); the 64-channel
-# forward (k_ru_thin_bf16) measured slower than the two calls and is only used
-# with SEL_RU_FUSED=1; SEL_RU_FUSED=0 turns every fused path off
+# channels (register-resident 1x1, k_ru32_fwd / k_ru32_bwd) and for the
+# 64-channel forward (k_ru64_fwd: the 1x1's h fragments exchanged between the
+# two slice waves through LDS); SEL_RU_FUSED=0 turns every fused path off
 RU_FUSED = os.environ.get("SEL_RU_FUSED", "")
 
 
@@ -415,14 +415,14 @@ def _ru_shape_ok(d1, dtype):
 
 def ru_fused_ok(d1, dtype):
     """Fused residual-unit forward for this conv1 descriptor?"""
-    if RU_FUSED == "0" or not _ru_shape_ok(d1, dtype):
-        return False
-    return d1.C == 32 or RU_FUSED == "1"
+    # SEL_RU_FUSED=32: the 32-channel unit only (A/B of the 64-channel forward)
+    return RU_FUSED != "0" and _ru_shape_ok(d1, dtype) and (RU_FUSED != "32" or d1.C == 32)
 
 
 def ru_bwd_fused_ok(d1, dtype):
     """Fused residual-unit backward (32 channels only)?"""
-    return RU_FUSED != "0" and _ru_shape_ok(d1, dtype) and d1.C == 32
+    # SEL_RU_FUSED=32: the 32-channel unit only (A/B of the 64-channel forward)
+    return RU_FUSED != "0" and _ru_shape_ok(d1, dtype) and (RU_FUSED != "32" or d1.C == 32) and d1.C == 32
 
 
 def resunit_bwd(d1, gf, h, xf, wd1, wd2, want_gh):
@@ -457,7 +457,7 @@ def _ru_meta(d1, xf, wp1, wp2):
     es = xf.element_size()
     nbytes = 3 * d1.rows * d1.C * es + (wp1.numel() + wp2.numel()) * es
     flops = 2.0 * d1.rows * d1.N * d1.C * (d1.K + 1)
-    return ("k_ru32_fwd<256>" if d1.C == 32 else "k_ru_thin_bf16<64, 7, 64>"), nbytes, flops
+    return ("k_ru32_fwd<256>" if d1.C == 32 else "k_ru64_fwd<128>"), nbytes, flops
 
 
 class ResidualUnitFn(torch.autograd.Function):
