@@ -3588,7 +3588,8 @@ struct UnpackSpec {
   int kind, cout, cin, k, stride;
 };
 int wgrad_impl(const sel_conv_desc* d, int dtype, const void* gout, const void* in, float* gwout,
-               const UnpackSpec* up, float* gbias, void* ws, size_t ws_bytes, sel_stream_t stream);
+               const UnpackSpec* up, float* gbias, void* ws, size_t ws_bytes, sel_stream_t stream,
+               int* partials_only = nullptr);
 }  // namespace conv
 }  // namespace sel
 
@@ -3614,7 +3615,8 @@ int sel_conv_wgrad_unpacked(const sel_conv_desc* d, int dtype, const void* gout,
 namespace sel {
 namespace conv {
 int wgrad_impl(const sel_conv_desc* d, int dtype, const void* gout, const void* in, float* gwpack,
-               const UnpackSpec* up, float* gbias, void* ws, size_t ws_bytes, sel_stream_t stream) {
+               const UnpackSpec* up, float* gbias, void* ws, size_t ws_bytes, sel_stream_t stream,
+               int* partials_only) {
   if (int rc = check_desc(d)) return rc;
   SEL_REQUIRE(d->K * 2 <= WB_MAXJ * 1 || dtype == SEL_F32, SEL_ERR_UNSUPPORTED, "wgrad: K=%d too large", d->K);
   SEL_REQUIRE(dtype == SEL_BF16 || d->K * (kWgBN / 16) * 2 <= 4 * WG_MAXT, SEL_ERR_UNSUPPORTED,
@@ -3695,6 +3697,10 @@ int wgrad_impl(const sel_conv_desc* d, int dtype, const void* gout, const void* 
     set_error("bad dtype %d", dtype);
     return SEL_ERR_ARG;
   }
+  if (partials_only) {  // sel_conv_wgrad_partials: the reduction is batched later
+    *partials_only = p.nsplit;
+    return SEL_OK;
+  }
   // two-pass split reduction; the second-level partials live after the first-level ones
   const int64_t nw = int64_t(d->N) * d->K * d->C;
   const int ng = (p.nsplit + SPLIT_GROUP - 1) / SPLIT_GROUP;
@@ -3737,9 +3743,137 @@ int wgrad_impl(const sel_conv_desc* d, int dtype, const void* gout, const void* 
 }  // namespace conv
 }  // namespace sel
 
+namespace sel {
+namespace conv {
+// Batched split reduction (sel_wgrad_finish_many), with exactly the arithmetic
+// of k_split_sum1 + k_split_sum2_unpack / k_split_sum2 (and of k_split_finish1,
+// the one-group case of the same formula): group sums of 32 splits
+// (split_group_sum), then the groups in order, four at a time.  A weight block
+// owns 64 consecutive PACKED elements of one job (coalesced partial reads): its
+// 4 waves compute the group sums of groups w, w + 4, ... into LDS, wave 0 adds
+// them in order and scatters to the torch layout.  A bias block owns one bias
+// element: its threads compute the (group, column) sums, thread 0 adds them in
+// order.  Block ranges per job come in the kernel argument.
+constexpr int FM_MAXJ = 24;
+constexpr int FM_MAXG = 32;  // split groups per job (nsplit <= 1024)
+struct FinishJobs {
+  sel_wgrad_job j[FM_MAXJ];
+  int wblocks[FM_MAXJ];  // weight blocks of job j; its bias blocks follow
+  int bstart[FM_MAXJ + 1];
+  int njobs;
+};
+
+// packed weight index -> torch-layout index (-1: a structural zero of the strided form)
+__device__ __forceinline__ int64_t pack_dst(int kind, int64_t j, int cout, int cin, int K, int s) {
+  if (kind < 0) return j;
+  const int ci = int(j % cin);
+  if (kind == SEL_PACK_FWD) {
+    const int k = int((j / cin) % K);
+    const int64_t co = j / (int64_t(cin) * K);
+    return (co * cin + ci) * K + k;
+  }
+  if (kind == SEL_PACK_FWD_STRIDED) {
+    const int ph = int((j / cin) % s);
+    const int tap = int((j / (int64_t(s) * cin)) % 3);
+    const int64_t co = j / (int64_t(3) * s * cin);
+    const int k = tap == 0 ? (ph >= 1 ? ph - 1 : -1) : (tap == 1 ? ph + s - 1 : (ph == 0 ? 2 * s - 1 : -1));
+    return k < 0 ? -1 : (co * cin + ci) * (2 * s) + k;
+  }
+  const int tap = int((j / cin) % 2);
+  const int64_t r = j / (int64_t(2) * cin);
+  const int ph = int(r / cout), co = int(r % cout);
+  const int k = tap ? ph : ph + s;
+  return (int64_t(ci) * cout + co) * (2 * s) + k;
+}
+
+__global__ __launch_bounds__(256) void k_wgrad_finish_many(FinishJobs fj) {
+  __shared__ float gs[FM_MAXG][65];
+  int jb = 0;
+  while (jb + 1 < fj.njobs && int(blockIdx.x) >= fj.bstart[jb + 1]) ++jb;  // block-uniform
+  const sel_wgrad_job& J = fj.j[jb];
+  const int lb = int(blockIdx.x) - fj.bstart[jb];
+  const int ng = (J.nsplit + SPLIT_GROUP - 1) / SPLIT_GROUP;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  auto group = [&](const float* p, int g, int64_t n) {
+    const int s0 = g * SPLIT_GROUP, cnt = J.nsplit - s0 < SPLIT_GROUP ? J.nsplit - s0 : SPLIT_GROUP;
+    return split_group_sum(p + int64_t(s0) * n, cnt, n);
+  };
+  if (lb < fj.wblocks[jb]) {
+    const int64_t j = int64_t(lb) * 64 + lane;
+    if (j < J.nw)
+      for (int g = wave; g < ng; g += 4) gs[g][lane] = group(J.part + j, g, J.nw);
+    __syncthreads();
+    if (wave == 0 && j < J.nw) {
+      float acc = 0.f;
+      int g = 0;
+      for (; g + 4 <= ng; g += 4) acc += (gs[g][lane] + gs[g + 1][lane]) + (gs[g + 2][lane] + gs[g + 3][lane]);
+      for (; g < ng; ++g) acc += gs[g][lane];
+      const int64_t i = pack_dst(J.kind, j, J.cout, J.cin, J.k, J.stride);
+      if (i >= 0) J.gw[i] = acc;
+    }
+  } else {
+    const int jb2 = lb - fj.wblocks[jb];  // bias element
+    const int M = J.N / J.bias_period;     // columns folded into it
+    const float* bp = J.part + int64_t(J.nsplit) * J.nw;
+    float* const ts = &gs[0][0];           // [g][m]
+    for (int t = tid; t < ng * M; t += 256) ts[t] = group(bp + jb2 + int64_t(t % M) * J.bias_period, t / M, J.N);
+    __syncthreads();
+    if (tid == 0) {
+      float acc = 0.f;
+      for (int t = 0; t < ng * M; ++t) acc += ts[t];
+      J.gb[jb2] = acc;
+    }
+  }
+}
+}  // namespace conv
+}  // namespace sel
+
 extern "C" {
 
+int sel_conv_wgrad_partials(const sel_conv_desc* d, int dtype, const void* gout, const void* in, int want_bias,
+                            void* ws, size_t ws_bytes, int* nsplit, sel_stream_t stream) {
+  SEL_REQUIRE(nsplit, SEL_ERR_ARG, "null nsplit");
+  int ns = 0;
+  // a non-null bias pointer only selects the bias partials (it is never written here)
+  float dummy = 0.f;
+  const int rc = sel::conv::wgrad_impl(d, dtype, gout, in, nullptr, nullptr, want_bias ? &dummy : nullptr, ws,
+                                       ws_bytes, stream, &ns);
+  *nsplit = ns;
+  return rc;
+}
+
+int sel_wgrad_finish_many(const sel_wgrad_job* jobs, int njobs, sel_stream_t stream) {
+  using namespace sel::conv;
+  SEL_REQUIRE(njobs >= 0 && (njobs == 0 || jobs), SEL_ERR_ARG, "bad job list");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  for (int j0 = 0; j0 < njobs; j0 += FM_MAXJ) {
+    FinishJobs fj{};
+    fj.njobs = std::min(FM_MAXJ, njobs - j0);
+    int64_t blocks = 0;
+    for (int j = 0; j < fj.njobs; ++j) {
+      const sel_wgrad_job& J = jobs[j0 + j];
+      SEL_REQUIRE(J.part && J.gw && J.nsplit > 0 && J.nsplit <= FM_MAXG * SPLIT_GROUP && J.nw > 0 && J.N > 0 &&
+                      (J.gb == nullptr || (J.bias_period > 0 && J.N % J.bias_period == 0 &&
+                                           (J.N / J.bias_period) * ((J.nsplit + SPLIT_GROUP - 1) / SPLIT_GROUP) <=
+                                               FM_MAXG * 65)),
+                  SEL_ERR_ARG, "bad wgrad job %d", j0 + j);
+      fj.j[j] = J;
+      fj.wblocks[j] = int((J.nw + 63) / 64);
+      fj.bstart[j] = int(blocks);
+      blocks += fj.wblocks[j] + (J.gb ? J.bias_period : 0);
+    }
+    fj.bstart[fj.njobs] = int(blocks);
+    SEL_REQUIRE(blocks < (int64_t(1) << 31), SEL_ERR_ARG, "wgrad jobs too large");
+    if (blocks > 0) {
+      hipLaunchKernelGGL(k_wgrad_finish_many, dim3(unsigned(blocks)), dim3(256), 0, s, fj);
+      SEL_LAUNCH_CHECK();
+    }
+  }
+  return SEL_OK;
+}
+
 int sel_pack_weight(int kind, const float* w, int cout, int cin, int k, int stride, int dtype, void* wpack,
+
                     sel_stream_t stream) {
   SEL_REQUIRE(kind >= SEL_PACK_FWD && kind <= SEL_PACK_CONVT, SEL_ERR_ARG, "bad pack kind");
   SEL_REQUIRE(kind == SEL_PACK_FWD || k == 2 * stride, SEL_ERR_UNSUPPORTED,

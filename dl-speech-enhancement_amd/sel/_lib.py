@@ -49,6 +49,8 @@ SIGNATURES = {
     "sel_resunit_bwd": (I32, [P, I32, P, P, P, P, P, P, P, P]),
     "sel_conv_wgrad_workspace": (SZ, [P]),
     "sel_conv_wgrad": (I32, [P, I32, P, P, P, P, P, SZ, P]),
+    "sel_conv_wgrad_partials": (I32, [P, I32, P, P, I32, P, SZ, P, P]),
+    "sel_wgrad_finish_many": (I32, [P, I32, P]),
     "sel_pack_weight": (I32, [I32, P, I32, I32, I32, I32, I32, P, P]),
     "sel_pack_dgrad": (I32, [P, I32, I32, I32, I32, P, P]),
     "sel_unpack_wgrad": (I32, [I32, P, I32, I32, I32, I32, P, P]),

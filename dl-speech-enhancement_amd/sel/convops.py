@@ -310,9 +310,75 @@ def wgrad(desc, gout, x, want_bias):
     return gwp, gb
 
 
-def wgrad_torch(desc, gout, x, kind, w_shape, stride, want_bias):
+class _WgradJob(ctypes.Structure):
+    """include/sel.h sel_wgrad_job"""
+    _fields_ = [("part", ctypes.c_void_p), ("gw", ctypes.c_void_p), ("gb", ctypes.c_void_p),
+                ("nw", ctypes.c_int64), ("nsplit", ctypes.c_int32), ("N", ctypes.c_int32),
+                ("bias_period", ctypes.c_int32), ("kind", ctypes.c_int32), ("cout", ctypes.c_int32),
+                ("cin", ctypes.c_int32), ("k", ctypes.c_int32), ("stride", ctypes.c_int32)]
+
+
+# Deferred weight-gradient reductions (SEL_WGRAD_DEFER=0: off).  Inside a
+# backward pass every layer's split-row partial kernel runs where the layer's
+# gradient is produced, but the reductions of all layers run as ONE launch
+# (sel_wgrad_finish_many) from an autograd final callback, i.e. before
+# backward() returns and before anything reads a .grad: ~25 reduction launches
+# of 5-10 us per C3 step become one.  Only where nothing can read the gradient
+# tensor in between: the parameter is a leaf whose .grad is None (AccumulateGrad
+# then takes the returned tensor itself, no copy or add), no create_graph, no
+# multi-rank process group (DDP copies gradients into its buckets from hooks as
+# they arrive).  The flush checks that every deferred tensor is still the one
+# AccumulateGrad kept and raises otherwise.
+WGRAD_DEFER = os.environ.get("SEL_WGRAD_DEFER", "1") != "0"
+_DEFERRED = []
+_DEFER_LOCK = threading.Lock()
+
+
+def _can_defer(params):
+    """params: the leaf parameters the returned gradients go to, in order (gw, gb)."""
+    if not WGRAD_DEFER or torch.is_grad_enabled() or not params:
+        return False
+    try:
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            return False
+        for p in params:
+            if p is None or not p.is_leaf or p.grad is not None:
+                return False
+            # the engine accumulates into .grad in this backward (not autograd.grad(inputs=...))
+            if not torch._C._will_engine_execute_node(torch.autograd.graph.get_gradient_edge(p).node):
+                return False
+    except (ImportError, RuntimeError, AttributeError):
+        return False
+    return True
+
+
+def _flush_deferred():
+    with _DEFER_LOCK:
+        pending = list(_DEFERRED)
+        _DEFERRED.clear()
+    if not pending:
+        return
+    for _job, _ws, refs, _st in pending:
+        for ref, ptr in refs:
+            p_ = ref()
+            if p_ is None or p_.grad is None or p_.grad.data_ptr() != ptr:
+                raise L.SelError("sel: a deferred weight gradient did not become the parameter's .grad "
+                                 "(set SEL_WGRAD_DEFER=0 for this use)")
+    # one launch per stream the partial kernels ran on (normally one)
+    for st in dict.fromkeys(e[3] for e in pending):
+        group = [e[0] for e in pending if e[3] == st]
+        jobs = (_WgradJob * len(group))(*group)
+        L.call("sel_wgrad_finish_many", ctypes.cast(jobs, ctypes.c_void_p), len(group), ctypes.c_void_p(st))
+    # the workspaces are released here; the finish kernel is already enqueued on
+    # this stream ahead of any later use of that memory
+
+
+def wgrad_torch(desc, gout, x, kind, w_shape, stride, want_bias, params=None):
     """Weight (torch layout, fp32) and bias gradient of one layer; the unpack is
-    fused into the kernel's final reduction pass (sel_conv_wgrad_unpacked)."""
+    fused into the kernel's final reduction pass (sel_conv_wgrad_unpacked).
+    `params`: (weight, bias if want_bias) leaf parameters that receive the
+    returned gradients (enables the deferred, batched reduction; WGRAD_DEFER)."""
     lib = L.lib()
     ws = L.workspace(lib.sel_conv_wgrad_workspace(ctypes.byref(desc)), x.device)
     gw = torch.empty(w_shape, dtype=torch.float32, device=x.device)
@@ -321,6 +387,24 @@ def wgrad_torch(desc, gout, x, kind, w_shape, stride, want_bias):
         cin, cout, k = w_shape
     else:
         cout, cin, k = w_shape
+    if params is not None and len(params) == 1 + int(gb is not None) and _can_defer(params):
+        try:
+            torch.autograd.Variable._execution_engine.queue_callback(_flush_deferred)
+        except RuntimeError:  # not inside a backward pass
+            pass
+        else:
+            ns = ctypes.c_int()
+            st = L.stream()
+            L.call("sel_conv_wgrad_partials", ctypes.byref(desc), _code(x.dtype), L.ptr(gout), L.ptr(x),
+                   int(want_bias), L.ptr(ws), ws.numel(), ctypes.byref(ns), st)
+            job = _WgradJob(ws.data_ptr(), gw.data_ptr(), gb.data_ptr() if gb is not None else None,
+                            desc.N * desc.K * desc.C, ns.value, desc.N, desc.bias_period, kind, cout, cin, k,
+                            stride)
+            refs = [(weakref.ref(params[0]), gw.data_ptr())] + \
+                ([(weakref.ref(params[1]), gb.data_ptr())] if gb is not None else [])
+            with _DEFER_LOCK:
+                _DEFERRED.append((job, ws, refs, st.value))
+            return gw, gb
     L.call("sel_conv_wgrad_unpacked", ctypes.byref(desc), _code(x.dtype), L.ptr(gout), L.ptr(x), kind, cout, cin,
            k, stride, L.ptr(gw), L.ptr(gb), L.ptr(ws), ws.numel(), L.stream())
     return gw, gb
@@ -354,6 +438,20 @@ def _layer_desc(kind, B, T_in, cin, cout, k, stride, dil, has_bias):
     return d, T_in * stride, cout
 
 
+def _live(*refs):
+    """Parameters behind the weak references of the gradients a wgrad call
+    returns (None entries: gradient not requested); None if one has died."""
+    out = []
+    for r in refs:
+        if r is None:
+            continue
+        p_ = r()
+        if p_ is None:
+            return None
+        out.append(p_)
+    return out or None
+
+
 class ConvLayerFn(torch.autograd.Function):
     """One reference conv layer (causal / strided / transposed), channels-last."""
 
@@ -376,6 +474,7 @@ class ConvLayerFn(torch.autograd.Function):
         y = prim(desc, x, wp, bias=bias)
         ctx.save_for_backward(x, wp, wd)
         ctx.meta = (desc, kind, stride, tuple(w.shape), b is not None)
+        ctx.prefs = (weakref.ref(w), weakref.ref(b) if b is not None else None)
         return y.view(B, T_out, c_out)
 
     @staticmethod
@@ -393,7 +492,9 @@ class ConvLayerFn(torch.autograd.Function):
                        L.ptr(gx), L.stream())
             gx = gx.view(x.shape)
         if ctx.needs_input_grad[1] or (has_bias and ctx.needs_input_grad[2]):
-            gw, gb = wgrad_torch(desc, gy, x, kind, w_shape, stride, has_bias and ctx.needs_input_grad[2])
+            want_b = has_bias and ctx.needs_input_grad[2]
+            params = _live(ctx.prefs[0], ctx.prefs[1] if want_b else None) if ctx.needs_input_grad[1] else None
+            gw, gb = wgrad_torch(desc, gy, x, kind, w_shape, stride, want_b, params)
             if not ctx.needs_input_grad[1]:
                 gw = None
         return gx, gw, gb, None, None, None
@@ -486,6 +587,7 @@ class ResidualUnitFn(torch.autograd.Function):
             out = prim(d2, h, wp2, bias=bb2, res=xf)
         ctx.save_for_backward(x, h, wd1, wd2)
         ctx.meta = (d1, d2, tuple(w1.shape), tuple(w2.shape))
+        ctx.prefs = tuple(weakref.ref(p_) if p_ is not None else None for p_ in (w1, b1, w2, b2))
         return out.view(B, T, C)
 
     @staticmethod
@@ -508,13 +610,18 @@ class ResidualUnitFn(torch.autograd.Function):
             # dL/dh = (W2^T g) * ELU'(h)
             gh = prim(d2.adjoint(), gf, wd2, aux=h)
         gw1 = gb1 = gw2 = gb2 = None
+        pr = ctx.prefs
         if ctx.needs_input_grad[3] or ctx.needs_input_grad[4]:
-            gw2, gb2 = wgrad_torch(d2, gf, h, PACK_FWD, s2, 1, d2.bias_period > 0 and ctx.needs_input_grad[4])
+            want_b = d2.bias_period > 0 and ctx.needs_input_grad[4]
+            params = _live(pr[2], pr[3] if want_b else None) if ctx.needs_input_grad[3] else None
+            gw2, gb2 = wgrad_torch(d2, gf, h, PACK_FWD, s2, 1, want_b, params)
             gw2 = gw2 if ctx.needs_input_grad[3] else None
         if ctx.needs_input_grad[0] and gx is None:
             # dL/dx = g + (conv_adjoint(gh)) * ELU'(x)
             gx = prim(d1.adjoint(), gh, wd1, aux=xf, res=gf).view(B, T, C)
         if need_w1:
-            gw1, gb1 = wgrad_torch(d1, gh, xf, PACK_FWD, s1, 1, d1.bias_period > 0 and ctx.needs_input_grad[2])
+            want_b = d1.bias_period > 0 and ctx.needs_input_grad[2]
+            params = _live(pr[0], pr[1] if want_b else None) if ctx.needs_input_grad[1] else None
+            gw1, gb1 = wgrad_torch(d1, gh, xf, PACK_FWD, s1, 1, want_b, params)
             gw1 = gw1 if ctx.needs_input_grad[1] else None
         return gx, gw1, gb1, gw2, gb2, None

@@ -193,6 +193,23 @@ int sel_conv_wgrad(const sel_conv_desc* d, int dtype, const void* gout, const vo
 int sel_conv_wgrad_unpacked(const sel_conv_desc* d, int dtype, const void* gout, const void* in, int kind,
                             int cout, int cin, int k, int stride, float* gw, float* gbias, void* ws,
                             size_t ws_bytes, sel_stream_t stream);
+/* Deferred weight gradients (one reduction launch for many layers):
+ * sel_conv_wgrad_partials runs only the split-row partial kernel of
+ * sel_conv_wgrad into ws (same plan, same partials) and returns the split count
+ * in *nsplit; sel_wgrad_finish_many then reduces up to any number of such
+ * workspaces in one launch per 24 jobs, with the arithmetic of the per-layer
+ * reduction passes (same bits), unpacking into the torch layout (kind >= 0) or
+ * writing the packed form (kind < 0).  `jobs` is a HOST array. */
+typedef struct sel_wgrad_job {
+  const float* part;  /* the workspace of sel_conv_wgrad_partials */
+  float* gw;          /* weight gradient (torch layout when kind >= 0) */
+  float* gb;          /* bias gradient (bias_period entries) or NULL */
+  int64_t nw;         /* N * K * C (packed weight elements) */
+  int32_t nsplit, N, bias_period, kind, cout, cin, k, stride;
+} sel_wgrad_job;
+int sel_conv_wgrad_partials(const sel_conv_desc* d, int dtype, const void* gout, const void* in, int want_bias,
+                            void* ws, size_t ws_bytes, int* nsplit, sel_stream_t stream);
+int sel_wgrad_finish_many(const sel_wgrad_job* jobs, int njobs, sel_stream_t stream);
 /* Repack fp32 torch weights (kind SEL_PACK_*) into Wp (dtype), and the dgrad
  * form of a packed Wp[N][K][C] -> Wd[C][K][N] with taps reversed (the adjoint is
  * the same primitive with pad' = (K-1)*dil - pad). */

@@ -472,3 +472,49 @@ def test_resunit32_autograd_fused_vs_unfused(gpu, monkeypatch, C):
     _ulp_close(res[""][1], res["0"][1])          # gx
     for a_, b_ in zip(res[""][2:], res["0"][2:]):  # weight / bias grads (fp32) through the same gh
         assert ((a_ - b_).norm() / b_.norm()).item() < 1e-3
+
+
+def test_deferred_wgrad_reduction_bit_identical(gpu, monkeypatch):
+    """Batched weight-gradient reductions (sel_conv_wgrad_partials + one
+    sel_wgrad_finish_many launch from the autograd final callback) give the
+    same bits as the per-layer reduction passes, for a residual unit (fused
+    bwd path: k7 + 1x1, with biases), a strided conv, a transposed conv and a
+    single-channel first conv; with a pre-existing .grad (accumulation) the
+    layer is not deferred and the sum is still exact."""
+    from sel import convops as CO
+    torch.manual_seed(11)
+    B, T = 2, 3000
+
+    def run(defer, accumulate=False):
+        monkeypatch.setattr(CO, "WGRAD_DEFER", defer)
+        g = torch.Generator(device=gpu).manual_seed(3)
+        x0 = (0.5 * torch.randn(B, T, 1, device=gpu, generator=g)).to(torch.bfloat16)
+        w0 = (0.3 * torch.randn(32, 1, 7, device=gpu, generator=g)).requires_grad_(True)
+        w1 = (0.1 * torch.randn(32, 32, 7, device=gpu, generator=g)).requires_grad_(True)
+        b1 = torch.randn(32, device=gpu, generator=g).requires_grad_(True)
+        w2 = (0.2 * torch.randn(32, 32, 1, device=gpu, generator=g)).requires_grad_(True)
+        b2 = torch.randn(32, device=gpu, generator=g).requires_grad_(True)
+        ws = (0.1 * torch.randn(64, 32, 6, device=gpu, generator=g)).requires_grad_(True)
+        bs = torch.randn(64, device=gpu, generator=g).requires_grad_(True)
+        wt = (0.1 * torch.randn(64, 32, 6, device=gpu, generator=g)).requires_grad_(True)
+        bt = torch.randn(32, device=gpu, generator=g).requires_grad_(True)
+        params = (w0, w1, b1, w2, b2, ws, bs, wt, bt)
+        if accumulate:
+            for p_ in params:
+                p_.grad = torch.ones_like(p_)
+        h = CO.ConvLayerFn.apply(x0, w0, None, CO.PACK_FWD, 1, 1)
+        h = CO.ResidualUnitFn.apply(h, w1, b1, w2, b2, 3)
+        h = CO.ConvLayerFn.apply(h, ws, bs, CO.PACK_FWD, 3, 1)
+        y = CO.ConvLayerFn.apply(h, wt, bt, CO.PACK_CONVT, 3, 1)
+        y.float().square().mean().backward()
+        torch.cuda.synchronize()
+        return [p_.grad.clone() for p_ in params]
+
+    ref = run(False)
+    got = run(True)
+    assert not CO._DEFERRED
+    for i, (a_, b_) in enumerate(zip(got, ref)):
+        assert torch.equal(a_, b_), (i, (a_ - b_).abs().max().item())
+    acc = run(True, accumulate=True)
+    for a_, b_ in zip(acc, ref):
+        assert torch.equal(a_, b_ + 1.0)
