@@ -904,6 +904,55 @@ __global__ __launch_bounds__(256) void k_dbias_part(D d, const T* __restrict__ g
   if (ly == 0 && go < nb) bpart[int64_t(blockIdx.y) * nb + go] = (red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]);
 }
 
+// Vector form (bf16, So == 1, 8-aligned contiguous columns): a thread sums 8
+// consecutive columns with 16-B loads over every 32nd row of the split, the 32
+// row lanes are added in order through LDS (the scalar kernel above issued one
+// 2-byte load per lane and row: ~1 TB/s).
+__global__ __launch_bounds__(256) void k_dbias_part_v(D d, const __bf16* __restrict__ gout, int rows_per_split,
+                                                      float* __restrict__ bpart) {
+  __shared__ float red[32][65];
+  const int64_t nb = int64_t(d.G) * d.Ng;
+  const int64_t total_rows = int64_t(d.B) * d.Tvalid;
+  const int64_t r0 = int64_t(blockIdx.y) * rows_per_split;
+  const int64_t r1 = r0 + rows_per_split < total_rows ? r0 + rows_per_split : total_rows;
+  const int cg = threadIdx.x & 7, ly = threadIdx.x >> 3;
+  const int64_t c0 = int64_t(blockIdx.x) * 64 + cg * 8;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c0 < nb) {
+    int64_t rr = r0 + ly;
+    int b = int(rr / d.Tvalid), j = int(rr - int64_t(b) * d.Tvalid);
+    for (; rr < r1; rr += 32) {
+      const uint4 raw = *reinterpret_cast<const uint4*>(gout + (int64_t(b) * d.Tvo + j) * d.ldo + c0);
+      const __bf16* v = reinterpret_cast<const __bf16*>(&raw);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += float(v[e]);
+      j += 32;
+      while (j >= d.Tvalid) j -= d.Tvalid, ++b;
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[ly][cg * 8 + e] = acc[e];
+  __syncthreads();
+  const int64_t go = int64_t(blockIdx.x) * 64 + threadIdx.x;
+  if (threadIdx.x < 64 && go < nb) {
+    float t = 0.f;
+    for (int l = 0; l < 32; ++l) t += red[l][threadIdx.x];
+    bpart[int64_t(blockIdx.y) * nb + go] = t;
+  }
+}
+
+// bias partials of a forward layer's gout: the vector kernel where it applies
+// (tune key 25 = 1: the scalar one)
+void launch_dbias_part(const sel_dconv_desc* d, const __bf16* gout, int rows_per_split, int bsplit, float* bpart,
+                       hipStream_t s) {
+  const int64_t nb = int64_t(d->G) * d->So * d->Ng;
+  dim3 bg(unsigned((nb + 63) / 64), unsigned(bsplit));
+  if (d->So == 1 && nb % 8 == 0 && d->ldo % 8 == 0 && tune(25) != 1)
+    hipLaunchKernelGGL(k_dbias_part_v, bg, dim3(256), 0, s, *d, gout, rows_per_split, bpart);
+  else
+    hipLaunchKernelGGL(k_dbias_part<__bf16>, bg, dim3(256), 0, s, *d, gout, rows_per_split, bpart);
+}
+
 // Partial sums over groups of PRESUM splits (coalesced over the weights), so the
 // final per-output reduction reads at most PRESUM partials.
 constexpr int PRESUM = 16;
@@ -1077,10 +1126,39 @@ __host__ __device__ inline PackGeo pack_geo(int N, int Cg, int Kt, int s, int pa
 
 // one block per output channel n: ||v_n|| then the packed weights
 template <typename T>
+__device__ __forceinline__ void dpack_channel(const PackGeo& pg, int mode, const float* __restrict__ w,
+                                              const float* __restrict__ wg, T* __restrict__ out, int n);
+
+template <typename T>
 __global__ __launch_bounds__(256) void k_dpack(PackGeo pg, int mode, const float* __restrict__ w,
                                                const float* __restrict__ wg, T* __restrict__ out) {
+  dpack_channel<T>(pg, mode, w, wg, out, blockIdx.x);
+}
+
+// batched form: block ranges per job in the kernel argument
+constexpr int DPM_MAXJ = 24;
+struct DPackJobs {
+  PackGeo pg[DPM_MAXJ];
+  const float* w[DPM_MAXJ];
+  const float* wg[DPM_MAXJ];
+  void* out[DPM_MAXJ];
+  int mode[DPM_MAXJ];
+  int bstart[DPM_MAXJ + 1];
+  int njobs;
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_dpack_many(DPackJobs dj) {
+  int j = 0;
+  while (j + 1 < dj.njobs && int(blockIdx.x) >= dj.bstart[j + 1]) ++j;  // block-uniform
+  dpack_channel<T>(dj.pg[j], dj.mode[j], dj.w[j], dj.wg[j], static_cast<T*>(dj.out[j]),
+                   int(blockIdx.x) - dj.bstart[j]);
+}
+
+template <typename T>
+__device__ __forceinline__ void dpack_channel(const PackGeo& pg, int mode, const float* __restrict__ w,
+                                              const float* __restrict__ wg, T* __restrict__ out, int n) {
   __shared__ float red[16];
-  const int n = blockIdx.x;
   const int per = pg.Cg * pg.Kt;
   float scale = 1.f;
   if (wg) {
@@ -1711,12 +1789,7 @@ hipError_t wgrad_fill(const sel_dconv_desc* d, int dtype, const WgPlanD& p, cons
     SEL_W3(2, 1, 1) SEL_W3(2, 1, 2) SEL_W3(2, 1, 4) SEL_W3(2, 1, 8) SEL_W3(2, 2, 1) SEL_W3(2, 2, 2)
     SEL_W3(2, 2, 4) SEL_W3(2, 2, 8) { return hipErrorInvalidValue; }
 #undef SEL_W3
-    if (bpart) {
-      const int64_t nb = int64_t(d->G) * width;
-      dim3 bg(unsigned((nb + 63) / 64), unsigned(p.bsplit));
-      hipLaunchKernelGGL(k_dbias_part<__bf16>, bg, dim3(256), 0, s, *d, static_cast<const __bf16*>(gout),
-                         p.brows_per_split, bpart);
-    }
+    if (bpart) launch_dbias_part(d, static_cast<const __bf16*>(gout), p.brows_per_split, p.bsplit, bpart, s);
     return hipGetLastError();
   }
   if (p.mfma) {
@@ -1729,12 +1802,7 @@ hipError_t wgrad_fill(const sel_dconv_desc* d, int dtype, const WgPlanD& p, cons
     else
       hipLaunchKernelGGL(k_dwgrad_mfma<1>, grid, dim3(256), lds, s, *d, static_cast<const __bf16*>(gout),
                          static_cast<const __bf16*>(x), p.tiles_per_seq, p.tiles_per_split, p.ntg, part);
-    if (bpart) {
-      const int64_t nb = int64_t(d->G) * width;
-      dim3 bg(unsigned((nb + 63) / 64), unsigned(p.bsplit));
-      hipLaunchKernelGGL(k_dbias_part<__bf16>, bg, dim3(256), 0, s, *d, static_cast<const __bf16*>(gout),
-                         p.brows_per_split, bpart);
-    }
+    if (bpart) launch_dbias_part(d, static_cast<const __bf16*>(gout), p.brows_per_split, p.bsplit, bpart, s);
     return hipGetLastError();
   }
   const int64_t nw = int64_t(d->G) * width * d->K * nred;
@@ -1852,6 +1920,38 @@ int sel_dconv_pack(int mode, const float* w, const float* wg, int N, int Cg, int
     return SEL_ERR_UNSUPPORTED;
   }
   SEL_LAUNCH_CHECK();
+  return SEL_OK;
+}
+
+int sel_dconv_pack_many(const sel_dpack_job* jobs, int njobs, int dtype, sel_stream_t stream) {
+  SEL_REQUIRE(njobs >= 0 && (njobs == 0 || jobs) && (dtype == SEL_BF16 || dtype == SEL_F32), SEL_ERR_ARG,
+              "bad dconv pack job list");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  for (int j0 = 0; j0 < njobs; j0 += DPM_MAXJ) {
+    DPackJobs dj{};
+    dj.njobs = std::min(DPM_MAXJ, njobs - j0);
+    int blocks = 0;
+    for (int j = 0; j < dj.njobs; ++j) {
+      const sel_dpack_job& J = jobs[j0 + j];
+      SEL_REQUIRE(J.w && J.out && J.N > 0 && J.Cg > 0 && J.Kt > 0 && J.stride > 0 && J.pad >= 0 && J.G > 0 &&
+                      J.N % J.G == 0 && (J.mode == 0 || J.mode == 1),
+                  SEL_ERR_ARG, "bad dconv pack job %d", j0 + j);
+      dj.pg[j] = pack_geo(J.N, J.Cg, J.Kt, J.stride, J.pad, J.G);
+      dj.w[j] = J.w;
+      dj.wg[j] = J.wg;
+      dj.out[j] = J.out;
+      dj.mode[j] = J.mode;
+      dj.bstart[j] = blocks;
+      blocks += J.N;
+    }
+    dj.bstart[dj.njobs] = blocks;
+    if (blocks == 0) continue;
+    if (dtype == SEL_BF16)
+      hipLaunchKernelGGL(k_dpack_many<__bf16>, dim3(unsigned(blocks)), dim3(256), 0, s, dj);
+    else
+      hipLaunchKernelGGL(k_dpack_many<float>, dim3(unsigned(blocks)), dim3(256), 0, s, dj);
+    SEL_LAUNCH_CHECK();
+  }
   return SEL_OK;
 }
 

@@ -80,6 +80,7 @@ SIGNATURES = {
     "sel_dconv_fwd": (I32, [P, I32, P, P, P, P, P, P, P]),
     "sel_dconv_geometry": (I32, [I32, I32, I32, P, P]),
     "sel_dconv_pack": (I32, [I32, P, P, I32, I32, I32, I32, I32, I32, I32, P, P]),
+    "sel_dconv_pack_many": (I32, [P, I32, I32, P]),
     "sel_dconv_wgrad_workspace": (SZ, [P, I32]),
     "sel_dconv_wgrad": (I32, [P, I32, P, P, I32, I32, I32, I32, I32, P, P, P, P, P, P, SZ, P]),
     "sel_avgpool1d_fwd": (I32, [P, I32, I32, I32, I32, I32, I32, I32, I32, P, P]),

@@ -98,6 +98,12 @@ def _dgrad_desc(sp, Bs, T_alloc_in, T_out, T_out_alloc, slope, prev_leaky, T_in=
                      Ns=sp.cin, Ng=sp.cin // sp.groups, act=0, slope=slope)
 
 
+class _DPackJob(ctypes.Structure):
+    """include/sel.h sel_dpack_job"""
+    _fields_ = [("w", ctypes.c_void_p), ("wg", ctypes.c_void_p), ("out", ctypes.c_void_p)] + \
+        [(n, ctypes.c_int32) for n in ("mode", "N", "Cg", "Kt", "stride", "pad", "G", "reserved")]
+
+
 class _DPackCache:
     """Packed forms of the discriminator weights, reused until the parameter
     changes: the version counter (copy_, load_state_dict, foreach Adam) or an
@@ -117,6 +123,33 @@ class _DPackCache:
         out = _pack(sp, w, wg, dtype, mode)
         self._e[key] = (weakref.ref(w), ver, out)
         return out
+
+    def prefetch(self, items):
+        """Pack every stale (sp, w, wg, dtype, mode) of `items` in ONE
+        sel_dconv_pack_many launch (per dtype) instead of one launch per layer
+        and mode at first use (a GAN step repacks ~100 discriminator forms)."""
+        miss = []
+        for sp, w, wg, dtype, mode in items:
+            key = (id(w), mode, dtype, sp.Kt, sp.stride, sp.pad, sp.groups)
+            ver = (w._version, wg._version if wg is not None else None)
+            hit = self._e.get(key)
+            if hit is not None and hit[0]() is w and hit[1] == ver:
+                continue
+            miss.append((key, ver, sp, w, wg, dtype, mode))
+        for dtype in dict.fromkeys(m[5] for m in miss):
+            group = [m for m in miss if m[5] == dtype]
+            jobs = (_DPackJob * len(group))()
+            keep = []
+            for i, (key, ver, sp, w, wg, _dt, mode) in enumerate(group):
+                N, Cg = sp.cout, sp.cin // sp.groups
+                out = torch.empty(N * sp.K * sp.stride * Cg, dtype=dtype, device=w.device)
+                wc = w.detach().contiguous().float()
+                gc = wg.detach().contiguous().float() if wg is not None else None
+                keep += [wc, gc]
+                jobs[i] = _DPackJob(wc.data_ptr(), gc.data_ptr() if gc is not None else None, out.data_ptr(), mode,
+                                    N, Cg, sp.Kt, sp.stride, sp.pad, sp.groups, 0)
+                self._e[key] = (weakref.ref(w), ver, out)
+            L.call("sel_dconv_pack_many", ctypes.cast(jobs, ctypes.c_void_p), len(group), _code(dtype), L.stream())
 
     def mark_stale(self, params):
         ids = {id(p) for p in params}
@@ -221,6 +254,14 @@ class ChainFn(torch.autograd.Function):
         Bs = x0.shape[0]
         per = 3 if wn else 2
         bufs, views, geo = [], [], []
+        # every stale packed form of the chain in one launch (forward forms, and
+        # the adjoint forms when a gradient can flow back through the chain)
+        adj = any(ctx.needs_input_grad)
+        items = []
+        for li, sp in enumerate(specs):
+            w, wg, _b = _layer_params(params, li, wn)
+            items += [(sp, w, wg, dtype, m) for m in ((0, 1) if adj else (0,))]
+        DPACKS.prefetch(items)
         T_in, T_alloc_in, x = T0, x0.shape[1], x0
         for li, sp in enumerate(specs):
             w, wg, b = _layer_params(params, li, wn)

@@ -344,6 +344,15 @@ int sel_dconv_geometry(int Kt, int stride, int pad, int* K, int* q0);
  * form Wp[g][n][i][r][c] (mode 0) or the adjoint form Wd[g][(r,c)][K-1-i][n] (mode 1). */
 int sel_dconv_pack(int mode, const float* w, const float* wg, int N, int Cg, int Kt, int stride, int pad, int G,
                    int dtype, void* out, sel_stream_t stream);
+/* Batched sel_dconv_pack: many (layer, mode) packs in one launch per 24 jobs
+ * (`jobs` is a HOST array; the same arithmetic per element as sel_dconv_pack). */
+typedef struct sel_dpack_job {
+  const float* w;    /* torch weight (or weight_v) */
+  const float* wg;   /* weight_g or NULL */
+  void* out;         /* packed form (dtype) */
+  int32_t mode, N, Cg, Kt, stride, pad, G, reserved;
+} sel_dpack_job;
+int sel_dconv_pack_many(const sel_dpack_job* jobs, int njobs, int dtype, sel_stream_t stream);
 /* weight/bias gradient of a forward layer descriptor (So = 1): gw[N][Cg][Kt] fp32
  * in the torch layout, or, with weight norm (v = the weight_v parameter, wg =
  * weight_g): gw = dL/dv and gg[N] = dL/dg; gb[N] = sum of gout when non-NULL. */

@@ -194,3 +194,28 @@ def test_ws_tiles_match_fp64_and_pf(gpu, shape):
     assert rel(gin[:, :T], ref_gin) <= 1e-2, (tag, "adjoint", rel(gin[:, :T], ref_gin))
     assert rel(y, y_pf.double()) <= 5e-3, (tag, "fwd vs pf", rel(y, y_pf.double()))
     assert rel(gin, gin_pf.double()) <= 5e-3, (tag, "adjoint vs pf", rel(gin, gin_pf.double()))
+
+
+def test_pack_many_matches_per_layer_pack(gpu):
+    """sel_dconv_pack_many (one launch for a chain's stale forms) writes the same
+    bytes as one sel_dconv_pack per (layer, mode), with and without weight norm."""
+    from sel import dconvops as DC
+    torch.manual_seed(7)
+    specs = [DC.LayerSpec(1, 32, 5, 3, 2, 1, True), DC.LayerSpec(32, 128, 5, 3, 2, 1, True),
+             DC.LayerSpec(128, 128, 41, 2, 20, 4, True), DC.LayerSpec(256, 512, 41, 4, 20, 16, True),
+             DC.LayerSpec(1024, 1, 3, 1, 1, 1, False)]
+    for dt in (torch.bfloat16, torch.float32):
+        for wn in (False, True):
+            cache = DC._DPackCache()
+            items, ws = [], []
+            for sp in specs:
+                w = torch.randn(sp.cout, sp.cin // sp.groups, sp.Kt, device=gpu)
+                wg = torch.rand(sp.cout, 1, 1, device=gpu) + 0.5 if wn else None
+                ws.append((sp, w, wg))
+                items += [(sp, w, wg, dt, 0), (sp, w, wg, dt, 1)]
+            cache.prefetch(items)
+            for sp, w, wg in ws:
+                for mode in (0, 1):
+                    got = cache.get(sp, w, wg, dt, mode)
+                    ref = DC._pack(sp, w, wg, dt, mode)
+                    assert torch.equal(got, ref), (sp.cin, sp.cout, sp.Kt, mode, dt, wn)
