@@ -728,7 +728,7 @@ constexpr int W3_BM = 128, W3_HALO = 64;
 template <int NT, int CT, int MAXT>
 __global__ __launch_bounds__(256) void k_dwgrad_w3(D d, const __bf16* __restrict__ gout, const __bf16* __restrict__ x,
                                                    int tiles_per_seq, int64_t n_tiles, int tiles_per_split,
-                                                   float* __restrict__ part) {
+                                                   float* __restrict__ part, int flat_p) {
   constexpr int NB = 32 * NT, CB = 32 * CT;
   constexpr int XROWS = W3_BM + W3_HALO;
   constexpr int GV = W3_BM * NB / 8 / 256;
@@ -756,13 +756,16 @@ __global__ __launch_bounds__(256) void k_dwgrad_w3(D d, const __bf16* __restrict
   uint4 gr[GV], xr[XV];
   bool gok[GV], xok[XV];
   auto load = [&](int64_t tile) {
+    // flat_p > 0: one row space over all sequences (pitch flat_p, zero gaps; see
+    // conv.hip dconv_ws_fwd), rows valid by their position in their sequence
     const int b = int(tile / tiles_per_seq);
     const int j0 = int(tile % tiles_per_seq) * W3_BM;
+    const int nflat = flat_p * d.B;
 #pragma unroll
     for (int u = 0; u < GV; ++u) {
       const int v = tid + u * 256;
       const int j = j0 + v / (NB / 8);
-      gok[u] = j < d.Tvalid;
+      gok[u] = flat_p ? j < nflat && j % flat_p < d.Tvalid : j < d.Tvalid;
       gr[u] = *reinterpret_cast<const uint4*>(gout + (int64_t(b) * d.Tvo + (gok[u] ? j : 0)) * d.ldo + n0 +
                                               (v % (NB / 8)) * 8);
     }
@@ -771,7 +774,7 @@ __global__ __launch_bounds__(256) void k_dwgrad_w3(D d, const __bf16* __restrict
       const int v = tid + u * 256;
       const int r = v / (CB / 8);
       const int t = j0 + d.q0 + r;
-      xok[u] = r < span && t >= 0 && t < d.Tv;
+      xok[u] = r < span && t >= 0 && (flat_p ? t < nflat && t % flat_p < d.Tv : t < d.Tv);
       if (u * 256 / (CB / 8) < span)
         xr[u] = *reinterpret_cast<const uint4*>(x + (int64_t(b) * d.Tvs + (xok[u] ? t : 0)) * d.ldx + c0 +
                                                 (v % (CB / 8)) * 8);
@@ -1658,6 +1661,7 @@ int dispatch_fwd(const sel_dconv_desc* d, const void* x, const void* wp, const f
 }
 
 struct WgPlanD {
+  int flat_p;  // k_dwgrad_w3 flat tiling pitch (0: per-sequence tiles)
   bool mfma, shortk, w3;
   int w3_nt, w3_ct, w3_maxt;
   int nsplit, bsplit;
@@ -1691,8 +1695,14 @@ WgPlanD wg_plan(const sel_dconv_desc* d, int dtype) {
     const int RG = P >= WPN ? 1 : WPN / P, WPP = WPN / RG;
     const int need = (P + WPP - 1) / WPP;
     p.w3_maxt = need <= 1 ? 1 : need <= 2 ? 2 : need <= 4 ? 4 : 8;
-    p.tiles_per_seq = (d->Tvalid + W3_BM - 1) / W3_BM;
-    const int64_t ntiles = int64_t(d->B) * p.tiles_per_seq;
+    // flat tiling across zero-gapped sequences (the conditions of conv.hip
+    // dconv_ws_fwd; tune key 26 = 1: off): short MPD columns fill whole tiles
+    const int P_ = d->Tvo;
+    p.flat_p = tune(26) != 1 && d->Tvs == P_ && P_ - d->Tv >= -d->q0 && P_ - d->Tvalid >= d->q0 + d->K - 1 &&
+                       int64_t(d->B) * P_ < (int64_t(1) << 31)
+                   ? P_ : 0;
+    p.tiles_per_seq = p.flat_p ? int((int64_t(d->B) * P_ + W3_BM - 1) / W3_BM) : (d->Tvalid + W3_BM - 1) / W3_BM;
+    const int64_t ntiles = p.flat_p ? p.tiles_per_seq : int64_t(d->B) * p.tiles_per_seq;
     const int64_t blocks = int64_t(width / (32 * p.w3_nt)) * (nred / (32 * p.w3_ct));
     int64_t want = std::max<int64_t>(1, (512 + blocks - 1) / blocks);
     want = std::min<int64_t>(want, std::max<int64_t>(1, (int64_t(64) << 20) / (nw * 4)));
@@ -1782,9 +1792,9 @@ hipError_t wgrad_fill(const sel_dconv_desc* d, int dtype, const WgPlanD& p, cons
   if (p.w3) {
     const int NB = 32 * p.w3_nt, CB = 32 * p.w3_ct;
     const size_t lds = 2 * (size_t(p.w3_nt) * W3_BM * 32 + size_t(p.w3_ct) * (W3_BM + W3_HALO) * 32) * sizeof(__bf16);
-    const int64_t ntiles = int64_t(d->B) * p.tiles_per_seq;
+    const int64_t ntiles = p.flat_p ? p.tiles_per_seq : int64_t(d->B) * p.tiles_per_seq;
     dim3 grid(unsigned(p.nsplit), unsigned(width / NB), unsigned(nred / CB));
-#define SEL_W3(NT_, CT_, MT_)                                                                                    if (p.w3_nt == NT_ && p.w3_ct == CT_ && p.w3_maxt == MT_) {                                                      auto kern = k_dwgrad_w3<NT_, CT_, MT_>;                                                                        if (lds > 64 * 1024) {                                                                                           const hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,                                                int(lds));                                                            if (e != hipSuccess) return e;                                                                               }                                                                                                              hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, *d, static_cast<const __bf16*>(gout),                                            static_cast<const __bf16*>(x), p.tiles_per_seq, ntiles, p.tiles_per_split, part);         } else
+#define SEL_W3(NT_, CT_, MT_)                                                                                    if (p.w3_nt == NT_ && p.w3_ct == CT_ && p.w3_maxt == MT_) {                                                      auto kern = k_dwgrad_w3<NT_, CT_, MT_>;                                                                        if (lds > 64 * 1024) {                                                                                           const hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,                                                int(lds));                                                            if (e != hipSuccess) return e;                                                                               }                                                                                                              hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, *d, static_cast<const __bf16*>(gout),                                            static_cast<const __bf16*>(x), p.tiles_per_seq, ntiles, p.tiles_per_split, part, p.flat_p);         } else
     SEL_W3(1, 1, 1) SEL_W3(1, 1, 2) SEL_W3(1, 1, 4) SEL_W3(1, 2, 1) SEL_W3(1, 2, 2) SEL_W3(1, 2, 4)
     SEL_W3(2, 1, 1) SEL_W3(2, 1, 2) SEL_W3(2, 1, 4) SEL_W3(2, 1, 8) SEL_W3(2, 2, 1) SEL_W3(2, 2, 2)
     SEL_W3(2, 2, 4) SEL_W3(2, 2, 8) { return hipErrorInvalidValue; }

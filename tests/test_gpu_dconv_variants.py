@@ -219,3 +219,43 @@ def test_pack_many_matches_per_layer_pack(gpu):
                     got = cache.get(sp, w, wg, dt, mode)
                     ref = DC._pack(sp, w, wg, dt, mode)
                     assert torch.equal(got, ref), (sp.cin, sp.cout, sp.Kt, mode, dt, wn)
+
+
+@pytest.mark.parametrize("shape", [("mpd4_s1", 1024, 1024, 5, 1, 2, 96, 54), ("mpd3_s3", 512, 1024, 5, 3, 2, 96, 162)],
+                         ids=["mpd4_s1", "mpd3_s3"])
+def test_wgrad_flat_tiles(gpu, shape):
+    """k_dwgrad_w3 over the period chain's zero-gapped layout (row pitch P =
+    valid rows + 2): flat tiles across sequences (default) vs per-sequence tiles
+    (tune key 26 = 1) vs fp64 torch; the gradient's gap rows hold garbage, which
+    the row-validity masks must drop."""
+    from sel import _lib as Lb
+    from sel import dconvops as DC
+    lib = Lb.lib()
+    tag, cin, cout, Kt, s, pad, Bs, T = shape
+    sp = DC.LayerSpec(cin, cout, Kt, s, pad, 1, True)
+    torch.manual_seed(cout + T)
+    T_out = sp.t_out(T)
+    P = T_out + 2                      # output rows per sequence (2 gap rows)
+    Ta = P * s                         # input rows per sequence (phase view: P rows)
+    x = torch.zeros(Bs, Ta, cin, device=gpu)
+    x[:, :T] = torch.randn(Bs, T, cin, device=gpu)
+    x = x.to(torch.bfloat16)
+    g = torch.randn(Bs, P, cout, device=gpu).to(torch.bfloat16)  # gap rows: garbage
+    d = DC._fwd_desc(sp, Bs, T, Ta, T_out, P, 0.1)
+    w = torch.randn(cout, cin, Kt, device=gpu)
+    prev = lib.sel_tune(26, 0)
+    try:
+        gw, _, gb = DC.wgrad(sp, d, g, x, w, None, True, True)
+        lib.sel_tune(26, 1)
+        gw1, _, gb1 = DC.wgrad(sp, d, g, x, w, None, True, True)
+    finally:
+        lib.sel_tune(26, prev)
+    xr = x[:, :T].double().clone()
+    wr = w.double().clone().requires_grad_(True)
+    pre = torch.nn.functional.conv1d(xr.permute(0, 2, 1), wr, None, stride=s, padding=pad).permute(0, 2, 1)
+    pre.backward(g[:, :T_out].double())
+    rel = lambda a, r: ((a.double() - r).norm() / r.norm()).item()  # noqa: E731
+    assert rel(gw, wr.grad) <= 1e-4, (tag, rel(gw, wr.grad))
+    assert rel(gw1, wr.grad) <= 1e-4, (tag, rel(gw1, wr.grad))
+    gbr = g[:, :T_out].double().sum((0, 1))
+    assert rel(gb, gbr) <= 1e-5 and rel(gb1, gbr) <= 1e-5
