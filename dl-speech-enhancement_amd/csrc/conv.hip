@@ -555,6 +555,7 @@ constexpr int WS_SPR = WS_CK / 8;             // 16-B slots per LDS row
 constexpr int WS_XROWS = WS_BM + F4_HALOMAX;  // staged input rows per chunk (multiple of WS_RPI)
 constexpr int WS_CMAX = 4096;                 // input channels the zero source covers
 constexpr int WS_EP = WS_BN + 4;              // fp32 epilogue tile pitch (conflict-free 16-B writes)
+constexpr int kWsK2Default = 0;               // K = 2 generator layers on the ws kernel (tune key 27 flips bits)
 
 __device__ __attribute__((aligned(64))) __bf16 g_ws_zero[WS_CMAX];
 
@@ -3025,9 +3026,24 @@ int launch_ws(const Args& a, const void* in, const void* wp, const float* bias, 
 // the warp-specialised kernel's legal shapes: K in {3, 7}, 128-multiple N,
 // 16-multiple C within the zero source, halo within the staged span, the
 // 4-slot ring within 160 KB
+// tune key 27 bit 0: also the K = 2 layers (the transposed convs' 2-tap form)
+// at >= 16 k rows, bit 1: and the 512 -> 256 one at 5120 rows
 bool ws_ok(const Args& a) {
-  return (a.K == 3 || a.K == 7) && a.N % WS_BN == 0 && a.C % WS_CK == 0 && a.C <= WS_CMAX &&
+  const bool k2 = a.K == 2 && (kWsK2Default ^ tune(27)) & 1;
+  return (a.K == 3 || a.K == 7 || k2) && a.N % WS_BN == 0 && a.C % WS_CK == 0 && a.C <= WS_CMAX &&
          (a.K - 1) * a.dil <= F4_HALOMAX && ws_lds_bytes(a.K) <= 160 * 1024;
+}
+
+template <typename TO>
+int launch_ws_k(const Args& a, const void* in, const void* wp, const float* bias, const void* aux, const void* res,
+                void* out, hipStream_t s) {
+  return a.K == 7 ? launch_ws<7, TO>(a, in, wp, bias, aux, res, out, s)
+         : a.K == 3 ? launch_ws<3, TO>(a, in, wp, bias, aux, res, out, s)
+                    : launch_ws<2, TO>(a, in, wp, bias, aux, res, out, s);
+}
+
+bool ws_small_k2(const Args& a) {
+  return a.K == 2 && a.N >= 512 && ((kWsK2Default ^ tune(27)) & 2) && ws_ok(a);
 }
 
 // Variant the dispatcher picks for a bf16 forward launch (see fwd4_variant);
@@ -3036,6 +3052,7 @@ int fwd4_choice(const Args& a) {
   const int v = tune(0);
   if (!((a.C % CK) == 0 && (a.K - 1) * a.dil <= F4_HALOMAX && a.K <= 8 && (v == 0 || v > 20))) return -1;
   if (v > 20 && (v != 27 || ws_ok(a))) return v;
+  if (ws_small_k2(a)) return 27;
   if (a.N <= 32 || (a.N % 64) != 0 || a.rows < 8192) return 22;
   if (a.N >= 256 && a.K == 1) return 26;
   if (a.N >= 256 && a.rows >= 16384) return ws_ok(a) ? 27 : 24;
@@ -3059,13 +3076,13 @@ int fwd4_variant(int v, const Args& a, const void* in, const void* wp, const flo
     case 26: return launch_fwd4<64, 128, 1, KMAX, TO>(a, in, wp, bias, aux, res, out, s);
     case 27:
       if (!ws_ok(a)) break;
-      return a.K == 7 ? launch_ws<7, TO>(a, in, wp, bias, aux, res, out, s)
-                      : launch_ws<3, TO>(a, in, wp, bias, aux, res, out, s);
+      return launch_ws_k<TO>(a, in, wp, bias, aux, res, out, s);
     default: break;
   }
   // heuristic from tools/conv_bench.py on the C3 layer shapes (profiles/r1_conv_bench.md):
   // narrow / non-64-multiple outputs and short row counts favour 128x32 tiles
   // (more workgroups in flight); wide layers 128x64 or 256x64.
+  if (ws_small_k2(a)) return launch_ws_k<TO>(a, in, wp, bias, aux, res, out, s);
   if (a.N <= 32 || (a.N % 64) != 0 || a.rows < 8192)
     return launch_fwd4<128, 32, 4, KMAX, TO>(a, in, wp, bias, aux, res, out, s);
   // 256-wide 1x1 (RU256 1x1 fwd 27.5 -> 20.9 us, dgrad 22.5 -> 19.2): 64x128 tiles
@@ -3075,9 +3092,7 @@ int fwd4_variant(int v, const Args& a, const void* in, const void* wp, const flo
   // RU256 k7 fwd+dgrad 43.5 -> 38.4 us, down2 46.6 -> 41.8), else 256x64 tiles
   // (RU256 k7 fwd 50.7 -> 36.2 us, dgrad 54.2 -> 43.0, down2 51.2 -> 43.1)
   if (a.N >= 256 && a.rows >= 16384) {
-    if (ws_ok(a) && (a.K == 7 || a.K == 3))
-      return a.K == 7 ? launch_ws<7, TO>(a, in, wp, bias, aux, res, out, s)
-                      : launch_ws<3, TO>(a, in, wp, bias, aux, res, out, s);
+    if (ws_ok(a)) return launch_ws_k<TO>(a, in, wp, bias, aux, res, out, s);
     return launch_fwd4<256, 64, 4, KMAX, TO>(a, in, wp, bias, aux, res, out, s);
   }
   if (a.N <= 64 || a.rows < 65536) return launch_fwd4<128, 64, 2, KMAX, TO>(a, in, wp, bias, aux, res, out, s);
@@ -3088,8 +3103,7 @@ int fwd4_variant(int v, const Args& a, const void* in, const void* wp, const flo
   // tools/conv_bench.py.  Tune key 17: 1 = every 128-wide layer, 2 = none.
   if (a.N == 128 && ws_ok(a) && tune(17) != 2 &&
       (tune(17) == 1 || a.K == 3 || (a.K == 7 && a.pad == 0 && !a.in_elu)))
-    return a.K == 7 ? launch_ws<7, TO>(a, in, wp, bias, aux, res, out, s)
-                    : launch_ws<3, TO>(a, in, wp, bias, aux, res, out, s);
+    return launch_ws_k<TO>(a, in, wp, bias, aux, res, out, s);
   // 128-wide k7 dgrad at 2000 samples (pad 0, no input ELU): 128x32 tiles (76.5 -> 62.6 us)
   if (a.N == 128 && a.K > 1 && a.pad == 0 && !a.in_elu)
     return launch_fwd4<128, 32, 4, KMAX, TO>(a, in, wp, bias, aux, res, out, s);

@@ -1158,6 +1158,49 @@ __global__ __launch_bounds__(256) void k_dpack_many(DPackJobs dj) {
                    int(blockIdx.x) - dj.bstart[j]);
 }
 
+// mode-2 jobs: the adjoint form as a tiled transpose of the forward form just
+// packed (Wp[g][nl][i][rc] -> Wd[g][rc][K-1-i][nl]): pure data movement, so the
+// adjoint holds exactly the forward form's values, with coalesced reads and
+// writes (the per-channel adjoint pack writes every element Ng apart).
+// Block = (job, group, 64 output channels, 64 (tap, reduction) columns).
+struct DPackTrJobs {
+  PackGeo pg[DPM_MAXJ];
+  const void* src[DPM_MAXJ];
+  void* out[DPM_MAXJ];
+  int ntn[DPM_MAXJ], ntc[DPM_MAXJ];  // channel / column tiles per group
+  int bstart[DPM_MAXJ + 1];
+  int njobs;
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_dpack_tr_many(DPackTrJobs dj) {
+  __shared__ T tile[64][65];
+  int j = 0;
+  while (j + 1 < dj.njobs && int(blockIdx.x) >= dj.bstart[j + 1]) ++j;  // block-uniform
+  const PackGeo& pg = dj.pg[j];
+  const T* __restrict__ src = static_cast<const T*>(dj.src[j]);
+  T* __restrict__ out = static_cast<T*>(dj.out[j]);
+  const int lb = int(blockIdx.x) - dj.bstart[j];
+  const int ct = lb % dj.ntc[j], nt = (lb / dj.ntc[j]) % dj.ntn[j], g = lb / (dj.ntc[j] * dj.ntn[j]);
+  const int Ng = pg.N / pg.G, nred = pg.s * pg.Cg, cols = pg.K * nred;
+  const int nl0 = nt * 64, c0 = ct * 64;
+  const int t = threadIdx.x, lo = t & 63, hi = t >> 6;
+#pragma unroll 4
+  for (int r = hi; r < 64; r += 4) {  // rows = output channels, columns = (i, rc) contiguous
+    const int nl = nl0 + r, c = c0 + lo;
+    if (nl < Ng && c < cols) tile[r][lo] = src[(int64_t(g) * Ng + nl) * cols + c];
+  }
+  __syncthreads();
+#pragma unroll 4
+  for (int q = hi; q < 64; q += 4) {  // column q of the tile -> one Wd row, channels contiguous
+    const int c = c0 + q, nl = nl0 + lo;
+    if (nl < Ng && c < cols) {
+      const int i = c / nred, rc = c - i * nred;
+      out[((int64_t(g) * nred + rc) * pg.K + (pg.K - 1 - i)) * Ng + nl] = tile[lo][q];
+    }
+  }
+}
+
 template <typename T>
 __device__ __forceinline__ void dpack_channel(const PackGeo& pg, int mode, const float* __restrict__ w,
                                               const float* __restrict__ wg, T* __restrict__ out, int n) {
@@ -1937,30 +1980,61 @@ int sel_dconv_pack_many(const sel_dpack_job* jobs, int njobs, int dtype, sel_str
   SEL_REQUIRE(njobs >= 0 && (njobs == 0 || jobs) && (dtype == SEL_BF16 || dtype == SEL_F32), SEL_ERR_ARG,
               "bad dconv pack job list");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  for (int j0 = 0; j0 < njobs; j0 += DPM_MAXJ) {
-    DPackJobs dj{};
-    dj.njobs = std::min(DPM_MAXJ, njobs - j0);
-    int blocks = 0;
-    for (int j = 0; j < dj.njobs; ++j) {
-      const sel_dpack_job& J = jobs[j0 + j];
-      SEL_REQUIRE(J.w && J.out && J.N > 0 && J.Cg > 0 && J.Kt > 0 && J.stride > 0 && J.pad >= 0 && J.G > 0 &&
-                      J.N % J.G == 0 && (J.mode == 0 || J.mode == 1),
-                  SEL_ERR_ARG, "bad dconv pack job %d", j0 + j);
-      dj.pg[j] = pack_geo(J.N, J.Cg, J.Kt, J.stride, J.pad, J.G);
-      dj.w[j] = J.w;
-      dj.wg[j] = J.wg;
-      dj.out[j] = J.out;
-      dj.mode[j] = J.mode;
-      dj.bstart[j] = blocks;
-      blocks += J.N;
+  for (int j = 0; j < njobs; ++j) {
+    const sel_dpack_job& J = jobs[j];
+    SEL_REQUIRE(J.w && J.out && J.N > 0 && J.Cg > 0 && J.Kt > 0 && J.stride > 0 && J.pad >= 0 && J.G > 0 &&
+                    J.N % J.G == 0 && (J.mode == 0 || J.mode == 1 || J.mode == 2),
+                SEL_ERR_ARG, "bad dconv pack job %d", j);
+  }
+  // modes 0 / 1 from the torch weights, then the mode-2 transposes of forward
+  // forms (possibly packed by the first launch: stream order)
+  for (int pass = 0; pass < 2; ++pass) {
+    int j = 0;
+    while (j < njobs) {
+      DPackJobs dj{};
+      DPackTrJobs tj{};
+      int n = 0, blocks = 0;
+      for (; j < njobs && n < DPM_MAXJ; ++j) {
+        const sel_dpack_job& J = jobs[j];
+        if ((J.mode == 2) != (pass == 1)) continue;
+        const PackGeo pg = pack_geo(J.N, J.Cg, J.Kt, J.stride, J.pad, J.G);
+        if (pass == 0) {
+          dj.pg[n] = pg;
+          dj.w[n] = J.w;
+          dj.wg[n] = J.wg;
+          dj.out[n] = J.out;
+          dj.mode[n] = J.mode;
+          dj.bstart[n] = blocks;
+          blocks += J.N;
+        } else {
+          tj.pg[n] = pg;
+          tj.src[n] = J.w;
+          tj.out[n] = J.out;
+          tj.ntn[n] = (J.N / J.G + 63) / 64;
+          tj.ntc[n] = (pg.K * J.stride * J.Cg + 63) / 64;
+          tj.bstart[n] = blocks;
+          blocks += J.G * tj.ntn[n] * tj.ntc[n];
+        }
+        ++n;
+      }
+      if (n == 0 || blocks == 0) continue;
+      if (pass == 0) {
+        dj.njobs = n;
+        dj.bstart[n] = blocks;
+        if (dtype == SEL_BF16)
+          hipLaunchKernelGGL(k_dpack_many<__bf16>, dim3(unsigned(blocks)), dim3(256), 0, s, dj);
+        else
+          hipLaunchKernelGGL(k_dpack_many<float>, dim3(unsigned(blocks)), dim3(256), 0, s, dj);
+      } else {
+        tj.njobs = n;
+        tj.bstart[n] = blocks;
+        if (dtype == SEL_BF16)
+          hipLaunchKernelGGL(k_dpack_tr_many<__bf16>, dim3(unsigned(blocks)), dim3(256), 0, s, tj);
+        else
+          hipLaunchKernelGGL(k_dpack_tr_many<float>, dim3(unsigned(blocks)), dim3(256), 0, s, tj);
+      }
+      SEL_LAUNCH_CHECK();
     }
-    dj.bstart[dj.njobs] = blocks;
-    if (blocks == 0) continue;
-    if (dtype == SEL_BF16)
-      hipLaunchKernelGGL(k_dpack_many<__bf16>, dim3(unsigned(blocks)), dim3(256), 0, s, dj);
-    else
-      hipLaunchKernelGGL(k_dpack_many<float>, dim3(unsigned(blocks)), dim3(256), 0, s, dj);
-    SEL_LAUNCH_CHECK();
   }
   return SEL_OK;
 }

@@ -140,14 +140,30 @@ class _DPackCache:
             group = [m for m in miss if m[5] == dtype]
             jobs = (_DPackJob * len(group))()
             keep = []
+            fresh = {}  # forward forms packed by this call: id(w) etc. -> buffer
+            # forward forms first, so an adjoint form can be their transpose (mode 2)
+            group.sort(key=lambda m: m[6])
             for i, (key, ver, sp, w, wg, _dt, mode) in enumerate(group):
                 N, Cg = sp.cout, sp.cin // sp.groups
                 out = torch.empty(N * sp.K * sp.stride * Cg, dtype=dtype, device=w.device)
-                wc = w.detach().contiguous().float()
-                gc = wg.detach().contiguous().float() if wg is not None else None
-                keep += [wc, gc]
-                jobs[i] = _DPackJob(wc.data_ptr(), gc.data_ptr() if gc is not None else None, out.data_ptr(), mode,
-                                    N, Cg, sp.Kt, sp.stride, sp.pad, sp.groups, 0)
+                fkey = (key[0], 0) + key[2:]
+                src = fresh.get(fkey)
+                if mode == 1 and src is None:
+                    hit = self._e.get(fkey)
+                    if hit is not None and hit[0]() is w and hit[1] == ver:
+                        src = hit[2]
+                if mode == 1 and src is not None:
+                    keep.append(src)
+                    jobs[i] = _DPackJob(src.data_ptr(), None, out.data_ptr(), 2, N, Cg, sp.Kt, sp.stride, sp.pad,
+                                        sp.groups, 0)
+                else:
+                    wc = w.detach().contiguous().float()
+                    gc = wg.detach().contiguous().float() if wg is not None else None
+                    keep += [wc, gc]
+                    jobs[i] = _DPackJob(wc.data_ptr(), gc.data_ptr() if gc is not None else None, out.data_ptr(),
+                                        mode, N, Cg, sp.Kt, sp.stride, sp.pad, sp.groups, 0)
+                if mode == 0:
+                    fresh[key] = out
                 self._e[key] = (weakref.ref(w), ver, out)
             L.call("sel_dconv_pack_many", ctypes.cast(jobs, ctypes.c_void_p), len(group), _code(dtype), L.stream())
 

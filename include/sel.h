@@ -345,9 +345,11 @@ int sel_dconv_geometry(int Kt, int stride, int pad, int* K, int* q0);
 int sel_dconv_pack(int mode, const float* w, const float* wg, int N, int Cg, int Kt, int stride, int pad, int G,
                    int dtype, void* out, sel_stream_t stream);
 /* Batched sel_dconv_pack: many (layer, mode) packs in one launch per 24 jobs
- * (`jobs` is a HOST array; the same arithmetic per element as sel_dconv_pack). */
+ * (`jobs` is a HOST array; the same arithmetic per element as sel_dconv_pack).
+ * mode 2: the adjoint form as the transpose of a forward form (dtype) at `w`,
+ * e.g. one packed by a mode-0 job of the same call (run after all mode 0 / 1 jobs). */
 typedef struct sel_dpack_job {
-  const float* w;    /* torch weight (or weight_v) */
+  const float* w;    /* torch weight (or weight_v); mode 2: the packed forward form */
   const float* wg;   /* weight_g or NULL */
   void* out;         /* packed form (dtype) */
   int32_t mode, N, Cg, Kt, stride, pad, G, reserved;
