@@ -311,7 +311,8 @@ MFMA_BF16_PEAK_TFS = 2500.0  # MI355X dense bf16 (MI355X_MICROARCH.md)
 
 
 # newest committed PMC traffic table of the C3 bench (tools/pmc_round.sh)
-PMC_FILE = next((f for f in (os.path.join(REPO, "profiles", n) for n in ("r2_c3_pmc_traffic.json",
+PMC_FILE = next((f for f in (os.path.join(REPO, "profiles", n) for n in ("r2_c3_pmc_traffic_v2.json",
+                                                                          "r2_c3_pmc_traffic.json",
                                                                           "r1_c3_pmc_traffic.json"))
                  if os.path.exists(f)), "")
 
