@@ -1696,10 +1696,18 @@ int dispatch_fwd(const sel_dconv_desc* d, const void* x, const void* wp, const f
   }
   // narrow groups: 32-wide tiles; short sequences / few rows: 64-row tiles
   if (width <= 32) {
-    if (rows * d->G < 131072) return launch_mfma<T, 128, 32>(d, x, wp, bias, aux, res, out, s);
-    return launch_mfma<T, 256, 32>(d, x, wp, bias, aux, res, out, s);
+    // tune key 28 bit 1: one tile size up (256 / 512 rows)
+    const bool up = sizeof(T) == 2 && (tune(28) & 2);
+    if (rows * d->G < 131072)
+      return up ? launch_mfma<T, 256, 32>(d, x, wp, bias, aux, res, out, s)
+                : launch_mfma<T, 128, 32>(d, x, wp, bias, aux, res, out, s);
+    return up ? launch_mfma<T, 512, 32>(d, x, wp, bias, aux, res, out, s)
+              : launch_mfma<T, 256, 32>(d, x, wp, bias, aux, res, out, s);
   }
   if (rows * d->G * (width / 64) < 65536) return launch_mfma<T, 64, 64>(d, x, wp, bias, aux, res, out, s);
+  // 256-row tiles: each staged tap group of weights serves twice the rows (the
+  // MSD's 41-tap grouped layers: C5 50.5 -> 49.7 ms/step; tune key 28 bit 0 = 128 rows)
+  if (sizeof(T) == 2 && !(tune(28) & 1)) return launch_mfma<T, 256, 64>(d, x, wp, bias, aux, res, out, s);
   return launch_mfma<T, 128, 64>(d, x, wp, bias, aux, res, out, s);
 }
 
