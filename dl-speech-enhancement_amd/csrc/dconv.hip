@@ -662,9 +662,18 @@ __global__ __launch_bounds__(256) void k_dwgrad_mfma(D d, const __bf16* __restri
     const int b = int(tile / tiles_per_seq);
     const int j0 = int(tile % tiles_per_seq) * WG_BM;
     __syncthreads();
+    // forward layers (So == 1): the 8 outputs of a vector are contiguous columns
+    const bool vec = d.So == 1 && (d.ldo & 7) == 0 && (d.Ng & 7) == 0;
     for (int idx = tid; idx < WG_BM * (BN / 8); idx += 256) {
       const int rr = idx / (BN / 8), v = (idx % (BN / 8)) * 8;
       const int j = j0 + rr;
+      if (vec) {
+        uint4 val = make_uint4(0, 0, 0, 0);
+        if (j < d.Tvalid && o0 + v < no_per_g)
+          val = *reinterpret_cast<const uint4*>(gout + (int64_t(b) * d.Tvo + j) * d.ldo + out_col(d, g, o0 + v));
+        *reinterpret_cast<uint4*>(gs + rr * PG + v) = val;
+        continue;
+      }
       __bf16 vals[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
