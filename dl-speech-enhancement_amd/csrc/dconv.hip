@@ -83,6 +83,67 @@ constexpr int KC = 8;   // taps per staged weight group
 // sub-tiles).  LDS: x span [BM + K - 1][P] of the current 32-channel chunk,
 // weights [BN][KC][P] of the current tap group.
 // ---------------------------------------------------------------------------
+// Epilogue of one 32x32 accumulator (operands swapped: lane -> output row
+// lane & 31, element e -> output channel ob + (e & 3) + 8 (e >> 2) + 4 (lane >> 5)):
+// + bias, + res, * LeakyReLU'(aux), LeakyReLU; rows past Tvalid written as exact
+// zeros.  bf16 with contiguous output columns (col = col0 + o - o0): each run
+// of 4 channels is one 8-byte load / store; otherwise per element.
+template <typename T>
+__device__ __forceinline__ void dconv_epilogue(const D& d, int g, int ob, int no_per_g, int64_t orow, bool valid,
+                                               const floatx16& a, const float* __restrict__ bias,
+                                               const T* __restrict__ aux, const T* __restrict__ res,
+                                               T* __restrict__ out, bool contig) {
+  const int hl = (threadIdx.x & 63) >> 5;
+  if constexpr (sizeof(T) == 2) {
+    if (contig) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int o = ob + 8 * q + 4 * hl;
+        if (o >= no_per_g) continue;  // no_per_g % 4 == 0 (contig)
+        const int64_t col = out_col(d, g, o);
+        typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+        bf16x4 rv = {}, av = {}, ov;
+        if (valid && res) rv = *reinterpret_cast<const bf16x4*>(res + orow + col);
+        if (valid && aux) av = *reinterpret_cast<const bf16x4*>(aux + orow + col);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float v = 0.f;
+          if (valid) {
+            v = a[4 * q + e];
+            if (bias) v += bias[col + e];
+            if (res) v += float(rv[e]);
+            if (aux) v *= leaky_grad(float(av[e]), d.slope);
+            if (d.act) v = leaky(v, d.slope);
+          }
+          ov[e] = __bf16(v);
+        }
+        *reinterpret_cast<bf16x4*>(out + orow + col) = ov;
+      }
+      return;
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int o = ob + (e & 3) + 8 * (e >> 2) + 4 * hl;
+    if (o >= no_per_g) continue;
+    const int64_t col = out_col(d, g, o);
+    float v = 0.f;
+    if (valid) {
+      v = a[e];
+      if (bias) v += bias[col];
+      if (res) v += to_f(res[orow + col]);
+      if (aux) v *= leaky_grad(to_f(aux[orow + col]), d.slope);
+      if (d.act) v = leaky(v, d.slope);
+    }
+    out[orow + col] = from_f<T>(v);
+  }
+}
+
+// output columns of a group contiguous in runs of 4 (8-byte aligned)
+__device__ __forceinline__ bool dconv_contig4(const D& d) {
+  return (d.So == 1 || d.Ns == d.Ng) && (d.Ng & 3) == 0 && (d.ldo & 3) == 0 && (d.G == 1 || d.So == 1);
+}
+
 template <typename T, int BM, int BN>
 __global__ __launch_bounds__(256) void k_dconv_mfma(D d, const T* __restrict__ x, const T* __restrict__ wp,
                                                     const float* __restrict__ bias, const T* __restrict__ aux,
@@ -181,27 +242,13 @@ __global__ __launch_bounds__(256) void k_dconv_mfma(D d, const T* __restrict__ x
 
   // epilogue (operands swapped: lane -> output row lane & 31 of its sub-tile,
   // element e -> channel (e & 3) + 8 (e >> 2) + 4 (lane >> 5) of the wave's 32)
+  const bool contig = dconv_contig4(d);
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int j = j0 + lrow[i];
     if (j >= d.Tvo) continue;
     const int64_t orow = (int64_t(b) * d.Tvo + j) * d.ldo;
-    const bool valid = j < d.Tvalid;
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int o = o0 + wn * 32 + (e & 3) + 8 * (e >> 2) + 4 * half;
-      if (o >= no_per_g) continue;
-      const int64_t col = out_col(d, g, o);
-      float v = 0.f;
-      if (valid) {
-        v = acc[i][e];
-        if (bias) v += bias[col];
-        if (res) v += to_f(res[orow + col]);
-        if (aux) v *= leaky_grad(to_f(aux[orow + col]), d.slope);
-        if (d.act) v = leaky(v, d.slope);
-      }
-      out[orow + col] = from_f<T>(v);
-    }
+    dconv_epilogue<T>(d, g, o0 + wn * 32, no_per_g, orow, j < d.Tvalid, acc[i], bias, aux, res, out, contig);
   }
 }
 
@@ -322,27 +369,13 @@ __global__ __launch_bounds__(256) void k_dconv_pf(D d, const __bf16* __restrict_
   }
 
   // epilogue as k_dconv_mfma
+  const bool contig = dconv_contig4(d);
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int j = j0 + lrow[i];
     if (j >= d.Tvo) continue;
     const int64_t orow = (int64_t(b) * d.Tvo + j) * d.ldo;
-    const bool valid = j < d.Tvalid;
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int o = o0 + wn * 32 + (e & 3) + 8 * (e >> 2) + 4 * hl;
-      if (o >= no_per_g) continue;
-      const int64_t col = out_col(d, 0, o);
-      float v = 0.f;
-      if (valid) {
-        v = acc[i][e];
-        if (bias) v += bias[col];
-        if (res) v += to_f(res[orow + col]);
-        if (aux) v *= leaky_grad(to_f(aux[orow + col]), d.slope);
-        if (d.act) v = leaky(v, d.slope);
-      }
-      out[orow + col] = from_f<__bf16>(v);
-    }
+    dconv_epilogue<__bf16>(d, 0, o0 + wn * 32, no_per_g, orow, j < d.Tvalid, acc[i], bias, aux, res, out, contig);
   }
 }
 
