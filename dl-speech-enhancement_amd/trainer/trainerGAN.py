@@ -12,7 +12,6 @@ import abc
 import json
 import logging
 import os
-from collections import defaultdict
 
 import torch
 
@@ -20,6 +19,102 @@ try:
     from tqdm import tqdm
 except ImportError:  # pragma: no cover
     tqdm = None
+
+
+class LossTotals(dict):
+    """Running loss totals (name -> float or 0-d tensor) like the reference's
+    defaultdict(float) + per-step `total[name] += loss.item()`, without a host
+    sync and without one tiny add kernel per recorded scalar: device values are
+    queued and folded into one accumulator vector (one concatenation + one add
+    per flush) when the totals are read or the queue grows."""
+
+    _FLUSH_AT = 256
+
+    def __init__(self):
+        super().__init__()
+        self._pending = []  # (names, detached tensor with len(names) elements)
+        self._acc_names = None
+        self._acc = None
+
+    def add(self, name, value):
+        if torch.is_tensor(value):
+            self.add_vector([name], value)
+        else:
+            self._materialize()
+            dict.__setitem__(self, name, dict.get(self, name, 0.0) + value)
+
+    def add_vector(self, names, value):
+        self._pending.append((list(names), value.detach()))
+        if len(self._pending) >= self._FLUSH_AT:
+            self._flush()
+
+    def _flush(self):
+        if not self._pending:
+            return
+        names = [n for ns, _ in self._pending for n in ns]
+        vals = torch.cat([v.reshape(-1).float() for _, v in self._pending])
+        self._pending = []
+        # entries of one name recorded several times before this flush: fold them
+        uniq = list(dict.fromkeys(names))
+        if len(uniq) != len(names):
+            idx = torch.tensor([uniq.index(n) for n in names], device=vals.device)
+            vals = torch.zeros(len(uniq), dtype=vals.dtype, device=vals.device).index_add_(0, idx, vals)
+            names = uniq
+        if self._acc is not None and self._acc_names == names:
+            self._acc += vals
+        else:
+            self._materialize()
+            self._acc_names, self._acc = names, vals
+
+    def _materialize(self):
+        self._flush_pending_only()
+        if self._acc is None:
+            return
+        names, acc = self._acc_names, self._acc
+        self._acc_names = self._acc = None
+        for i, n in enumerate(names):
+            dict.__setitem__(self, n, dict.get(self, n, 0.0) + acc[i])
+
+    def _flush_pending_only(self):
+        if self._pending:
+            pend, self._pending = self._pending, []
+            names = [n for ns, _ in pend for n in ns]
+            vals = torch.cat([v.reshape(-1).float() for _, v in pend])
+            for i, n in enumerate(names):
+                dict.__setitem__(self, n, dict.get(self, n, 0.0) + vals[i])
+
+    # reads see every recorded value
+    def __getitem__(self, key):
+        self._materialize()
+        return dict.__getitem__(self, key) if dict.__contains__(self, key) else 0.0
+
+    def __setitem__(self, key, value):
+        self._materialize()
+        dict.__setitem__(self, key, value)
+
+    def __contains__(self, key):
+        self._materialize()
+        return dict.__contains__(self, key)
+
+    def keys(self):
+        self._materialize()
+        return dict.keys(self)
+
+    def items(self):
+        self._materialize()
+        return dict.items(self)
+
+    def values(self):
+        self._materialize()
+        return dict.values(self)
+
+    def __iter__(self):
+        self._materialize()
+        return dict.__iter__(self)
+
+    def __len__(self):
+        self._materialize()
+        return dict.__len__(self)
 
 
 class ScalarWriter:
@@ -57,8 +152,8 @@ class TrainerGAN(abc.ABC):
         self.config = config
         self.device = device
         self.writer = ScalarWriter(config.get("outdir"))
-        self.total_train_loss = defaultdict(float)
-        self.total_eval_loss = defaultdict(float)
+        self.total_train_loss = LossTotals()
+        self.total_eval_loss = LossTotals()
         self.train_max_steps = config.get("train_max_steps", 0)
         self.tqdm = _NullBar()
 
@@ -137,7 +232,7 @@ class TrainerGAN(abc.ABC):
             self.total_eval_loss[key] = float(self.total_eval_loss[key]) / max(eval_steps_per_epoch, 1)
             logging.info(f"(Steps: {self.steps}) {key} = {self.total_eval_loss[key]:.4f}.")
         self._write_to_tensorboard(self.total_eval_loss)
-        self.total_eval_loss = defaultdict(float)
+        self.total_eval_loss = LossTotals()
         for key in self.model.keys():
             self.model[key].train()
 
@@ -200,12 +295,10 @@ class TrainerGAN(abc.ABC):
 
     def _record_loss(self, name, loss, mode="train"):
         """Accumulate without a host sync; converted to float when written."""
-        if torch.is_tensor(loss):
-            loss = loss.detach()
         if mode == "train":
-            self.total_train_loss[f"train/{name}"] = self.total_train_loss[f"train/{name}"] + loss
+            self.total_train_loss.add(f"train/{name}", loss)
         elif mode == "eval":
-            self.total_eval_loss[f"eval/{name}"] = self.total_eval_loss[f"eval/{name}"] + loss
+            self.total_eval_loss.add(f"eval/{name}", loss)
         else:
             raise NotImplementedError(f"Mode ({mode}) is not supported!")
 
@@ -228,7 +321,7 @@ class TrainerGAN(abc.ABC):
                 self.total_train_loss[key] = float(self.total_train_loss[key]) / self.config["log_interval_steps"]
                 logging.info(f"(Steps: {self.steps}) {key} = {self.total_train_loss[key]:.4f}.")
             self._write_to_tensorboard(self.total_train_loss)
-            self.total_train_loss = defaultdict(float)
+            self.total_train_loss = LossTotals()
 
     def _check_train_finish(self):
         self.finish_train = self.steps >= self.train_max_steps
@@ -238,9 +331,12 @@ class TrainerGAN(abc.ABC):
 class TrainerVQGAN(TrainerGAN):
     def _perplexity(self, perplexity, label=None, mode="train"):
         name = f"{mode}/ppl_{label}" if label else f"{mode}/ppl"
+        if mode not in ("train", "eval"):
+            raise NotImplementedError(f"Mode ({mode}) is not supported!")
+        totals = self.total_train_loss if mode == "train" else self.total_eval_loss
         if torch.numel(perplexity) > 1:
-            for idx in range(torch.numel(perplexity)):
-                self._record_loss(f"{name}_{idx}", perplexity[idx], mode=mode)
+            # one entry per codebook stage (keys {mode}/{name}_{idx}), added as one vector
+            totals.add_vector([f"{mode}/{name}_{idx}" for idx in range(torch.numel(perplexity))], perplexity)
         else:
             self._record_loss(name, perplexity, mode=mode)
 
