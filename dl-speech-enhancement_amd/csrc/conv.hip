@@ -1683,6 +1683,184 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
   }
 }
 
+// Residual unit at 64 channels, backward in ONE launch (the k_ru32_bwd scheme
+// with 32-channel output slices per wave, as k_ru64_fwd): g (grad of out) is
+// staged over the tile + anti-causal halo; gh = (W2^T g) * ELU'(h) per (32-row
+// sub-tile, slice) into a [2][SPAN][P] LDS tile (and HBM for the weight
+// gradient); after one barrier gx = conv1^T(gh) * ELU'(x) + g per (row group,
+// slice) from the dgrad-packed weights in VGPRs.  Same MFMA order, rounding
+// points and epilogue arithmetic as the two thin adjoint launches (1x1 with
+// ELU'(h), then k7 with ELU'(x) + g): bit-identical to them.
+template <int R>
+struct Ru64B {
+  static constexpr int C = 64, K = 7, P = F4_P;
+  static constexpr int SPAN = R + F4_HALOMAX;
+  static constexpr int CV = C / 8;
+  static constexpr int XV = (SPAN * CV + 255) / 256;
+  static constexpr int WR = R / 2;
+  static constexpr int TM = WR / 32;
+  static constexpr int NSUBMAX = (SPAN + 31) / 32;
+  static constexpr int UPW = (NSUBMAX * 2 + 3) / 4;  // gh (sub-tile, slice) units per wave
+  static constexpr size_t LDS = size_t(4) * SPAN * P * 2;  // g planes + gh planes
+};
+
+template <int R>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_ru64_bwd(
+    Args a, const __bf16* __restrict__ g, const __bf16* __restrict__ h, const __bf16* __restrict__ x,
+    const __bf16* __restrict__ wd1, const __bf16* __restrict__ wd2, __bf16* __restrict__ ghout,
+    __bf16* __restrict__ gx, int tiles_per_block) {
+  using G = Ru64B<R>;
+  constexpr int P = G::P, C = G::C, K = G::K, CV = G::CV;
+  extern __shared__ __align__(16) unsigned char smem[];
+  __bf16* const gs = reinterpret_cast<__bf16*>(smem);  // [2][SPAN][P]: g rows t0 ..
+  __bf16* const ghs = gs + 2 * G::SPAN * P;            // [2][SPAN][P]: gh rows t0 ..
+  const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ns = wave & 1, rg = wave >> 1;
+  const int halo = (K - 1) * a.dil;
+  const int span = R + halo;
+  const int nsub = (span + 31) / 32;
+  const int tps = (a.T + R - 1) / R;
+  int64_t tile0, tile_end;
+  if (!ru_tiles((a.rows / a.T) * tps, tiles_per_block, tile0, tile_end)) return;
+
+  bf16x8 wf[K][C / 16], wf2[C / 16];
+  {
+    const __bf16* wrow = wd1 + int64_t(ns * 32 + (lane & 31)) * K * C + 8 * hl;
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+#pragma unroll
+      for (int q = 0; q < C / 16; ++q) wf[k][q] = *reinterpret_cast<const bf16x8*>(wrow + k * C + 16 * q);
+    const __bf16* wrow2 = wd2 + int64_t(ns * 32 + (lane & 31)) * C + 8 * hl;
+#pragma unroll
+    for (int q = 0; q < C / 16; ++q) wf2[q] = *reinterpret_cast<const bf16x8*>(wrow2 + 16 * q);
+  }
+
+  uint4 xr[G::XV];
+  bool xok[G::XV];
+  auto load = [&](int64_t tile) {  // g rows t0 .. t0 + span (rows >= T: zero)
+    const int64_t b = tile / tps;
+    const int t0 = int(tile % tps) * R;
+#pragma unroll
+    for (int u = 0; u < G::XV; ++u) {
+      const int v = tid + u * 256;
+      const int r = v / CV, c = (v % CV) * 8;
+      const int ti = t0 + r;
+      xok[u] = r < span && ti < a.T;
+      if ((u * 256) / CV < span) xr[u] = *reinterpret_cast<const uint4*>(g + (b * a.T + (xok[u] ? ti : 0)) * C + c);
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int u = 0; u < G::XV; ++u) {
+      const int v = tid + u * 256;
+      const int r = v / CV, c = (v % CV) * 8;
+      if (r >= span) continue;
+      *reinterpret_cast<uint4*>(gs + ((c >> 5) * G::SPAN + r) * P + (c & 31)) = xok[u] ? xr[u] : make_uint4(0, 0, 0, 0);
+    }
+  };
+
+  load(tile0);
+  for (int64_t tile = tile0; tile < tile_end; ++tile) {
+    const int64_t b = tile / tps;
+    const int t0 = int(tile % tps) * R;
+    const int mrows = a.T - t0 < R ? a.T - t0 : R;
+    __syncthreads();  // every wave is done with the previous tile's gs / ghs
+    store();
+    __syncthreads();
+    if (tile + 1 < tile_end) load(tile + 1);
+
+    // gh = (W2^T g) * ELU'(h), units u = (sub-tile, slice) round-robin over the waves
+#pragma unroll
+    for (int uu = 0; uu < G::UPW; ++uu) {
+      const int unit = wave + 4 * uu;
+      if (unit >= 2 * nsub) break;  // wave-uniform
+      const int sb = unit >> 1, sl = unit & 1;
+      const int lr = sb * 32 + (lane & 31);
+      const int ti = t0 + lr;
+      const bool inside = ti < a.T;
+      const int64_t orow = (b * a.T + (inside ? ti : 0)) * C + sl * 32;
+      uint2 hq[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) hq[q] = inside ? *reinterpret_cast<const uint2*>(h + orow + 8 * q + 4 * hl) : make_uint2(0, 0);
+      // the slice-sl weights of the 1x1 adjoint: rows n = sl*32 + (lane & 31)
+      bf16x8 w2q[C / 16];
+      {
+        const __bf16* wr2 = wd2 + int64_t(sl * 32 + (lane & 31)) * C + 8 * hl;
+#pragma unroll
+        for (int q = 0; q < C / 16; ++q) w2q[q] = sl == ns ? wf2[q] : *reinterpret_cast<const bf16x8*>(wr2 + 16 * q);
+      }
+      floatx16 acc;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+      const __bf16* gw = gs + lr * P + 8 * hl;
+#pragma unroll
+      for (int q = 0; q < C / 16; ++q)
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w2q[q], *reinterpret_cast<const bf16x8*>(gw + (q >> 1) * G::SPAN * P + 16 * (q & 1)),
+                                                      acc, 0, 0, 0);
+      float v[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const __bf16* hv = reinterpret_cast<const __bf16*>(&hq[q]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[4 * q + e] = __fmul_rn(acc[4 * q + e], elu_grad_fast(float(hv[e])));
+      }
+      bf16x8 ghf[2];
+      ru_acc_to_frags(v, ghf);
+      if (lr < span) {
+        *reinterpret_cast<bf16x8*>(ghs + (sl * G::SPAN + lr) * P + 8 * hl) = ghf[0];
+        *reinterpret_cast<bf16x8*>(ghs + (sl * G::SPAN + lr) * P + 16 + 8 * hl) = ghf[1];
+      }
+      if (ghout && lr < mrows) {
+        *reinterpret_cast<bf16x8*>(ghout + orow + 8 * hl) = ghf[0];
+        *reinterpret_cast<bf16x8*>(ghout + orow + 16 + 8 * hl) = ghf[1];
+      }
+    }
+    __syncthreads();
+    // gx = conv1^T(gh) * ELU'(x) + g (k_conv_thin_bf16 order: taps, chunks, sub-tiles)
+    floatx16 acc[G::TM];
+#pragma unroll
+    for (int i = 0; i < G::TM; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
+    const __bf16* hw = ghs + (rg * G::WR + (lane & 31)) * P + 8 * hl;
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+#pragma unroll
+      for (int q = 0; q < C / 16; ++q) {
+        const __bf16* hb = hw + ((q >> 1) * G::SPAN + k * a.dil) * P + 16 * (q & 1);
+#pragma unroll
+        for (int i = 0; i < G::TM; ++i)
+          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[k][q], *reinterpret_cast<const bf16x8*>(hb + i * 32 * P),
+                                                           acc[i], 0, 0, 0);
+      }
+#pragma unroll
+    for (int i = 0; i < G::TM; ++i) {
+      const int lr = rg * G::WR + i * 32 + (lane & 31);
+      if (__builtin_amdgcn_readfirstlane(rg * G::WR + i * 32) >= mrows) break;
+      const bool valid = lr < mrows;
+      const int64_t orow = (b * a.T + t0 + (valid ? lr : 0)) * C + ns * 32;
+      float v[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint2 xq = valid ? *reinterpret_cast<const uint2*>(x + orow + 8 * q + 4 * hl) : make_uint2(0, 0);
+        const uint2 graw = *reinterpret_cast<const uint2*>(gs + (ns * G::SPAN + lr) * P + 8 * q + 4 * hl);
+        const __bf16* xv = reinterpret_cast<const __bf16*>(&xq);
+        const __bf16* gv = reinterpret_cast<const __bf16*>(&graw);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          v[4 * q + e] = __fadd_rn(__fmul_rn(acc[i][4 * q + e], elu_grad_fast(float(xv[e]))), float(gv[e]));
+      }
+      bf16x8 of[2];
+      ru_acc_to_frags(v, of);
+      if (valid) {
+        *reinterpret_cast<bf16x8*>(gx + orow + 8 * hl) = of[0];
+        *reinterpret_cast<bf16x8*>(gx + orow + 16 + 8 * hl) = of[1];
+      }
+    }
+  }
+}
+
 // Backward: gh = (W2^T g) * ELU'(h) over the tile + its anti-causal halo (the
 // adjoint of the causal conv reads rows t .. t + 6 dil), in registers -> LDS
 // (and HBM when the weight gradient needs it); gx = conv1^T(gh) * ELU'(x) + g.
@@ -3286,6 +3464,29 @@ int launch_ru64_fwd(const Args& a, const void* x, const void* w1p, const float* 
 }
 
 template <int R>
+int launch_ru64_bwd(const Args& a, const void* g, const void* h, const void* x, const void* wd1, const void* wd2,
+                    void* gh, void* gx, hipStream_t s) {
+  const int64_t ntiles = (a.rows / a.T) * ((a.T + R - 1) / R);
+  if (ntiles == 0) return SEL_OK;
+  static const int64_t slots = [] {
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_ru64_bwd<R>, 256, Ru64B<R>::LDS) != hipSuccess)
+      return int64_t(0);
+    return int64_t(cus) * per_cu / 8 * 8;
+  }();
+  const int64_t target = slots > 0 ? slots : 1024;
+  const int64_t tpb = std::max<int64_t>(1, (ntiles + target - 1) / target);
+  const unsigned nb = unsigned(((ntiles + tpb - 1) / tpb + 7) / 8 * 8);
+  hipLaunchKernelGGL(k_ru64_bwd<R>, dim3(nb), dim3(256), Ru64B<R>::LDS, s, a, static_cast<const __bf16*>(g),
+                     static_cast<const __bf16*>(h), static_cast<const __bf16*>(x), static_cast<const __bf16*>(wd1),
+                     static_cast<const __bf16*>(wd2), static_cast<__bf16*>(gh), static_cast<__bf16*>(gx), int(tpb));
+  SEL_LAUNCH_CHECK();
+  return SEL_OK;
+}
+
+template <int R>
 int launch_ru32_bwd(const Args& a, const void* g, const void* h, const void* x, const void* wd1, const void* wd2,
                     void* gh, void* gx, hipStream_t s) {
   const int64_t ntiles = (a.rows / a.T) * ((a.T + R - 1) / R);
@@ -3581,9 +3782,11 @@ int sel_resunit_bwd(const sel_conv_desc* d1, int dtype, const void* g, const voi
                     const void* wd1pack, const void* wd2pack, void* gh, void* gx, sel_stream_t stream) {
   if (int rc = check_desc(d1)) return rc;
   const Args a = to_args(d1);
-  SEL_REQUIRE(dtype == SEL_BF16 && ru_fused_ok(a) && a.C == 32, SEL_ERR_UNSUPPORTED,
-              "sel_resunit_bwd: fused path needs bf16, C = N = 32, K = 7, causal zero pad, ELU prologue");
+  SEL_REQUIRE(dtype == SEL_BF16 && ru_fused_ok(a), SEL_ERR_UNSUPPORTED,
+              "sel_resunit_bwd: fused path needs bf16, C = N in {32, 64}, K = 7, causal zero pad, ELU prologue");
   SEL_REQUIRE(g && h && x && wd1pack && wd2pack && gx, SEL_ERR_ARG, "null pointer");
+  if (a.C == 64)
+    return launch_ru64_bwd<128>(a, g, h, x, wd1pack, wd2pack, gh, gx, reinterpret_cast<hipStream_t>(stream));
   return launch_ru32_bwd<128>(a, g, h, x, wd1pack, wd2pack, gh, gx, reinterpret_cast<hipStream_t>(stream));
 }
 

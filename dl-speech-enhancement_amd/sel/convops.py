@@ -521,9 +521,9 @@ def ru_fused_ok(d1, dtype):
 
 
 def ru_bwd_fused_ok(d1, dtype):
-    """Fused residual-unit backward (32 channels only)?"""
-    # SEL_RU_FUSED=32: the 32-channel unit only (A/B of the 64-channel forward)
-    return RU_FUSED != "0" and _ru_shape_ok(d1, dtype) and (RU_FUSED != "32" or d1.C == 32) and d1.C == 32
+    """Fused residual-unit backward (k_ru32_bwd / k_ru64_bwd)?"""
+    # SEL_RU_FUSED=32: the 32-channel unit only (A/B of the 64-channel kernels)
+    return RU_FUSED != "0" and _ru_shape_ok(d1, dtype) and (RU_FUSED != "32" or d1.C == 32)
 
 
 def resunit_bwd(d1, gf, h, xf, wd1, wd2, want_gh):
@@ -541,7 +541,7 @@ def _ru_bwd_meta(d1, xf, want_gh):
     es = xf.element_size()
     nbytes = (4 + int(want_gh)) * d1.rows * d1.C * es
     flops = 2.0 * d1.rows * d1.N * d1.C * (d1.K + 1)
-    return "k_ru32_bwd<128>", nbytes, flops
+    return ("k_ru32_bwd<128>" if d1.C == 32 else "k_ru64_bwd<128>"), nbytes, flops
 
 
 def resunit_fwd(d1, xf, wp1, b1, wp2, b2):

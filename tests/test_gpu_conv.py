@@ -400,18 +400,20 @@ def test_fused_residual_unit_matches_two_calls(gpu, shape, monkeypatch):
         assert e < 1e-2, e
 
 
-RU32_BWD_SHAPES = [(1, 0, 2, 1000), (3, 1, 3, 777), (9, 1, 2, 1000), (9, 0, 2, 40), (9, 1, 4, 24000)]
+RU32_BWD_SHAPES = [(32, 1, 0, 2, 1000), (32, 3, 1, 3, 777), (32, 9, 1, 2, 1000), (32, 9, 0, 2, 40),
+                   (32, 9, 1, 4, 24000), (64, 1, 0, 2, 500), (64, 3, 1, 3, 333), (64, 9, 0, 2, 40),
+                   (64, 9, 1, 8, 8000)]
 
 
-@pytest.mark.parametrize("shape", RU32_BWD_SHAPES, ids=lambda s: "d{}b{}B{}T{}".format(*s))
+@pytest.mark.parametrize("shape", RU32_BWD_SHAPES, ids=lambda s: "C{}d{}b{}B{}T{}".format(*s))
 def test_resunit32_bwd_matches_two_calls(gpu, shape):
-    """sel_resunit_bwd (one launch, k_ru32_bwd) against the two adjoint primitive
-    calls of ResidualUnitFn's unfused backward on the same bf16 operands: gh
-    and gx bit-identical (same MFMA order, same rounding points), ragged tails,
-    T < halo and the C3 size (T = 24000)."""
+    """sel_resunit_bwd (one launch, k_ru32_bwd / k_ru64_bwd) against the two
+    adjoint primitive calls of ResidualUnitFn's unfused backward on the same
+    bf16 operands: gh bit-identical, gx within one bf16 ulp on < 0.1% of the
+    elements (same MFMA order, same rounding points), ragged tails, T < halo and
+    the C3 sizes (T = 24000 at 32 channels, 8000 at 64)."""
     from sel import convops as CO
-    dil, bias, B, T = shape
-    C = 32
+    C, dil, bias, B, T = shape
     torch.manual_seed(dil + T)
     x = (0.5 * torch.randn(B * T, C, device=gpu)).to(torch.bfloat16)
     h = (0.5 * torch.randn(B * T, C, device=gpu)).to(torch.bfloat16)
