@@ -3220,6 +3220,15 @@ int launch_ws_k(const Args& a, const void* in, const void* wp, const float* bias
                     : launch_ws<2, TO>(a, in, wp, bias, aux, res, out, s);
 }
 
+// wide outputs over few rows (the decoder's first transposed conv and the
+// encoder's last strided conv's dgrad at 80 frames x 64 clips: N' = 1280 over
+// 5120 rows): 128 x 128 tiles re-read the rows for 4x fewer column tiles than
+// 128 x 32 (tune key 29 bit 0 flips kWideSmallDefault)
+constexpr int kWideSmallDefault = 0;
+bool wide_small(const Args& a) {
+  return ((kWideSmallDefault ^ tune(29)) & 1) && a.rows < 8192 && a.N >= 512 && a.N % 128 == 0 && a.K <= 3;
+}
+
 bool ws_small_k2(const Args& a) {
   return a.K == 2 && a.N >= 512 && ((kWsK2Default ^ tune(27)) & 2) && ws_ok(a);
 }
@@ -3231,6 +3240,7 @@ int fwd4_choice(const Args& a) {
   if (!((a.C % CK) == 0 && (a.K - 1) * a.dil <= F4_HALOMAX && a.K <= 8 && (v == 0 || v > 20))) return -1;
   if (v > 20 && (v != 27 || ws_ok(a))) return v;
   if (ws_small_k2(a)) return 27;
+  if (wide_small(a)) return 25;
   if (a.N <= 32 || (a.N % 64) != 0 || a.rows < 8192) return 22;
   if (a.N >= 256 && a.K == 1) return 26;
   if (a.N >= 256 && a.rows >= 16384) return ws_ok(a) ? 27 : 24;
@@ -3261,6 +3271,7 @@ int fwd4_variant(int v, const Args& a, const void* in, const void* wp, const flo
   // narrow / non-64-multiple outputs and short row counts favour 128x32 tiles
   // (more workgroups in flight); wide layers 128x64 or 256x64.
   if (ws_small_k2(a)) return launch_ws_k<TO>(a, in, wp, bias, aux, res, out, s);
+  if (wide_small(a)) return launch_fwd4<128, 128, 2, KMAX, TO>(a, in, wp, bias, aux, res, out, s);
   if (a.N <= 32 || (a.N % 64) != 0 || a.rows < 8192)
     return launch_fwd4<128, 32, 4, KMAX, TO>(a, in, wp, bias, aux, res, out, s);
   // 256-wide 1x1 (RU256 1x1 fwd 27.5 -> 20.9 us, dgrad 22.5 -> 19.2): 64x128 tiles

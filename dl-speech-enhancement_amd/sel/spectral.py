@@ -8,6 +8,8 @@ Reference semantics restated here (file:line under the reference root):
 * mel L1                     losses/mel_loss.py:151-154
 """
 import numpy as np
+import os
+
 import torch
 
 from . import _lib as L
@@ -193,6 +195,10 @@ class LogMel(torch.autograd.Function):
         return gx, None, None, None, None, None, None, None, None, None
 
 
+# SEL_MEL_PAIR=0: the two log-mel forwards of the L1 loss as two launches
+MEL_PAIR_ONE_LAUNCH = os.environ.get("SEL_MEL_PAIR", "1") != "0"
+
+
 class MelL1(torch.autograd.Function):
     """mean |logmel(x) - logmel(y)| with grad w.r.t. x (mel_loss.py:151-154)."""
 
@@ -203,13 +209,22 @@ class MelL1(torch.autograd.Function):
         B, T = x.shape
         M = melmat.shape[1]
         F = _frames(T, hop)
-        a = torch.empty(B, M, F, device=x.device, dtype=torch.float32)
-        b = torch.empty_like(a)
         s = L.stream()
-        for src, dst in ((x, a), (y, b)):
-            L.call("sel_logmel_fwd", L.ptr(src), B, T, n_fft, hop, win_length, L.ptr(window),
-                                       L.ptr(melmat), L.ptr(krange), M, float(eps), log_kind,
-                                       L.ptr(dst), s)
+        if MEL_PAIR_ONE_LAUNCH:
+            # both signals' log-mels in ONE launch over the (2B, T) pair: one frame
+            # grid of twice the frames instead of two launches with their tails
+            ab = torch.empty(2 * B, M, F, device=x.device, dtype=torch.float32)
+            xy = torch.cat((x, y))
+            L.call("sel_logmel_fwd", L.ptr(xy), 2 * B, T, n_fft, hop, win_length, L.ptr(window),
+                   L.ptr(melmat), L.ptr(krange), M, float(eps), log_kind, L.ptr(ab), s)
+            a, b = ab[:B], ab[B:]
+        else:
+            a = torch.empty(B, M, F, device=x.device, dtype=torch.float32)
+            b = torch.empty_like(a)
+            for src, dst in ((x, a), (y, b)):
+                L.call("sel_logmel_fwd", L.ptr(src), B, T, n_fft, hop, win_length, L.ptr(window),
+                                           L.ptr(melmat), L.ptr(krange), M, float(eps), log_kind,
+                                           L.ptr(dst), s)
         n = a.numel()
         loss = torch.empty((), device=x.device, dtype=torch.float32)
         ws = L.workspace(lib.sel_l1_workspace(n), x.device)
