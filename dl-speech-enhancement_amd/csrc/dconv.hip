@@ -253,6 +253,143 @@ __global__ __launch_bounds__(256) void k_dconv_mfma(D d, const T* __restrict__ x
 }
 
 // ---------------------------------------------------------------------------
+// k_dconv_mfma with a register-prefetched pipeline (bf16): the (32-channel
+// chunk, 8-tap group) stages run in the same order with the same MFMAs (same
+// bits), but the next stage's weight slice (and, at a chunk boundary, the next
+// input span) is fetched into registers while the current stage's MFMAs run;
+// k_dconv_mfma staged both synchronously, exposing a load latency per stage
+// (the MSD's 41-tap grouped convs: 2 chunks x 6 tap groups per tile).
+// ---------------------------------------------------------------------------
+template <int BM, int BN>
+__global__ __launch_bounds__(256) void k_dconv_gpf(D d, const __bf16* __restrict__ x, const __bf16* __restrict__ wp,
+                                                   const float* __restrict__ bias, const __bf16* __restrict__ aux,
+                                                   const __bf16* __restrict__ res, __bf16* __restrict__ out) {
+  constexpr int P = Elt<__bf16>::P;
+  constexpr int WAVES_N = BN / 32, WAVES_M = 4 / WAVES_N;
+  constexpr int TM = BM / (32 * WAVES_M);
+  constexpr int XV = ((BM + KC * 8) * 4 + 255) / 256;  // span rows (<= BM + K - 1 <= BM + 63) x 4 vectors
+  constexpr int WV = (BN * KC * 4 + 255) / 256;
+  static_assert(TM >= 1 && WAVES_N * WAVES_M == 4, "tile");
+  extern __shared__ __align__(16) unsigned char smem[];
+  __bf16* const xs = reinterpret_cast<__bf16*>(smem);
+  const int span = BM + d.K - 1;
+  __bf16* const ws = xs + span * P;  // [BN][KC][P]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+  const int tps = (d.Tvo + BM - 1) / BM;
+  const int b = blockIdx.x / tps;
+  const int j0 = (blockIdx.x % tps) * BM;
+  const int no_per_g = d.So * d.Ng;
+  const int ntile_g = (no_per_g + BN - 1) / BN;
+  const int g = blockIdx.y / ntile_g;
+  const int o0 = (blockIdx.y % ntile_g) * BN;
+  const int64_t xrow0 = int64_t(b) * d.Tvs;
+  const int nred = d.S * d.Cg;
+  const int nchunk = (nred + CH - 1) / CH;
+  const int ntg = (d.K + KC - 1) / KC;
+  const int nstage = nchunk * ntg;
+
+  floatx16 acc[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
+  int lrow[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) lrow[i] = wm * (BM / WAVES_M) + i * 32 + (lane & 31);
+  const int half = lane >> 5;
+  const int nw_ = wn * 32 + (lane & 31);
+
+  uint4 xr[XV], wr[WV];
+  bool xok[XV], wok[WV];
+  auto load_x = [&](int cc) {
+#pragma unroll
+    for (int u = 0; u < XV; ++u) {
+      const int idx = tid + u * 256;
+      const int rr = idx >> 2, v = idx & 3;
+      const int t = j0 + d.q0 + rr;
+      const int ch = cc + v * 8;
+      xok[u] = rr < span && t >= 0 && t < d.Tv && ch < nred;
+      const int rph = (xok[u] ? ch : 0) / d.Cg, c = (xok[u] ? ch : 0) - rph * d.Cg;
+      if ((u * 256) / 4 < span)
+        xr[u] = *reinterpret_cast<const uint4*>(x + (xrow0 + (xok[u] ? t : 0)) * d.ldx + in_col(d, g, rph, c));
+    }
+  };
+  auto store_x = [&]() {
+#pragma unroll
+    for (int u = 0; u < XV; ++u) {
+      const int idx = tid + u * 256;
+      const int rr = idx >> 2, v = idx & 3;
+      if (rr >= span) continue;
+      *reinterpret_cast<uint4*>(xs + rr * P + v * 8) = xok[u] ? xr[u] : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto load_w = [&](int cc, int k0) {
+    const int kn = d.K - k0 < KC ? d.K - k0 : KC;
+#pragma unroll
+    for (int u = 0; u < WV; ++u) {
+      const int idx = tid + u * 256;
+      const int v = idx & 3, kk = (idx >> 2) % KC, n = idx / (4 * KC);
+      wok[u] = n < BN && kk < kn && o0 + n < no_per_g && cc + v * 8 < nred;
+      wr[u] = *reinterpret_cast<const uint4*>(
+          wp + ((int64_t(g) * no_per_g + (wok[u] ? o0 + n : 0)) * d.K + (wok[u] ? k0 + kk : 0)) * nred +
+          (wok[u] ? cc + v * 8 : 0));
+    }
+  };
+  auto store_w = [&]() {
+#pragma unroll
+    for (int u = 0; u < WV; ++u) {
+      const int idx = tid + u * 256;
+      const int v = idx & 3, kk = (idx >> 2) % KC, n = idx / (4 * KC);
+      if (n >= BN) continue;
+      *reinterpret_cast<uint4*>(ws + (n * KC + kk) * P + v * 8) = wok[u] ? wr[u] : make_uint4(0, 0, 0, 0);
+    }
+  };
+
+  load_x(0);
+  load_w(0, 0);
+  for (int st = 0; st < nstage; ++st) {
+    const int ci = st / ntg, tg = st - ci * ntg;
+    const int cc = ci * CH, k0 = tg * KC;
+    __syncthreads();  // every wave is done with the previous stage's LDS
+    if (tg == 0) store_x();
+    store_w();
+    __syncthreads();
+    if (st + 1 < nstage) {  // next stage's operands in flight during this stage's MFMAs
+      const int ci1 = (st + 1) / ntg, tg1 = (st + 1) - ci1 * ntg;
+      if (tg1 == 0) load_x(ci1 * CH);
+      load_w(ci1 * CH, tg1 * KC);
+    }
+    const int kn = d.K - k0 < KC ? d.K - k0 : KC;
+    const int chn = nred - cc < CH ? nred - cc : CH;
+    for (int kk = 0; kk < kn; ++kk) {
+      const int k = k0 + kk;
+#pragma unroll
+      for (int h = 0; h < CH / 16; ++h) {
+        if (h * 16 >= chn) break;
+        const int co = 16 * h + 8 * half;
+        const bf16x8 bw = *reinterpret_cast<const bf16x8*>(ws + (nw_ * KC + kk) * P + co);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const bf16x8 af = *reinterpret_cast<const bf16x8*>(xs + (lrow[i] + k) * P + co);
+          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bw, af, acc[i], 0, 0, 0);
+        }
+      }
+    }
+  }
+
+  const bool contig = dconv_contig4(d);
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int j = j0 + lrow[i];
+    if (j >= d.Tvo) continue;
+    const int64_t orow = (int64_t(b) * d.Tvo + j) * d.ldo;
+    dconv_epilogue<__bf16>(d, g, o0 + wn * 32, no_per_g, orow, j < d.Tvalid, acc[i], bias, aux, res, out, contig);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Register-prefetched MFMA primitive for one group with a contiguous reduction
 // row (G == 1, S == 1 or Cs == Cg: every MPD layer and the MSD's dense ones)
 // and K <= 8 taps: the next 32-channel chunk's input span and ALL K weight
@@ -1608,6 +1745,20 @@ int launch_mfma(const sel_dconv_desc* d, const void* x, const void* wp, const fl
   const int tps = (d->Tvo + BM - 1) / BM;
   const int ntg = (d->So * d->Ng + BN - 1) / BN;
   dim3 grid(unsigned(int64_t(d->B) * tps), unsigned(ntg * d->G));
+  if constexpr (sizeof(T) == 2) {
+    // register-prefetched pipeline (same stages, same bits; tune key 30 = 1: off);
+    // its prefetch registers cover a span of BM + 63 rows
+    if (tune(30) != 1 && d->K - 1 <= KC * 8) {
+      auto kg = k_dconv_gpf<BM, BN>;
+      if (lds > 64 * 1024)
+        SEL_HIP(hipFuncSetAttribute((const void*)kg, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
+      hipLaunchKernelGGL(kg, grid, dim3(256), lds, s, *d, static_cast<const __bf16*>(x),
+                         static_cast<const __bf16*>(wp), bias, static_cast<const __bf16*>(aux),
+                         static_cast<const __bf16*>(res), static_cast<__bf16*>(out));
+      SEL_LAUNCH_CHECK();
+      return SEL_OK;
+    }
+  }
   auto kern = k_dconv_mfma<T, BM, BN>;
   if (lds > 64 * 1024)
     SEL_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));

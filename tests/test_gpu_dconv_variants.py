@@ -259,3 +259,42 @@ def test_wgrad_flat_tiles(gpu, shape):
     assert rel(gw1, wr.grad) <= 1e-4, (tag, rel(gw1, wr.grad))
     gbr = g[:, :T_out].double().sum((0, 1))
     assert rel(gb, gbr) <= 1e-5 and rel(gb1, gbr) <= 1e-5
+
+
+GROUPED_LAYERS = [
+    ("msd1_g4_s2", 128, 128, 41, 2, 20, 4, 2, 6000),
+    ("msd2_g16_s2", 128, 256, 41, 2, 20, 16, 2, 3000),
+    ("msd3_g16_s4", 256, 512, 41, 4, 20, 16, 2, 1500),
+    ("msd4_g16_s4", 512, 1024, 41, 4, 20, 16, 4, 752),
+    ("msd5_g16_s1", 1024, 1024, 41, 1, 20, 16, 4, 188),
+]
+
+
+@pytest.mark.parametrize("shape", GROUPED_LAYERS, ids=[s[0] for s in GROUPED_LAYERS])
+def test_grouped_prefetch_bit_identical(gpu, shape):
+    """k_dconv_gpf (register-prefetched stages, default) gives the same bits as
+    the synchronous k_dconv_mfma (tune key 30 = 1) for the MSD's grouped,
+    strided 41-tap layers, forward (bias + LeakyReLU) and adjoint (So phases)."""
+    from sel import _lib as Lb
+    lib = Lb.lib()
+    tag, cin, cout, Kt, s, pad, G, Bs, T = shape
+    from sel import dconvops as DC
+    sp = DC.LayerSpec(cin, cout, Kt, s, pad, G, True)
+    torch.manual_seed(Kt * 3 + cout + G)
+    T_out = sp.t_out(T)
+    Ta = DC._roundup(T, s)
+    x = torch.zeros(Bs, Ta, cin, device=gpu)
+    x[:, :T] = torch.randn(Bs, T, cin, device=gpu)
+    x = x.to(torch.bfloat16)
+    w = torch.randn(cout, cin // G, Kt, device=gpu) / (cin // G * Kt) ** 0.5
+    b = torch.randn(cout, device=gpu)
+    g = torch.randn(Bs, T_out, cout, device=gpu).to(torch.bfloat16)
+    prev = lib.sel_tune(30, 1)
+    try:
+        ref = _run(sp, x, w, b, g, (Bs, T, Ta, T_out), torch.bfloat16)
+        lib.sel_tune(30, 0)
+        got = _run(sp, x, w, b, g, (Bs, T, Ta, T_out), torch.bfloat16)
+    finally:
+        lib.sel_tune(30, prev)
+    for name, r, o in zip(("fwd", "adjoint"), ref, got):
+        assert torch.equal(r, o), (tag, name, float((r.float() - o.float()).abs().max()))
