@@ -822,28 +822,86 @@ __global__ __launch_bounds__(256) void k_dwgrad_mfma(D d, const __bf16* __restri
   const int64_t tb = int64_t(split) * tiles_per_split;
   const int64_t te = tb + tiles_per_split < ntiles ? tb + tiles_per_split : ntiles;
   const int npairs = kn * 2;
-  const int gq = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int gq_ = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
 
   floatx4 acc[MAXJ];
 #pragma unroll
   for (int j = 0; j < MAXJ; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  for (int64_t tile = tb; tile < te; ++tile) {
+  // forward layers (So == 1): the 8 outputs of a vector are contiguous columns,
+  // and the next tile's gout / x vectors are fetched into registers while this
+  // tile's MFMAs run (same MFMAs in the same order as the synchronous loop below)
+  const bool vec = d.So == 1 && (d.ldo & 7) == 0 && (d.Ng & 7) == 0;
+  if (vec) {
+    constexpr int GQ = (WG_BM * (BN / 8) + 255) / 256;
+    constexpr int XQ = ((WG_BM + WG_TAPS - 1) * 4 + 255) / 256;
+    uint4 gq[GQ], xq[XQ];
+    bool gok[GQ], xok[XQ];
+    auto load = [&](int64_t tile) {
+      const int b = int(tile / tiles_per_seq);
+      const int j0 = int(tile % tiles_per_seq) * WG_BM;
+#pragma unroll
+      for (int u = 0; u < GQ; ++u) {
+        const int idx = tid + u * 256;
+        const int rr = idx / (BN / 8), v = (idx % (BN / 8)) * 8;
+        const int j = j0 + rr;
+        gok[u] = idx < WG_BM * (BN / 8) && j < d.Tvalid && o0 + v < no_per_g;
+        gq[u] = *reinterpret_cast<const uint4*>(gout + (int64_t(b) * d.Tvo + (gok[u] ? j : 0)) * d.ldo +
+                                                out_col(d, g, gok[u] ? o0 + v : 0));
+      }
+#pragma unroll
+      for (int u = 0; u < XQ; ++u) {
+        const int idx = tid + u * 256;
+        const int rr = idx >> 2, v = (idx & 3) * 8;
+        const int t = j0 + d.q0 + k0 + rr;
+        const int ch = cc + v;
+        xok[u] = rr < span && t >= 0 && t < d.Tv && ch < nred;
+        const int rph = (xok[u] ? ch : 0) / d.Cg, c = (xok[u] ? ch : 0) - rph * d.Cg;
+        if ((u * 256) / 4 < span)
+          xq[u] = *reinterpret_cast<const uint4*>(x + (int64_t(b) * d.Tvs + (xok[u] ? t : 0)) * d.ldx +
+                                                  in_col(d, g, rph, c));
+      }
+    };
+    if (tb < te) load(tb);
+    for (int64_t tile = tb; tile < te; ++tile) {
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < GQ; ++u) {
+        const int idx = tid + u * 256;
+        if (idx >= WG_BM * (BN / 8)) continue;
+        const int rr = idx / (BN / 8), v = (idx % (BN / 8)) * 8;
+        *reinterpret_cast<uint4*>(gs + rr * PG + v) = gok[u] ? gq[u] : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < XQ; ++u) {
+        const int idx = tid + u * 256;
+        const int rr = idx >> 2, v = (idx & 3) * 8;
+        if (rr >= span) continue;
+        *reinterpret_cast<uint4*>(xs + rr * PX + v) = xok[u] ? xq[u] : make_uint4(0, 0, 0, 0);
+      }
+      __syncthreads();
+      if (tile + 1 < te) load(tile + 1);
+#pragma unroll
+      for (int grp = 0; grp < WG_BM / 32; ++grp) {
+        const bf16x8 A = tr_frag(gs + (grp * 32 + 4 * gq_ + q) * PG + nt * 16 + 4 * p, PG);
+#pragma unroll
+        for (int j = 0; j < MAXJ; ++j) {
+          const int pr = wsub + WPN * j;
+          if (pr >= npairs) break;
+          const int k = pr >> 1, ct = pr & 1;
+          const bf16x8 Bf = tr_frag(xs + (grp * 32 + 4 * gq_ + q + k) * PX + ct * 16 + 4 * p, PX);
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, Bf, acc[j], 0, 0, 0);
+        }
+      }
+    }
+  }
+  for (int64_t tile = vec ? te : tb; tile < te; ++tile) {
     const int b = int(tile / tiles_per_seq);
     const int j0 = int(tile % tiles_per_seq) * WG_BM;
     __syncthreads();
-    // forward layers (So == 1): the 8 outputs of a vector are contiguous columns
-    const bool vec = d.So == 1 && (d.ldo & 7) == 0 && (d.Ng & 7) == 0;
     for (int idx = tid; idx < WG_BM * (BN / 8); idx += 256) {
       const int rr = idx / (BN / 8), v = (idx % (BN / 8)) * 8;
       const int j = j0 + rr;
-      if (vec) {
-        uint4 val = make_uint4(0, 0, 0, 0);
-        if (j < d.Tvalid && o0 + v < no_per_g)
-          val = *reinterpret_cast<const uint4*>(gout + (int64_t(b) * d.Tvo + j) * d.ldo + out_col(d, g, o0 + v));
-        *reinterpret_cast<uint4*>(gs + rr * PG + v) = val;
-        continue;
-      }
       __bf16 vals[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -867,13 +925,13 @@ __global__ __launch_bounds__(256) void k_dwgrad_mfma(D d, const __bf16* __restri
     __syncthreads();
 #pragma unroll
     for (int grp = 0; grp < WG_BM / 32; ++grp) {
-      const bf16x8 A = tr_frag(gs + (grp * 32 + 4 * gq + q) * PG + nt * 16 + 4 * p, PG);
+      const bf16x8 A = tr_frag(gs + (grp * 32 + 4 * gq_ + q) * PG + nt * 16 + 4 * p, PG);
 #pragma unroll
       for (int j = 0; j < MAXJ; ++j) {
         const int pr = wsub + WPN * j;
         if (pr >= npairs) break;
         const int k = pr >> 1, ct = pr & 1;
-        const bf16x8 Bf = tr_frag(xs + (grp * 32 + 4 * gq + q + k) * PX + ct * 16 + 4 * p, PX);
+        const bf16x8 Bf = tr_frag(xs + (grp * 32 + 4 * gq_ + q + k) * PX + ct * 16 + 4 * p, PX);
         acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, Bf, acc[j], 0, 0, 0);
       }
     }
