@@ -1724,16 +1724,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
   int64_t tile0, tile_end;
   if (!ru_tiles((a.rows / a.T) * tps, tiles_per_block, tile0, tile_end)) return;
 
-  bf16x8 wf[K][C / 16], wf2[C / 16];
+  bf16x8 wf[K][C / 16];  // the 1x1 adjoint's fragments are read per gh unit (L1-hot)
   {
     const __bf16* wrow = wd1 + int64_t(ns * 32 + (lane & 31)) * K * C + 8 * hl;
 #pragma unroll
     for (int k = 0; k < K; ++k)
 #pragma unroll
       for (int q = 0; q < C / 16; ++q) wf[k][q] = *reinterpret_cast<const bf16x8*>(wrow + k * C + 16 * q);
-    const __bf16* wrow2 = wd2 + int64_t(ns * 32 + (lane & 31)) * C + 8 * hl;
-#pragma unroll
-    for (int q = 0; q < C / 16; ++q) wf2[q] = *reinterpret_cast<const bf16x8*>(wrow2 + 16 * q);
   }
 
   uint4 xr[G::XV];
@@ -1769,6 +1766,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     store();
     __syncthreads();
     if (tile + 1 < tile_end) load(tile + 1);
+    // x rows of this wave's gx sub-tiles (the ELU'(x) factor), requested before
+    // the gh phase so their HBM latency hides behind it
+    uint2 xpre[G::TM][4];
+#pragma unroll
+    for (int i = 0; i < G::TM; ++i) {
+      const int lr = rg * G::WR + i * 32 + (lane & 31);
+      const bool in = lr < mrows;
+      const int64_t orow = (b * a.T + t0 + (in ? lr : 0)) * C + ns * 32 + 4 * hl;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) xpre[i][q] = in ? *reinterpret_cast<const uint2*>(x + orow + 8 * q) : make_uint2(0, 0);
+    }
 
     // gh = (W2^T g) * ELU'(h), units u = (sub-tile, slice) round-robin over the waves
 #pragma unroll
@@ -1788,7 +1796,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
       {
         const __bf16* wr2 = wd2 + int64_t(sl * 32 + (lane & 31)) * C + 8 * hl;
 #pragma unroll
-        for (int q = 0; q < C / 16; ++q) w2q[q] = sl == ns ? wf2[q] : *reinterpret_cast<const bf16x8*>(wr2 + 16 * q);
+        for (int q = 0; q < C / 16; ++q) w2q[q] = *reinterpret_cast<const bf16x8*>(wr2 + 16 * q);
       }
       floatx16 acc;
 #pragma unroll
@@ -1843,9 +1851,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
       float v[16];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const uint2 xq = valid ? *reinterpret_cast<const uint2*>(x + orow + 8 * q + 4 * hl) : make_uint2(0, 0);
         const uint2 graw = *reinterpret_cast<const uint2*>(gs + (ns * G::SPAN + lr) * P + 8 * q + 4 * hl);
-        const __bf16* xv = reinterpret_cast<const __bf16*>(&xq);
+        const __bf16* xv = reinterpret_cast<const __bf16*>(&xpre[i][q]);
         const __bf16* gv = reinterpret_cast<const __bf16*>(&graw);
 #pragma unroll
         for (int e = 0; e < 4; ++e)
