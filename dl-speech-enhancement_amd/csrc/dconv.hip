@@ -1794,6 +1794,81 @@ bool mfma_ok(const sel_dconv_desc* d, int dtype) {
          (width >= 16 || d->K * d->S * d->Cg >= 256);
 }
 
+// Very narrow outputs with a short reduction (the MPD first layer's adjoint:
+// 3 output phases x 1 channel from 2 taps x 32 channels of gout): one thread
+// per output row computes all `width` outputs from 16-B input vectors, weights
+// in LDS as fp32 (the generic VALU kernel walked the reduction with one 2-byte
+// load per product and thread).  bf16, one group, contiguous reduction row.
+template <int MAXW>
+__global__ __launch_bounds__(256) void k_dconv_tiny(D d, const __bf16* __restrict__ x, const __bf16* __restrict__ wp,
+                                                    const float* __restrict__ bias, const __bf16* __restrict__ aux,
+                                                    const __bf16* __restrict__ res, __bf16* __restrict__ out) {
+  extern __shared__ float wsm[];  // [width][K][nred]
+  const int width = d.So * d.Ng, nred = d.S * d.Cg;
+  for (int e = threadIdx.x; e < width * d.K * nred; e += 256) wsm[e] = float(wp[e]);
+  __syncthreads();
+  const int64_t rows = int64_t(d.B) * d.Tvo;
+  for (int64_t row = int64_t(blockIdx.x) * 256 + threadIdx.x; row < rows; row += int64_t(gridDim.x) * 256) {
+    const int b = int(row / d.Tvo), j = int(row - int64_t(b) * d.Tvo);
+    const bool valid = j < d.Tvalid;
+    float acc[MAXW];
+#pragma unroll
+    for (int o = 0; o < MAXW; ++o) acc[o] = 0.f;
+    if (valid) {
+      for (int i = 0; i < d.K; ++i) {
+        const int t = j + d.q0 + i;
+        if (t < 0 || t >= d.Tv) continue;
+        const __bf16* xr = x + (int64_t(b) * d.Tvs + t) * d.ldx;
+        for (int v = 0; v < nred; v += 8) {
+          const uint4 raw = *reinterpret_cast<const uint4*>(xr + v);
+          const __bf16* xv = reinterpret_cast<const __bf16*>(&raw);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float xf = float(xv[e]);
+#pragma unroll
+            for (int o = 0; o < MAXW; ++o)
+              if (o < width) acc[o] = fmaf(wsm[(o * d.K + i) * nred + v + e], xf, acc[o]);
+          }
+        }
+      }
+    }
+    const int64_t orow = (int64_t(b) * d.Tvo + j) * d.ldo;
+#pragma unroll
+    for (int o = 0; o < MAXW; ++o) {
+      if (o >= width) break;
+      const int64_t col = out_col(d, 0, o);
+      float v = 0.f;
+      if (valid) {
+        v = acc[o];
+        if (bias) v += bias[col];
+        if (res) v += float(res[orow + col]);
+        if (aux) v *= leaky_grad(float(aux[orow + col]), d.slope);
+        if (d.act) v = leaky(v, d.slope);
+      }
+      out[orow + col] = __bf16(v);
+    }
+  }
+}
+
+bool tiny_ok(const sel_dconv_desc* d, int dtype) {
+  const int width = d->So * d->Ng, nred = d->S * d->Cg;
+  return dtype == SEL_BF16 && d->G == 1 && (d->S == 1 || d->Cs == d->Cg) && width <= 4 && nred % 8 == 0 &&
+         d->ldx % 8 == 0 && size_t(width) * d->K * nred * sizeof(float) <= 48 * 1024 && tune(31) != 1;
+}
+
+int launch_tiny(const sel_dconv_desc* d, const void* x, const void* wp, const float* bias, const void* aux,
+                const void* res, void* out, hipStream_t s) {
+  const int width = d->So * d->Ng, nred = d->S * d->Cg;
+  const size_t lds = size_t(width) * d->K * nred * sizeof(float);
+  const int64_t rows = int64_t(d->B) * d->Tvo;
+  const unsigned blocks = unsigned(std::min<int64_t>((rows + 255) / 256, 4096));
+  hipLaunchKernelGGL(k_dconv_tiny<4>, dim3(blocks), dim3(256), lds, s, *d, static_cast<const __bf16*>(x),
+                     static_cast<const __bf16*>(wp), bias, static_cast<const __bf16*>(aux),
+                     static_cast<const __bf16*>(res), static_cast<__bf16*>(out));
+  SEL_LAUNCH_CHECK();
+  return SEL_OK;
+}
+
 template <typename T, int BM, int BN>
 int launch_mfma(const sel_dconv_desc* d, const void* x, const void* wp, const float* bias, const void* aux,
                 const void* res, void* out, hipStream_t s) {
@@ -1922,6 +1997,8 @@ int dispatch_fwd(const sel_dconv_desc* d, const void* x, const void* wp, const f
   if (tune(9) == 1) return launch_valu<T>(d, x, wp, bias, aux, res, out, s);
   if (!mfma_ok(d, dtype)) {
     if (short_ok(d)) return launch_short<T>(d, x, wp, bias, aux, res, out, s);
+    // tune key 31 = 1: the generic VALU kernel instead of the narrow-output one
+    if (tiny_ok(d, dtype)) return launch_tiny(d, x, wp, bias, aux, res, out, s);
     return launch_valu<T>(d, x, wp, bias, aux, res, out, s);
   }
   const int width = d->So * d->Ng;

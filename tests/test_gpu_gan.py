@@ -121,6 +121,7 @@ C5_LAYERS = [
     ("mpd3_s3", 512, 1024, 5, 3, 2, 1, 6, 75),
     ("mpd4_s1", 1024, 1024, 5, 1, 2, 1, 6, 25),
     ("msd0_c1", 1, 128, 15, 1, 7, 1, 2, 3000),
+    ("mpd0_c1_s3", 1, 32, 5, 3, 2, 1, 6, 6001),
     ("msd7_n1", 1024, 1, 3, 1, 1, 1, 2, 48),
     ("mpd_out_n1", 1024, 1, 2, 1, 1, 1, 6, 25),
 ]
