@@ -489,14 +489,17 @@ class GanReduceFn(torch.autograd.Function):
         gbuf = torch.empty_like(base) if base is not a else torch.empty_like(a)
         ga = torch.as_strided(gbuf, a.shape, a.stride(), a.storage_offset()) if base is not a else gbuf
         gs = (ctypes.c_int64 * nd)(*ga.permute(perm).stride())
-        gc = (g.float() * scale).reshape(1).contiguous()
+        # the upstream scalar is read in place (the kernel multiplies by `scale`):
+        # no separate scaling launch per term
+        gc = g if (g.dtype == torch.float32 and g.numel() == 1) else g.float().reshape(1).contiguous()
         L.call("sel_gan_grad", kind, _code(a.dtype), L.ptr(a), sa, ta, L.ptr(b), sb, tb, nd, float(target),
-               L.ptr(gc), 1.0, L.ptr(ga), gs, 0, L.stream())
+               ctypes.c_void_p(gc.data_ptr()), float(scale), L.ptr(ga), gs, 0, L.stream())
         return ga, None, None, None, None
 
 
-def l1_mean(a, b):
-    return GanReduceFn.apply(a, b.detach(), L1, 0.0, 1.0 / a.numel())
+def l1_mean(a, b, weight=1.0):
+    """weight * mean |a - b| (the weight folded into the kernel's scale)."""
+    return GanReduceFn.apply(a, b.detach(), L1, 0.0, float(weight) / a.numel())
 
 
 def mse_to(a, target):
