@@ -75,12 +75,19 @@ def test_bench_launcher_starts_world_size_ranks(tmp_path):
     sys.path.insert(0, REPO)
     import bench
     import socket
-    with socket.socket() as sk:
-        sk.bind(("127.0.0.1", 0))
-        port = sk.getsockname()[1]
-    cmd = bench.launch_cmd(2, port, [])
-    cmd[-1] = str(probe)
-    out = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
+    # loopback for gloo's own sockets; one retry on a fresh port (the probe port
+    # is released before torch.distributed.run binds it, so another process can
+    # take it in between: a rendezvous failure, not a launcher one)
+    env = dict(os.environ, GLOO_SOCKET_IFNAME="lo")
+    for attempt in range(2):
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        cmd = bench.launch_cmd(2, port, [])
+        cmd[-1] = str(probe)
+        out = subprocess.run(cmd, capture_output=True, text=True, timeout=120, env=env)
+        if out.returncode == 0:
+            break
     assert out.returncode == 0, out.stderr[-2000:]
     lines = sorted(l for l in out.stdout.splitlines() if l.startswith("RANK"))
     assert lines == ["RANK 0 2 2", "RANK 1 2 2"], out.stdout
