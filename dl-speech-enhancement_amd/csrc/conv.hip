@@ -604,14 +604,18 @@ __device__ __forceinline__ void ws_elu_pieces(unsigned char* lane_base, int pw, 
   }
 }
 
-template <int KT, typename TO>
-__global__ __launch_bounds__(768) void k_conv_ws_bf16(Args a, const __bf16* __restrict__ in,
+template <int KT, typename TO, int NC>
+__global__ __launch_bounds__((NC + 4) * 64) void k_conv_ws_bf16(Args a, const __bf16* __restrict__ in,
                                                       const __bf16* __restrict__ wp,
                                                       const float* __restrict__ bias, const TO* __restrict__ aux,
                                                       const TO* __restrict__ res, TO* __restrict__ out, int ncol,
                                                       int dbg) {
   constexpr int BM = WS_BM, BN = WS_BN;
-  constexpr int TM = 2, TN = 2, WTM = 64, WTN = 64;
+  // NC consumer waves as 4 x 2 (64 x 64 each) or 2 x 2 (128 x 64: six fragment
+  // reads per eight MFMAs instead of four per four)
+  static_assert(NC == 8 || NC == 4, "consumer waves");
+  constexpr int NT = (NC + 4) * 64;
+  constexpr int TM = 16 / NC, TN = 2, WTM = 32 * TM, WTN = 64;
   constexpr int XI = WS_XROWS / WS_RPI;  // DMA pieces (1 KB) per chunk: input span
   constexpr int WI = KT * BN / WS_RPI;   // weight slices
   constexpr int TI = XI + WI;
@@ -639,9 +643,9 @@ __global__ __launch_bounds__(768) void k_conv_ws_bf16(Args a, const __bf16* __re
   const int n0 = nt * BN;
   const int nchunk = a.C / WS_CK;
 
-  if (wave >= 8) {
+  if (wave >= NC) {
     // ---------------- producers ----------------
-    const int pw = wave - 8;
+    const int pw = wave - NC;
     // DMA piece q (1 KB) goes to producer wave q % 4 (the input pieces, which
     // get the ELU pass, spread over all four); a wave short of PW repeats its last
     const __bf16* src[PW];
@@ -791,16 +795,16 @@ __global__ __launch_bounds__(768) void k_conv_ws_bf16(Args a, const __bf16* __re
   if (dbg & 4) return;  // diagnostic: no epilogue (tune key 13 bit 2)
   __syncthreads();
 
-  // epilogue by all 12 waves: 8 consecutive channels per thread, row-contiguous
+  // epilogue by all NC + 4 waves: 8 consecutive channels per thread, row-contiguous
   // 16-B global accesses (aux / res fetched for every vector first)
   struct alignas(16) V8 { TO v[8]; };
-  constexpr int EV = (BM * BN / 8 + 767) / 768;
+  constexpr int EV = (BM * BN / 8 + NT - 1) / NT;
   const float* const tile = reinterpret_cast<const float*>(smem);
   const int nvec = mrows * (BN / 8);
   V8 av[EV], rv[EV];
 #pragma unroll
   for (int u = 0; u < EV; ++u) {
-    const int v = tid + u * 768;
+    const int v = tid + u * NT;
     if (v >= nvec) break;
     const int64_t o = (m0 + (v >> 4)) * a.ldo + n0 + (v & 15) * 8;
     if (aux) av[u] = *reinterpret_cast<const V8*>(aux + o);
@@ -808,7 +812,7 @@ __global__ __launch_bounds__(768) void k_conv_ws_bf16(Args a, const __bf16* __re
   }
 #pragma unroll
   for (int u = 0; u < EV; ++u) {
-    const int v = tid + u * 768;
+    const int v = tid + u * NT;
     if (v >= nvec) break;
     const int row = v >> 4, c8 = (v & 15) * 8;
     const int64_t o = (m0 + row) * a.ldo + n0 + c8;
@@ -3190,6 +3194,7 @@ int launch_fwd4(const Args& a, const void* in, const void* wp, const float* bias
   return SEL_OK;
 }
 
+// tune key 32: 1 = four consumer waves of 128 x 64 (NC = 4) instead of eight of 64 x 64
 template <int KT, typename TO>
 int launch_ws(const Args& a, const void* in, const void* wp, const float* bias, const void* aux, const void* res,
               void* out, hipStream_t s) {
@@ -3199,9 +3204,10 @@ int launch_ws(const Args& a, const void* in, const void* wp, const float* bias, 
   if (tiles == 0) return SEL_OK;
   const bool xcd = ncol > 1 && tune(8) == 0 && tiles * ncol < (int64_t(1) << 31);
   const dim3 grid = xcd ? dim3(unsigned(tiles * ncol)) : dim3(unsigned(tiles), unsigned(ncol));
-  auto kern = k_conv_ws_bf16<KT, TO>;
+  const bool nc4 = tune(32) == 1;
+  auto kern = nc4 ? k_conv_ws_bf16<KT, TO, 4> : k_conv_ws_bf16<KT, TO, 8>;
   SEL_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
-  hipLaunchKernelGGL(kern, grid, dim3(768), lds, s, a, static_cast<const __bf16*>(in),
+  hipLaunchKernelGGL(kern, grid, dim3(nc4 ? 512 : 768), lds, s, a, static_cast<const __bf16*>(in),
                      static_cast<const __bf16*>(wp), bias, static_cast<const TO*>(aux), static_cast<const TO*>(res),
                      static_cast<TO*>(out), xcd ? ncol : 0, tune(13));
   SEL_LAUNCH_CHECK();
