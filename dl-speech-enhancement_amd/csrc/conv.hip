@@ -534,7 +534,7 @@ __global__ __launch_bounds__(256) void k_conv_fwd_bf16(Args a, const __bf16* __r
 //   waves 0-7  consumers: 4 x 2 grid of 64 x 64 wave tiles; per 16-channel
 //              chunk K taps x 4 MFMAs, the next tap's fragments read while the
 //              current tap's MFMAs run;
-//   waves 8-11 producers: global -> LDS DMA (global_load_lds_dwordx4) of the
+//   waves NC..NC+3 producers: global -> LDS DMA (global_load_lds_dwordx4) of the
 //              input span and the K weight slices three chunks ahead into a
 //              4-slot LDS ring, then the input ELU in place one chunk ahead;
 //   all 12:    the epilogue, through an fp32 LDS tile with row-contiguous 16-B
@@ -699,12 +699,15 @@ __global__ __launch_bounds__((NC + 4) * 64) void k_conv_ws_bf16(Args a, const __
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     for (int ch = 0; ch < nchunk; ++ch) {
+      // issue first: slot (ch+D)%NBUF = (ch-1)%NBUF was released by the last
+      // barrier, and the count below assumes chunks up to min(ch+D, nchunk-1)
+      // are out (issued after the wait, chunk ch+1 was never waited for)
+      if (ch + D < nchunk) issue(ch + D);
       if (ch + 1 < nchunk) {
         // chunk ch+1 landed (later ones may still be in flight), then its ELU
         wait_chunk(std::min(D - 1, nchunk - 2 - ch));
         if (a.in_elu && !(dbg & 16)) elu_pass(ch + 1);
       }
-      if (ch + D < nchunk) issue(ch + D);  // slot (ch+D)%NBUF = (ch-1)%NBUF, released by the last barrier
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
     }
