@@ -566,8 +566,9 @@ __device__ __forceinline__ int ws_swzbits(int row) { return WS_CK == 16 ? (row >
 __device__ __forceinline__ int ws_swz(int row, int slot) { return row * WS_CK + ((slot ^ ws_swzbits(row)) << 3); }
 
 inline size_t ws_buf_bytes(int K) { return (size_t(WS_XROWS) + size_t(K) * WS_BN) * WS_CK * 2; }
-inline size_t ws_lds_bytes(int K) {
-  return std::max(WS_NBUF * ws_buf_bytes(K), size_t(WS_BM) * WS_EP * sizeof(float));
+// CPB chunks per barrier: the ring has 4 * CPB slots and slots free CPB at a time
+inline size_t ws_lds_bytes(int K, int cpb = 1) {
+  return std::max(size_t(WS_NBUF) * cpb * ws_buf_bytes(K), size_t(WS_BM) * WS_EP * sizeof(float));
 }
 
 // s_waitcnt vmcnt(N) alone (expcnt / lgkmcnt left at their no-wait maxima)
@@ -604,7 +605,7 @@ __device__ __forceinline__ void ws_elu_pieces(unsigned char* lane_base, int pw, 
   }
 }
 
-template <int KT, typename TO, int NC>
+template <int KT, typename TO, int NC, int CPB>
 __global__ __launch_bounds__((NC + 4) * 64) void k_conv_ws_bf16(Args a, const __bf16* __restrict__ in,
                                                       const __bf16* __restrict__ wp,
                                                       const float* __restrict__ bias, const TO* __restrict__ aux,
@@ -667,7 +668,7 @@ __global__ __launch_bounds__((NC + 4) * 64) void k_conv_ws_bf16(Args a, const __
       }
     }
     auto issue = [&](int ch) {
-      unsigned char* const base = smem + (ch % WS_NBUF) * (BUF * 2);
+      unsigned char* const base = smem + (ch % (WS_NBUF * CPB)) * (BUF * 2);
 #pragma unroll
       for (int u = 0; u < PW; ++u) {
         const int q = ws_piece<TI>(u, pw);
@@ -679,34 +680,45 @@ __global__ __launch_bounds__((NC + 4) * 64) void k_conv_ws_bf16(Args a, const __
     };
       const int xi_used = (span + WS_RPI - 1) / WS_RPI;  // input pieces holding rows < span (the rest stay zero)
     auto elu_pass = [&](int ch) __attribute__((always_inline)) {
-      ws_elu_pieces<PW>(smem + (ch % WS_NBUF) * (BUF * 2) + lane * 16, pw, xi_used);
+      ws_elu_pieces<PW>(smem + (ch % (WS_NBUF * CPB)) * (BUF * 2) + lane * 16, pw, xi_used);
     };
+    // stages of CPB chunks, one barrier per stage
+    const int nst = (nchunk + CPB - 1) / CPB;
     if (dbg & 1) {  // diagnostic: consumers alone (tune key 13 bit 0)
-      for (int ch = 0; ch <= nchunk; ++ch) __syncthreads();
+      for (int st = 0; st <= nst; ++st) __syncthreads();
     } else {
-    // prefetch distance D = WS_NBUF - 1 chunks; wait_chunk(n): chunk landed
-    // with n younger chunks still allowed in flight
-    constexpr int D = WS_NBUF - 1;
-    static_assert(D >= 1 && D <= 3, "ring depth");
+    // ring of NB = 4 CPB slots, prefetch distance D = NB - CPB chunks (slots are
+    // released a stage at a time); wait_chunk(n): chunk landed with n younger
+    // chunks still allowed in flight
+    constexpr int NB = WS_NBUF * CPB, D = NB - CPB;
+    static_assert(D >= 1 && 2 * CPB * PW < 64, "ring depth / vmcnt range");
     auto wait_chunk = [&](int younger) __attribute__((always_inline)) {
-      if (younger >= 2) ws_wait_vm<(D >= 3 ? 2 * PW : 0)>();
-      else if (younger == 1) ws_wait_vm<(D >= 2 ? PW : 0)>();
+      if (younger >= 4 && 2 * CPB >= 4) ws_wait_vm<(2 * CPB >= 4 ? 4 * PW : 0)>();
+      else if (younger == 3 && 2 * CPB >= 3) ws_wait_vm<(2 * CPB >= 3 ? 3 * PW : 0)>();
+      else if (younger >= 2) ws_wait_vm<2 * PW>();
+      else if (younger == 1) ws_wait_vm<PW>();
       else ws_wait_vm<0>();
     };
     for (int c = 0; c < D && c < nchunk; ++c) issue(c);
-    wait_chunk(std::min(D, nchunk) - 1);
-    if (a.in_elu && !(dbg & 16)) elu_pass(0);  // bit 4: diagnostic without the ELU pass
+    // stage 0 landed (its last chunk with the younger ones in flight), then its ELU
+    wait_chunk(std::min(D, nchunk) - std::min(CPB, nchunk));
+    if (a.in_elu && !(dbg & 16))  // bit 4: diagnostic without the ELU pass
+      for (int c = 0; c < CPB && c < nchunk; ++c) elu_pass(c);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    for (int ch = 0; ch < nchunk; ++ch) {
-      // issue first: slot (ch+D)%NBUF = (ch-1)%NBUF was released by the last
-      // barrier, and the count below assumes chunks up to min(ch+D, nchunk-1)
-      // are out (issued after the wait, chunk ch+1 was never waited for)
-      if (ch + D < nchunk) issue(ch + D);
-      if (ch + 1 < nchunk) {
-        // chunk ch+1 landed (later ones may still be in flight), then its ELU
-        wait_chunk(std::min(D - 1, nchunk - 2 - ch));
-        if (a.in_elu && !(dbg & 16)) elu_pass(ch + 1);
+    for (int st = 0; st < nst; ++st) {
+      // issue first: the slots of stage st-1 were released by the last barrier,
+      // and the count below assumes chunks up to min(st CPB + D + CPB - 1,
+      // nchunk - 1) are out
+      const int c0 = st * CPB;
+      for (int c = c0 + D; c < c0 + D + CPB && c < nchunk; ++c) issue(c);
+      if (c0 + CPB < nchunk) {
+        // stage st+1 landed (later chunks may still be in flight), then its ELU
+        const int issued = std::min(c0 + D + CPB, nchunk) - 1;
+        const int need = std::min(c0 + 2 * CPB, nchunk) - 1;
+        wait_chunk(issued - need);
+        if (a.in_elu && !(dbg & 16))
+          for (int c = c0 + CPB; c < c0 + 2 * CPB && c < nchunk; ++c) elu_pass(c);
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
@@ -736,11 +748,13 @@ __global__ __launch_bounds__((NC + 4) * 64) void k_conv_ws_bf16(Args a, const __
   // 13 bit 7 = diagnostic without)
   if (!(dbg & 128)) __builtin_amdgcn_s_setprio(2);
   for (int ch = 0; ch < nchunk; ++ch) {
+    // one barrier per stage of CPB chunks (after its last chunk)
+    const bool stage_end = (ch + 1) % CPB == 0 || ch + 1 == nchunk;
     if (dbg & 2) {  // diagnostic: producers alone (tune key 13 bit 1)
-      __syncthreads();
+      if (stage_end) __syncthreads();
       continue;
     }
-    const __bf16* const xb = lds + (ch % WS_NBUF) * BUF;
+    const __bf16* const xb = lds + (ch % (WS_NBUF * CPB)) * BUF;
     bf16x8 fa[2][TM], fb[2][TN];
     constexpr int NS = KT * (WS_CK / 16);  // (tap, 16-channel half) steps
     // slot bit 1 <-> element offset bit 4 (row * 32 keeps bits 0-4 clear)
@@ -768,7 +782,7 @@ __global__ __launch_bounds__((NC + 4) * 64) void k_conv_ws_bf16(Args a, const __
       __builtin_amdgcn_sched_barrier(0);
     }
     }
-    __syncthreads();
+    if (stage_end) __syncthreads();
   }
 
   __builtin_amdgcn_s_setprio(0);
@@ -3201,14 +3215,19 @@ int launch_fwd4(const Args& a, const void* in, const void* wp, const float* bias
 template <int KT, typename TO>
 int launch_ws(const Args& a, const void* in, const void* wp, const float* bias, const void* aux, const void* res,
               void* out, hipStream_t s) {
-  const size_t lds = ws_lds_bytes(KT);
+  // tune key 33 = 1: two chunks per barrier for the two-tap layers (8 MFMAs per
+  // wave per chunk); measured neutral on C5 (44.38/44.43 vs 44.23/44.28 ms
+  // median, alternating in one call), so off
+  constexpr int CPB = KT == 2 ? 2 : 1;
+  const bool cpb2 = CPB == 2 && tune(33) == 1;
+  const size_t lds = ws_lds_bytes(KT, cpb2 ? 2 : 1);
   const int64_t tiles = (a.rows / a.T) * ((a.T + WS_BM - 1) / WS_BM);
   const int ncol = a.N / WS_BN;
   if (tiles == 0) return SEL_OK;
   const bool xcd = ncol > 1 && tune(8) == 0 && tiles * ncol < (int64_t(1) << 31);
   const dim3 grid = xcd ? dim3(unsigned(tiles * ncol)) : dim3(unsigned(tiles), unsigned(ncol));
-  const bool nc4 = tune(32) == 1;
-  auto kern = nc4 ? k_conv_ws_bf16<KT, TO, 4> : k_conv_ws_bf16<KT, TO, 8>;
+  const bool nc4 = tune(32) == 1 && !cpb2;
+  auto kern = cpb2 ? k_conv_ws_bf16<KT, TO, 8, CPB> : nc4 ? k_conv_ws_bf16<KT, TO, 4, 1> : k_conv_ws_bf16<KT, TO, 8, 1>;
   SEL_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
   hipLaunchKernelGGL(kern, grid, dim3(nc4 ? 512 : 768), lds, s, a, static_cast<const __bf16*>(in),
                      static_cast<const __bf16*>(wp), bias, static_cast<const TO*>(aux), static_cast<const TO*>(res),
