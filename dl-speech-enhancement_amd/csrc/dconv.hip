@@ -657,7 +657,7 @@ __global__ __launch_bounds__(256) void k_dconv_short(D d, const T* __restrict__ 
 template <typename T, int K, int NR>
 __global__ __launch_bounds__(256) void k_dconv_shortx(D d, const T* __restrict__ x, const T* __restrict__ wp,
                                                       const float* __restrict__ bias, const T* __restrict__ aux,
-                                                      const T* __restrict__ res, T* __restrict__ out) {
+                                                      const T* __restrict__ res, T* __restrict__ out, bool prefetch) {
   constexpr int KR = K * NR, RW = 8, XW = (RW + K - 1) * NR;
   extern __shared__ float sh[];
   float* const wsh = sh;            // [KR][Ng]
@@ -669,14 +669,32 @@ __global__ __launch_bounds__(256) void k_dconv_shortx(D d, const T* __restrict__
   const int n8 = d.Ng / 8, RL = 256 / n8, RB = RL * RW;
   const int rl = threadIdx.x / n8, n0 = (threadIdx.x - rl * n8) * 8;
   const int tps = (d.Tvo + RB - 1) / RB, ntiles = d.B * tps;
+  // a window of at most one value per thread (the MSD's k15 1 -> 128 conv: 142)
+  // is fetched into a register one tile ahead, so the fetch latency overlaps
+  // the current tile's FMAs instead of sitting between two barriers
+  // (tune key 34 = 1; measured neutral on C5: 44.45/44.40 vs 44.42/44.41 ms
+  // median, alternating in one call, so off)
+  const int np = (RB + K - 1) * NR;
+  const bool pf = np <= 256 && prefetch;
+  auto fetch = [&](int tile) {
+    const int b = tile / tps, j0 = (tile - b * tps) * RB, p = threadIdx.x;
+    const int t = j0 + d.q0 + p / NR;
+    return (p < np && t >= 0 && t < d.Tv) ? to_f(x[(int64_t(b) * d.Tvs + t) * NR + p % NR]) : 0.f;
+  };
+  float nxt = pf && int(blockIdx.x) < ntiles ? fetch(blockIdx.x) : 0.f;
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int b = tile / tps, j0 = (tile - b * tps) * RB;
     __syncthreads();  // the previous tile's window reads are done (and the weights are in)
-    for (int p = threadIdx.x; p < (RB + K - 1) * NR; p += 256) {
-      const int t = j0 + d.q0 + p / NR;
-      xs[p] = (t >= 0 && t < d.Tv) ? to_f(x[(int64_t(b) * d.Tvs + t) * NR + p % NR]) : 0.f;
+    if (pf) {
+      if (int(threadIdx.x) < np) xs[threadIdx.x] = nxt;
+    } else {
+      for (int p = threadIdx.x; p < np; p += 256) {
+        const int t = j0 + d.q0 + p / NR;
+        xs[p] = (t >= 0 && t < d.Tv) ? to_f(x[(int64_t(b) * d.Tvs + t) * NR + p % NR]) : 0.f;
+      }
     }
     __syncthreads();
+    if (pf && tile + int(gridDim.x) < ntiles) nxt = fetch(tile + gridDim.x);
     const int jr = rl * RW;
     if (j0 + jr >= d.Tvo) continue;
     float xw[XW];
@@ -1953,7 +1971,8 @@ int launch_short(const sel_dconv_desc* d, const void* x, const void* wp, const f
     if (lds > 64 * 1024)
       SEL_HIP(hipFuncSetAttribute((const void*)kx, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
     hipLaunchKernelGGL(kx, dim3(blocks), dim3(256), lds, s, *d, static_cast<const T*>(x), static_cast<const T*>(wp),
-                       bias, static_cast<const T*>(aux), static_cast<const T*>(res), static_cast<T*>(out));
+                       bias, static_cast<const T*>(aux), static_cast<const T*>(res), static_cast<T*>(out),
+                       tune(34) == 1);
     SEL_LAUNCH_CHECK();
     return SEL_OK;
   }
