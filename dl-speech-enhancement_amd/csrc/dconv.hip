@@ -700,21 +700,32 @@ __global__ __launch_bounds__(256) void k_dconv_shortx(D d, const T* __restrict__
     float xw[XW];
 #pragma unroll
     for (int u = 0; u < XW; ++u) xw[u] = xs[jr * NR + u];
-    float acc[RW][8];
+    // channel pairs as 2-vectors: one packed fp32 FMA (v_pk_fma_f32) per pair,
+    // per element the same fused multiply-add as fmaf, so bit-identical
+    typedef float shx_f2 __attribute__((ext_vector_type(2)));
+    shx_f2 acc2[RW][4];
 #pragma unroll
     for (int q = 0; q < RW; ++q)
 #pragma unroll
-      for (int c = 0; c < 8; ++c) acc[q][c] = 0.f;
+      for (int c = 0; c < 4; ++c) acc2[q][c] = shx_f2{0.f, 0.f};
 #pragma unroll
     for (int e = 0; e < KR; ++e) {
       const float4 w0 = *reinterpret_cast<const float4*>(wsh + e * d.Ng + n0);
       const float4 w1 = *reinterpret_cast<const float4*>(wsh + e * d.Ng + n0 + 4);
-      const float w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+      const shx_f2 w[4] = {shx_f2{w0.x, w0.y}, shx_f2{w0.z, w0.w}, shx_f2{w1.x, w1.y}, shx_f2{w1.z, w1.w}};
 #pragma unroll
-      for (int q = 0; q < RW; ++q)
+      for (int q = 0; q < RW; ++q) {
+        const float xv = xw[q * NR + e];
+        const shx_f2 x2 = shx_f2{xv, xv};
 #pragma unroll
-        for (int c = 0; c < 8; ++c) acc[q][c] = fmaf(w[c], xw[q * NR + e], acc[q][c]);
+        for (int c = 0; c < 4; ++c) acc2[q][c] = __builtin_elementwise_fma(w[c], x2, acc2[q][c]);
+      }
     }
+    float acc[RW][8];
+#pragma unroll
+    for (int q = 0; q < RW; ++q)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[q][2 * c] = acc2[q][c].x, acc[q][2 * c + 1] = acc2[q][c].y;
 #pragma unroll
     for (int q = 0; q < RW; ++q) {
       const int j = j0 + jr + q;
