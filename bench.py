@@ -203,6 +203,49 @@ def c3_cpu_baseline(B_sample=4, steps=20):
                                       f"after 1 warm-up, on {_cpu_model()}")
 
 
+C1_CONFIG = "symAD_24Mel"
+
+
+def c1_cpu_baseline(B=2, steps=5):
+    """BASELINE configs[0] as named: the reference's CPU case — train_denoise.py's
+    default symAD_24Mel step (without-PQC generator, 45 x mel + 0 x SNR, clip
+    norm 1, Adam; :213-263 before the discriminator is enabled) at B = 2 x 1 s @
+    24 kHz, on the oracle's op-for-op restatement."""
+    from oracle import ref_ops as R
+    from oracle.melfilters import mel as melbank
+    from sel import configs
+    from models.autoencoder_without_PQC.AudioDec import Generator
+    cfg = configs.get(C1_CONFIG)
+    mp = cfg["mel_loss_params"]
+    mm = torch.from_numpy(melbank(sr=mp["fs"], n_fft=2048, n_mels=80, fmin=mp["fmin"], fmax=mp["fmax"]).T.copy())
+    torch.manual_seed(93)
+    P = {k: v.clone() for k, v in Generator(**cfg["generator_params"]).state_dict().items()}
+    train = [k for k in P if k.startswith(("encoder.", "decoder.conv_blocks", "decoder.conv2"))
+             and not k.endswith("pad_buffer")]
+    for k in train:
+        P[k].requires_grad_(True)
+    params = [P[k] for k in train]
+    opt = torch.optim.Adam(params, **cfg["generator_optimizer_params"])
+    geo = R.generator_geometry(**cfg["generator_params"])
+    clean, noise = synthetic_batch(B, SR)
+    mixed = R.add_noise(clean, noise, 15)
+    win = R.hann(2048)
+
+    def step():
+        y = R.generator_forward(P, mixed, geo, pqc=False)
+        loss = cfg["lambda_mel_loss"] * R.multi_mel_loss(y, clean, [(2048, 300, 2048)], [win], [mm], 1e-10, None)
+        opt.zero_grad()
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(params, cfg["generator_grad_norm"])
+        opt.step()
+    step()
+    dt = _median_time(step, steps)
+    return {"value": round(B * SR / HOP / dt, 1), "unit": "frames/s", "ms_per_step": round(dt * 1e3, 1),
+            "sample": (f"configs[0] as named: {C1_CONFIG} train_denoise step (without-PQC generator, mel, clip, "
+                       f"Adam), B={B} x 1 s @ 24 kHz, fp32 oracle, median of {steps} steps after 1 warm-up, on "
+                       f"{_cpu_model()}")}
+
+
 # ---------------------------------------------------------------------------
 # c5: GAN-mode denoise step at 48 kHz (generator + HiFi-GAN MSD/MPD discriminator)
 # ---------------------------------------------------------------------------
@@ -250,7 +293,7 @@ def c5_setup(dev, B, world, local, dtype=torch.bfloat16):
     return step
 
 
-def c5_cpu_baseline(B_sample=1, steps=3):
+def c5_cpu_baseline(B_sample=1, steps=5):
     """Oracle (op-for-op PyTorch-CPU restatement) of the same GAN step, fp32."""
     from oracle import ref_ops as R
     from oracle.melfilters import mel as melbank
@@ -310,15 +353,22 @@ def c5_cpu_baseline(B_sample=1, steps=3):
 MFMA_BF16_PEAK_TFS = 2500.0  # MI355X dense bf16 (MI355X_MICROARCH.md)
 
 
-# newest committed PMC traffic table of the C3 bench (tools/pmc_round.sh)
-PMC_FILE = next((f for f in (os.path.join(REPO, "profiles", n) for n in ("r2_c3_pmc_traffic_v2.json",
-                                                                          "r2_c3_pmc_traffic.json",
-                                                                          "r1_c3_pmc_traffic.json"))
-                 if os.path.exists(f)), "")
+def pmc_file(cfg):
+    """Newest committed PMC traffic table of a config's bench (tools/gpu.sh pmc):
+    profiles/r<round>_<cfg>_pmc_traffic[_v<k>].json, highest (round, k) wins."""
+    import glob
+    import re
+    best, key = "", (-1, -1)
+    for f in glob.glob(os.path.join(REPO, "profiles", f"r*_{cfg}_pmc_traffic*.json")):
+        m = re.match(rf"r(\d+)_{cfg}_pmc_traffic(?:_v(\d+))?\.json$", os.path.basename(f))
+        if m and (int(m.group(1)), int(m.group(2) or 0)) > key:
+            best, key = f, (int(m.group(1)), int(m.group(2) or 0))
+    return best
 
 
 def _mangled_fragment(tag):
-    """'k_conv_fwd_bf16<128, 64, 2, 8, bf16>' -> 'k_conv_fwd_bf16ILi128ELi64ELi2ELi8EDF16bE' (Itanium)."""
+    """'k_conv_fwd_bf16<128, 64, 2, 8, bf16>' -> 'k_conv_fwd_bf16ILi128ELi64ELi2ELi8EDF16b' (Itanium;
+    a prefix: a tag may name the leading template arguments only, 'k_conv_ws_bf16<5>')."""
     import re
     m = re.match(r"(\w+)<(.*)>", tag)
     if not m:
@@ -326,17 +376,21 @@ def _mangled_fragment(tag):
     parts = []
     for a in (x.strip() for x in m.group(2).split(",")):
         parts.append({"bf16": "DF16b", "float": "f"}.get(a, f"Li{a}E"))
-    return m.group(1) + "I" + "".join(parts) + "E"
+    return m.group(1) + "I" + "".join(parts)
 
 
-def pmc_traffic(tag, B, steps_cfg="c3"):
+DEFAULT_BATCH = {"c2": 32, "c3": 64, "c5": 16}
+
+
+def pmc_traffic(tag, B, cfg="c3"):
     """HBM bytes per launch of kernel `tag` from the committed rocprofv3 PMC passes
     (tools/pmc_traffic.py over FETCH_SIZE / WRITE_SIZE runs of this same bench
     command, gfx950 corrections applied there), or None if not measured."""
-    if steps_cfg != "c3" or B != 64 or not PMC_FILE:
+    path = pmc_file(cfg)
+    if B != DEFAULT_BATCH.get(cfg) or not path:
         return None
     frag = _mangled_fragment(tag)
-    with open(PMC_FILE) as f:
+    with open(path) as f:
         table = json.load(f)
     # a tag can cover several compiled variants (e.g. the thin kernel's
     # epilogue-prefetch template flag: ...ELb0E / ...ELb1E): launch-weighted mean
@@ -374,7 +428,8 @@ def roofline(cfg, timer, dom, B, steps):
     r.update({"kernel": tag, "launches": n, "event_timed_steps": 1, "avg_launch_us": round(1e3 * ms / n, 2),
               "bytes_per_launch": int(nbytes / n), "flops_per_launch": int(flops / n),
               "share_of_timed_conv_ms": round(ms / sum(v[1] for v in summ.values()), 3),
-              "traffic": pmc_traffic(tag, B, cfg), "traffic_unit": "bytes/launch (rocprofv3 PMC, profiles/)"})
+              "traffic": pmc_traffic(tag, B, cfg), "traffic_unit": "bytes/launch (rocprofv3 PMC, profiles/)",
+              "traffic_file": os.path.basename(pmc_file(cfg)) or None})
     return r
 
 
@@ -564,6 +619,8 @@ def main():
         torch.set_num_threads(ncores)
         v, sample = {"c2": c2_cpu_baseline, "c3": c3_cpu_baseline, "c5": c5_cpu_baseline}[cfg]()
         cpu = {"value": round(v, 1), "unit": "frames/s", "cores": ncores, "kind": "port", "sample": sample}
+        if cfg == "c3":
+            cpu["c1"] = c1_cpu_baseline()
 
     if rank == 0:
         out = {

@@ -659,7 +659,10 @@ __global__ __launch_bounds__((NC + 4) * 64) void k_conv_ws_bf16(Args a, const __
         const bool valid =
             R < span && (a.seq_pitch > 0 ? ti >= 0 && ti < a.T && ti % a.seq_pitch < a.tin_valid
                                          : (ti >= 0 && ti < a.tin_valid) || a.pad_mode == SEL_PAD_REPLICATE);
-        ti = ti < 0 ? 0 : (ti >= a.tin_valid ? a.tin_valid - 1 : ti);
+        // flat tiling: ti is a row of the whole row space (b == 0) and `valid`
+        // already keeps it in range; only the per-sequence form clamps into
+        // the sequence (replicate pad)
+        if (a.seq_pitch == 0) ti = ti < 0 ? 0 : (ti >= a.tin_valid ? a.tin_valid - 1 : ti);
         src[u] = valid ? in + (b * a.tin_pitch + ti) * a.ldx + 8 * ls : g_ws_zero + 8 * ls;
       } else {
         const int R = (q - XI) * WS_RPI + lane / WS_SPR, ls = (lane % WS_SPR) ^ ws_swzbits(R);
@@ -3722,15 +3725,14 @@ hipError_t launch_wgrad3(const WgPlan& p, const Args& a, const __bf16* gout, con
 // any other shape (the caller keeps its own kernels).
 namespace sel {
 namespace conv {
-int dconv_ws_fwd(const sel_dconv_desc* d, const void* x, const void* wp, const float* bias, const void* aux,
-                 const void* res, void* out, hipStream_t s) {
+int dconv_ws_mode(const sel_dconv_desc* d) {
   const int width = d->So * d->Ng, nred = d->S * d->Cg;
   const bool ok = d->G == 1 && (d->S == 1 || d->Cs == d->Cg) && (d->So == 1 || d->Ns == d->Ng) &&
                   (d->K == 2 || d->K == 3 || d->K == 5 || d->K == 7) && width % WS_BN == 0 &&
                   nred % WS_CK == 0 && nred <= WS_CMAX && d->ldx % 8 == 0 && d->ldo % 8 == 0 &&
                   d->ldx >= nred && d->ldo >= width && d->Tvo > 0 && d->B > 0 && d->Tv <= d->Tvs &&
                   d->K - 1 <= F4_HALOMAX && -d->q0 <= F4_HALOMAX && ws_lds_bytes(d->K) <= 160 * 1024;
-  if (!ok) return SEL_ERR_UNSUPPORTED;
+  if (!ok) return -1;
   // flat tiling (tune key 22: 1 = off) where the layout leaves zero gaps
   // between sequences (sel.dconvops allocates the MPD chain so; its deep layers
   // have 54-300 rows per period column, a 256-row sample-aligned tile wastes up
@@ -3739,6 +3741,16 @@ int dconv_ws_fwd(const sel_dconv_desc* d, const void* x, const void* wp, const f
   const int P = d->Tvo;
   const bool flat = tune(22) != 1 && d->Tvs == P && P - d->Tv >= -d->q0 && P - d->Tvalid >= d->q0 + d->K - 1 &&
                     int64_t(d->B) * P < (int64_t(1) << 31);
+  return flat ? 1 : 0;
+}
+
+int dconv_ws_fwd(const sel_dconv_desc* d, const void* x, const void* wp, const float* bias, const void* aux,
+                 const void* res, void* out, hipStream_t s) {
+  const int mode = dconv_ws_mode(d);
+  if (mode < 0) return SEL_ERR_UNSUPPORTED;
+  const bool flat = mode == 1;
+  const int width = d->So * d->Ng, nred = d->S * d->Cg;
+  const int P = d->Tvo;
   Args a;
   a.rows = int64_t(d->B) * d->Tvo;
   a.T = flat ? int(a.rows) : d->Tvo;

@@ -42,6 +42,8 @@ namespace conv {
 // conv.hip: discriminator layers on the generator's warp-specialised kernel
 int dconv_ws_fwd(const sel_dconv_desc* d, const void* x, const void* wp, const float* bias, const void* aux,
                  const void* res, void* out, hipStream_t s);
+// -1: shape not supported there, 0: per-sequence tiles, 1: flat tiles across sequences
+int dconv_ws_mode(const sel_dconv_desc* d);
 }  // namespace conv
 namespace dconv {
 
@@ -2021,51 +2023,91 @@ bool pf_ok(const sel_dconv_desc* d, int dtype) {
   return dtype == SEL_BF16 && d->G == 1 && (d->S == 1 || d->Cs == d->Cg) && d->K <= PF_KMAX && tune(16) != 1;
 }
 
-template <typename T>
-int dispatch_fwd(const sel_dconv_desc* d, const void* x, const void* wp, const float* bias, const void* aux,
-                 const void* res, void* out, hipStream_t s, int dtype) {
-  if (tune(9) == 1) return launch_valu<T>(d, x, wp, bias, aux, res, out, s);
+// Kernel family a forward / adjoint launch of this shape takes (include/sel.h
+// SEL_DPATH_*): the single decision both the launcher and sel_dconv_kernel use.
+struct FwdPlan {
+  int path, bm, bn;
+};
+
+FwdPlan plan_fwd(const sel_dconv_desc* d, int dtype) {
+  if (tune(9) == 1) return {SEL_DPATH_VALU, 0, 0};
   if (!mfma_ok(d, dtype)) {
-    if (short_ok(d)) return launch_short<T>(d, x, wp, bias, aux, res, out, s);
+    if (short_ok(d)) return {shortx_kernel<float>(d) ? SEL_DPATH_SHORTX : SEL_DPATH_SHORT, 0, 0};
     // tune key 31 = 1: the generic VALU kernel instead of the narrow-output one
-    if (tiny_ok(d, dtype)) return launch_tiny(d, x, wp, bias, aux, res, out, s);
-    return launch_valu<T>(d, x, wp, bias, aux, res, out, s);
+    if (tiny_ok(d, dtype)) return {SEL_DPATH_TINY, 0, 0};
+    return {SEL_DPATH_VALU, 0, 0};
   }
   const int width = d->So * d->Ng;
   const int64_t rows = int64_t(d->B) * d->Tvo;
-  if constexpr (sizeof(T) == 2) {
+  const bool bf = dtype == SEL_BF16;
+  if (bf) {
     // the MPD's >= 128-wide one-group layers and adjoints: warp-specialised
     // 256 x 128 tiles (conv.hip k_conv_ws_bf16; tune key 21: 1 = off)
     if (tune(21) != 1 && width % 128 == 0 && d->S * d->Cg >= 64 && rows * (width / 128) >= 65536) {
-      const int rc = sel::conv::dconv_ws_fwd(d, x, wp, bias, aux, res, out, s);
-      if (rc != SEL_ERR_UNSUPPORTED) return rc;
+      const int m = sel::conv::dconv_ws_mode(d);
+      if (m >= 0) return {m == 1 ? SEL_DPATH_WS_FLAT : SEL_DPATH_WS, 256, 128};
     }
     if (width > 32 && pf_ok(d, dtype)) {
-      // tune key 19: tile A/B (1: 256x64, 2: 128x128, 3: 256x128, 4: the <= 64-wide tiles below)
-      if (tune(19) == 1) return launch_pf<256, 64>(d, x, wp, bias, aux, res, out, s);
-      if (tune(19) == 3 && width % 128 == 0) return launch_pf<256, 128>(d, x, wp, bias, aux, res, out, s);
+      // tune key 19: tile A/B (1: 256x64, 2: 128x128, 3: 256x128)
+      if (tune(19) == 1) return {SEL_DPATH_PF, 256, 64};
+      if (tune(19) == 3 && width % 128 == 0) return {SEL_DPATH_PF, 256, 128};
       // 128-column tiles halve the input re-staging per output (MPD 512 -> 1024 k5 s3: 8.4 -> 5.5 ms,
       // 1024 -> 1024 k5: 1.22 -> 0.80 ms at the probe's sizes, tools/dconv_probe.py, bit-identical)
       if (width % 128 == 0 && (tune(19) == 2 || (tune(19) == 0 && rows * (width / 128) >= 65536)))
-        return launch_pf<128, 128>(d, x, wp, bias, aux, res, out, s);
-      if (rows * (width / 64) < 65536) return launch_pf<64, 64>(d, x, wp, bias, aux, res, out, s);
-      return launch_pf<128, 64>(d, x, wp, bias, aux, res, out, s);
+        return {SEL_DPATH_PF, 128, 128};
+      if (rows * (width / 64) < 65536) return {SEL_DPATH_PF, 64, 64};
+      return {SEL_DPATH_PF, 128, 64};
     }
   }
+  int bm, bn;
   // narrow groups: 32-wide tiles; short sequences / few rows: 64-row tiles
   if (width <= 32) {
     // tune key 28 bit 1: one tile size up (256 / 512 rows)
-    const bool up = sizeof(T) == 2 && (tune(28) & 2);
-    if (rows * d->G < 131072)
-      return up ? launch_mfma<T, 256, 32>(d, x, wp, bias, aux, res, out, s)
-                : launch_mfma<T, 128, 32>(d, x, wp, bias, aux, res, out, s);
-    return up ? launch_mfma<T, 512, 32>(d, x, wp, bias, aux, res, out, s)
-              : launch_mfma<T, 256, 32>(d, x, wp, bias, aux, res, out, s);
+    const bool up = bf && (tune(28) & 2);
+    bn = 32;
+    bm = rows * d->G < 131072 ? (up ? 256 : 128) : (up ? 512 : 256);
+  } else if (rows * d->G * (width / 64) < 65536) {
+    bm = 64, bn = 64;
+  } else {
+    // 256-row tiles: each staged tap group of weights serves twice the rows (the
+    // MSD's 41-tap grouped layers: C5 50.5 -> 49.7 ms/step; tune key 28 bit 0 = 128 rows)
+    bm = bf && !(tune(28) & 1) ? 256 : 128, bn = 64;
   }
-  if (rows * d->G * (width / 64) < 65536) return launch_mfma<T, 64, 64>(d, x, wp, bias, aux, res, out, s);
-  // 256-row tiles: each staged tap group of weights serves twice the rows (the
-  // MSD's 41-tap grouped layers: C5 50.5 -> 49.7 ms/step; tune key 28 bit 0 = 128 rows)
-  if (sizeof(T) == 2 && !(tune(28) & 1)) return launch_mfma<T, 256, 64>(d, x, wp, bias, aux, res, out, s);
+  // register-prefetched pipeline (same stages, same bits; tune key 30 = 1: off)
+  const bool gpf = bf && tune(30) != 1 && d->K - 1 <= KC * 8;
+  return {gpf ? SEL_DPATH_GPF : SEL_DPATH_MFMA, bm, bn};
+}
+
+template <typename T>
+int dispatch_fwd(const sel_dconv_desc* d, const void* x, const void* wp, const float* bias, const void* aux,
+                 const void* res, void* out, hipStream_t s, int dtype) {
+  const FwdPlan p = plan_fwd(d, dtype);
+  switch (p.path) {
+    case SEL_DPATH_VALU: return launch_valu<T>(d, x, wp, bias, aux, res, out, s);
+    case SEL_DPATH_SHORT:
+    case SEL_DPATH_SHORTX: return launch_short<T>(d, x, wp, bias, aux, res, out, s);
+    case SEL_DPATH_TINY: return launch_tiny(d, x, wp, bias, aux, res, out, s);
+    default: break;
+  }
+  if constexpr (sizeof(T) == 2) {
+    if (p.path == SEL_DPATH_WS || p.path == SEL_DPATH_WS_FLAT)
+      return sel::conv::dconv_ws_fwd(d, x, wp, bias, aux, res, out, s);
+    if (p.path == SEL_DPATH_PF) {
+      if (p.bm == 256 && p.bn == 64) return launch_pf<256, 64>(d, x, wp, bias, aux, res, out, s);
+      if (p.bm == 256) return launch_pf<256, 128>(d, x, wp, bias, aux, res, out, s);
+      if (p.bn == 128) return launch_pf<128, 128>(d, x, wp, bias, aux, res, out, s);
+      if (p.bm == 64) return launch_pf<64, 64>(d, x, wp, bias, aux, res, out, s);
+      return launch_pf<128, 64>(d, x, wp, bias, aux, res, out, s);
+    }
+  }
+  // k_dconv_mfma / k_dconv_gpf (launch_mfma makes the same gpf choice)
+  if (p.bn == 32) {
+    if (p.bm == 128) return launch_mfma<T, 128, 32>(d, x, wp, bias, aux, res, out, s);
+    if (p.bm == 256) return launch_mfma<T, 256, 32>(d, x, wp, bias, aux, res, out, s);
+    return launch_mfma<T, 512, 32>(d, x, wp, bias, aux, res, out, s);
+  }
+  if (p.bm == 64) return launch_mfma<T, 64, 64>(d, x, wp, bias, aux, res, out, s);
+  if (p.bm == 256) return launch_mfma<T, 256, 64>(d, x, wp, bias, aux, res, out, s);
   return launch_mfma<T, 128, 64>(d, x, wp, bias, aux, res, out, s);
 }
 
@@ -2265,10 +2307,24 @@ int sel_dconv_fwd(const sel_dconv_desc* d, int dtype, const void* x, const void*
   return SEL_ERR_UNSUPPORTED;
 }
 
-int sel_dconv_uses_mfma(const sel_dconv_desc* d, int dtype) {
-  if (!d || tune(9) == 1) return 0;
-  if (mfma_ok(d, dtype)) return (d->So * d->Ng > 32 && pf_ok(d, dtype)) ? 3 : 1;
-  return short_ok(d) ? 2 : 0;
+int sel_dconv_kernel(const sel_dconv_desc* d, int dtype, char* name, size_t cap) {
+  if (!d || check(d) != SEL_OK || (dtype != SEL_BF16 && dtype != SEL_F32)) return -1;
+  const FwdPlan p = plan_fwd(d, dtype);
+  if (name && cap) {
+    const char* t = dtype == SEL_BF16 ? "bf16" : "float";
+    switch (p.path) {
+      case SEL_DPATH_WS:
+      case SEL_DPATH_WS_FLAT: snprintf(name, cap, "k_conv_ws_bf16<%d>", d->K); break;
+      case SEL_DPATH_PF: snprintf(name, cap, "k_dconv_pf<%d, %d>", p.bm, p.bn); break;
+      case SEL_DPATH_GPF: snprintf(name, cap, "k_dconv_gpf<%d, %d>", p.bm, p.bn); break;
+      case SEL_DPATH_MFMA: snprintf(name, cap, "k_dconv_mfma<%s, %d, %d>", t, p.bm, p.bn); break;
+      case SEL_DPATH_SHORTX: snprintf(name, cap, "k_dconv_shortx<%s, %d, %d>", t, d->K, d->S * d->Cg); break;
+      case SEL_DPATH_SHORT: snprintf(name, cap, "k_dconv_short<%s, %d>", t, d->K * d->S * d->Cg); break;
+      case SEL_DPATH_TINY: snprintf(name, cap, "k_dconv_tiny<4>"); break;
+      default: snprintf(name, cap, "k_dconv_valu<%s>", t); break;
+    }
+  }
+  return p.path;
 }
 
 size_t sel_dconv_wgrad_workspace(const sel_dconv_desc* d, int dtype) {

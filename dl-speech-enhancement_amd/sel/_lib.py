@@ -76,7 +76,7 @@ SIGNATURES = {
     "sel_shape_loss_workspace": (SZ, [I64, I64, I32]),
     "sel_shape_loss_fwd": (I32, [P, P, I64, I64, I32, P, P, P, P, SZ, P]),
     "sel_shape_loss_bwd": (I32, [P, I64, I64, I32, P, P, P, F32, P, P]),
-    "sel_dconv_uses_mfma": (I32, [P, I32]),
+    "sel_dconv_kernel": (I32, [P, I32, ctypes.c_char_p, SZ]),
     "sel_dconv_fwd": (I32, [P, I32, P, P, P, P, P, P, P]),
     "sel_dconv_geometry": (I32, [I32, I32, I32, P, P]),
     "sel_dconv_pack": (I32, [I32, P, P, I32, I32, I32, I32, I32, I32, I32, P, P]),

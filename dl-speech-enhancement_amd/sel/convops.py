@@ -325,7 +325,9 @@ class _WgradJob(ctypes.Structure):
 # backward() returns and before anything reads a .grad: ~25 reduction launches
 # of 5-10 us per C3 step become one.  Only where nothing can read the gradient
 # tensor in between: the parameter is a leaf whose .grad is None (AccumulateGrad
-# then takes the returned tensor itself, no copy or add), no create_graph, no
+# then takes the returned tensor itself, no copy or add) and has no tensor or
+# post-accumulate hook (a hook that reads .grad early should set
+# SEL_WGRAD_DEFER=0 if it is attached some other way), no create_graph, no
 # multi-rank process group (DDP copies gradients into its buckets from hooks as
 # they arrive).  The flush checks that every deferred tensor is still the one
 # AccumulateGrad kept and raises otherwise.
@@ -344,6 +346,10 @@ def _can_defer(params):
             return False
         for p in params:
             if p is None or not p.is_leaf or p.grad is not None:
+                return False
+            # a tensor hook or a post-accumulate hook (e.g. an optimizer-in-backward)
+            # would read the gradient before the final callback computes it
+            if getattr(p, "_backward_hooks", None) or getattr(p, "_post_accumulate_grad_hooks", None):
                 return False
             # the engine accumulates into .grad in this backward (not autograd.grad(inputs=...))
             if not torch._C._will_engine_execute_node(torch.autograd.graph.get_gradient_edge(p).node):

@@ -58,6 +58,25 @@ def period_alloc(Lv, specs, gap=FLAT_GAP):
     return max(_roundup(Lv, specs[0].stride), prod * (T + gap))
 
 
+def chain_layout(specs, T0, T_alloc0):
+    """Per layer (T_in, T_alloc_in, T_out, T_out_alloc) of a chain on T0 valid
+    of T_alloc0 allocated input rows: outputs padded to the next layer's stride,
+    or — where the input pitch allows it — sharing the phase-view input's row
+    pitch with >= FLAT_GAP zero rows per sequence (the period_alloc layout)."""
+    out = []
+    T_in, T_alloc_in = T0, T_alloc0
+    for li, sp in enumerate(specs):
+        T_out = sp.t_out(T_in)
+        nxt = specs[li + 1].stride if li + 1 < len(specs) else 1
+        T_out_alloc = _roundup(T_out, nxt)
+        if T_alloc_in % sp.stride == 0 and (T_alloc_in // sp.stride) % nxt == 0 and \
+                T_alloc_in // sp.stride - T_out >= FLAT_GAP:
+            T_out_alloc = T_alloc_in // sp.stride
+        out.append((T_in, T_alloc_in, T_out, T_out_alloc))
+        T_in, T_alloc_in = T_out, T_out_alloc
+    return out
+
+
 class LayerSpec:
     """One conv of a sub-discriminator: torch Conv1d(cin, cout, Kt, stride,
     padding=pad, groups) (or Conv2d (Kt, 1) on the period axis), LeakyReLU after
@@ -214,14 +233,28 @@ def prim(desc, x, wp, out, bias=None, aux=None, res=None, tag=""):
     return out
 
 
+PATH_NAMES = {0: "valu", 1: "mfma", 2: "short", 3: "pf", 4: "ws", 5: "ws_flat", 6: "tiny", 7: "gpf", 8: "shortx"}
+
+
+def kernel(desc, dtype):
+    """(path, kernel name) a sel_dconv_fwd launch of this descriptor takes
+    (include/sel.h SEL_DPATH_*; the launcher's own decision, no GPU needed)."""
+    buf = ctypes.create_string_buffer(96)
+    path = L.load().sel_dconv_kernel(ctypes.byref(desc), _code(dtype), buf, 96)
+    if path < 0:
+        raise L.SelError(f"sel_dconv_kernel: invalid descriptor: {L.load().sel_last_error().decode()}")
+    return PATH_NAMES[path], buf.value.decode()
+
+
 def _meta(d, x, out, tag):
-    """(kernel tag, algorithmic bytes, flops) of one launch for the bench timer."""
+    """(kernel name, algorithmic bytes, flops) of one launch for the bench
+    timer: launches are classified by the kernel they run (the name rocprofv3
+    lists), so the live roofline and the kernel trace group the same launches."""
     es = x.element_size()
     width = d.So * d.Ng
     flops = 2.0 * d.B * d.Tvalid * d.G * width * d.K * d.S * d.Cg
     nbytes = es * (d.B * d.Tvs * d.ldx + d.B * d.Tvo * d.ldo + d.G * width * d.K * d.S * d.Cg)
-    mf = L.lib().sel_dconv_uses_mfma(ctypes.byref(d), _code(x.dtype))
-    return (f"k_dconv_{('valu', 'mfma', 'short', 'pf')[mf]}{tag}", nbytes, flops)
+    return (kernel(d, x.dtype)[1], nbytes, flops)
 
 
 def wgrad(sp, desc, gout, x, w_or_v, wg, want_w, want_b):
@@ -278,25 +311,18 @@ class ChainFn(torch.autograd.Function):
             w, wg, _b = _layer_params(params, li, wn)
             items += [(sp, w, wg, dtype, m) for m in ((0, 1) if adj else (0,))]
         DPACKS.prefetch(items)
-        T_in, T_alloc_in, x = T0, x0.shape[1], x0
-        for li, sp in enumerate(specs):
+        x = x0
+        for li, (sp, g) in enumerate(zip(specs, chain_layout(specs, T0, x0.shape[1]))):
             w, wg, b = _layer_params(params, li, wn)
-            T_out = sp.t_out(T_in)
-            nxt = specs[li + 1].stride if li + 1 < len(specs) else 1
-            T_out_alloc = _roundup(T_out, nxt)
-            if T_alloc_in % sp.stride == 0 and (T_alloc_in // sp.stride) % nxt == 0 and \
-                    T_alloc_in // sp.stride - T_out >= FLAT_GAP:
-                # input pitch / s: one row pitch for the layer's phase-view input and its
-                # output, with >= FLAT_GAP zero rows per sequence (period_alloc)
-                T_out_alloc = T_alloc_in // sp.stride
+            T_in, T_alloc_in, T_out, T_out_alloc = g
             d = _fwd_desc(sp, Bs, T_in, T_alloc_in, T_out, T_out_alloc, slope)
             wp = pack(sp, w, wg, dtype, 0)
             y = torch.empty(Bs, T_out_alloc, sp.cout, dtype=dtype, device=x0.device)
             prim(d, x, wp, y, bias=b.detach().float().contiguous() if b is not None else None, tag=f"_fwd{li}")
             bufs.append(y)
             views.append(_view(y, kind, B, T_out, p))
-            geo.append((T_in, T_alloc_in, T_out, T_out_alloc))
-            x, T_in, T_alloc_in = y, T_out, T_out_alloc
+            geo.append(g)
+            x = y
         ctx.save_for_backward(x0, *bufs, *params)
         ctx.cfg = (specs, slope, wn, geo, len(bufs), kind, B, p, per, frozen)
         return tuple(views)

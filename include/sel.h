@@ -330,10 +330,22 @@ typedef struct sel_dconv_desc {
   int32_t act;     /* 0 none, 1 LeakyReLU */
   float slope;     /* LeakyReLU negative slope (nonlinear_activation_params) */
 } sel_dconv_desc;
-/* kernel a launch of this shape uses: 1 matrix cores, 3 matrix cores with the
- * register prefetch (one group, K <= 8), 2 short-reduction VALU kernel
- * (1-channel convs), 0 generic VALU kernel */
-int sel_dconv_uses_mfma(const sel_dconv_desc* d, int dtype);
+/* kernel family a sel_dconv_fwd launch of this shape takes (the launcher's own
+ * decision, current tune knobs included); writes the kernel's name as rocprofv3
+ * lists it (template arguments of the tile) into name[cap] when name != NULL.
+ * Returns -1 for an invalid descriptor. */
+enum {
+  SEL_DPATH_VALU = 0,    /* generic VALU kernel */
+  SEL_DPATH_MFMA = 1,    /* matrix-core tile, synchronous stages (grouped layers) */
+  SEL_DPATH_SHORT = 2,   /* short reduction (1-channel convs), unstaged */
+  SEL_DPATH_PF = 3,      /* matrix-core tile with register prefetch (one group, K <= 8) */
+  SEL_DPATH_WS = 4,      /* warp-specialised 256 x 128 kernel, per-sequence tiles */
+  SEL_DPATH_WS_FLAT = 5, /* warp-specialised kernel, flat tiles across zero-gapped sequences */
+  SEL_DPATH_TINY = 6,    /* narrow outputs (<= 4 columns) */
+  SEL_DPATH_GPF = 7,     /* grouped matrix-core tile with register-prefetched stages */
+  SEL_DPATH_SHORTX = 8   /* short reduction with the input tile staged in LDS */
+};
+int sel_dconv_kernel(const sel_dconv_desc* d, int dtype, char* name, size_t cap);
 int sel_dconv_fwd(const sel_dconv_desc* d, int dtype, const void* x, const void* wpack, const float* bias,
                   const void* aux, const void* res, void* out, sel_stream_t stream);
 /* phase-view tap geometry of a torch conv (kernel Kt, stride, symmetric pad):

@@ -1,0 +1,136 @@
+"""The data-parallel PRODUCT step, executed: two ranks on the box's one GPU.
+
+Each rank is a fresh child process (tests/ddp_product_worker.py; the pytest
+process is never exec'ed) in a world-size-2 gloo process group over CUDA
+tensors.  RCCL cannot place two ranks on one device; gloo can, and everything
+above the backend is what bench.py / train_denoise.py run over RCCL on 8 GPUs:
+DDP's bucket hooks on the HIP autograd ops, the deferred weight-gradient
+opt-out under a multi-rank group (sel/convops.py _can_defer), the packed-weight
+refresh after the DDP-averaged Adam step, the batch-global add_noise exchange
+(sel.dist.add_noise_global), the spectral-convergence exchange through the real
+STFT-loss autograd op (sel.dist.global_loss_sums, losses/stft_loss.py:56), the
+frozen-D generator pass on the unwrapped discriminator and the single
+concatenated-batch D step under DDP (train_denoise.py DenoiseStep), and the
+global SNR surrogate (train_denoise._global_snr_term).
+
+Reference: the same step in THIS process without a process group, on the
+concatenated global batch (data parallelism must reproduce the
+single-device step).  Loss terms: the mean over ranks of each rank's value
+equals the single-device value (every term is a shard mean or an exchanged
+global quantity) to 1e-5.  Weights after two Adam steps: the bounds of
+test_gpu_glue.py (<= 2% of weights flip their update direction, <= 10%
+norm-wise update error; the per-rank gradient sums run in another order).
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+WORKER = os.path.join(HERE, "ddp_product_worker.py")
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run_ranks(case, tmp_path, world=2, timeout=240):
+    port = _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK="0", LOCAL_WORLD_SIZE=str(world),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+        log = open(tmp_path / f"rank{r}.log", "w")
+        procs.append((subprocess.Popen([sys.executable, "-u", WORKER, case, str(tmp_path / f"rank{r}.pt")],
+                                       env=env, stdout=log, stderr=subprocess.STDOUT), log))
+    rcs = []
+    try:
+        for p, _ in procs:
+            rcs.append(p.wait(timeout=timeout))
+    finally:
+        for p, log in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+            log.close()
+    if any(rcs):
+        logs = "\n".join((tmp_path / f"rank{r}.log").read_text()[-3000:] for r in range(world))
+        raise AssertionError(f"ranks exited {rcs}:\n{logs}")
+    return [torch.load(tmp_path / f"rank{r}.pt", weights_only=True) for r in range(world)]
+
+
+def _update_check(p0, ref, got, lr):
+    """(#weights whose update moved > lr/2 from the reference's, #weights,
+    squared update error, squared reference update)."""
+    du_ref = ref.double() - p0.double()
+    du = got.double() - p0.double()
+    return (((du - du_ref).abs() > 0.5 * lr).sum().item(), du.numel(), ((du - du_ref) ** 2).sum().item(),
+            (du_ref ** 2).sum().item())
+
+
+@pytest.mark.parametrize("case", ["pqc", "gan"])
+def test_ddp_product_step_matches_single_process(gpu, case, tmp_path):
+    import ddp_product_worker as W
+    ranks = _run_ranks(case, tmp_path)
+    assert [tuple(r["rank_world"]) for r in ranks] == [(0, 2), (1, 2)]
+    assert all(r["deferred_pending"] == 0 for r in ranks)
+    # DDP keeps the replicas identical
+    for k, v in ranks[0]["params"].items():
+        assert torch.equal(v, ranks[1]["params"][k]), k
+    # initial weights: the same seeded construction, in this process
+    torch.manual_seed(0)
+    ref = W.run_case(case, gpu)
+    torch.cuda.synchronize()
+    for s, ref_s in enumerate(ref["steps"]):
+        for name, v in ref_s.items():
+            got = sum(r["steps"][s][name] for r in ranks) / len(ranks)
+            assert abs(got - v) <= 1e-5 * abs(v) + 1e-7, (case, s, name, got, v, [r["steps"][s][name] for r in ranks])
+    # the exchanged terms are load-bearing: without them the rank values would differ
+    if case == "pqc":
+        sc = [r["steps"][0]["train/spectral_convergence_loss"] for r in ranks]
+        assert sc[0] == pytest.approx(sc[1], rel=1e-6), sc  # global SC: the same scalar on both ranks
+    # weight updates of two Adam steps (lr: generator 1e-4, discriminator 2e-4)
+    p0 = _initial_params(case, gpu)
+    groups = {}
+    for k, v in ref["params"].items():
+        lr = 2e-4 if k.startswith("D.") else 1e-4
+        a, n, num, den = _update_check(p0[k], v, ranks[0]["params"][k], 2 * lr)
+        g = groups.setdefault(k.split(".")[0] if case == "gan" else "G", [0, 0, 0.0, 0.0])
+        g[0] += a
+        g[1] += n
+        g[2] += num
+        g[3] += den
+    for name, (flips, tot, num, den) in groups.items():
+        assert tot > 0 and flips <= 0.02 * tot, (case, name, flips, tot)
+        assert (num / den) ** 0.5 <= 0.10, (case, name, (num / den) ** 0.5)
+
+
+def _initial_params(case, dev):
+    """The seeded initial weights of run_case (same construction order)."""
+    import warnings
+    import ddp_product_worker as W
+    from sel import configs
+    torch.manual_seed(0)
+    if case == "pqc":
+        from models.autoencoder.AudioDec import Generator
+        cfg = configs.get("symAD_libritts_24000_hop300")
+        G = Generator(**dict(cfg["generator_params"], **W.GP))
+        return {k: p.detach().clone() for k, p in G.named_parameters()}
+    from models.autoencoder_without_PQC.AudioDec import Generator
+    from models.vocoder.HiFiGAN import Discriminator
+    cfg = configs.get("symAD_vctk_48000_hop300")
+    G = Generator(**dict(cfg["generator_params"], **W.GP))
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        Dm = Discriminator(**W.D_PARAMS)
+    out = {f"G.{k}": p.detach().clone() for k, p in G.named_parameters()}
+    out.update({f"D.{k}": p.detach().clone() for k, p in Dm.named_parameters()})
+    return out

@@ -143,6 +143,39 @@ def test_dconv_geometry_matches_torch_conv_lengths():
         assert any(0 <= s * (q0 + K - 1) + r + pad < Kt for r in range(s))
 
 
+def test_c5_mpd_layers_take_the_flat_warp_specialised_tiles():
+    """The launcher's own decision (sel_dconv_kernel, no GPU needed) for the MPD
+    chain at C5 sizes in the period_alloc layout: the wide layers (1-4 forward,
+    2-4 adjoint) run on k_conv_ws_bf16 with flat tiles across sequences
+    (SEL_DPATH_WS_FLAT), which tests/test_gpu_c5.py checks numerically; tune
+    key 22 = 1 moves them to per-sequence tiles."""
+    import ctypes
+    from oracle import ref_ops as R
+    from sel import _lib as L
+    from sel import dconvops as DC
+    specs = [DC.LayerSpec(ci, co, k, s, p, 1, lk) for (ci, co, k, s, p, lk) in R.period_discriminator_plan()]
+    lib = L.load()
+    for clips in (16, 32):
+        for p in (2, 3, 5, 7, 11):
+            Lv, Bs = (48000 + p - 1) // p, clips * p
+            geo = DC.chain_layout(specs, Lv, DC.period_alloc(Lv, specs))
+            fwd, adj = [], []
+            for li, (sp, (Ti, Ta, To, Toa)) in enumerate(zip(specs, geo)):
+                fwd.append(DC.kernel(DC._fwd_desc(sp, Bs, Ti, Ta, To, Toa, 0.1), torch.bfloat16))
+                adj.append(DC.kernel(DC._dgrad_desc(sp, Bs, Ta, To, Toa, 0.1, li > 0, T_in=Ti), torch.bfloat16))
+            assert [f[0] for f in fwd[1:5]] == ["ws_flat"] * 4, (clips, p, fwd)
+            assert [a[0] for a in adj[2:5]] == ["ws_flat"] * 3, (clips, p, adj)
+            assert fwd[4][1] == "k_conv_ws_bf16<5>" and fwd[1][1] == "k_conv_ws_bf16<2>"
+            prev = lib.sel_tune(22, 1)
+            try:
+                d = DC._fwd_desc(specs[2], Bs, *geo[2], 0.1)
+                assert DC.kernel(d, torch.bfloat16)[0] == "ws"
+            finally:
+                lib.sel_tune(22, prev)
+    # invalid descriptors are reported, not guessed
+    assert lib.sel_dconv_kernel(ctypes.byref(DC.DConvDesc()), 1, None, 0) == -1
+
+
 def test_trainer_checkpoint_roundtrip_with_reference_file(tmp_path):
     """TrainerGAN.save_checkpoint / load_checkpoint (trainerGAN.py:95-149): our
     trainer loads the checkpoint the REFERENCE trainer saved

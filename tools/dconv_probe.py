@@ -85,5 +85,5 @@ print(f"staged vs unstaged short wgrad: rel diff w {rel[0]:.2e} b {rel[1]:.2e} |
 for knob in (0, 1):
     lib.sel_tune(9, knob)
     print(f"layer {a} tune9={knob}: fwd {timed(fwd):.1f} us  wgrad {timed(wg):.1f} us  "
-          f"mfma/short/pf={lib.sel_dconv_uses_mfma(ctypes.byref(desc), 1)}", flush=True)
+          f"path={lib.sel_dconv_kernel(ctypes.byref(desc), 1, None, 0)}", flush=True)
 lib.sel_tune(9, 0)
