@@ -1404,7 +1404,8 @@ struct Ru32Stage {
     }
   }
   // raw != nullptr: rows [raw_off, raw_off + R) are also stored un-ELU'd into raw
-  __device__ __forceinline__ void store(__bf16* xs, int span, bool elu, __bf16* raw = nullptr, int raw_off = 0) {
+  __device__ __forceinline__ void store(__bf16* xs, int span, bool elu, __bf16* raw = nullptr, int raw_off = 0,
+                                        int pitch = F4_P) {
 #pragma unroll
     for (int u = 0; u < Ru32<R>::XV; ++u) {
       const int v = threadIdx.x + u * 256;
@@ -1415,7 +1416,7 @@ struct Ru32Stage {
       if (elu) {
         val = elu8(val);
       }
-      *reinterpret_cast<uint4*>(xs + row * F4_P + c) = val;
+      *reinterpret_cast<uint4*>(xs + row * pitch + c) = val;
     }
   }
 };
@@ -2353,6 +2354,228 @@ __device__ __forceinline__ bf16x8 tr_frag(const __bf16* p, int pitch) {
   const v4i16 hi = tr_read(p + 16 * pitch);
   const v8i16 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
   return __builtin_bit_cast(bf16x8, v);
+}
+
+// ---------------------------------------------------------------------------
+// Residual unit at 32 channels: backward AND both weight gradients in one
+// launch (the encoder's units, whose weights train; residual_unit.py:43-46,
+// conv_layer.py:139-142).  k_ru32_bwd's two phases (gh, then gx), plus:
+//  * ELU(bf16 h) of the tile rows -> LDS, from the h rows the gh phase already
+//    holds for ELU'(h); ELU(x) of the tile + its causal halo -> LDS, staged with
+//    g (the operands conv1 and the 1x1 consumed in the forward, same elu8);
+//  * after gx, the 7 conv1 taps and the 1x1 as eight 32x32 MFMA accumulators,
+//    two per wave (waves 0-2: taps 2w, 2w+1 sharing the gh operand; wave 3:
+//    tap 6 and the 1x1), reduced over the tile rows with transposing LDS reads
+//    (ds_read_b64_tr_b16: the k_wgrad3_bf16 operand scheme) and carried across
+//    all of the block's tiles;
+//  * one fp32 partial per block of each weight (+ the bias column sums of gh
+//    and g, waves 0 and 3), in the packed [N][K][C] layout that
+//    sel_wgrad_finish_many reduces in block order (deterministic).
+// HBM per row: reads g, h, x and writes gx; the unfused path also wrote gh and
+// re-read g, h, gh, x for the two weight-gradient launches (9 tensors).
+// The gh and gx phases are k_ru32_bwd's arithmetic exactly (same bits).
+// ---------------------------------------------------------------------------
+template <int R>
+struct Ru32W {
+  static constexpr int P = F4_P;   // g / gh rows (80 B: conflict-free ds_read_b128 of the gx phase)
+  static constexpr int PW = 32;    // ELU(x) / ELU(h) rows (64 B: conflict-free transposing reads)
+  static constexpr int SPAN = R + F4_HALOMAX;
+  static constexpr int NW1 = RU_C * RU_K * RU_C, NW2 = RU_C * RU_C;  // packed weight elements
+  static constexpr size_t LDS = size_t(2) * SPAN * P * 2 + size_t(SPAN + R) * PW * 2;
+  static_assert(R % 128 == 0, "ru32 tile rows");
+};
+
+template <int R>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_ru32_bwdw(Args a, const __bf16* __restrict__ g,
+                                                   const __bf16* __restrict__ h, const __bf16* __restrict__ x,
+                                                   const __bf16* __restrict__ wd1, const __bf16* __restrict__ wd2,
+                                                   __bf16* __restrict__ gx, float* __restrict__ part1,
+                                                   float* __restrict__ part2, int tiles_per_block) {
+  using G = Ru32W<R>;
+  constexpr int P = G::P, PW = G::PW;
+  extern __shared__ __align__(16) unsigned char smem[];
+  __bf16* const gs = reinterpret_cast<__bf16*>(smem);  // [SPAN][P]: g rows t0 ..
+  __bf16* const ghs = gs + G::SPAN * P;                // [SPAN][P]: gh rows t0 ..
+  __bf16* const xs = ghs + G::SPAN * P;                // [SPAN][PW]: ELU(x) rows t0 - halo ..
+  __bf16* const es = xs + G::SPAN * PW;                // [R][PW]: ELU(h) rows t0 ..
+  const int lane = threadIdx.x & 63, hl = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int halo = (RU_K - 1) * a.dil;
+  const int span = R + halo;
+  const int nsub = (span + 31) / 32;
+  const int tps = (a.T + R - 1) / R;
+
+  // weight-gradient jobs of this wave: job 0 = conv1 tap k0 (A = gh), job 1 =
+  // conv1 tap k0 + 1 (waves 0-2, same A) or the 1x1 (wave 3: A = g, B = ELU(h))
+  const int k0 = wave < 3 ? 2 * wave : 6;
+  floatx16 wacc[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) wacc[j][e] = 0.f;
+  float bsum = 0.f;  // wave 0: column sums of gh (conv1 bias), wave 3: of g (1x1 bias)
+  // transposing-read lane geometry (k_wgrad3_bf16): rows 4 hl + q and 8 + 4 hl + q, 4 columns at col
+  const int tq = (lane & 15) >> 2;
+  const int tcol = ((lane >> 4) & 1) * 16 + 4 * (lane & 3);
+  auto trfrag = [&](const __bf16* base, int pitch, int r0) {
+    const v4i16 lo = tr_read(base + (r0 + 4 * hl + tq) * pitch + tcol);
+    const v4i16 hi = tr_read(base + (r0 + 8 + 4 * hl + tq) * pitch + tcol);
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  };
+
+  int64_t tile0, tile_end;
+  if (ru_tiles((a.rows / a.T) * tps, tiles_per_block, tile0, tile_end)) {
+    bf16x8 wf[RU_K][2], w2f[1][2];
+    ru_wfrags<RU_K>(wd1, wf);
+    ru_wfrags<1>(wd2, w2f);
+
+    Ru32Stage<R> st, sx;
+    st.load(a, g, tile0 / tps, int(tile0 % tps) * R, 0, span);
+    sx.load(a, x, tile0 / tps, int(tile0 % tps) * R, -halo, span);
+    for (int64_t tile = tile0; tile < tile_end; ++tile) {
+      const int64_t b = tile / tps;
+      const int t0 = int(tile % tps) * R;
+      const int mrows = a.T - t0 < R ? a.T - t0 : R;
+      __syncthreads();  // every wave is done with the previous tile's rows
+      st.store(gs, span, false);
+      sx.store(xs, span, true, nullptr, 0, PW);
+      __syncthreads();
+      if (tile + 1 < tile_end) {
+        st.load(a, g, (tile + 1) / tps, int((tile + 1) % tps) * R, 0, span);
+        sx.load(a, x, (tile + 1) / tps, int((tile + 1) % tps) * R, -halo, span);
+      }
+      constexpr int NSUB_W = (G::SPAN / 32 + 3) / 4;
+      uint2 hpre[NSUB_W][4], xpre[Ru32<R>::TM][4];
+#pragma unroll
+      for (int j = 0; j < NSUB_W; ++j) {
+        const int ti = t0 + (wave + 4 * j) * 32 + (lane & 31);
+        const bool in = wave + 4 * j < nsub && ti < a.T;
+        const int64_t orow = (b * a.T + (in ? ti : 0)) * RU_C;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          hpre[j][q] = in ? *reinterpret_cast<const uint2*>(h + orow + 8 * q + 4 * hl) : make_uint2(0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < Ru32<R>::TM; ++i) {
+        const int lr = wave * (R / 4) + i * 32 + (lane & 31);
+        const bool in = lr < mrows;
+        const int64_t orow = (b * a.T + t0 + (in ? lr : 0)) * RU_C;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          xpre[i][q] = in ? *reinterpret_cast<const uint2*>(x + orow + 8 * q + 4 * hl) : make_uint2(0, 0);
+      }
+      // gh for rows t0 .. t0 + span (k_ru32_bwd); ELU(h) of the tile rows -> es
+#pragma unroll
+      for (int j = 0; j < NSUB_W; ++j) {
+        const int sb = wave + 4 * j;
+        if (sb >= nsub) break;
+        const int lr = sb * 32 + (lane & 31);
+        floatx16 acc;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+        const __bf16* gw = gs + lr * P + 8 * hl;
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w2f[0][c], *reinterpret_cast<const bf16x8*>(gw + 16 * c), acc, 0,
+                                                        0, 0);
+        float v[16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const __bf16* hv = reinterpret_cast<const __bf16*>(&hpre[j][q]);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[4 * q + e] = acc[4 * q + e] * elu_grad_fast(float(hv[e]));
+        }
+        bf16x8 ghf[2];
+        ru_acc_to_frags(v, ghf);
+        if (lr < span) {
+          *reinterpret_cast<bf16x8*>(ghs + lr * P + 8 * hl) = ghf[0];
+          *reinterpret_cast<bf16x8*>(ghs + lr * P + 16 + 8 * hl) = ghf[1];
+        }
+        if (sb < R / 32) {  // wave-uniform: a tile sub-tile (rows past T hold h = 0 -> ELU = 0)
+#pragma unroll
+          for (int qq = 0; qq < 2; ++qq) {
+            const uint4 e8 = elu8(make_uint4(hpre[j][2 * qq].x, hpre[j][2 * qq].y, hpre[j][2 * qq + 1].x,
+                                             hpre[j][2 * qq + 1].y));
+            *reinterpret_cast<uint2*>(es + lr * PW + 16 * qq + 4 * hl) = make_uint2(e8.x, e8.y);
+            *reinterpret_cast<uint2*>(es + lr * PW + 16 * qq + 8 + 4 * hl) = make_uint2(e8.z, e8.w);
+          }
+        }
+      }
+      __syncthreads();
+      // gx = conv1^T(gh) * ELU'(x) + g (k_ru32_bwd)
+#pragma unroll
+      for (int i = 0; i < Ru32<R>::TM; ++i) {
+        const int lr = wave * (R / 4) + i * 32 + (lane & 31);
+        if (__builtin_amdgcn_readfirstlane(wave * (R / 4) + i * 32) >= mrows) break;
+        floatx16 acc;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+        const __bf16* hw = ghs + lr * P + 8 * hl;
+#pragma unroll
+        for (int k = 0; k < RU_K; ++k)
+#pragma unroll
+          for (int c = 0; c < 2; ++c)
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[k][c],
+                                                          *reinterpret_cast<const bf16x8*>(hw + k * a.dil * P + 16 * c),
+                                                          acc, 0, 0, 0);
+        const bool valid = lr < mrows;
+        const int64_t orow = (b * a.T + t0 + (valid ? lr : 0)) * RU_C;
+        float v[16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint2 graw = *reinterpret_cast<const uint2*>(gs + lr * P + 8 * q + 4 * hl);
+          const __bf16* xv = reinterpret_cast<const __bf16*>(&xpre[i][q]);
+          const __bf16* gv = reinterpret_cast<const __bf16*>(&graw);
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            v[4 * q + e] = __fadd_rn(__fmul_rn(acc[4 * q + e], elu_grad_fast(float(xv[e]))), float(gv[e]));
+        }
+        bf16x8 of[2];
+        ru_acc_to_frags(v, of);
+        if (valid) {
+          *reinterpret_cast<bf16x8*>(gx + orow + 8 * hl) = of[0];
+          *reinterpret_cast<bf16x8*>(gx + orow + 16 + 8 * hl) = of[1];
+        }
+      }
+      // weight gradients over the tile rows (rows past T: g = 0 -> gh = 0)
+      const __bf16* b0p = xs + k0 * a.dil * PW;
+      const __bf16* b1p = wave < 3 ? b0p + a.dil * PW : es;
+#pragma unroll
+      for (int kh = 0; kh < R / 16; ++kh) {
+        const bf16x8 A0 = trfrag(ghs, P, kh * 16);
+        const bf16x8 B0 = trfrag(b0p, PW, kh * 16);
+        const bf16x8 B1 = trfrag(b1p, PW, kh * 16);
+        wacc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0, B0, wacc[0], 0, 0, 0);
+        if (wave < 3) {
+          wacc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0, B1, wacc[1], 0, 0, 0);
+          if (wave == 0) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) bsum += float(A0[e]);
+          }
+        } else {
+          const bf16x8 A1 = trfrag(gs, P, kh * 16);
+          wacc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1, B1, wacc[1], 0, 0, 0);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) bsum += float(A1[e]);
+        }
+      }
+    }
+  }
+  // this block's partials (zeros from a block without tiles): accumulator
+  // element r of lane l -> n = (r & 3) + 8 (r >> 2) + 4 hl, c = l & 31
+  const int nb = gridDim.x;
+  float* const p1 = part1 + int64_t(blockIdx.x) * G::NW1;
+  float* const p2 = part2 + int64_t(blockIdx.x) * G::NW2;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int n = (r & 3) + 8 * (r >> 2) + 4 * hl, c = lane & 31;
+    p1[(n * RU_K + k0) * RU_C + c] = wacc[0][r];
+    if (wave < 3) p1[(n * RU_K + k0 + 1) * RU_C + c] = wacc[1][r];
+    else p2[n * RU_C + c] = wacc[1][r];
+  }
+  bsum += __shfl_xor(bsum, 32, 64);
+  if (wave == 0 && lane < 32) part1[int64_t(nb) * G::NW1 + int64_t(blockIdx.x) * RU_C + lane] = bsum;
+  if (wave == 3 && lane < 32) part2[int64_t(nb) * G::NW2 + int64_t(blockIdx.x) * RU_C + lane] = bsum;
 }
 
 constexpr int WB_BM = 64;
@@ -3549,6 +3772,36 @@ int launch_ru32_bwd(const Args& a, const void* g, const void* h, const void* x, 
   return SEL_OK;
 }
 
+// fused 32-channel backward with the weight gradients: one block per partial
+template <int R>
+int ru32w_blocks(int64_t ntiles, int64_t& tpb) {
+  static const int64_t slots = [] {
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_ru32_bwdw<R>, 256, Ru32W<R>::LDS) != hipSuccess)
+      return int64_t(0);
+    return int64_t(cus) * per_cu / 8 * 8;
+  }();
+  const int64_t target = tune(35) > 0 ? tune(35) : (slots > 0 ? slots : 512);
+  tpb = std::max<int64_t>(1, (ntiles + target - 1) / target);
+  return int(((ntiles + tpb - 1) / tpb + 7) / 8 * 8);
+}
+
+template <int R>
+int launch_ru32_bwdw(const Args& a, const void* g, const void* h, const void* x, const void* wd1, const void* wd2,
+                     void* gx, float* part1, float* part2, int nsplit, hipStream_t s) {
+  const int64_t ntiles = (a.rows / a.T) * ((a.T + R - 1) / R);
+  int64_t tpb = 1;
+  const int nb = ru32w_blocks<R>(ntiles, tpb);
+  SEL_REQUIRE(nb == nsplit, SEL_ERR_ARG, "sel_resunit_bwd_wgrad: nsplit %d, this shape needs %d", nsplit, nb);
+  hipLaunchKernelGGL(k_ru32_bwdw<R>, dim3(unsigned(nb)), dim3(256), Ru32W<R>::LDS, s, a, static_cast<const __bf16*>(g),
+                     static_cast<const __bf16*>(h), static_cast<const __bf16*>(x), static_cast<const __bf16*>(wd1),
+                     static_cast<const __bf16*>(wd2), static_cast<__bf16*>(gx), part1, part2, int(tpb));
+  SEL_LAUNCH_CHECK();
+  return SEL_OK;
+}
+
 bool ru_fused_ok(const Args& a) {
   return (a.C == 32 || a.C == 64) && a.N == a.C && a.K == 7 && a.pad == (a.K - 1) * a.dil &&
          a.pad_mode == SEL_PAD_ZERO && a.in_elu == 1 && (a.K - 1) * a.dil <= F4_HALOMAX &&
@@ -3846,6 +4099,27 @@ int sel_resunit_bwd(const sel_conv_desc* d1, int dtype, const void* g, const voi
   if (a.C == 64)
     return launch_ru64_bwd<128>(a, g, h, x, wd1pack, wd2pack, gh, gx, reinterpret_cast<hipStream_t>(stream));
   return launch_ru32_bwd<128>(a, g, h, x, wd1pack, wd2pack, gh, gx, reinterpret_cast<hipStream_t>(stream));
+}
+
+int sel_resunit_wgrad_splits(const sel_conv_desc* d1, int dtype) {
+  if (int rc = check_desc(d1)) return rc;
+  const Args a = to_args(d1);
+  SEL_REQUIRE(dtype == SEL_BF16 && ru_fused_ok(a) && a.C == 32 && a.rows > 0, SEL_ERR_UNSUPPORTED,
+              "sel_resunit_bwd_wgrad: needs bf16, C = N = 32, K = 7, causal zero pad, ELU prologue");
+  int64_t tpb = 1;
+  return ru32w_blocks<128>((a.rows / a.T) * ((a.T + 127) / 128), tpb);
+}
+
+int sel_resunit_bwd_wgrad(const sel_conv_desc* d1, int dtype, const void* g, const void* h, const void* x,
+                          const void* wd1pack, const void* wd2pack, void* gx, float* part1, float* part2, int nsplit,
+                          sel_stream_t stream) {
+  if (int rc = check_desc(d1)) return rc;
+  const Args a = to_args(d1);
+  SEL_REQUIRE(dtype == SEL_BF16 && ru_fused_ok(a) && a.C == 32 && a.rows > 0, SEL_ERR_UNSUPPORTED,
+              "sel_resunit_bwd_wgrad: needs bf16, C = N = 32, K = 7, causal zero pad, ELU prologue");
+  SEL_REQUIRE(g && h && x && wd1pack && wd2pack && gx && part1 && part2, SEL_ERR_ARG, "null pointer");
+  return launch_ru32_bwdw<128>(a, g, h, x, wd1pack, wd2pack, gx, part1, part2, nsplit,
+                               reinterpret_cast<hipStream_t>(stream));
 }
 
 size_t sel_conv_wgrad_workspace(const sel_conv_desc* d) {

@@ -47,6 +47,8 @@ SIGNATURES = {
     "sel_conv_fwd": (I32, [P, I32, I32, P, P, P, P, P, P, P]),
     "sel_resunit_fwd": (I32, [P, I32, P, P, P, P, P, P, P, P]),
     "sel_resunit_bwd": (I32, [P, I32, P, P, P, P, P, P, P, P]),
+    "sel_resunit_wgrad_splits": (I32, [P, I32]),
+    "sel_resunit_bwd_wgrad": (I32, [P, I32, P, P, P, P, P, P, P, P, I32, P]),
     "sel_conv_wgrad_workspace": (SZ, [P]),
     "sel_conv_wgrad": (I32, [P, I32, P, P, P, P, P, SZ, P]),
     "sel_conv_wgrad_partials": (I32, [P, I32, P, P, I32, P, SZ, P, P]),

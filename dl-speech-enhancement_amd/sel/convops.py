@@ -359,6 +359,23 @@ def _can_defer(params):
     return True
 
 
+def _queue_flush():
+    """Arrange the batched reduction at the end of the running backward pass
+    (False outside one: then nothing may be deferred)."""
+    try:
+        torch.autograd.Variable._execution_engine.queue_callback(_flush_deferred)
+    except RuntimeError:  # not inside a backward pass
+        return False
+    return True
+
+
+def _defer(job, ws, params, gw, gb, st):
+    refs = [(weakref.ref(params[0]), gw.data_ptr())] + \
+        ([(weakref.ref(params[1]), gb.data_ptr())] if gb is not None else [])
+    with _DEFER_LOCK:
+        _DEFERRED.append((job, ws, refs, st.value))
+
+
 def _flush_deferred():
     with _DEFER_LOCK:
         pending = list(_DEFERRED)
@@ -393,24 +410,16 @@ def wgrad_torch(desc, gout, x, kind, w_shape, stride, want_bias, params=None):
         cin, cout, k = w_shape
     else:
         cout, cin, k = w_shape
-    if params is not None and len(params) == 1 + int(gb is not None) and _can_defer(params):
-        try:
-            torch.autograd.Variable._execution_engine.queue_callback(_flush_deferred)
-        except RuntimeError:  # not inside a backward pass
-            pass
-        else:
-            ns = ctypes.c_int()
-            st = L.stream()
-            L.call("sel_conv_wgrad_partials", ctypes.byref(desc), _code(x.dtype), L.ptr(gout), L.ptr(x),
-                   int(want_bias), L.ptr(ws), ws.numel(), ctypes.byref(ns), st)
-            job = _WgradJob(ws.data_ptr(), gw.data_ptr(), gb.data_ptr() if gb is not None else None,
-                            desc.N * desc.K * desc.C, ns.value, desc.N, desc.bias_period, kind, cout, cin, k,
-                            stride)
-            refs = [(weakref.ref(params[0]), gw.data_ptr())] + \
-                ([(weakref.ref(params[1]), gb.data_ptr())] if gb is not None else [])
-            with _DEFER_LOCK:
-                _DEFERRED.append((job, ws, refs, st.value))
-            return gw, gb
+    if params is not None and len(params) == 1 + int(gb is not None) and _can_defer(params) and _queue_flush():
+        ns = ctypes.c_int()
+        st = L.stream()
+        L.call("sel_conv_wgrad_partials", ctypes.byref(desc), _code(x.dtype), L.ptr(gout), L.ptr(x),
+               int(want_bias), L.ptr(ws), ws.numel(), ctypes.byref(ns), st)
+        job = _WgradJob(ws.data_ptr(), gw.data_ptr(), gb.data_ptr() if gb is not None else None,
+                        desc.N * desc.K * desc.C, ns.value, desc.N, desc.bias_period, kind, cout, cin, k,
+                        stride)
+        _defer(job, ws, params, gw, gb, st)
+        return gw, gb
     L.call("sel_conv_wgrad_unpacked", ctypes.byref(desc), _code(x.dtype), L.ptr(gout), L.ptr(x), kind, cout, cin,
            k, stride, L.ptr(gw), L.ptr(gb), L.ptr(ws), ws.numel(), L.stream())
     return gw, gb
@@ -542,12 +551,55 @@ def resunit_bwd(d1, gf, h, xf, wd1, wd2, want_gh):
     return gx, gh
 
 
-def _ru_bwd_meta(d1, xf, want_gh):
-    """Algorithmic bytes: read g, h, x once, write gx (and gh)."""
+def _ru_bwd_meta(d1, xf, want_gh, wgrad=False):
+    """Algorithmic bytes: read g, h, x once, write gx (and gh); flops of the two
+    adjoints (and of the two weight gradients)."""
     es = xf.element_size()
     nbytes = (4 + int(want_gh)) * d1.rows * d1.C * es
-    flops = 2.0 * d1.rows * d1.N * d1.C * (d1.K + 1)
+    flops = 2.0 * d1.rows * d1.N * d1.C * (d1.K + 1) * (2 if wgrad else 1)
+    if wgrad:
+        return "k_ru32_bwdw<128>", nbytes, flops
     return ("k_ru32_bwd<128>" if d1.C == 32 else "k_ru64_bwd<128>"), nbytes, flops
+
+
+# fused 32-channel backward with both weight gradients (SEL_RU_WGRAD=0: off)
+RU_WGRAD = os.environ.get("SEL_RU_WGRAD", "1") != "0"
+
+
+def resunit_bwd_wgrad(d1, gf, h, xf, wd1, wd2, s1, s2, want_b1, want_b2, params1, params2):
+    """gx and both weight gradients of a 32-channel residual unit: ONE launch
+    (k_ru32_bwdw: gh, gx, and per-block partials of conv1 and the 1x1), then the
+    block-order reduction into the torch layouts, deferred to the end of the
+    backward like wgrad_torch's when the parameters allow it (params1 / params2:
+    the (weight, bias) leaves receiving gw1, gb1 / gw2, gb2, or None)."""
+    lib = L.lib()
+    ns = lib.sel_resunit_wgrad_splits(ctypes.byref(d1), _code(xf.dtype))
+    if ns <= 0:
+        raise L.SelError(f"sel_resunit_wgrad_splits failed ({ns}): {lib.sel_last_error().decode()}")
+    N = d1.N
+    nw1, nw2 = N * d1.K * d1.C, N * N
+    n1 = ns * (nw1 + N)
+    ws = torch.empty(n1 + ns * (nw2 + N), dtype=torch.float32, device=xf.device)
+    gx = torch.empty_like(xf)
+    st = L.stream()
+    L.call("sel_resunit_bwd_wgrad", ctypes.byref(d1), _code(xf.dtype), L.ptr(gf), L.ptr(h), L.ptr(xf), L.ptr(wd1),
+           L.ptr(wd2), L.ptr(gx), ctypes.c_void_p(ws.data_ptr()), ctypes.c_void_p(ws.data_ptr() + 4 * n1), ns, st,
+           meta=lambda: _ru_bwd_meta(d1, xf, False, wgrad=True))
+    out, jobs = [], []
+    for (shape, want_b, params, off, nw, k) in ((s1, want_b1, params1, 0, nw1, d1.K), (s2, want_b2, params2, n1, nw2, 1)):
+        gw = torch.empty(shape, dtype=torch.float32, device=xf.device)
+        gb = torch.empty(N, dtype=torch.float32, device=xf.device) if want_b else None
+        job = _WgradJob(ws.data_ptr() + 4 * off, gw.data_ptr(), gb.data_ptr() if gb is not None else None, nw, ns, N,
+                        N, PACK_FWD, shape[0], shape[1], k, 1)
+        if params is not None and len(params) == 1 + int(want_b) and _can_defer(params) and _queue_flush():
+            _defer(job, ws, params, gw, gb, st)
+        else:
+            jobs.append(job)
+        out += [gw, gb]
+    if jobs:
+        arr = (_WgradJob * len(jobs))(*jobs)
+        L.call("sel_wgrad_finish_many", ctypes.cast(arr, ctypes.c_void_p), len(jobs), st)
+    return (gx, *out)
 
 
 def resunit_fwd(d1, xf, wp1, b1, wp2, b2):
@@ -607,7 +659,19 @@ class ResidualUnitFn(torch.autograd.Function):
         gf = g.view(B * T, C)
         xf = x.view(B * T, C)
         need_w1 = ctx.needs_input_grad[1] or ctx.needs_input_grad[2]
+        need_w2 = ctx.needs_input_grad[3] or ctx.needs_input_grad[4]
         gx = None
+        pr = ctx.prefs
+        if (RU_WGRAD and ctx.needs_input_grad[0] and need_w1 and need_w2 and d1.C == 32
+                and ru_bwd_fused_ok(d1, x.dtype)):
+            # one launch: gx and both weight gradients (k_ru32_bwdw)
+            want_b1 = d1.bias_period > 0 and ctx.needs_input_grad[2]
+            want_b2 = d2.bias_period > 0 and ctx.needs_input_grad[4]
+            p1 = _live(pr[0], pr[1] if want_b1 else None) if ctx.needs_input_grad[1] else None
+            p2 = _live(pr[2], pr[3] if want_b2 else None) if ctx.needs_input_grad[3] else None
+            gx, gw1, gb1, gw2, gb2 = resunit_bwd_wgrad(d1, gf, h, xf, wd1, wd2, s1, s2, want_b1, want_b2, p1, p2)
+            return (gx.view(B, T, C), gw1 if ctx.needs_input_grad[1] else None, gb1,
+                    gw2 if ctx.needs_input_grad[3] else None, gb2, None)
         if ctx.needs_input_grad[0] and ru_bwd_fused_ok(d1, x.dtype):
             # one launch: gh = (W2^T g) * ELU'(h) and gx = g + conv_adjoint(gh) * ELU'(x)
             gx, gh = resunit_bwd(d1, gf, h, xf, wd1, wd2, need_w1)
@@ -616,7 +680,6 @@ class ResidualUnitFn(torch.autograd.Function):
             # dL/dh = (W2^T g) * ELU'(h)
             gh = prim(d2.adjoint(), gf, wd2, aux=h)
         gw1 = gb1 = gw2 = gb2 = None
-        pr = ctx.prefs
         if ctx.needs_input_grad[3] or ctx.needs_input_grad[4]:
             want_b = d2.bias_period > 0 and ctx.needs_input_grad[4]
             params = _live(pr[2], pr[3] if want_b else None) if ctx.needs_input_grad[3] else None

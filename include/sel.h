@@ -182,6 +182,17 @@ int sel_resunit_fwd(const sel_conv_desc* d1, int dtype, const void* x, const voi
  * dgrad-packed weights (sel_pack_dgrad); gh may be NULL. */
 int sel_resunit_bwd(const sel_conv_desc* d1, int dtype, const void* g, const void* h, const void* x,
                     const void* wd1pack, const void* wd2pack, void* gh, void* gx, sel_stream_t stream);
+/* The same backward WITH both weight gradients of the unit, in one launch (the
+ * residual units whose weights train; 32 channels): gx as sel_resunit_bwd, and
+ * per-block fp32 partials of conv1 (part1: nsplit x 32*7*32 packed [N][K][C],
+ * then nsplit x 32 bias column sums of gh) and of the 1x1 (part2: nsplit x
+ * 32*32, then nsplit x 32 of g).  nsplit = sel_resunit_wgrad_splits(d1, dtype)
+ * (a negative code for an unsupported shape); reduce the partials with
+ * sel_wgrad_finish_many (kind SEL_PACK_FWD, k 7 and 1). */
+int sel_resunit_wgrad_splits(const sel_conv_desc* d1, int dtype);
+int sel_resunit_bwd_wgrad(const sel_conv_desc* d1, int dtype, const void* g, const void* h, const void* x,
+                          const void* wd1pack, const void* wd2pack, void* gx, float* part1, float* part2,
+                          int nsplit, sel_stream_t stream);
 /* weight/bias gradient of the same primitive: gwpack[N][K][C] (fp32) and, when
  * gbias != NULL, gbias[bias_period] = sum over rows and phases of gout. */
 size_t sel_conv_wgrad_workspace(const sel_conv_desc* d);
