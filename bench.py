@@ -433,55 +433,50 @@ def roofline(cfg, timer, dom, B, steps):
     return r
 
 
-def stft_kernel_roofline(dev):
+def stft_kernel_roofline(dev, B=2048):
     """North-star STFT target: the |X| kernel (sel_stft_mag_fwd, the a1 row) at
-    SURVEY §8d's HBM-measurement size (B = 512 x 1 s, beyond the 256 MB Infinity
-    Cache), 1024/120/600, timed with HIP events on its launch stream, against
-    the 8 TB/s spec and against this box's measured copy bandwidth."""
+    1024/120/600 on B = 2048 x 1 s (0.2 GB in, 0.85 GB out: a working set 4x the
+    256 MB Infinity Cache, so nothing is served from it across launches), timed
+    with a HIP event pair around each launch on its stream, against the 8 TB/s
+    spec and against two measured copy rates of this box: a float4 stream-copy
+    kernel (sel_probe_copy_f4, 4 x 16-B loads in flight per thread, one resident
+    round of workgroups) and torch's copy_, each over 1 GiB buffers."""
     from sel import _lib as L
-    B, T, (n, h, w) = 512, SR, STFT_RES[0]
+    T, (n, h, w) = SR, STFT_RES[0]
     F, K = 1 + T // h, n // 2 + 1
     x = 0.1 * torch.randn(B, T, device=dev)
     win = torch.hann_window(w, device=dev)
     mag = torch.empty(B, F, K, device=dev)
     src = torch.empty(2 ** 28, device=dev)
     dst = torch.empty_like(src)
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
 
-    def timed(fn, iters=10):
+    def timed(fn, iters=5):
+        """mean of per-launch event pairs (back-to-back Python launches leave host
+        gaps between short kernels that one pair around a loop would count)"""
         for _ in range(2):
             fn()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(iters):
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(iters)]
+        for e0, e1 in ev:
+            e0.record()
             fn()
-        e1.record()
+            e1.record()
         torch.cuda.synchronize()
-        return e0.elapsed_time(e1) / iters * 1e-3
+        return sum(e0.elapsed_time(e1) for e0, e1 in ev) / iters * 1e-3
 
-    t_copy = timed(lambda: dst.copy_(src))
-    copy_gbs = 2 * src.numel() * 4 / t_copy / 1e9
-
-    def launch():
-        L.call("sel_stft_mag_fwd", L.ptr(x), B, T, n, h, w, L.ptr(win), 1e-7, L.ptr(mag), L.stream())
-
-    # average launch duration: a HIP event pair around each of ten launches
-    # (back-to-back Python launches leave host gaps between these ~80 us kernels,
-    # which an event pair around the whole loop would count)
-    for _ in range(2):
-        launch()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(10)]
-    for e0, e1 in ev:
-        e0.record()
-        launch()
-        e1.record()
-    torch.cuda.synchronize()
-    t = sum(e0.elapsed_time(e1) for e0, e1 in ev) / len(ev) * 1e-3
+    copy_bytes = 2 * src.numel() * 4
+    t_torch = timed(lambda: dst.copy_(src))
+    t_f4 = timed(lambda: L.call("sel_probe_copy_f4", L.ptr(src), L.ptr(dst), src.numel() // 4, 8 * cus, L.stream()))
+    torch_gbs, f4_gbs = copy_bytes / t_torch / 1e9, copy_bytes / t_f4 / 1e9
+    del src, dst
+    t = timed(lambda: L.call("sel_stft_mag_fwd", L.ptr(x), B, T, n, h, w, L.ptr(win), 1e-7, L.ptr(mag), L.stream()))
     nbytes = 4 * B * (T + F * K)
     gbs = nbytes / t / 1e9
     return {"kernel": "k_stft_mag_fwd<10>", "shape": f"B={B} x {T}, n_fft/hop/win {n}/{h}/{w}",
             "avg_launch_us": round(t * 1e6, 1), "alg_bytes": nbytes, "achieved": round(gbs, 1), "unit": "GB/s",
-            "frac_of_spec": round(gbs / HBM_PEAK_GBS, 4), "measured_copy_GBs": round(copy_gbs, 1),
-            "frac_of_measured": round(gbs / copy_gbs, 4)}
+            "frac_of_spec": round(gbs / HBM_PEAK_GBS, 4),
+            "copy_f4_GBs": round(f4_gbs, 1), "frac_of_copy_f4": round(gbs / f4_gbs, 4),
+            "torch_copy_GBs": round(torch_gbs, 1), "frac_of_torch_copy": round(gbs / torch_gbs, 4)}
 
 
 def launch_cmd(n, port, argv):

@@ -555,7 +555,6 @@ constexpr int WS_SPR = WS_CK / 8;             // 16-B slots per LDS row
 constexpr int WS_XROWS = WS_BM + F4_HALOMAX;  // staged input rows per chunk (multiple of WS_RPI)
 constexpr int WS_CMAX = 4096;                 // input channels the zero source covers
 constexpr int WS_EP = WS_BN + 4;              // fp32 epilogue tile pitch (conflict-free 16-B writes)
-constexpr int kWsK2Default = 0;               // K = 2 generator layers on the ws kernel (tune key 27 flips bits)
 
 __device__ __attribute__((aligned(64))) __bf16 g_ws_zero[WS_CMAX];
 
@@ -1791,6 +1790,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     store();
     __syncthreads();
     if (tile + 1 < tile_end) load(tile + 1);
+    // h rows of a gh unit (the ELU'(h) factor), one unit ahead of its MFMAs
+    auto load_h = [&](int unit, uint2 (&hq)[4]) {
+      const int sb = unit >> 1, sl = unit & 1;
+      const int ti = t0 + sb * 32 + (lane & 31);
+      const bool inside = unit < 2 * nsub && ti < a.T;
+      const int64_t orow = (b * a.T + (inside ? ti : 0)) * C + sl * 32;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        hq[q] = inside ? *reinterpret_cast<const uint2*>(h + orow + 8 * q + 4 * hl) : make_uint2(0, 0);
+    };
+    uint2 hnext[4];
+    load_h(wave, hnext);
     // x rows of this wave's gx sub-tiles (the ELU'(x) factor), requested before
     // the gh phase so their HBM latency hides behind it
     uint2 xpre[G::TM][4];
@@ -1815,7 +1826,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
       const int64_t orow = (b * a.T + (inside ? ti : 0)) * C + sl * 32;
       uint2 hq[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) hq[q] = inside ? *reinterpret_cast<const uint2*>(h + orow + 8 * q + 4 * hl) : make_uint2(0, 0);
+      for (int q = 0; q < 4; ++q) hq[q] = hnext[q];
+      if (uu + 1 < G::UPW) load_h(unit + 4, hnext);
       // the slice-sl weights of the 1x1 adjoint: rows n = sl*32 + (lane & 31)
       bf16x8 w2q[C / 16];
       {
@@ -2136,12 +2148,12 @@ __global__ __launch_bounds__(256) void k_conv_c1_bf16(Args a, const __bf16* __re
 // each block walks its contiguous range of sample-aligned 256-row tiles with the
 // samples staged in LDS, then reduces its lanes (shuffles, LDS over waves) into
 // one partial per block.
+template <int NG>  // 1, 2, 4 or 8 n-groups (N / 8)
 __global__ __launch_bounds__(256) void k_wgrad_c1_bf16(Args a, const __bf16* __restrict__ gout,
                                                        const __bf16* __restrict__ in, int64_t tiles_per_split,
                                                        float* __restrict__ part, float* __restrict__ bpart) {
   __shared__ float xs[C1_TR + C1_HALO];
   __shared__ float red[4][C1_NMAX * (C1_KMAX + 1)];
-  const int NG = a.N / 8;  // 1, 2, 4 or 8 n-groups
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int grp = tid % NG, rl = tid / NG, nrl = 256 / NG;
   const int tps = (a.T + C1_TR - 1) / C1_TR;
@@ -2172,10 +2184,25 @@ __global__ __launch_bounds__(256) void k_wgrad_c1_bf16(Args a, const __bf16* __r
       pre[u] = ok && a.in_elu ? elu_fast(v) : v;
     }
   };
-  if (tb < te) fetch(tb);
-  constexpr int MAXR = C1_TR / 32;  // rows per thread at NG = 8
-  for (int64_t tile = tb; tile < te; ++tile) {
+  constexpr int MAXR = C1_TR * NG / 256;  // rows per thread and tile
+  // this tile's gout rows (next tile's: requested before this tile's FMAs)
+  uint4 gq[MAXR];
+  auto fetch_g = [&](int64_t tile) {
     const int64_t b = tile / tps;
+    const int t0 = int(tile % tps) * C1_TR;
+    const int rows = a.T - t0 < C1_TR ? a.T - t0 : C1_TR;
+#pragma unroll
+    for (int j = 0; j < MAXR; ++j) {
+      const int r = rl + j * nrl;
+      if (j * nrl < C1_TR && r < rows)
+        gq[j] = *reinterpret_cast<const uint4*>(gout + (b * a.T + t0 + r) * a.N + grp * 8);
+    }
+  };
+  if (tb < te) {
+    fetch(tb);
+    fetch_g(tb);
+  }
+  for (int64_t tile = tb; tile < te; ++tile) {
     const int t0 = int(tile % tps) * C1_TR;
     __syncthreads();
 #pragma unroll
@@ -2184,19 +2211,18 @@ __global__ __launch_bounds__(256) void k_wgrad_c1_bf16(Args a, const __bf16* __r
     __syncthreads();
     if (tile + 1 < te) fetch(tile + 1);
     const int rows = a.T - t0 < C1_TR ? a.T - t0 : C1_TR;
-    uint4 gq[MAXR];
+    uint4 gc[MAXR];
 #pragma unroll
-    for (int j = 0; j < MAXR; ++j) {
-      const int r = rl + j * nrl;
-      if (j * nrl < C1_TR && r < rows)
-        gq[j] = *reinterpret_cast<const uint4*>(gout + (b * a.T + t0 + r) * a.N + grp * 8);
-    }
+    for (int j = 0; j < MAXR; ++j) gc[j] = gq[j];
+    if (tile + 1 < te) fetch_g(tile + 1);
+    __bf16 gvs[MAXR][8];
+#pragma unroll
+    for (int j = 0; j < MAXR; ++j) *reinterpret_cast<uint4*>(gvs[j]) = gc[j];
 #pragma unroll
     for (int j = 0; j < MAXR; ++j) {
       const int r = rl + j * nrl;
       if (j * nrl >= C1_TR || r >= rows) break;
-      __bf16 gv[8];
-      *reinterpret_cast<uint4*>(gv) = gq[j];
+      const __bf16* gv = gvs[j];
       float xv[C1_KMAX];
 #pragma unroll
       for (int k = 0; k < C1_KMAX; ++k) xv[k] = k < a.K ? xs[r + k * a.dil] : 0.f;
@@ -2976,18 +3002,35 @@ __global__ __launch_bounds__(256) void k_wgrad3_bf16(Args a, const __bf16* __res
       const __bf16* gb = base + buf * (GS + XS) + (bcol >> 5) * (W2_BM * 32) + (bcol & 31);
       for (int r = brow; r < W2_BM; r += 256 / NB) bsum += float(gb[r * 32]);
     }
-    for (int kh = 0; kh < RROWS / 16; ++kh) {
+    // 16-row steps, software-pipelined: the next step's fragments are read while
+    // this step's MFMAs run (sched_barrier-pinned; the compiler's counted
+    // lgkmcnt waits then cover only the older reads).  Steps per tile: 8 / RG (even)
+    auto frag = [&](const __bf16* p) {
+      const v4i16 lo = tr_read(p), hi = tr_read(p + 8 * 32);
+      return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+    };
+    bf16x8 fA[2], fB[2][MAXT];
+    auto fetch = [&](int kh, int q) __attribute__((always_inline)) {
       const int R = (rg * RROWS + kh * 16) * 32 + lrow;
-      const v4i16 a0 = tr_read(g + R);
-      const v4i16 a1 = tr_read(g + R + 8 * 32);
-      const bf16x8 A = __builtin_bit_cast(bf16x8, __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7));
+      fA[q] = frag(g + R);
 #pragma unroll
-      for (int j = 0; j < MAXT; ++j) {
-        const v4i16 b0 = tr_read(x + xoff[j] + R);
-        const v4i16 b1 = tr_read(x + xoff[j] + R + 8 * 32);
-        const bf16x8 Bf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7));
-        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, Bf, acc[j], 0, 0, 0);
-      }
+      for (int j = 0; j < MAXT; ++j) fB[q][j] = frag(x + xoff[j] + R);
+    };
+    auto mma = [&](int q) __attribute__((always_inline)) {
+#pragma unroll
+      for (int j = 0; j < MAXT; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fA[q], fB[q][j], acc[j], 0, 0, 0);
+    };
+    const int nkh = RROWS / 16;
+    fetch(0, 0);
+    for (int kh = 0; kh < nkh; kh += 2) {
+      fetch(kh + 1, 1);
+      __builtin_amdgcn_sched_barrier(0);
+      mma(0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (kh + 2 < nkh) fetch(kh + 2, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      mma(1);
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
 
@@ -3437,25 +3480,20 @@ int launch_fwd4(const Args& a, const void* in, const void* wp, const float* bias
   return SEL_OK;
 }
 
-// tune key 32: 1 = four consumer waves of 128 x 64 (NC = 4) instead of eight of 64 x 64
+// (measured and dropped in round 2: four consumer waves of 128 x 64, two
+// chunks per barrier for the two-tap layers)
 template <int KT, typename TO>
 int launch_ws(const Args& a, const void* in, const void* wp, const float* bias, const void* aux, const void* res,
               void* out, hipStream_t s) {
-  // tune key 33 = 1: two chunks per barrier for the two-tap layers (8 MFMAs per
-  // wave per chunk); measured neutral on C5 (44.38/44.43 vs 44.23/44.28 ms
-  // median, alternating in one call), so off
-  constexpr int CPB = KT == 2 ? 2 : 1;
-  const bool cpb2 = CPB == 2 && tune(33) == 1;
-  const size_t lds = ws_lds_bytes(KT, cpb2 ? 2 : 1);
+  const size_t lds = ws_lds_bytes(KT, 1);
   const int64_t tiles = (a.rows / a.T) * ((a.T + WS_BM - 1) / WS_BM);
   const int ncol = a.N / WS_BN;
   if (tiles == 0) return SEL_OK;
   const bool xcd = ncol > 1 && tune(8) == 0 && tiles * ncol < (int64_t(1) << 31);
   const dim3 grid = xcd ? dim3(unsigned(tiles * ncol)) : dim3(unsigned(tiles), unsigned(ncol));
-  const bool nc4 = tune(32) == 1 && !cpb2;
-  auto kern = cpb2 ? k_conv_ws_bf16<KT, TO, 8, CPB> : nc4 ? k_conv_ws_bf16<KT, TO, 4, 1> : k_conv_ws_bf16<KT, TO, 8, 1>;
+  auto kern = k_conv_ws_bf16<KT, TO, 8, 1>;
   SEL_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
-  hipLaunchKernelGGL(kern, grid, dim3(nc4 ? 512 : 768), lds, s, a, static_cast<const __bf16*>(in),
+  hipLaunchKernelGGL(kern, grid, dim3(768), lds, s, a, static_cast<const __bf16*>(in),
                      static_cast<const __bf16*>(wp), bias, static_cast<const TO*>(aux), static_cast<const TO*>(res),
                      static_cast<TO*>(out), xcd ? ncol : 0, tune(13));
   SEL_LAUNCH_CHECK();
@@ -3465,11 +3503,8 @@ int launch_ws(const Args& a, const void* in, const void* wp, const float* bias, 
 // the warp-specialised kernel's legal shapes: K in {3, 7}, 128-multiple N,
 // 16-multiple C within the zero source, halo within the staged span, the
 // 4-slot ring within 160 KB
-// tune key 27 bit 0: also the K = 2 layers (the transposed convs' 2-tap form)
-// at >= 16 k rows, bit 1: and the 512 -> 256 one at 5120 rows
 bool ws_ok(const Args& a) {
-  const bool k2 = a.K == 2 && (kWsK2Default ^ tune(27)) & 1;
-  return (a.K == 3 || a.K == 7 || k2) && a.N % WS_BN == 0 && a.C % WS_CK == 0 && a.C <= WS_CMAX &&
+  return (a.K == 3 || a.K == 7) && a.N % WS_BN == 0 && a.C % WS_CK == 0 && a.C <= WS_CMAX &&
          (a.K - 1) * a.dil <= F4_HALOMAX && ws_lds_bytes(a.K) <= 160 * 1024;
 }
 
@@ -3481,18 +3516,6 @@ int launch_ws_k(const Args& a, const void* in, const void* wp, const float* bias
                     : launch_ws<2, TO>(a, in, wp, bias, aux, res, out, s);
 }
 
-// wide outputs over few rows (the decoder's first transposed conv and the
-// encoder's last strided conv's dgrad at 80 frames x 64 clips: N' = 1280 over
-// 5120 rows): 128 x 128 tiles re-read the rows for 4x fewer column tiles than
-// 128 x 32 (tune key 29 bit 0 flips kWideSmallDefault)
-constexpr int kWideSmallDefault = 0;
-bool wide_small(const Args& a) {
-  return ((kWideSmallDefault ^ tune(29)) & 1) && a.rows < 8192 && a.N >= 512 && a.N % 128 == 0 && a.K <= 3;
-}
-
-bool ws_small_k2(const Args& a) {
-  return a.K == 2 && a.N >= 512 && ((kWsK2Default ^ tune(27)) & 2) && ws_ok(a);
-}
 
 // Variant the dispatcher picks for a bf16 forward launch (see fwd4_variant);
 // -1 when the generic (non-pipelined) kernel is used.
@@ -3500,15 +3523,11 @@ int fwd4_choice(const Args& a) {
   const int v = tune(0);
   if (!((a.C % CK) == 0 && (a.K - 1) * a.dil <= F4_HALOMAX && a.K <= 8 && (v == 0 || v > 20))) return -1;
   if (v > 20 && (v != 27 || ws_ok(a))) return v;
-  if (ws_small_k2(a)) return 27;
-  if (wide_small(a)) return 25;
   if (a.N <= 32 || (a.N % 64) != 0 || a.rows < 8192) return 22;
   if (a.N >= 256 && a.K == 1) return 26;
   if (a.N >= 256 && a.rows >= 16384) return ws_ok(a) ? 27 : 24;
   if (a.N <= 64 || a.rows < 65536) return 23;
-  if (a.N == 128 && ws_ok(a) && tune(17) != 2 &&
-      (tune(17) == 1 || a.K == 3 || (a.K == 7 && a.pad == 0 && !a.in_elu)))
-    return 27;
+  if (a.N == 128 && ws_ok(a) && (a.K == 3 || (a.K == 7 && a.pad == 0 && !a.in_elu))) return 27;
   if (a.N == 128 && a.K > 1 && a.pad == 0 && !a.in_elu) return 22;
   return 24;
 }
@@ -3531,8 +3550,6 @@ int fwd4_variant(int v, const Args& a, const void* in, const void* wp, const flo
   // heuristic from tools/conv_bench.py on the C3 layer shapes (profiles/r1_conv_bench.md):
   // narrow / non-64-multiple outputs and short row counts favour 128x32 tiles
   // (more workgroups in flight); wide layers 128x64 or 256x64.
-  if (ws_small_k2(a)) return launch_ws_k<TO>(a, in, wp, bias, aux, res, out, s);
-  if (wide_small(a)) return launch_fwd4<128, 128, 2, KMAX, TO>(a, in, wp, bias, aux, res, out, s);
   if (a.N <= 32 || (a.N % 64) != 0 || a.rows < 8192)
     return launch_fwd4<128, 32, 4, KMAX, TO>(a, in, wp, bias, aux, res, out, s);
   // 256-wide 1x1 (RU256 1x1 fwd 27.5 -> 20.9 us, dgrad 22.5 -> 19.2): 64x128 tiles
@@ -3550,9 +3567,8 @@ int fwd4_variant(int v, const Args& a, const void* in, const void* wp, const flo
   // 128-column tile: no input re-read across column tiles) for the k7 dgrads
   // (RU128 d9: 63.6 -> 53.2 us) and the k3 convs (down1: 49.3 -> 44.1 us), not
   // the k7 forwards with their ELU'd 54-row halo (48.6 -> 52.9 us);
-  // tools/conv_bench.py.  Tune key 17: 1 = every 128-wide layer, 2 = none.
-  if (a.N == 128 && ws_ok(a) && tune(17) != 2 &&
-      (tune(17) == 1 || a.K == 3 || (a.K == 7 && a.pad == 0 && !a.in_elu)))
+  // tools/conv_bench.py.
+  if (a.N == 128 && ws_ok(a) && (a.K == 3 || (a.K == 7 && a.pad == 0 && !a.in_elu)))
     return launch_ws_k<TO>(a, in, wp, bias, aux, res, out, s);
   // 128-wide k7 dgrad at 2000 samples (pad 0, no input ELU): 128x32 tiles (76.5 -> 62.6 us)
   if (a.N == 128 && a.K > 1 && a.pad == 0 && !a.in_elu)
@@ -4177,7 +4193,9 @@ int wgrad_impl(const sel_conv_desc* d, int dtype, const void* gout, const void* 
   float* part = static_cast<float*>(ws);
   float* bpart = gbias ? part + size_t(p.nsplit) * d->N * d->K * d->C : nullptr;
   if (d->rows > 0 && p.mode == 4) {
-    hipLaunchKernelGGL(k_wgrad_c1_bf16, dim3(unsigned(p.nsplit)), dim3(256), 0, s, a,
+    auto kc1 = d->N == 8 ? k_wgrad_c1_bf16<1> : d->N == 16 ? k_wgrad_c1_bf16<2>
+               : d->N == 32 ? k_wgrad_c1_bf16<4> : k_wgrad_c1_bf16<8>;
+    hipLaunchKernelGGL(kc1, dim3(unsigned(p.nsplit)), dim3(256), 0, s, a,
                        static_cast<const __bf16*>(gout), static_cast<const __bf16*>(in), int64_t(p.tiles_per_split),
                        part, bpart);
     SEL_LAUNCH_CHECK();

@@ -659,7 +659,7 @@ __global__ __launch_bounds__(256) void k_dconv_short(D d, const T* __restrict__ 
 template <typename T, int K, int NR>
 __global__ __launch_bounds__(256) void k_dconv_shortx(D d, const T* __restrict__ x, const T* __restrict__ wp,
                                                       const float* __restrict__ bias, const T* __restrict__ aux,
-                                                      const T* __restrict__ res, T* __restrict__ out, bool prefetch) {
+                                                      const T* __restrict__ res, T* __restrict__ out) {
   constexpr int KR = K * NR, RW = 8, XW = (RW + K - 1) * NR;
   extern __shared__ float sh[];
   float* const wsh = sh;            // [KR][Ng]
@@ -671,32 +671,17 @@ __global__ __launch_bounds__(256) void k_dconv_shortx(D d, const T* __restrict__
   const int n8 = d.Ng / 8, RL = 256 / n8, RB = RL * RW;
   const int rl = threadIdx.x / n8, n0 = (threadIdx.x - rl * n8) * 8;
   const int tps = (d.Tvo + RB - 1) / RB, ntiles = d.B * tps;
-  // a window of at most one value per thread (the MSD's k15 1 -> 128 conv: 142)
-  // is fetched into a register one tile ahead, so the fetch latency overlaps
-  // the current tile's FMAs instead of sitting between two barriers
-  // (tune key 34 = 1; measured neutral on C5: 44.45/44.40 vs 44.42/44.41 ms
-  // median, alternating in one call, so off)
+  // (a one-tile-ahead register fetch of the window was measured neutral on C5
+  // in round 2 and dropped)
   const int np = (RB + K - 1) * NR;
-  const bool pf = np <= 256 && prefetch;
-  auto fetch = [&](int tile) {
-    const int b = tile / tps, j0 = (tile - b * tps) * RB, p = threadIdx.x;
-    const int t = j0 + d.q0 + p / NR;
-    return (p < np && t >= 0 && t < d.Tv) ? to_f(x[(int64_t(b) * d.Tvs + t) * NR + p % NR]) : 0.f;
-  };
-  float nxt = pf && int(blockIdx.x) < ntiles ? fetch(blockIdx.x) : 0.f;
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int b = tile / tps, j0 = (tile - b * tps) * RB;
     __syncthreads();  // the previous tile's window reads are done (and the weights are in)
-    if (pf) {
-      if (int(threadIdx.x) < np) xs[threadIdx.x] = nxt;
-    } else {
-      for (int p = threadIdx.x; p < np; p += 256) {
-        const int t = j0 + d.q0 + p / NR;
-        xs[p] = (t >= 0 && t < d.Tv) ? to_f(x[(int64_t(b) * d.Tvs + t) * NR + p % NR]) : 0.f;
-      }
+    for (int p = threadIdx.x; p < np; p += 256) {
+      const int t = j0 + d.q0 + p / NR;
+      xs[p] = (t >= 0 && t < d.Tv) ? to_f(x[(int64_t(b) * d.Tvs + t) * NR + p % NR]) : 0.f;
     }
     __syncthreads();
-    if (pf && tile + int(gridDim.x) < ntiles) nxt = fetch(tile + gridDim.x);
     const int jr = rl * RW;
     if (j0 + jr >= d.Tvo) continue;
     float xw[XW];
@@ -1094,18 +1079,34 @@ __global__ __launch_bounds__(256) void k_dwgrad_w3(D d, const __bf16* __restrict
     if (tile + 1 < te) load(tile + 1);
     const __bf16* g = base + buf * (GS + XS) + nt * (W3_BM * 32);
     const __bf16* xx = base + buf * (GS + XS) + GS;
-    for (int kh = 0; kh < RROWS / 16; ++kh) {
+    // 16-row steps, software-pipelined as k_wgrad3_bf16 (conv.hip): the next
+    // step's fragments are read while this step's MFMAs run
+    auto frag = [&](const __bf16* p) {
+      const v4i16 lo = tr_read(p), hi = tr_read(p + 8 * 32);
+      return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+    };
+    bf16x8 fA[2], fB[2][MAXT];
+    auto fetch = [&](int kh, int q) __attribute__((always_inline)) {
       const int R = (rg * RROWS + kh * 16) * 32 + lrow;
-      const v4i16 a0 = tr_read(g + R);
-      const v4i16 a1 = tr_read(g + R + 8 * 32);
-      const bf16x8 A = __builtin_bit_cast(bf16x8, __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7));
+      fA[q] = frag(g + R);
 #pragma unroll
-      for (int j = 0; j < MAXT; ++j) {
-        const v4i16 b0 = tr_read(xx + xoff[j] + R);
-        const v4i16 b1 = tr_read(xx + xoff[j] + R + 8 * 32);
-        const bf16x8 Bf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7));
-        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, Bf, acc[j], 0, 0, 0);
-      }
+      for (int j = 0; j < MAXT; ++j) fB[q][j] = frag(xx + xoff[j] + R);
+    };
+    auto mma = [&](int q) __attribute__((always_inline)) {
+#pragma unroll
+      for (int j = 0; j < MAXT; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fA[q], fB[q][j], acc[j], 0, 0, 0);
+    };
+    const int nkh = RROWS / 16;
+    fetch(0, 0);
+    for (int kh = 0; kh < nkh; kh += 2) {
+      fetch(kh + 1, 1);
+      __builtin_amdgcn_sched_barrier(0);
+      mma(0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (kh + 2 < nkh) fetch(kh + 2, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      mma(1);
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
 
@@ -1984,8 +1985,7 @@ int launch_short(const sel_dconv_desc* d, const void* x, const void* wp, const f
     if (lds > 64 * 1024)
       SEL_HIP(hipFuncSetAttribute((const void*)kx, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
     hipLaunchKernelGGL(kx, dim3(blocks), dim3(256), lds, s, *d, static_cast<const T*>(x), static_cast<const T*>(wp),
-                       bias, static_cast<const T*>(aux), static_cast<const T*>(res), static_cast<T*>(out),
-                       tune(34) == 1);
+                       bias, static_cast<const T*>(aux), static_cast<const T*>(res), static_cast<T*>(out));
     SEL_LAUNCH_CHECK();
     return SEL_OK;
   }
@@ -2062,10 +2062,8 @@ FwdPlan plan_fwd(const sel_dconv_desc* d, int dtype) {
   int bm, bn;
   // narrow groups: 32-wide tiles; short sequences / few rows: 64-row tiles
   if (width <= 32) {
-    // tune key 28 bit 1: one tile size up (256 / 512 rows)
-    const bool up = bf && (tune(28) & 2);
     bn = 32;
-    bm = rows * d->G < 131072 ? (up ? 256 : 128) : (up ? 512 : 256);
+    bm = rows * d->G < 131072 ? 128 : 256;
   } else if (rows * d->G * (width / 64) < 65536) {
     bm = 64, bn = 64;
   } else {
@@ -2103,8 +2101,7 @@ int dispatch_fwd(const sel_dconv_desc* d, const void* x, const void* wp, const f
   // k_dconv_mfma / k_dconv_gpf (launch_mfma makes the same gpf choice)
   if (p.bn == 32) {
     if (p.bm == 128) return launch_mfma<T, 128, 32>(d, x, wp, bias, aux, res, out, s);
-    if (p.bm == 256) return launch_mfma<T, 256, 32>(d, x, wp, bias, aux, res, out, s);
-    return launch_mfma<T, 512, 32>(d, x, wp, bias, aux, res, out, s);
+    return launch_mfma<T, 256, 32>(d, x, wp, bias, aux, res, out, s);
   }
   if (p.bm == 64) return launch_mfma<T, 64, 64>(d, x, wp, bias, aux, res, out, s);
   if (p.bm == 256) return launch_mfma<T, 256, 64>(d, x, wp, bias, aux, res, out, s);

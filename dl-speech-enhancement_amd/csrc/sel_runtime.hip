@@ -115,3 +115,34 @@ extern "C" int sel_probe_buffer_b64(const float* x, int n, int mode, float* out,
   SEL_LAUNCH_CHECK();
   return SEL_OK;
 }
+
+// ---------------------------------------------------------------------------
+// Measurement denominator for the STFT roofline (bench.py stft_kernel): a
+// float4 stream copy, 4 independent 16-B loads in flight per thread, one
+// resident round of workgroups striding over the buffer (the guide's
+// "measured copy" shape), so a kernel's GB/s can be set against what this box's
+// HBM sustains for a plain read + write of the same bytes.
+// ---------------------------------------------------------------------------
+namespace {
+__global__ __launch_bounds__(256) void k_probe_copy_f4(const float4* __restrict__ src, float4* __restrict__ dst,
+                                                       int64_t n) {
+  const int64_t stride = int64_t(gridDim.x) * 256 * 4;
+  for (int64_t i = int64_t(blockIdx.x) * 256 * 4 + threadIdx.x; i < n; i += stride) {
+    float4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (i + u * 256 < n) v[u] = src[i + u * 256];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (i + u * 256 < n) dst[i + u * 256] = v[u];
+  }
+}
+}  // namespace
+
+extern "C" int sel_probe_copy_f4(const void* src, void* dst, int64_t n16, int blocks, sel_stream_t stream) {
+  SEL_REQUIRE(src && dst && n16 > 0 && blocks > 0, SEL_ERR_ARG, "bad copy probe arguments");
+  hipLaunchKernelGGL(k_probe_copy_f4, dim3(unsigned(blocks)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     static_cast<const float4*>(src), static_cast<float4*>(dst), n16);
+  SEL_LAUNCH_CHECK();
+  return SEL_OK;
+}

@@ -784,6 +784,17 @@ constexpr int mag_block() {
   return (SEL_STFT_VMA && Geo<LOGN>::LPF <= 64) ? SEL_STFT_BS : 256;
 }
 
+// |X| leaves as streaming (non-temporal) stores: the magnitudes (4/5 of the
+// kernel's bytes) are written once and not read back by this launch, so they
+// should not displace the signal rows in the caches (SEL_STFT_NT=0: plain stores)
+#ifndef SEL_STFT_NT
+#define SEL_STFT_NT 1
+#endif
+__device__ __forceinline__ void mag_store(float* p, float v) {
+  if constexpr (SEL_STFT_NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
 template <int LOGN, int BS = mag_block<LOGN>()>
 __global__ __launch_bounds__(BS) SEL_FFT_OCC void k_stft_mag_fwd(const float* __restrict__ x, FrameArgs a,
                                                      const float* __restrict__ window, float floor_,
@@ -840,10 +851,10 @@ __global__ __launch_bounds__(BS) SEL_FFT_OCC void k_stft_mag_fwd(const float* __
         float* out = mag + int64_t(cur.fr) * K;
 #pragma unroll
         for (int q = 0; q < H; ++q) {
-          out[l + G::LPF * q] = clamp_sqrt(pwr[q], floor_);
-          out[G::M - l - G::LPF * q] = clamp_sqrt(pwr[H + q], floor_);
+          mag_store(&out[l + G::LPF * q], clamp_sqrt(pwr[q], floor_));
+          mag_store(&out[G::M - l - G::LPF * q], clamp_sqrt(pwr[H + q], floor_));
         }
-        if (l == 0) out[G::M / 2] = clamp_sqrt(pmid, floor_);
+        if (l == 0) mag_store(&out[G::M / 2], clamp_sqrt(pmid, floor_));
       }
       if (pf) vm_wait_raw<(SEL_STFT_ABL & 1) ? 0 : kVmStores>(raw);
       u = un;

@@ -49,6 +49,10 @@ int sel_tune(int key, int value);
  * mode 0: elements taken as scalars, mode 1: __builtin_bit_cast of the vector
  * elements (miscompiled by ROCm 7.2 clang: element 0 twice) */
 int sel_probe_buffer_b64(const float* x, int n, int mode, float* out, sel_stream_t stream);
+/* measurement: copy n16 16-byte elements (float4) src -> dst with `blocks`
+ * workgroups striding over the buffer (the HBM copy-rate denominator of the
+ * STFT roofline in bench.py) */
+int sel_probe_copy_f4(const void* src, void* dst, int64_t n16, int blocks, sel_stream_t stream);
 
 /* ---- STFT magnitude: losses/stft_loss.py:19-35 (stft) ------------------
  * x (B,T) -> mag (B, F, K), F = 1 + T/hop, K = n_fft/2 + 1.
