@@ -1079,34 +1079,18 @@ __global__ __launch_bounds__(256) void k_dwgrad_w3(D d, const __bf16* __restrict
     if (tile + 1 < te) load(tile + 1);
     const __bf16* g = base + buf * (GS + XS) + nt * (W3_BM * 32);
     const __bf16* xx = base + buf * (GS + XS) + GS;
-    // 16-row steps, software-pipelined as k_wgrad3_bf16 (conv.hip): the next
-    // step's fragments are read while this step's MFMAs run
-    auto frag = [&](const __bf16* p) {
-      const v4i16 lo = tr_read(p), hi = tr_read(p + 8 * 32);
-      return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-    };
-    bf16x8 fA[2], fB[2][MAXT];
-    auto fetch = [&](int kh, int q) __attribute__((always_inline)) {
+    for (int kh = 0; kh < RROWS / 16; ++kh) {
       const int R = (rg * RROWS + kh * 16) * 32 + lrow;
-      fA[q] = frag(g + R);
+      const v4i16 a0 = tr_read(g + R);
+      const v4i16 a1 = tr_read(g + R + 8 * 32);
+      const bf16x8 A = __builtin_bit_cast(bf16x8, __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7));
 #pragma unroll
-      for (int j = 0; j < MAXT; ++j) fB[q][j] = frag(xx + xoff[j] + R);
-    };
-    auto mma = [&](int q) __attribute__((always_inline)) {
-#pragma unroll
-      for (int j = 0; j < MAXT; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fA[q], fB[q][j], acc[j], 0, 0, 0);
-    };
-    const int nkh = RROWS / 16;
-    fetch(0, 0);
-    for (int kh = 0; kh < nkh; kh += 2) {
-      fetch(kh + 1, 1);
-      __builtin_amdgcn_sched_barrier(0);
-      mma(0);
-      __builtin_amdgcn_sched_barrier(0);
-      if (kh + 2 < nkh) fetch(kh + 2, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      mma(1);
-      __builtin_amdgcn_sched_barrier(0);
+      for (int j = 0; j < MAXT; ++j) {
+        const v4i16 b0 = tr_read(xx + xoff[j] + R);
+        const v4i16 b1 = tr_read(xx + xoff[j] + R + 8 * 32);
+        const bf16x8 Bf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7));
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, Bf, acc[j], 0, 0, 0);
+      }
     }
   }
 
