@@ -3918,7 +3918,9 @@ WgPlan wgrad_plan(const sel_conv_desc* d, int mode) {
     if (tiles_per_wave(p.nt, p.ct) > 4 && p.ct == 2) p.ct = 1;
     if (tiles_per_wave(p.nt, p.ct) > 4 && p.nt == 2) p.nt = 1;
     const int tpw = tiles_per_wave(p.nt, p.ct);
-    p.maxt = tpw <= 1 ? 1 : (tpw <= 2 ? 2 : (tpw <= 4 ? 4 : 8));
+    // exact per-wave tile count (the strided k3 layers at 64 input channels per
+    // block: 3 pairs per wave, which the 4-slot form ran with a never-stored slot)
+    p.maxt = tpw <= 4 ? tpw : 8;
     bn = 32 * p.nt;
     bc = 32 * p.ct;
   } else {
@@ -3960,6 +3962,7 @@ hipError_t launch_wgrad3(const WgPlan& p, const Args& a, const __bf16* gout, con
   }
   if (p.maxt == 1) SEL_WG3(1)
   else if (p.maxt == 2) SEL_WG3(2)
+  else if (p.maxt == 3) SEL_WG3(3)
   else if (p.maxt == 4) SEL_WG3(4)
   else SEL_WG3(8)
 #undef SEL_WG3

@@ -41,3 +41,21 @@ class Discriminator(nn.Module):
         if channel != 1:
             x = x.reshape(batch * channel, 1, time)
         return self.msd(x) + self.mpd(x)
+
+    def stash_first_half(self, x):
+        """No-grad forward of B clips x into per-layer buffers sized for 2B clips,
+        kept for forward_second_half (train_denoise.DenoiseStep: the generator
+        step's D(target) is the D step's real half); returns x's outputs."""
+        batch, channel, time = x.size()
+        if channel != 1:
+            x = x.reshape(batch * channel, 1, time)
+        return self.msd.stash_first_half(x) + self.mpd.stash_first_half(x)
+
+    def forward_second_half(self, x):
+        """forward(torch.cat([stashed clips, x])) without recomputing the stashed
+        half: the same outputs (the kernels compute every output row the same
+        way for any batch), one autograd graph over all 2B clips."""
+        batch, channel, time = x.size()
+        if channel != 1:
+            x = x.reshape(batch * channel, 1, time)
+        return self.msd.forward_second_half(x) + self.mpd.forward_second_half(x)

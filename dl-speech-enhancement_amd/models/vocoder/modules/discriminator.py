@@ -104,22 +104,50 @@ class HiFiGANPeriodDiscriminator(nn.Module):
             self._plan = [DC.LayerSpec(*s) for s in self._specs]
         return self._plan
 
-    def forward(self, x):
-        """x (B, in_channels, T) -> list of each layer's output (B, C, T/p, p), the
-        last flattened to (B, T'/p * p) (discriminator.py:110-137)."""
+    def _x0(self, x):
+        """(B, 1, T) -> folded sequences (B*p, L_alloc, 1) in the compute dtype, L_valid."""
         b, c, t = x.shape
         if c != 1:
             raise NotImplementedError("the HIP period discriminator takes 1-channel input (in_channels=1)")
-        specs = self.plan()
         p = self.period
         Lv = (t + p - 1) // p
-        x2 = x.reshape(b, t).float()
-        seqs = DC.MpdFoldFn.apply(x2, p, DC.period_alloc(Lv, specs))
-        x0 = CO.cast(seqs, CO.compute_dtype()).unsqueeze(-1)
-        outs = list(DC.ChainFn.apply(x0, Lv, specs, self.slope, self.use_weight_norm, "period", b, p,
-                                     getattr(self, "_frozen", False), *self._params()))
+        seqs = DC.MpdFoldFn.apply(x.reshape(b, t).float(), p, DC.period_alloc(Lv, self.plan()))
+        return CO.cast(seqs, CO.compute_dtype()).unsqueeze(-1), Lv
+
+    def _outs(self, views):
+        outs = list(views)
         outs[-1] = torch.flatten(outs[-1], 1, -1)
         return outs
+
+    def forward(self, x):
+        """x (B, in_channels, T) -> list of each layer's output (B, C, T/p, p), the
+        last flattened to (B, T'/p * p) (discriminator.py:110-137)."""
+        x0, Lv = self._x0(x)
+        return self._outs(DC.ChainFn.apply(x0, Lv, self.plan(), self.slope, self.use_weight_norm, "period",
+                                           x.shape[0], self.period, getattr(self, "_frozen", False), None,
+                                           *self._params()))
+
+    @torch.no_grad()
+    def stash_first_half(self, x):
+        """forward(x) of B clips into buffers sized for 2B (the first half),
+        kept for forward_second_half; returns the B clips' outputs (no graph)."""
+        x0h, Lv = self._x0(x)
+        n = x0h.shape[0]
+        x0 = torch.empty((2 * n,) + tuple(x0h.shape[1:]), dtype=x0h.dtype, device=x0h.device)
+        x0[:n] = x0h
+        bufs, geo = DC.chain_forward(x0, Lv, self.plan(), self.slope, self.use_weight_norm, self._params(), 0, n)
+        self._stash = (x0, bufs, n, Lv)
+        b = x.shape[0]
+        return self._outs(DC._view(y[:n], "period", b, g[2], self.period) for y, g in zip(bufs, geo))
+
+    def forward_second_half(self, x):
+        """forward(cat[stashed clips, x]) with the stashed half not recomputed."""
+        x0, bufs, n, Lv = self._stash
+        self._stash = None
+        x0[n:] = self._x0(x)[0].detach()
+        return self._outs(DC.ChainFn.apply(x0, Lv, self.plan(), self.slope, self.use_weight_norm, "period",
+                                           2 * x.shape[0], self.period, getattr(self, "_frozen", False),
+                                           (n, bufs), *self._params()))
 
     def apply_weight_norm(self):
         def _apply_weight_norm(m):
@@ -150,6 +178,12 @@ class HiFiGANMultiPeriodDiscriminator(nn.Module):
 
     def forward(self, x):
         return [f(x) for f in self.discriminators]
+
+    def stash_first_half(self, x):
+        return [f.stash_first_half(x) for f in self.discriminators]
+
+    def forward_second_half(self, x):
+        return [f.forward_second_half(x) for f in self.discriminators]
 
 
 class HiFiGANScaleDiscriminator(nn.Module):
@@ -210,14 +244,34 @@ class HiFiGANScaleDiscriminator(nn.Module):
             self._plan = [DC.LayerSpec(*s) for s in self._specs]
         return self._plan
 
-    def forward(self, x):
-        """x (B, 1, T) -> list of each layer's output (B, C, T_l) (:337-352)."""
+    def _x0(self, x):
         b, c, t = x.shape
         if c != 1:
             raise NotImplementedError("the HIP scale discriminator takes 1-channel input (in_channels=1)")
-        x0 = CO.cast(x.reshape(b, t, 1).float(), CO.compute_dtype())
-        return list(DC.ChainFn.apply(x0, t, self.plan(), self.slope, False, "scale", b, 1,
-                                     getattr(self, "_frozen", False), *self._params()))
+        return CO.cast(x.reshape(b, t, 1).float(), CO.compute_dtype())
+
+    def forward(self, x):
+        """x (B, 1, T) -> list of each layer's output (B, C, T_l) (:337-352)."""
+        return list(DC.ChainFn.apply(self._x0(x), x.shape[2], self.plan(), self.slope, False, "scale", x.shape[0],
+                                     1, getattr(self, "_frozen", False), None, *self._params()))
+
+    @torch.no_grad()
+    def stash_first_half(self, x):
+        """as HiFiGANPeriodDiscriminator.stash_first_half"""
+        x0h = self._x0(x)
+        b, t = x.shape[0], x.shape[2]
+        x0 = torch.empty((2 * b,) + tuple(x0h.shape[1:]), dtype=x0h.dtype, device=x0h.device)
+        x0[:b] = x0h
+        bufs, geo = DC.chain_forward(x0, t, self.plan(), self.slope, False, self._params(), 0, b)
+        self._stash = (x0, bufs, b, t)
+        return [DC._view(y[:b], "scale", b, g[2], 1) for y, g in zip(bufs, geo)]
+
+    def forward_second_half(self, x):
+        x0, bufs, b, t = self._stash
+        self._stash = None
+        x0[b:] = self._x0(x).detach()
+        return list(DC.ChainFn.apply(x0, t, self.plan(), self.slope, False, "scale", 2 * b, 1,
+                                     getattr(self, "_frozen", False), (b, bufs), *self._params()))
 
     def apply_weight_norm(self):
         pass  # reference :354-362 matches Conv2d only
@@ -255,12 +309,24 @@ class HiFiGANMultiScaleDiscriminator(nn.Module):
         self._pool = (downsample_pooling_params.get("kernel_size"), downsample_pooling_params.get("stride"),
                       downsample_pooling_params.get("padding", 0))
 
-    def forward(self, x):
+    def _scales(self, x, fn):
         outs = []
         b = x.shape[0]
         k, s, p = self._pool
         s = k if s is None else s
         for f in self.discriminators:
-            outs += [f(x)]
+            outs += [fn(f, x)]
             x = DC.AvgPoolFn.apply(x.reshape(b, -1).float(), k, s, p).unsqueeze(1)
         return outs
+
+    def forward(self, x):
+        return self._scales(x, lambda f, v: f(v))
+
+    def stash_first_half(self, x):
+        with torch.no_grad():
+            return self._scales(x, lambda f, v: f.stash_first_half(v))
+
+    def forward_second_half(self, x):
+        with torch.no_grad():  # the waveform (a detached prediction) takes no gradient
+            pooled = self._scales(x, lambda f, v: v)
+        return [f.forward_second_half(v) for f, v in zip(self.discriminators, pooled)]

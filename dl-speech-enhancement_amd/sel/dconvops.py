@@ -286,23 +286,49 @@ def _view(y, kind, B, T, p):
     return y.view(B, p, La, C)[:, :, :T, :].permute(0, 3, 2, 1)
 
 
+def chain_forward(x0, T0, specs, slope, wn, params, lo=0, hi=None, bufs=None):
+    """The layers of one sub-discriminator over the sequences [lo, hi) of x0
+    (Bs, T0_alloc, 1) into the per-layer buffers `bufs` (allocated for all Bs
+    sequences when None; other sequences are left as they are).  Returns
+    (bufs, geo).  The kernels compute each output row the same way whatever
+    the launch's sequence count, so a chain run in two halves gives the bits of
+    one run over the whole batch."""
+    dtype = x0.dtype
+    Bs = x0.shape[0]
+    hi = Bs if hi is None else hi
+    geo = chain_layout(specs, T0, x0.shape[1])
+    if bufs is None:
+        bufs = [torch.empty(Bs, g[3], sp.cout, dtype=dtype, device=x0.device) for sp, g in zip(specs, geo)]
+    x = x0
+    for li, (sp, g) in enumerate(zip(specs, geo)):
+        w, wg, b = _layer_params(params, li, wn)
+        T_in, T_alloc_in, T_out, T_out_alloc = g
+        d = _fwd_desc(sp, hi - lo, T_in, T_alloc_in, T_out, T_out_alloc, slope)
+        y = bufs[li]
+        prim(d, x[lo:hi], pack(sp, w, wg, dtype, 0), y[lo:hi],
+             bias=b.detach().float().contiguous() if b is not None else None, tag=f"_fwd{li}")
+        x = y
+    return bufs, geo
+
+
 class ChainFn(torch.autograd.Function):
     """One sub-discriminator: x0 (Bs, T0_alloc, 1) in the compute dtype with T0
     valid rows -> the reference-layout views of every layer's output.
 
-    forward(ctx, x0, T0, specs, slope, wn, kind, B, p, frozen, *params): params
-    per layer are (w, bias) or, with weight norm (wn), (weight_v, weight_g, bias);
-    frozen = the parameters are constants here (no weight-gradient kernels, no
-    gradient returned for them)."""
+    forward(ctx, x0, T0, specs, slope, wn, kind, B, p, frozen, pre, *params):
+    params per layer are (w, bias) or, with weight norm (wn), (weight_v,
+    weight_g, bias); frozen = the parameters are constants here (no
+    weight-gradient kernels, no gradient returned for them); pre = None, or
+    (lo, bufs): the sequences below lo are already in bufs (chain_forward run
+    earlier with the same weights) and only [lo, Bs) is computed — the backward
+    still covers all Bs sequences."""
 
     @staticmethod
-    def forward(ctx, x0, T0, specs, slope, wn, kind, B, p, frozen, *params):
+    def forward(ctx, x0, T0, specs, slope, wn, kind, B, p, frozen, pre, *params):
         L.need_device(x0)
         ctx.set_materialize_grads(False)  # unused feature maps arrive as None
         dtype = x0.dtype
-        Bs = x0.shape[0]
         per = 3 if wn else 2
-        bufs, views, geo = [], [], []
         # every stale packed form of the chain in one launch (forward forms, and
         # the adjoint forms when a gradient can flow back through the chain)
         adj = any(ctx.needs_input_grad)
@@ -311,18 +337,9 @@ class ChainFn(torch.autograd.Function):
             w, wg, _b = _layer_params(params, li, wn)
             items += [(sp, w, wg, dtype, m) for m in ((0, 1) if adj else (0,))]
         DPACKS.prefetch(items)
-        x = x0
-        for li, (sp, g) in enumerate(zip(specs, chain_layout(specs, T0, x0.shape[1]))):
-            w, wg, b = _layer_params(params, li, wn)
-            T_in, T_alloc_in, T_out, T_out_alloc = g
-            d = _fwd_desc(sp, Bs, T_in, T_alloc_in, T_out, T_out_alloc, slope)
-            wp = pack(sp, w, wg, dtype, 0)
-            y = torch.empty(Bs, T_out_alloc, sp.cout, dtype=dtype, device=x0.device)
-            prim(d, x, wp, y, bias=b.detach().float().contiguous() if b is not None else None, tag=f"_fwd{li}")
-            bufs.append(y)
-            views.append(_view(y, kind, B, T_out, p))
-            geo.append(g)
-            x = y
+        lo, pb = pre if pre is not None else (0, None)
+        bufs, geo = chain_forward(x0, T0, specs, slope, wn, params, lo, None, pb)
+        views = [_view(y, kind, B, g[2], p) for y, g in zip(bufs, geo)]
         ctx.save_for_backward(x0, *bufs, *params)
         ctx.cfg = (specs, slope, wn, geo, len(bufs), kind, B, p, per, frozen)
         return tuple(views)
@@ -334,7 +351,7 @@ class ChainFn(torch.autograd.Function):
         x0, bufs, params = saved[0], saved[1:1 + nl], saved[1 + nl:]
         dtype = x0.dtype
         Bs = x0.shape[0]
-        npre = 9  # leading non-param inputs of forward
+        npre = 10  # leading non-param inputs of forward
         pgrads = [None] * len(params)
 
         def ext(li):
@@ -381,7 +398,7 @@ class ChainFn(torch.autograd.Function):
             if li == 0:
                 gx0 = gin
             gpre = gin
-        return (gx0, None, None, None, None, None, None, None, None, *pgrads)
+        return (gx0, None, None, None, None, None, None, None, None, None, *pgrads)
 
 
 def _layer_params(params, li, wn):

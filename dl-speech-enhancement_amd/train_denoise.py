@@ -17,7 +17,9 @@ Differences, all outside the numerics of a step:
     the global batch;
   * GAN mode (epoch >= epoch_to_enable_discriminator): the HiFi-GAN MSD + MPD
     discriminator runs on the HIP discriminator kernels; the discriminator step
-    scores D(target) and D(pred) in one pass over the concatenated batch.
+    scores D(target) and D(pred) as one batch (one backward), its real half
+    taken from the generator step's D(target) (same weights, same clips) in a
+    single process.
 
 Reference quirks reproduced on purpose: ``noise_dropout`` runs after mixing and
 never changes the model input (:313-319); validation also increments ``steps``
@@ -127,10 +129,19 @@ class DenoiseStep:
             # D only carries the gradient to the generator here (its own grads
             # are discarded by the D step's zero_grad): constant parameters, and
             # the unwrapped module so no DDP reducer waits for them
-            with frozen_parameters(_unwrap(self.model["discriminator"])) as D:
+            Dm = _unwrap(self.model["discriminator"])
+            with frozen_parameters(Dm) as D:
                 p_ = D(pred)
+            self._stashed = None
+            if self._reuse_real():
+                # D(target) is also the real half of the D step (:160): D's weights
+                # change only in that step's Adam update.  Computed once, into the
+                # D step's buffers (Discriminator.stash_first_half)
+                p = Dm.stash_first_half(target)
+                self._stashed = target.shape[0]
+            else:
                 with torch.no_grad():
-                    p = D(target)
+                    p = Dm(target)
             adv_loss = c["lambda_adv"] * self.criterion["gen_adv"](pred)  # :147 passes the waveform (quirk)
             feat_loss = c["lambda_feat_match"] * self.criterion["feat_match"](p_, p)
         return mel_loss + adv_loss + feat_loss + snr_loss, (("mel_loss", mel_loss), ("adv_loss", adv_loss),
@@ -142,11 +153,23 @@ class DenoiseStep:
         forward under DDP)."""
         D = self.model["discriminator"]
         B = target.shape[0]
-        outs = D(torch.cat([target, pred], 0))
+        if getattr(self, "_stashed", None) == B:
+            # the real half was computed in the generator step: only D(pred) runs
+            self._stashed = None
+            outs = _unwrap(D).forward_second_half(pred)
+        else:
+            outs = D(torch.cat([target, pred], 0))
         p = [[t[:B] for t in o] for o in outs]
         p_ = [[t[B:] for t in o] for o in outs]
         real_loss, fake_loss = self.criterion["dis_adv"](p_, p)
         return (real_loss + fake_loss) * self.config["lambda_adv"]
+
+    def _reuse_real(self):
+        """Reuse the generator step's D(target) as the D step's real half: one
+        process only (under DDP the D step stays ONE module call over the
+        concatenated batch, for the reducer's hooks); SEL_REUSE_REAL=0: off."""
+        return (os.environ.get("SEL_REUSE_REAL", "1") != "0" and not (D.is_dist() and D.rank_world()[1] > 1)
+                and hasattr(_unwrap(self.model["discriminator"]), "stash_first_half"))
 
     def model_step(self, target, x, mode="train"):
         gen = self.model["generator"]

@@ -328,3 +328,47 @@ def test_gan_step_bf16_runs_and_tracks_fp32(gpu):
         vals.append([gen.item(), dis.item()] + [float(v) for _, v in frags[:3]])
     for a, b in zip(vals[1], vals[0]):
         assert np.isfinite(a) and abs(a - b) <= 3e-2 * abs(b) + 1e-6, (vals[1], vals[0])
+
+
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+def test_gan_step_reused_real_half_matches_concatenated(gpu, dt, monkeypatch):
+    """The D step's real half reused from the generator step
+    (DenoiseStep._reuse_real: Discriminator.stash_first_half, then
+    forward_second_half) against ONE pass over the concatenated batch
+    (SEL_REUSE_REAL=0): same losses and the same discriminator gradients.  Both
+    run the same kernels per clip; the flat tiling may place the clips in
+    other tiles, so the bar is 1e-6 (fp32) / 1e-3 (bf16) norm-wise, not bit
+    equality."""
+    from models.autoencoder_without_PQC.AudioDec import Generator
+    from sel import configs
+    from sel.convops import precision
+    from train_denoise import DenoiseStep
+    g = golden("gan_step")
+    gp = dict(encode_channels=4, decode_channels=4, code_dim=64, codebook_num=2, codebook_size=64)
+    x, y = torch.from_numpy(g["x_noisy"]), torch.from_numpy(g["x_clean"])
+    res = []
+    for reuse in ("0", "1"):
+        monkeypatch.setenv("SEL_REUSE_REAL", reuse)
+        G = Generator(**gp)
+        G.load_state_dict({k[3:]: torch.from_numpy(v) for k, v in golden("generator_nopqc").items()
+                           if k.startswith("sd.")})
+        G = G.to(gpu)
+        D, _ = _disc(gpu)
+        step = DenoiseStep(configs.get("symAD_vctk_48000_hop300"), gpu, generator=G, discriminator=D)
+        step.discriminator_enabled = True
+        assert step._reuse_real() == (reuse == "1")
+        # no optimizer update: compare the gradients the D step leaves
+        step.optimizer["discriminator"].step = lambda *a, **k: None
+        with precision(torch.float32 if dt == "fp32" else torch.bfloat16):
+            gen, dis, frags = step.model_step(y, x)
+        torch.cuda.synchronize()
+        res.append(([gen.item(), dis.item()] + [float(v) for _, v in frags[:3]],
+                    [p.grad.detach().double().clone() for p in D.parameters()]))
+    tol = 1e-6 if dt == "fp32" else 1e-3
+    for a, b in zip(res[1][0], res[0][0]):
+        assert abs(a - b) <= tol * abs(b) + 1e-9, (res[1][0], res[0][0])
+    num = sum(((a - b) ** 2).sum().item() for a, b in zip(res[1][1], res[0][1]))
+    den = sum((b ** 2).sum().item() for b in res[0][1])
+    exact = all(torch.equal(a, b) for a, b in zip(res[1][1], res[0][1]))
+    print(f"reuse vs concatenated ({dt}): grad rel {(num / den) ** 0.5:.3e}, bit-equal {exact}")
+    assert (num / den) ** 0.5 <= tol, (num / den) ** 0.5
