@@ -901,6 +901,254 @@ __global__ __launch_bounds__((NC + 4) * 64) void k_conv_ws_bf16(Args a, const __
 }
 
 // ---------------------------------------------------------------------------
+// Eight-wave form of the warp-specialised kernel (k_conv_ws8).  Same LDS ring
+// layout, swizzle, DMA sources and (chunk, tap) MFMA order as k_conv_ws_bf16,
+// hence bit-identical outputs, but:
+//   - no producer waves: each of the 8 waves issues its share of the chunk's
+//     1-KB DMA pieces (q = 8u + wave) and ELUs the input pieces it DMA'd;
+//   - 128 x 64 per wave (4 x 2 MFMA tiles of 32 x 32): six fragment reads per
+//     eight MFMAs instead of four per four, at 2 waves per SIMD with the
+//     256-VGPR budget the 128 accumulators need;
+//   - block tiles of 256 x 256 (the MPD's 512 / 1024-wide layers: half the
+//     weight-slice DMA per flop of a 256 x 128 tile) or 512 x 128 (the 128-wide
+//     k7 dgrads at T = 2000: 4 tiles per sample, 256 per launch);
+//   - a 3-slot ring: chunk c + 2 is issued while chunk c is computed, chunk
+//     c + 1 is waited for (counted vmcnt, never 0 while a later chunk is in
+//     flight) after the first tap of chunk c, one raw barrier per chunk.
+// The LDS image per chunk is what the 12-wave kernel's producers build, so
+// the DMA and the ELU are unchanged; the LDS reads per flop fall by a quarter
+// and the DMA'd weight bytes per flop by up to a half.
+// ---------------------------------------------------------------------------
+template <int KT, int BM, int BN, int HALO, int TM = 4>
+struct Ws8 {
+  static constexpr int WTM = 32 * TM;               // wave tile rows (x 64 columns)
+  static constexpr int WM = BM / WTM, WN = BN / 64;  // wave grid
+  static_assert(WM * WN == 8 && BM % 128 == 0, "eight wave tiles");
+  static constexpr int XROWS = BM + HALO;           // staged input rows per chunk
+  static constexpr int XI = XROWS / WS_RPI;         // input pieces (1 KB = 32 rows x 16 channels)
+  static constexpr int WI = KT * BN / WS_RPI;       // weight pieces
+  static constexpr int TI = XI + WI;
+  static constexpr int PW = (TI + 7) / 8;           // pieces per wave per chunk
+  static constexpr int NB = 3;                      // ring slots
+  static constexpr int BUF = (XROWS + KT * BN) * WS_CK;  // bf16 elements per slot
+  static constexpr int EP = BN + 4;                 // fp32 epilogue pitch (conflict-free 16-B writes)
+  static constexpr size_t RING = size_t(NB) * BUF * 2, EPI = size_t(128) * EP * 4;
+  static constexpr size_t LDS = RING > EPI ? RING : EPI;
+  static_assert(XROWS % WS_RPI == 0 && WI * WS_RPI == KT * BN && LDS <= 160 * 1024, "LDS");
+  static_assert(2 * PW < 64, "vmcnt range");
+};
+
+template <int PW>
+__device__ __forceinline__ void ws8_elu_pieces(unsigned char* slot, int lane, int wave, int xi) {
+#pragma unroll
+  for (int u = 0; u < PW; ++u) {
+    const int q = u * 8 + wave;
+    if (q >= xi) break;
+    const unsigned addr = unsigned(reinterpret_cast<uintptr_t>(slot + q * 1024 + lane * 16));
+    bf16x8 val;
+    asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(val) : "v"(addr) : "memory");
+    val = __builtin_bit_cast(bf16x8, elu8(__builtin_bit_cast(uint4, val)));
+    asm volatile("ds_write_b128 %0, %1" : : "v"(addr), "v"(val) : "memory");
+  }
+}
+
+template <int KT, typename TO, int BM, int BN, int HALO, int TM>
+__global__ __launch_bounds__(512) void k_conv_ws8(Args a, const __bf16* __restrict__ in,
+                                                  const __bf16* __restrict__ wp, const float* __restrict__ bias,
+                                                  const TO* __restrict__ aux, const TO* __restrict__ res,
+                                                  TO* __restrict__ out, int ncol) {
+  using G = Ws8<KT, BM, BN, HALO, TM>;
+  constexpr int PW = G::PW, XI = G::XI, TI = G::TI, NB = G::NB, BUF = G::BUF, XROWS = G::XROWS;
+  extern __shared__ __align__(16) unsigned char smem[];
+  __bf16* const lds = reinterpret_cast<__bf16*>(smem);
+  const int span = BM + (KT - 1) * a.dil;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tps = (a.T + BM - 1) / BM;
+  int64_t mt;
+  int nt;
+  xcd_tile(ncol, mt, nt);
+  const int64_t b = mt / tps;
+  const int t0 = int(mt % tps) * BM;
+  const int64_t m0 = b * a.T + t0;
+  const int mrows = a.T - t0 < BM ? a.T - t0 : BM;
+  const int n0 = nt * BN;
+  const int nchunk = a.C / WS_CK;
+
+  // this wave's DMA pieces q = 8u + wave (past the last piece: the last one again)
+  const __bf16* src[PW];
+#pragma unroll
+  for (int u = 0; u < PW; ++u) {
+    const int q = u * 8 + wave < TI ? u * 8 + wave : TI - 1;
+    if (q < XI) {
+      const int R = q * WS_RPI + lane / WS_SPR, ls = (lane % WS_SPR) ^ ws_swzbits(R);
+      int ti = t0 - a.pad + R;
+      const bool valid =
+          R < span && (a.seq_pitch > 0 ? ti >= 0 && ti < a.T && ti % a.seq_pitch < a.tin_valid
+                                       : (ti >= 0 && ti < a.tin_valid) || a.pad_mode == SEL_PAD_REPLICATE);
+      if (a.seq_pitch == 0) ti = ti < 0 ? 0 : (ti >= a.tin_valid ? a.tin_valid - 1 : ti);
+      src[u] = valid ? in + (b * a.tin_pitch + ti) * a.ldx + 8 * ls : g_ws_zero + 8 * ls;
+    } else {
+      const int R = (q - XI) * WS_RPI + lane / WS_SPR, ls = (lane % WS_SPR) ^ ws_swzbits(R);
+      const int k = R / BN, n = R % BN;
+      src[u] = wp + (int64_t(n0 + n) * KT + k) * a.C + 8 * ls;
+    }
+  }
+  auto issue = [&](int ch) __attribute__((always_inline)) {
+    unsigned char* const base = smem + (ch % NB) * (BUF * 2);
+#pragma unroll
+    for (int u = 0; u < PW; ++u) {
+      const int q = u * 8 + wave < TI ? u * 8 + wave : TI - 1;
+      const int off = q < XI ? q * 1024 : XROWS * WS_CK * 2 + (q - XI) * 1024;
+      __builtin_amdgcn_global_load_lds((const void*)(src[u] + ch * WS_CK), (lds_ptr_t)(base + off), 16, 0, 0);
+    }
+  };
+  const int xi_used = (span + WS_RPI - 1) / WS_RPI;  // input pieces holding rows < span
+  auto elu_pass = [&](int ch) __attribute__((always_inline)) {
+    ws8_elu_pieces<PW>(smem + (ch % NB) * (BUF * 2), lane, wave, xi_used);
+  };
+
+  const int wm = wave / G::WN, wn = wave % G::WN;
+  const int hl = lane >> 5;
+  int arow[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) arow[i] = wm * G::WTM + i * 32 + (lane & 31);
+  int boff[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) boff[j] = XROWS * WS_CK + ws_swz(wn * 64 + j * 32 + (lane & 31), hl);
+  floatx16 acc[TM][2];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  // prologue: chunks 0 and 1 in flight, chunk 0 landed (and ELU'd) before the first barrier
+  constexpr int D = NB - 1;
+  for (int c = 0; c < D && c < nchunk; ++c) issue(c);
+  if (nchunk > 1) ws_wait_vm<PW>();
+  else ws_wait_vm<0>();
+  if (a.in_elu) elu_pass(0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  for (int ch = 0; ch < nchunk; ++ch) {
+    // chunk ch - 1's slot is free (every wave passed the barrier after reading it)
+    if (ch + D < nchunk) issue(ch + D);
+    const __bf16* const xb = lds + (ch % NB) * BUF;
+    bf16x8 fa[2][TM], fb[2][2];
+    auto fetch = [&](int k, int q) __attribute__((always_inline)) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) fb[q][j] = *reinterpret_cast<const bf16x8*>(xb + boff[j] + k * BN * WS_CK);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) fa[q][i] = *reinterpret_cast<const bf16x8*>(xb + ws_swz(arow[i] + k * a.dil, hl));
+    };
+    fetch(0, 0);
+#pragma unroll
+    for (int k = 0; k < KT; ++k) {
+      if (k + 1 < KT) fetch(k + 1, (k + 1) & 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[k & 1][j], fa[k & 1][i], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (k == 0 && ch + 1 < nchunk) {
+        // chunk ch + 1 landed (chunk ch + 2, when issued above, still in flight), then its ELU
+        if (ch + D < nchunk) ws_wait_vm<PW>();
+        else ws_wait_vm<0>();
+        if (a.in_elu) elu_pass(ch + 1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+
+  // epilogue in BM / 128 passes of 128 rows: the waves whose rows fall in pass p
+  // write their accumulators into an fp32 [128][BN + 4] tile over the (drained)
+  // ring, then all 8 waves run row-contiguous 16-B accesses (the 12-wave
+  // kernel's epilogue)
+  struct alignas(16) V8 { TO v[8]; };
+  constexpr int BNV = BN / 8, EV = 128 * BNV / 512, NP = BM / 128;
+  float* const tile = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    if (wm * G::WTM / 128 == p) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int r = wm * G::WTM % 128 + i * 32 + (lane & 31);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            floatx4 v4;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v4[e] = acc[i][j][4 * g + e];
+            *reinterpret_cast<floatx4*>(tile + r * G::EP + wn * 64 + j * 32 + 8 * g + 4 * hl) = v4;
+          }
+      }
+    }
+    __syncthreads();
+    const int prow = p * 128;
+#pragma unroll
+    for (int u = 0; u < EV; ++u) {
+      const int v = tid + u * 512;
+      const int row = v / BNV, c8 = (v % BNV) * 8;
+      if (prow + row >= mrows) continue;
+      const int64_t o = (m0 + prow + row) * a.ldo + n0 + c8;
+      V8 av, rv;
+      if (aux) av = *reinterpret_cast<const V8*>(aux + o);
+      if (res) rv = *reinterpret_cast<const V8*>(res + o);
+      const floatx4 lo = *reinterpret_cast<const floatx4*>(tile + row * G::EP + c8);
+      const floatx4 hi = *reinterpret_cast<const floatx4*>(tile + row * G::EP + c8 + 4);
+      float x[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      if (a.epi) {
+        const bool valid = (a.seq_pitch > 0 ? (t0 + prow + row) % a.seq_pitch : t0 + prow + row) < a.tout_valid;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float y = 0.f;
+          if (valid) {
+            y = x[e];
+            if (bias) y += bias[n0 + c8 + e];
+            if (res) y += to_f(rv.v[e]);
+            if (aux) y *= to_f(av.v[e]) > 0.f ? 1.f : a.slope;
+            if (a.act) y = y > 0.f ? y : y * a.slope;
+          }
+          x[e] = y;
+        }
+      } else {
+        if (bias && a.bias_period) {
+          if (a.bias_period % 8 == 0) {
+            const float* const bp = bias + (n0 + c8) % a.bias_period;
+            const floatx4 b0 = *reinterpret_cast<const floatx4*>(bp), b1 = *reinterpret_cast<const floatx4*>(bp + 4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) x[e] += b0[e], x[e + 4] += b1[e];
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) x[e] += bias[(n0 + c8 + e) % a.bias_period];
+          }
+        }
+        if (aux) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) x[e] *= elu_grad_fast(to_f(av.v[e]));
+        }
+        if (res) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) x[e] += to_f(rv.v[e]);
+        }
+      }
+      V8 ov;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ov.v[e] = from_f<TO>(x[e]);
+      *reinterpret_cast<V8*>(out + o) = ov;
+    }
+    if (p + 1 < NP) __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Weight-stationary streaming conv for the thin layers (32/64/96 input and
 // 32/64 output channels: the residual-unit convs at T = 24000 / 8000, their
 // dgrads, the first strided layer and the last transposed layer's dgrad).
@@ -3483,6 +3731,46 @@ int launch_ws(const Args& a, const void* in, const void* wp, const float* bias, 
   return SEL_OK;
 }
 
+template <int KT, typename TO, int BM, int BN, int HALO, int TM = 4>
+int launch_ws8(const Args& a, const void* in, const void* wp, const float* bias, const void* aux, const void* res,
+               void* out, hipStream_t s) {
+  using G = Ws8<KT, BM, BN, HALO, TM>;
+  SEL_REQUIRE(a.K == KT && a.N % BN == 0 && a.C % WS_CK == 0 && a.C <= WS_CMAX && (KT - 1) * a.dil <= HALO &&
+                  a.T > 0 && a.rows % a.T == 0,
+              SEL_ERR_ARG, "k_conv_ws8<%d, %d, %d>: bad shape C=%d N=%d K=%d dil=%d", KT, BM, BN, a.C, a.N, a.K,
+              a.dil);
+  const int64_t tiles = (a.rows / a.T) * ((a.T + BM - 1) / BM);
+  const int ncol = a.N / BN;
+  if (tiles == 0) return SEL_OK;
+  const bool xcd = ncol > 1 && tune(8) == 0 && tiles * ncol < (int64_t(1) << 31);
+  const dim3 grid = xcd ? dim3(unsigned(tiles * ncol)) : dim3(unsigned(tiles), unsigned(ncol));
+  auto kern = k_conv_ws8<KT, TO, BM, BN, HALO, TM>;
+  SEL_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, int(G::LDS)));
+  hipLaunchKernelGGL(kern, grid, dim3(512), G::LDS, s, a, static_cast<const __bf16*>(in),
+                     static_cast<const __bf16*>(wp), bias, static_cast<const TO*>(aux), static_cast<const TO*>(res),
+                     static_cast<TO*>(out), xcd ? ncol : 0);
+  SEL_LAUNCH_CHECK();
+  return SEL_OK;
+}
+
+// the eight-wave kernel's 512 x 128 tiles for the 128-wide k7 layers (legal
+// shapes; forced with tune key 0 = 28)
+bool ws8_gen_ok(const Args& a) {
+  return a.K == 7 && a.N == 128 && a.C % WS_CK == 0 && a.C <= WS_CMAX && (a.K - 1) * a.dil <= 64 && a.T >= 1024;
+}
+// ... and where the heuristic takes them: the k7 dgrads at >= 64 k rows (the C3
+// RU128 dgrads at T = 2000: 4 tiles per sample, 256 per launch); tune key 37:
+// 1 = off (the 12-wave kernel), 2 = the ELU-prologue forwards too
+bool ws8_gen_pick(const Args& a) {
+  return tune(37) != 1 && ws8_gen_ok(a) && a.rows >= 65536 && ((a.pad == 0 && !a.in_elu) || tune(37) == 2);
+}
+// eight waves of 64 x 64 on the 12-wave kernel's 256 x 128 tile (variant 29):
+// the 256-wide K = 3 / 7 layers at T = 400; tune key 38 = 1: on
+bool ws8w_ok(const Args& a) {
+  return (a.K == 7 || a.K == 3) && a.N % 128 == 0 && a.C % WS_CK == 0 && a.C <= WS_CMAX &&
+         (a.K - 1) * a.dil <= 64;
+}
+
 // the warp-specialised kernel's legal shapes: K in {3, 7}, 128-multiple N,
 // 16-multiple C within the zero source, halo within the staged span, the
 // 4-slot ring within 160 KB
@@ -3505,11 +3793,12 @@ int launch_ws_k(const Args& a, const void* in, const void* wp, const float* bias
 int fwd4_choice(const Args& a) {
   const int v = tune(0);
   if (!((a.C % CK) == 0 && (a.K - 1) * a.dil <= F4_HALOMAX && a.K <= 8 && (v == 0 || v > 20))) return -1;
-  if (v > 20 && (v != 27 || ws_ok(a))) return v;
+  if (v > 20 && (v != 27 || ws_ok(a)) && (v != 28 || ws8_gen_ok(a)) && (v != 29 || ws8w_ok(a))) return v;
   if (a.N <= 32 || (a.N % 64) != 0 || a.rows < 8192) return 22;
   if (a.N >= 256 && a.K == 1) return 26;
-  if (a.N >= 256 && a.rows >= 16384) return ws_ok(a) ? 27 : 24;
+  if (a.N >= 256 && a.rows >= 16384) return tune(38) == 1 && ws8w_ok(a) ? 29 : ws_ok(a) ? 27 : 24;
   if (a.N <= 64 || a.rows < 65536) return 23;
+  if (ws8_gen_pick(a)) return 28;
   if (a.N == 128 && ws_ok(a) && (a.K == 3 || (a.K == 7 && a.pad == 0 && !a.in_elu))) return 27;
   if (a.N == 128 && a.K > 1 && a.pad == 0 && !a.in_elu) return 22;
   return 24;
@@ -3528,6 +3817,13 @@ int fwd4_variant(int v, const Args& a, const void* in, const void* wp, const flo
     case 27:
       if (!ws_ok(a)) break;
       return launch_ws_k<TO>(a, in, wp, bias, aux, res, out, s);
+    case 28:
+      if (!ws8_gen_ok(a)) break;
+      return launch_ws8<7, TO, 512, 128, 64>(a, in, wp, bias, aux, res, out, s);
+    case 29:
+      if (!ws8w_ok(a)) break;
+      if (a.K == 7) return launch_ws8<7, TO, 256, 128, 64, 2>(a, in, wp, bias, aux, res, out, s);
+      return launch_ws8<3, TO, 256, 128, 64, 2>(a, in, wp, bias, aux, res, out, s);
     default: break;
   }
   // heuristic from tools/conv_bench.py on the C3 layer shapes (profiles/r1_conv_bench.md):
@@ -3542,6 +3838,7 @@ int fwd4_variant(int v, const Args& a, const void* in, const void* wp, const flo
   // RU256 k7 fwd+dgrad 43.5 -> 38.4 us, down2 46.6 -> 41.8), else 256x64 tiles
   // (RU256 k7 fwd 50.7 -> 36.2 us, dgrad 54.2 -> 43.0, down2 51.2 -> 43.1)
   if (a.N >= 256 && a.rows >= 16384) {
+    if (tune(38) == 1 && ws8w_ok(a)) return fwd4_variant<KMAX, TO>(29, a, in, wp, bias, aux, res, out, s);
     if (ws_ok(a)) return launch_ws_k<TO>(a, in, wp, bias, aux, res, out, s);
     return launch_fwd4<256, 64, 4, KMAX, TO>(a, in, wp, bias, aux, res, out, s);
   }
@@ -3551,6 +3848,7 @@ int fwd4_variant(int v, const Args& a, const void* in, const void* wp, const flo
   // (RU128 d9: 63.6 -> 53.2 us) and the k3 convs (down1: 49.3 -> 44.1 us), not
   // the k7 forwards with their ELU'd 54-row halo (48.6 -> 52.9 us);
   // tools/conv_bench.py.
+  if (ws8_gen_pick(a)) return launch_ws8<7, TO, 512, 128, 64>(a, in, wp, bias, aux, res, out, s);
   if (a.N == 128 && ws_ok(a) && (a.K == 3 || (a.K == 7 && a.pad == 0 && !a.in_elu)))
     return launch_ws_k<TO>(a, in, wp, bias, aux, res, out, s);
   // 128-wide k7 dgrad at 2000 samples (pad 0, no input ELU): 128x32 tiles (76.5 -> 62.6 us)
@@ -3999,6 +4297,12 @@ int dconv_ws_mode(const sel_dconv_desc* d) {
   return flat ? 1 : 0;
 }
 
+// the eight-wave kernel's 256 x 256 tiles for the MPD's 512 / 1024-wide K = 2 / 5
+// layers and adjoints (a dconv_ws_mode shape); tune key 37 = 1: off
+bool dconv_ws8_ok(const sel_dconv_desc* d) {
+  return tune(37) != 1 && (d->K == 2 || d->K == 5) && (d->So * d->Ng) % 256 == 0 && dconv_ws_mode(d) >= 0;
+}
+
 int dconv_ws_fwd(const sel_dconv_desc* d, const void* x, const void* wp, const float* bias, const void* aux,
                  const void* res, void* out, hipStream_t s) {
   const int mode = dconv_ws_mode(d);
@@ -4026,6 +4330,10 @@ int dconv_ws_fwd(const sel_dconv_desc* d, const void* x, const void* wp, const f
   a.epi = 1;
   a.act = d->act;
   a.slope = d->slope;
+  if (dconv_ws8_ok(d)) {
+    if (d->K == 2) return launch_ws8<2, __bf16, 256, 256, 32>(a, x, wp, bias, aux, res, out, s);
+    return launch_ws8<5, __bf16, 256, 256, 32>(a, x, wp, bias, aux, res, out, s);
+  }
   switch (d->K) {
     case 2: return launch_ws<2, __bf16>(a, x, wp, bias, aux, res, out, s);
     case 3: return launch_ws<3, __bf16>(a, x, wp, bias, aux, res, out, s);
@@ -4048,7 +4356,10 @@ int sel_conv_fwd_kernel_id(const sel_conv_desc* d, int in_dtype, int out_dtype, 
   }
   const int v = fwd4_choice(a);
   if (v < 0) return -1;
-  if (v == 27) return 900000000 + a.K;  // warp-specialised kernel: 9e8 + K
+  // warp-specialised kernels: 9e8 + K (12 waves), 9.1e8 + K (eight waves, 512 x 128)
+  if (v == 27) return 900000000 + a.K;
+  if (v == 28) return 910000000 + a.K;
+  if (v == 29) return 920000000 + a.K;
   const int kmax = a.K == 1 ? 1 : (a.K <= 3 ? 3 : 8);
   static const int bm[] = {256, 128, 128, 256, 128, 64}, bn[] = {32, 32, 64, 64, 128, 128}, wm[] = {4, 4, 2, 4, 2, 1};
   const int i = v - 21;

@@ -44,6 +44,8 @@ int dconv_ws_fwd(const sel_dconv_desc* d, const void* x, const void* wp, const f
                  const void* res, void* out, hipStream_t s);
 // -1: shape not supported there, 0: per-sequence tiles, 1: flat tiles across sequences
 int dconv_ws_mode(const sel_dconv_desc* d);
+// true: dconv_ws_fwd runs the shape on the eight-wave 256 x 256 kernel (k_conv_ws8)
+bool dconv_ws8_ok(const sel_dconv_desc* d);
 }  // namespace conv
 namespace dconv {
 
@@ -2053,7 +2055,7 @@ FwdPlan plan_fwd(const sel_dconv_desc* d, int dtype) {
     // 256 x 128 tiles (conv.hip k_conv_ws_bf16; tune key 21: 1 = off)
     if (tune(21) != 1 && width % 128 == 0 && d->S * d->Cg >= 64 && rows * (width / 128) >= 65536) {
       const int m = sel::conv::dconv_ws_mode(d);
-      if (m >= 0) return {m == 1 ? SEL_DPATH_WS_FLAT : SEL_DPATH_WS, 256, 128};
+      if (m >= 0) return {m == 1 ? SEL_DPATH_WS_FLAT : SEL_DPATH_WS, 256, sel::conv::dconv_ws8_ok(d) ? 256 : 128};
     }
     if (width > 32 && pf_ok(d, dtype)) {
       // tune key 19: tile A/B (1: 256x64, 2: 128x128, 3: 256x128)
@@ -2324,7 +2326,10 @@ int sel_dconv_kernel(const sel_dconv_desc* d, int dtype, char* name, size_t cap)
     const char* t = dtype == SEL_BF16 ? "bf16" : "float";
     switch (p.path) {
       case SEL_DPATH_WS:
-      case SEL_DPATH_WS_FLAT: snprintf(name, cap, "k_conv_ws_bf16<%d>", d->K); break;
+      case SEL_DPATH_WS_FLAT:
+        if (p.bn == 256) snprintf(name, cap, "k_conv_ws8<%d, bf16, 256, 256>", d->K);
+        else snprintf(name, cap, "k_conv_ws_bf16<%d>", d->K);
+        break;
       case SEL_DPATH_PF: snprintf(name, cap, "k_dconv_pf<%d, %d>", p.bm, p.bn); break;
       case SEL_DPATH_GPF: snprintf(name, cap, "k_dconv_gpf<%d, %d>", p.bm, p.bn); break;
       case SEL_DPATH_MFMA: snprintf(name, cap, "k_dconv_mfma<%s, %d, %d>", t, p.bm, p.bn); break;

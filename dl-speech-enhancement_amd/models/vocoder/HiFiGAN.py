@@ -5,9 +5,11 @@ The HiFi-GAN *generator* of the same reference file (:28-305) is the vocoder
 of the codec's pre-training and is outside the denoise hot path (SURVEY §2 row
 13); only the discriminator GAN mode needs (BASELINE config C5) is built.
 """
+import torch
 import torch.nn as nn
 
 from models.vocoder.modules.discriminator import HiFiGANMultiPeriodDiscriminator, HiFiGANMultiScaleDiscriminator
+from sel.streams import run_concurrent
 
 
 class Discriminator(nn.Module):
@@ -34,28 +36,38 @@ class Discriminator(nn.Module):
                                                   follow_official_norm=follow_official_norm)
         self.mpd = HiFiGANMultiPeriodDiscriminator(periods=periods, discriminator_params=period_discriminator_params)
 
+    def _chains(self, x, pooled, method):
+        """The 3 scale and 5 period sub-discriminators on `method` (None = the
+        module call), as independent chains on side streams (sel.streams: same
+        kernels, same bits); MSD outputs first, as the reference concatenates."""
+        fs = list(self.msd.discriminators) + list(self.mpd.discriminators)
+        xs = list(pooled) + [x] * len(self.mpd.discriminators)
+        calls = [(lambda f=f, v=v: f(v) if method is None else getattr(f, method)(v)) for f, v in zip(fs, xs)]
+        return run_concurrent(calls, [x] + list(pooled))
+
+    def _flat(self, x):
+        batch, channel, time = x.size()
+        return x.reshape(batch * channel, 1, time) if channel != 1 else x
+
     def forward(self, x):
         """x (B, C, T) -> list of lists of each sub-discriminator's layer outputs
         (MSD then MPD), HiFiGAN.py:380-395."""
-        batch, channel, time = x.size()
-        if channel != 1:
-            x = x.reshape(batch * channel, 1, time)
-        return self.msd(x) + self.mpd(x)
+        x = self._flat(x)
+        return self._chains(x, self.msd._scales(x, lambda f, v: v), None)
 
+    @torch.no_grad()
     def stash_first_half(self, x):
         """No-grad forward of B clips x into per-layer buffers sized for 2B clips,
         kept for forward_second_half (train_denoise.DenoiseStep: the generator
         step's D(target) is the D step's real half); returns x's outputs."""
-        batch, channel, time = x.size()
-        if channel != 1:
-            x = x.reshape(batch * channel, 1, time)
-        return self.msd.stash_first_half(x) + self.mpd.stash_first_half(x)
+        x = self._flat(x)
+        return self._chains(x, self.msd._scales(x, lambda f, v: v), "stash_first_half")
 
     def forward_second_half(self, x):
         """forward(torch.cat([stashed clips, x])) without recomputing the stashed
         half: the same outputs (the kernels compute every output row the same
         way for any batch), one autograd graph over all 2B clips."""
-        batch, channel, time = x.size()
-        if channel != 1:
-            x = x.reshape(batch * channel, 1, time)
-        return self.msd.forward_second_half(x) + self.mpd.forward_second_half(x)
+        x = self._flat(x)
+        with torch.no_grad():  # the waveform (a detached prediction) takes no gradient
+            pooled = self.msd._scales(x, lambda f, v: v)
+        return self._chains(x, pooled, "forward_second_half")

@@ -280,7 +280,11 @@ def fwd_kernel_name(desc, in_dtype, out_dtype, has_epilogue=False):
         k, n, c, r = kid % 10, (kid // 10) % 1000, (kid // 10000) % 1000, 32 * (kid // 10000000)
         return f"k_conv_thin_bf16<{c}, {n}, {k}, {r}, {'true' if e else 'false'}>"
     to = "bf16" if out_dtype == torch.bfloat16 else "float"
-    if kid >= 9 * 10 ** 8:  # warp-specialised double-buffered kernel: 9e8 + K
+    if kid >= 92 * 10 ** 7:  # eight-wave warp-specialised kernel, 256 x 128 tiles of 64 x 64 wave tiles: 9.2e8 + K
+        return f"k_conv_ws8<{kid - 92 * 10 ** 7}, {to}, 256, 128, 64, 2>"
+    if kid >= 91 * 10 ** 7:  # eight-wave warp-specialised kernel, 512 x 128 tiles: 9.1e8 + K
+        return f"k_conv_ws8<{kid - 91 * 10 ** 7}, {to}, 512, 128>"
+    if kid >= 9 * 10 ** 8:  # warp-specialised kernel (12 waves): 9e8 + K
         return f"k_conv_ws_bf16<{kid - 9 * 10 ** 8}, {to}>"
     kmax, kid = kid % 10, kid // 10
     wm, kid = kid % 10, kid // 10
@@ -334,6 +338,21 @@ class _WgradJob(ctypes.Structure):
 WGRAD_DEFER = os.environ.get("SEL_WGRAD_DEFER", "1") != "0"
 _DEFERRED = []
 _DEFER_LOCK = threading.Lock()
+# Deferred partial kernels on a side stream (SEL_WGRAD_STREAM=1): a layer's
+# weight-gradient partials depend only on its gout and input, which the
+# backward's next dgrad launches do not change, so they can run beside that
+# chain and fill the CUs its launches leave idle; the batched reduction runs
+# on the side stream and the current stream waits for it before backward()
+# returns.  Same kernels, same bits.
+WGRAD_STREAM = os.environ.get("SEL_WGRAD_STREAM", "0") != "0"
+_WG_STREAMS = {}
+
+
+def _wgrad_stream(device):
+    s = _WG_STREAMS.get(device.index)
+    if s is None:
+        s = _WG_STREAMS[device.index] = torch.cuda.Stream(device=device)
+    return s
 
 
 def _can_defer(params):
@@ -393,6 +412,9 @@ def _flush_deferred():
         group = [e[0] for e in pending if e[3] == st]
         jobs = (_WgradJob * len(group))(*group)
         L.call("sel_wgrad_finish_many", ctypes.cast(jobs, ctypes.c_void_p), len(group), ctypes.c_void_p(st))
+        side = next((s for s in _WG_STREAMS.values() if s.cuda_stream == st), None)
+        if side is not None:  # the gradients are read on the current stream from here on
+            torch.cuda.current_stream(side.device).wait_stream(side)
     # the workspaces are released here; the finish kernel is already enqueued on
     # this stream ahead of any later use of that memory
 
@@ -413,6 +435,12 @@ def wgrad_torch(desc, gout, x, kind, w_shape, stride, want_bias, params=None):
     if params is not None and len(params) == 1 + int(gb is not None) and _can_defer(params) and _queue_flush():
         ns = ctypes.c_int()
         st = L.stream()
+        if WGRAD_STREAM:
+            side = _wgrad_stream(x.device)
+            side.wait_stream(torch.cuda.current_stream(x.device))
+            for t in (gout, x, ws):
+                t.record_stream(side)
+            st = ctypes.c_void_p(side.cuda_stream)
         L.call("sel_conv_wgrad_partials", ctypes.byref(desc), _code(x.dtype), L.ptr(gout), L.ptr(x),
                int(want_bias), L.ptr(ws), ws.numel(), ctypes.byref(ns), st)
         job = _WgradJob(ws.data_ptr(), gw.data_ptr(), gb.data_ptr() if gb is not None else None,

@@ -1,7 +1,10 @@
 """Parity of the C3 (BASELINE configs[2]) bf16 path at the bench's own size.
 
 1. Every bf16 tile variant of the MFMA conv primitive (tune key 0 = 21..27,
-   conv.hip fwd4_variant; 27 = the warp-specialised k_conv_ws_bf16) on the real C3 layer shapes in primitive form,
+   conv.hip fwd4_variant; 27 = the warp-specialised k_conv_ws_bf16, 28 / 29 =
+   its eight-wave forms k_conv_ws8 (512 x 128 tiles of 128 x 64 wave tiles /
+   256 x 128 of 64 x 64), bit-identical to 27 where they apply)
+   on the real C3 layer shapes in primitive form,
    forward and dgrad (adjoint) forms, against an fp64 reference computed from
    the SAME bf16 operands.  Both accumulate exact bf16 products (fp32 vs fp64
    sums) and the kernel rounds once to bf16, so the bound is bf16 output
@@ -105,11 +108,12 @@ def test_fwd4_tile_variants_on_c3_shapes(gpu, shape, form):
     p4 = lib.sel_tune(4, 1)  # the weight-stationary thin kernel would pre-empt the tiled one
     try:
         default_name = CO.fwd_kernel_name(d, torch.bfloat16, torch.bfloat16)
-        assert default_name.startswith(("k_conv_fwd_bf16", "k_conv_ws_bf16")), default_name
+        assert default_name.startswith(("k_conv_fwd_bf16", "k_conv_ws_bf16", "k_conv_ws8")), default_name
         default = CO.prim(d, x, wp, bias=b, aux=a_, res=r_).clone()
         _check(default, ref, (form, "default", default_name))
         matched = False
-        for v in range(21, 28):
+        ws = {}
+        for v in range(21, 30):
             p0 = lib.sel_tune(0, v)
             try:
                 name = CO.fwd_kernel_name(d, torch.bfloat16, torch.bfloat16)
@@ -117,10 +121,17 @@ def test_fwd4_tile_variants_on_c3_shapes(gpu, shape, form):
             finally:
                 lib.sel_tune(0, p0)
             _check(got, ref, (form, v, name))
+            if name.startswith(("k_conv_ws_bf16", "k_conv_ws8")):
+                ws[name] = got
             if name == default_name:
                 matched = True
                 assert torch.equal(got, default), (form, v)
         assert matched, default_name
+        # the eight-wave kernel (variant 28, where legal) keeps the 12-wave kernel's
+        # (chunk, tap) MFMA order per output: same bits
+        first = next(iter(ws.values()), None)
+        for name, got in ws.items():
+            assert torch.equal(got, first), (form, list(ws), name)
     finally:
         lib.sel_tune(4, p4)
 

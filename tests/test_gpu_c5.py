@@ -9,7 +9,8 @@ MPD (models/vocoder/HiFiGAN.py:308-395, modules/discriminator.py:26-447).
    tiling (include/sel.h SEL_DPATH_WS_FLAT) — so the test cannot pass on a
    fallback — and the result must match fp64 torch on the same bf16 operands
    and be bit-identical to the per-sequence tiles (tune key 22 = 1, same MFMA
-   order per output).  The adjoint's gradient gap rows hold NaN: they must
+   order per output) and, on the 512 / 1024-wide layers, to the 12-wave kernel
+   (tune key 37 = 1; the default there is the eight-wave k_conv_ws8).  The adjoint's gradient gap rows hold NaN: they must
    never be read.  Both G-step (16 clips) and D-step (32 clips) batches.
 2. A full-chain backward whose feature-map gradients live in NaN-filled
    buffers (what GanReduceFn.backward hands over: only the view is written)
@@ -86,18 +87,20 @@ def test_mpd_ws_flat_layers_at_c5_shapes(gpu, period, clips):
                                              padding=sp.pad).permute(0, 2, 1)
             ref = torch.nn.functional.leaky_relu(pre, SLOPE)
             ys = []
-            for flat_off in (0, 1):
-                prev = lib.sel_tune(22, flat_off)
+            for flat_off, ws8_off in ((0, 0), (1, 0), (0, 1)):
+                prev, prev8 = lib.sel_tune(22, flat_off), lib.sel_tune(37, ws8_off)
                 try:
                     assert DC.kernel(d, dt)[0] == ("ws" if flat_off else "ws_flat"), (li, flat_off)
                     y = torch.full((Bs, To, sp.cout), 7.0, dtype=dt, device=gpu)
                     DC.prim(d, x, DC._pack(sp, w, None, dt, 0), y, bias=b)
                 finally:
                     lib.sel_tune(22, prev)
+                    lib.sel_tune(37, prev8)
                 ys.append(y)
             _check(ys[0][:, :T_out], ref, (period, clips, li, "fwd"))
             assert torch.count_nonzero(ys[0][:, T_out:]).item() == 0, (li, "rows past T_out")
             assert torch.equal(ys[0], ys[1]), (li, "flat vs per-sequence tiles")
+            assert torch.equal(ys[0], ys[2]), (li, "eight-wave vs 12-wave kernel")
         if adj_ws:
             n_flat += 1
             g = torch.full((Bs, To, sp.cout), float("nan"), device=gpu)
@@ -110,19 +113,21 @@ def test_mpd_ws_flat_layers_at_c5_shapes(gpu, period, clips):
                 0, 2, 1).backward(g[:, :T_out].double())
             ref = (xr.grad + res[:, :T_in].double()) * torch.where(aux[:, :T_in].double() > 0, 1.0, SLOPE)
             gs = []
-            for flat_off in (0, 1):
-                prev = lib.sel_tune(22, flat_off)
+            for flat_off, ws8_off in ((0, 0), (1, 0), (0, 1)):
+                prev, prev8 = lib.sel_tune(22, flat_off), lib.sel_tune(37, ws8_off)
                 try:
                     assert DC.kernel(db, dt)[0] == ("ws" if flat_off else "ws_flat"), (li, flat_off)
                     gin = torch.full((Bs, Ta, sp.cin), 7.0, dtype=dt, device=gpu)
                     DC.prim(db, g, DC._pack(sp, w, None, dt, 1), gin, aux=aux, res=res)
                 finally:
                     lib.sel_tune(22, prev)
+                    lib.sel_tune(37, prev8)
                 gs.append(gin)
             _check(gs[0][:, :T_in], ref, (period, clips, li, "adjoint"))
             tail = (T_in + s - 1) // s * s
             assert torch.count_nonzero(gs[0][:, tail:]).item() == 0, (li, "phase rows past the input")
             assert torch.equal(gs[0], gs[1]), (li, "adjoint flat vs per-sequence tiles")
+            assert torch.equal(gs[0], gs[2]), (li, "adjoint eight-wave vs 12-wave kernel")
     torch.cuda.synchronize()
     # at C5 sizes layers 1-4 forward and 2-4 adjoint are on the flat tiles (SEL_DPATH_WS_FLAT)
     assert n_flat >= 7, n_flat
