@@ -842,12 +842,19 @@ __global__ __launch_bounds__((NC + 4) * 64) void k_conv_ws_bf16(Args a, const __
       // discriminator epilogue (k_dconv_mfma order): + bias, + res, * LeakyReLU'(aux),
       // LeakyReLU; rows past the computed ones are the next layer's zero padding
       const bool valid = (a.seq_pitch > 0 ? (t0 + row) % a.seq_pitch : t0 + row) < a.tout_valid;
+      float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (bias) {
+        const floatx4 b0 = *reinterpret_cast<const floatx4*>(bias + n0 + c8);
+        const floatx4 b1 = *reinterpret_cast<const floatx4*>(bias + n0 + c8 + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bv[e] = b0[e], bv[e + 4] = b1[e];
+      }
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         float y = 0.f;
         if (valid) {
           y = x[e];
-          if (bias) y += bias[n0 + c8 + e];
+          if (bias) y += bv[e];
           if (res) y += to_f(rv[u].v[e]);
           if (aux) y *= to_f(av[u].v[e]) > 0.f ? 1.f : a.slope;
           if (a.act) y = y > 0.f ? y : y * a.slope;
@@ -956,7 +963,9 @@ template <int KT, typename TO, int BM, int BN, int HALO, int TM>
 __global__ __launch_bounds__(512) void k_conv_ws8(Args a, const __bf16* __restrict__ in,
                                                   const __bf16* __restrict__ wp, const float* __restrict__ bias,
                                                   const TO* __restrict__ aux, const TO* __restrict__ res,
-                                                  TO* __restrict__ out, int ncol) {
+                                                  TO* __restrict__ out, int ncol, int dbg) {
+  // dbg (tune key 13, diagnostics only): bit 0 = no DMA in the loop, bit 1 =
+  // no MFMAs, bit 2 = no barriers in the loop, bit 3 = no epilogue
   using G = Ws8<KT, BM, BN, HALO, TM>;
   constexpr int PW = G::PW, XI = G::XI, TI = G::TI, NB = G::NB, BUF = G::BUF, XROWS = G::XROWS;
   extern __shared__ __align__(16) unsigned char smem[];
@@ -1034,7 +1043,7 @@ __global__ __launch_bounds__(512) void k_conv_ws8(Args a, const __bf16* __restri
 
   for (int ch = 0; ch < nchunk; ++ch) {
     // chunk ch - 1's slot is free (every wave passed the barrier after reading it)
-    if (ch + D < nchunk) issue(ch + D);
+    if (ch + D < nchunk && !(dbg & 1)) issue(ch + D);
     const __bf16* const xb = lds + (ch % NB) * BUF;
     bf16x8 fa[2][TM], fb[2][2];
     auto fetch = [&](int k, int q) __attribute__((always_inline)) {
@@ -1048,23 +1057,26 @@ __global__ __launch_bounds__(512) void k_conv_ws8(Args a, const __bf16* __restri
     for (int k = 0; k < KT; ++k) {
       if (k + 1 < KT) fetch(k + 1, (k + 1) & 1);
       __builtin_amdgcn_sched_barrier(0);
+      if (!(dbg & 2)) {
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[k & 1][j], fa[k & 1][i], acc[i][j], 0, 0, 0);
+      }
       __builtin_amdgcn_sched_barrier(0);
       if (k == 0 && ch + 1 < nchunk) {
         // chunk ch + 1 landed (chunk ch + 2, when issued above, still in flight), then its ELU
-        if (ch + D < nchunk) ws_wait_vm<PW>();
+        if (ch + D < nchunk && !(dbg & 1)) ws_wait_vm<PW>();
         else ws_wait_vm<0>();
         if (a.in_elu) elu_pass(ch + 1);
         __builtin_amdgcn_sched_barrier(0);
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
+    if (!(dbg & 4)) __builtin_amdgcn_s_barrier();
   }
+  if (dbg & 8) return;
 
   // epilogue in BM / 128 passes of 128 rows: the waves whose rows fall in pass p
   // write their accumulators into an fp32 [128][BN + 4] tile over the (drained)
@@ -1106,12 +1118,19 @@ __global__ __launch_bounds__(512) void k_conv_ws8(Args a, const __bf16* __restri
       float x[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       if (a.epi) {
         const bool valid = (a.seq_pitch > 0 ? (t0 + prow + row) % a.seq_pitch : t0 + prow + row) < a.tout_valid;
+        float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (bias) {
+          const floatx4 b0 = *reinterpret_cast<const floatx4*>(bias + n0 + c8);
+          const floatx4 b1 = *reinterpret_cast<const floatx4*>(bias + n0 + c8 + 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) bv[e] = b0[e], bv[e + 4] = b1[e];
+        }
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           float y = 0.f;
           if (valid) {
             y = x[e];
-            if (bias) y += bias[n0 + c8 + e];
+            if (bias) y += bv[e];
             if (res) y += to_f(rv.v[e]);
             if (aux) y *= to_f(av.v[e]) > 0.f ? 1.f : a.slope;
             if (a.act) y = y > 0.f ? y : y * a.slope;
@@ -1604,6 +1623,18 @@ constexpr int RU_C = 32, RU_K = 7;
 
 // acc (one 32x32 MFMA result) -> bf16, re-laid out: frag[kc] = channels
 // 16 kc + 8 (lane >> 5) .. +8 of this lane's row (T21 of the HIP guide)
+// Global stores of the fused residual-unit kernels' outputs (h, out, gh, gx:
+// written once, read by a later launch).  SEL_RU_NT=1 builds them as streaming
+// (non-temporal) stores, the |X| kernel's lever (A/B library: make nt).
+#ifndef SEL_RU_NT
+#define SEL_RU_NT 0
+#endif
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void ru_store(__bf16* p, bf16x8 v) {
+  if constexpr (SEL_RU_NT) __builtin_nontemporal_store(__builtin_bit_cast(u32x4, v), reinterpret_cast<u32x4*>(p));
+  else *reinterpret_cast<bf16x8*>(p) = v;
+}
+
 __device__ __forceinline__ void ru_acc_to_frags(const float (&v)[16], bf16x8 (&frag)[2]) {
   unsigned pk[8];
 #pragma unroll
@@ -1747,8 +1778,8 @@ __global__ __launch_bounds__(256) void k_ru32_fwd(Args a, const __bf16* __restri
       bf16x8 hf[2];
       ru_acc_to_frags(v, hf);
       if (valid && !(dbg & 1)) {  // tune key 15 bit 0: diagnostic without the h store
-        *reinterpret_cast<bf16x8*>(hout + orow + 8 * hl) = hf[0];
-        *reinterpret_cast<bf16x8*>(hout + orow + 16 + 8 * hl) = hf[1];
+        ru_store(hout + orow + 8 * hl, hf[0]);
+        ru_store(hout + orow + 16 + 8 * hl, hf[1]);
       }
       floatx16 acc2;
 #pragma unroll
@@ -1770,8 +1801,8 @@ __global__ __launch_bounds__(256) void k_ru32_fwd(Args a, const __bf16* __restri
       bf16x8 of[2];
       ru_acc_to_frags(v, of);
       if (valid && !(dbg & 2)) {  // bit 1: diagnostic without the out store
-        *reinterpret_cast<bf16x8*>(out + orow + 8 * hl) = of[0];
-        *reinterpret_cast<bf16x8*>(out + orow + 16 + 8 * hl) = of[1];
+        ru_store(out + orow + 8 * hl, of[0]);
+        ru_store(out + orow + 16 + 8 * hl, of[1]);
       }
     }
   }
@@ -1915,8 +1946,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
       ru_acc_to_frags(v, hf);
       if (lr < mrows) {
         const int64_t orow = (b * a.T + t0 + lr) * C + ns * 32 + 8 * hl;
-        *reinterpret_cast<bf16x8*>(hout + orow) = hf[0];
-        *reinterpret_cast<bf16x8*>(hout + orow + 16) = hf[1];
+        ru_store(hout + orow, hf[0]);
+        ru_store(hout + orow + 16, hf[1]);
       }
 #pragma unroll
       for (int g = 0; g < 2; ++g)
@@ -1948,8 +1979,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
       ru_acc_to_frags(v, of);
       if (lr < mrows) {
         const int64_t orow = (b * a.T + t0 + lr) * C + ns * 32 + 8 * hl;
-        *reinterpret_cast<bf16x8*>(out + orow) = of[0];
-        *reinterpret_cast<bf16x8*>(out + orow + 16) = of[1];
+        ru_store(out + orow, of[0]);
+        ru_store(out + orow + 16, of[1]);
       }
     }
   }
@@ -2105,8 +2136,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
         *reinterpret_cast<bf16x8*>(ghs + (sl * G::SPAN + lr) * P + 16 + 8 * hl) = ghf[1];
       }
       if (ghout && lr < mrows) {
-        *reinterpret_cast<bf16x8*>(ghout + orow + 8 * hl) = ghf[0];
-        *reinterpret_cast<bf16x8*>(ghout + orow + 16 + 8 * hl) = ghf[1];
+        ru_store(ghout + orow + 8 * hl, ghf[0]);
+        ru_store(ghout + orow + 16 + 8 * hl, ghf[1]);
       }
     }
     __syncthreads();
@@ -2146,8 +2177,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
       bf16x8 of[2];
       ru_acc_to_frags(v, of);
       if (valid) {
-        *reinterpret_cast<bf16x8*>(gx + orow + 8 * hl) = of[0];
-        *reinterpret_cast<bf16x8*>(gx + orow + 16 + 8 * hl) = of[1];
+        ru_store(gx + orow + 8 * hl, of[0]);
+        ru_store(gx + orow + 16 + 8 * hl, of[1]);
       }
     }
   }
@@ -2241,8 +2272,8 @@ __global__ __launch_bounds__(256) void k_ru32_bwd(Args a, const __bf16* __restri
         *reinterpret_cast<bf16x8*>(ghs + lr * P + 16 + 8 * hl) = ghf[1];
       }
       if (ghout && lr < mrows) {
-        *reinterpret_cast<bf16x8*>(ghout + orow + 8 * hl) = ghf[0];
-        *reinterpret_cast<bf16x8*>(ghout + orow + 16 + 8 * hl) = ghf[1];
+        ru_store(ghout + orow + 8 * hl, ghf[0]);
+        ru_store(ghout + orow + 16 + 8 * hl, ghf[1]);
       }
     }
     __syncthreads();
@@ -2275,8 +2306,8 @@ __global__ __launch_bounds__(256) void k_ru32_bwd(Args a, const __bf16* __restri
       bf16x8 of[2];
       ru_acc_to_frags(v, of);
       if (valid) {
-        *reinterpret_cast<bf16x8*>(gx + orow + 8 * hl) = of[0];
-        *reinterpret_cast<bf16x8*>(gx + orow + 16 + 8 * hl) = of[1];
+        ru_store(gx + orow + 8 * hl, of[0]);
+        ru_store(gx + orow + 16 + 8 * hl, of[1]);
       }
     }
   }
@@ -2807,8 +2838,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
         bf16x8 of[2];
         ru_acc_to_frags(v, of);
         if (valid) {
-          *reinterpret_cast<bf16x8*>(gx + orow + 8 * hl) = of[0];
-          *reinterpret_cast<bf16x8*>(gx + orow + 16 + 8 * hl) = of[1];
+          ru_store(gx + orow + 8 * hl, of[0]);
+          ru_store(gx + orow + 16 + 8 * hl, of[1]);
         }
       }
       // weight gradients over the tile rows (rows past T: g = 0 -> gh = 0)
@@ -3748,7 +3779,7 @@ int launch_ws8(const Args& a, const void* in, const void* wp, const float* bias,
   SEL_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, int(G::LDS)));
   hipLaunchKernelGGL(kern, grid, dim3(512), G::LDS, s, a, static_cast<const __bf16*>(in),
                      static_cast<const __bf16*>(wp), bias, static_cast<const TO*>(aux), static_cast<const TO*>(res),
-                     static_cast<TO*>(out), xcd ? ncol : 0);
+                     static_cast<TO*>(out), xcd ? ncol : 0, tune(13));
   SEL_LAUNCH_CHECK();
   return SEL_OK;
 }
@@ -4297,10 +4328,14 @@ int dconv_ws_mode(const sel_dconv_desc* d) {
   return flat ? 1 : 0;
 }
 
-// the eight-wave kernel's 256 x 256 tiles for the MPD's 512 / 1024-wide K = 2 / 5
-// layers and adjoints (a dconv_ws_mode shape); tune key 37 = 1: off
+// the eight-wave kernel's 256 x 256 tiles for the MPD's 128 -> 512 stride-3
+// layer (K = 2 taps over 384 phase channels: 141 -> 126 us at period 2, D
+// step, tools/ws8_probe.py); the deeper K = 2 / 5 layers stay on the 12-wave
+// kernel (512 -> 1024 s3: 218 vs 248 us, 1024 -> 1024 k5: 279 vs 339 us: with
+// 64-96 chunks per tile the DMA issue the eight waves take on costs more than
+// the fragment reads they save); tune key 37 = 1: off
 bool dconv_ws8_ok(const sel_dconv_desc* d) {
-  return tune(37) != 1 && (d->K == 2 || d->K == 5) && (d->So * d->Ng) % 256 == 0 && dconv_ws_mode(d) >= 0;
+  return tune(37) != 1 && d->K == 2 && d->S * d->Cg <= 512 && (d->So * d->Ng) % 256 == 0 && dconv_ws_mode(d) >= 0;
 }
 
 int dconv_ws_fwd(const sel_dconv_desc* d, const void* x, const void* wp, const float* bias, const void* aux,

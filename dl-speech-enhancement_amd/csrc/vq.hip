@@ -408,26 +408,34 @@ __global__ __launch_bounds__(256) void k_rvq_prep(const float* __restrict__ embe
 
 constexpr int SM = 16;  // max stages of the matrix-core variant (per-stage state in LDS)
 
-__global__ __launch_bounds__(TM) __attribute__((amdgpu_waves_per_eu(4))) void k_rvq_mfma(
+// RG row groups of 16 rows per block share every codebook tile: each wave's
+// B operands (4 KB per 16-code tile, read from L2) feed RG independent MFMA
+// chains.  RG = 2 halves the codebook reads per row (the hypothesis: the L2 ->
+// CU rate binds at C3, 320 blocks x 8 stages x 256 KB) at the same busiest-CU
+// MFMA work, but measured slower (160 blocks, one per CU, at 2 waves per SIMD:
+// 169 -> 193 us per forward), so RG = 1 is the default (tune key 39 = 2: RG = 2).
+template <int RG>
+__global__ __launch_bounds__(TM) __attribute__((amdgpu_waves_per_eu(RG == 1 ? 4 : 2))) void k_rvq_mfma(
     const float* __restrict__ x, int64_t N, int D, const float* __restrict__ embeds, int S, int K,
     const float* __restrict__ ep_all, const float* __restrict__ en_all, float* __restrict__ out,
     int64_t* __restrict__ idx, double* __restrict__ partials) {
-  __shared__ float resT[DM * RM];  // [d][row]: the A-fragment reads hit 64 distinct banks
-  __shared__ float acc_o[RM * DM];
-  __shared__ float xn[RM];
-  __shared__ float red_d[NWM][RM];
-  __shared__ int red_k[NWM][RM];
-  __shared__ int sel_k[SM][RM];    // chosen codes, written to idx after the last stage
+  constexpr int RB = RM * RG;      // rows per block
+  __shared__ float resT[DM * RB];  // [d][row]: the A-fragment reads hit 64 distinct banks
+  __shared__ float acc_o[RB * DM];
+  __shared__ float xn[RB];
+  __shared__ float red_d[NWM][RB];
+  __shared__ int red_k[NWM][RB];
+  __shared__ int sel_k[SM][RB];    // chosen codes, written to idx after the last stage
   __shared__ float sq_t[SM][TM];   // per-thread SSE per stage, reduced after the last stage
   __shared__ double red[16];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int col = lane & 15, h = lane >> 4;
-  const int64_t r0 = int64_t(blockIdx.x) * RM;
-  for (int i = tid; i < RM * D; i += TM) {
+  const int64_t r0 = int64_t(blockIdx.x) * RB;
+  for (int i = tid; i < RB * D; i += TM) {
     const int r = i / D, d = i % D;
     const int64_t row = r0 + r;
-    resT[d * RM + r] = row < N ? x[row * D + d] : 0.f;
+    resT[d * RB + r] = row < N ? x[row * D + d] : 0.f;
     acc_o[r * D + d] = 0.f;
   }
   const int ns = D / 4;
@@ -454,73 +462,86 @@ __global__ __launch_bounds__(TM) __attribute__((amdgpu_waves_per_eu(4))) void k_
   for (int s = 0; s < S; ++s) {
     const float* __restrict__ E = embeds + int64_t(s) * D * K;
     const float* __restrict__ enS = en_all + int64_t(s) * K;
-    for (int r = wave; r < RM; r += NWM) {
+    for (int r = wave; r < RB; r += NWM) {
       float v = 0.f;
-      for (int d = lane; d < D; d += 64) v = fmaf(resT[d * RM + r], resT[d * RM + r], v);
+      for (int d = lane; d < D; d += 64) v = fmaf(resT[d * RB + r], resT[d * RB + r], v);
       v = wave_sum(v);
       if (lane == 0) xn[r] = v;
     }
-    float a[DM / 4];
+    float a[RG][DM / 4];
 #pragma unroll
-    for (int j = 0; j < DM / 4; ++j) a[j] = j < ns ? resT[(4 * j + h) * RM + col] : 0.f;
+    for (int q = 0; q < RG; ++q)
+#pragma unroll
+      for (int j = 0; j < DM / 4; ++j) a[q][j] = j < ns ? resT[(4 * j + h) * RB + RM * q + col] : 0.f;
     __syncthreads();
-    float xr[4];
+    float xr[RG][4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) xr[i] = xn[4 * h + i];
-    float bd[4];
-    int bk[4];
+    for (int q = 0; q < RG; ++q)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      bd[i] = __builtin_inff();
-      bk[i] = 0x7fffffff;
-    }
+      for (int i = 0; i < 4; ++i) xr[q][i] = xn[RM * q + 4 * h + i];
+    float bd[RG][4];
+    int bk[RG][4];
+#pragma unroll
+    for (int q = 0; q < RG; ++q)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        bd[q][i] = __builtin_inff();
+        bk[q][i] = 0x7fffffff;
+      }
     for (int p = wave; p < ntile; p += NWM) {
       if (p + NWM < ntile)
         load(s, p + NWM, nxt);
       else if (s + 1 < S)
         load(s + 1, wave, nxt);
-      f32x4 c = {0.f, 0.f, 0.f, 0.f};
+      f32x4 c[RG];
+#pragma unroll
+      for (int q = 0; q < RG; ++q) c[q] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int j = 0; j < DM / 4; ++j) {
         if (j < ns) {
           const float4 bv = cur[j >> 2];
           const float bj = (j & 3) == 0 ? bv.x : (j & 3) == 1 ? bv.y : (j & 3) == 2 ? bv.z : bv.w;
-          c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], bj, c, 0, 0, 0);
+#pragma unroll
+          for (int q = 0; q < RG; ++q) c[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[q][j], bj, c[q], 0, 0, 0);
         }
       }
       const int k = tile_of(p) * 16 + col;
       const bool kin = k < K;
       const float ek = kin ? enS[k] : 0.f;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {  // C/D map: col = lane & 15 (code), row = 4 (lane >> 4) + i
-        const float dist = (xr[i] - 2.f * c[i]) + ek;
-        const bool take = kin && better(dist, k, bd[i], bk[i]);
-        bd[i] = take ? dist : bd[i];
-        bk[i] = take ? k : bk[i];
-      }
+      for (int q = 0; q < RG; ++q)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {  // C/D map: col = lane & 15 (code), row = 4 (lane >> 4) + i
+          const float dist = (xr[q][i] - 2.f * c[q][i]) + ek;
+          const bool take = kin && better(dist, k, bd[q][i], bk[q][i]);
+          bd[q][i] = take ? dist : bd[q][i];
+          bk[q][i] = take ? k : bk[q][i];
+        }
 #pragma unroll
       for (int j4 = 0; j4 < DM / 16; ++j4) cur[j4] = nxt[j4];
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      float d0 = bd[i];
-      int k0 = bk[i];
+    for (int q = 0; q < RG; ++q)
 #pragma unroll
-      for (int o = 8; o > 0; o >>= 1) {  // the 16 lanes of one row group
-        const float d1 = __shfl_xor(d0, o, 64);
-        const int k1 = __shfl_xor(k0, o, 64);
-        if (better(d1, k1, d0, k0)) {
-          d0 = d1;
-          k0 = k1;
+      for (int i = 0; i < 4; ++i) {
+        float d0 = bd[q][i];
+        int k0 = bk[q][i];
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) {  // the 16 lanes of one row group
+          const float d1 = __shfl_xor(d0, o, 64);
+          const int k1 = __shfl_xor(k0, o, 64);
+          if (better(d1, k1, d0, k0)) {
+            d0 = d1;
+            k0 = k1;
+          }
+        }
+        if (col == 0) {
+          red_d[wave][RM * q + 4 * h + i] = d0;
+          red_k[wave][RM * q + 4 * h + i] = k0;
         }
       }
-      if (col == 0) {
-        red_d[wave][4 * h + i] = d0;
-        red_k[wave][4 * h + i] = k0;
-      }
-    }
     __syncthreads();
-    if (tid < RM) {
+    if (tid < RB) {
       float d0 = red_d[0][tid];
       int k0 = red_k[0][tid];
       for (int w = 1; w < NWM; ++w)
@@ -532,27 +553,27 @@ __global__ __launch_bounds__(TM) __attribute__((amdgpu_waves_per_eu(4))) void k_
     }
     __syncthreads();
     float sq = 0.f;
-    for (int i = tid; i < RM * D; i += TM) {
+    for (int i = tid; i < RB * D; i += TM) {
       const int r = i / D, d = i % D;
       if (r0 + r >= N) continue;
       const float q = E[int64_t(d) * K + sel_k[s][r]];
-      const float rv = resT[d * RM + r];
+      const float rv = resT[d * RB + r];
       const float diff = q - rv;
       sq = fmaf(diff, diff, sq);
       const float qst = rv + diff;
-      resT[d * RM + r] = rv - qst;
+      resT[d * RB + r] = rv - qst;
       acc_o[r * D + d] += qst;
     }
     sq_t[s][tid] = sq;
     __syncthreads();
   }
-  for (int i = tid; i < RM * D; i += TM) {
+  for (int i = tid; i < RB * D; i += TM) {
     const int r = i / D, d = i % D;
     const int64_t row = r0 + r;
     if (row < N) out[row * D + d] = acc_o[r * D + d];
   }
-  for (int i = tid; i < S * RM; i += TM) {
-    const int st = i / RM, r = i % RM;
+  for (int i = tid; i < S * RB; i += TM) {
+    const int st = i / RB, r = i % RB;
     if (r0 + r < N) idx[int64_t(st) * N + r0 + r] = sel_k[st][r];
   }
   for (int st = 0; st < S; ++st) {
@@ -658,7 +679,10 @@ int sel_rvq_fwd(const float* x, int64_t N, int D, const float* embeds, int S, in
   const int variant = tune(2);
   const bool mfma = D % 4 == 0 && D <= DM && K <= kHistMaxK && S <= SM && variant == 0;
   const bool staged = !mfma && D % DC == 0 && K % 4 == 0 && variant != 1;
-  const int rows = mfma ? RM : staged ? R2 : ROWS;
+  // matrix-core rows per block: one 16-row group (tune key 39 = 2: two groups
+  // sharing each codebook tile, measured slower at C3: 169 -> 193 us per RVQ
+  // forward with its prep / histogram / finish, alternating in one call)
+  const int rows = mfma ? ((N + 2 * RM - 1) / (2 * RM) >= 128 && tune(39) == 2 ? 2 * RM : RM) : staged ? R2 : ROWS;
   const int nb = int((N + rows - 1) / rows);
   double* part = static_cast<double*>(ws);
   if (nb > 0 && mfma) {
@@ -667,7 +691,10 @@ int sel_rvq_fwd(const float* x, int64_t N, int D, const float* embeds, int S, in
     const int64_t nprep = std::max<int64_t>(int64_t(S) * MfmaGeo(D, K).stage_floats() / 4, int64_t(S) * K);
     hipLaunchKernelGGL(k_rvq_prep, dim3(unsigned((nprep + 255) / 256)), dim3(256), 0, s, embeds, S, D, K, ep, en);
     SEL_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_rvq_mfma, dim3(nb), dim3(TM), 0, s, x, N, D, embeds, S, K, ep, en, out, idx, part);
+    if (rows == 2 * RM)
+      hipLaunchKernelGGL(k_rvq_mfma<2>, dim3(nb), dim3(TM), 0, s, x, N, D, embeds, S, K, ep, en, out, idx, part);
+    else
+      hipLaunchKernelGGL(k_rvq_mfma<1>, dim3(nb), dim3(TM), 0, s, x, N, D, embeds, S, K, ep, en, out, idx, part);
     SEL_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_rvq_hist, dim3(unsigned((N + kHistRows - 1) / kHistRows), unsigned(S)), dim3(512), 0, s,
                        idx, N, K, counts);

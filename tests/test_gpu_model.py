@@ -240,12 +240,14 @@ def test_rvq_kernels_bit_identical(gpu, N, D, K, S):
     emb = torch.randn(S, D, K, device=gpu)
     lib = L.lib()
     outs = []
-    for v in (1, 0, 2):
-        prev = lib.sel_tune(2, v)
+    # (key 2, key 39): direct, matrix-core, staged, matrix-core with two row groups per block
+    for v, g in ((1, 0), (0, 0), (2, 0), (0, 2)):
+        prev, prevg = lib.sel_tune(2, v), lib.sel_tune(39, g)
         try:
             outs.append([t.clone() for t in ResidualVQFn.apply(x, emb, 1.0)])
         finally:
             lib.sel_tune(2, prev)
+            lib.sel_tune(39, prevg)
     o1, l1, p1, i1 = outs[0]
     for o0, l0, p0, i0 in outs[1:]:
         assert torch.equal(i0, i1) and torch.equal(o0, o1) and torch.equal(p0, p1)

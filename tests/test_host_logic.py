@@ -165,12 +165,12 @@ def test_c5_mpd_layers_take_the_flat_warp_specialised_tiles():
                 adj.append(DC.kernel(DC._dgrad_desc(sp, Bs, Ta, To, Toa, 0.1, li > 0, T_in=Ti), torch.bfloat16))
             assert [f[0] for f in fwd[1:5]] == ["ws_flat"] * 4, (clips, p, fwd)
             assert [a[0] for a in adj[2:5]] == ["ws_flat"] * 3, (clips, p, adj)
-            # 512 / 1024-wide layers on the eight-wave 256 x 256 kernel, the 128-wide one on the 12-wave
-            assert fwd[4][1] == "k_conv_ws8<5, bf16, 256, 256>" and fwd[1][1] == "k_conv_ws_bf16<2>"
-            assert fwd[3][1] == "k_conv_ws8<2, bf16, 256, 256>"
+            # the 128 -> 512 layer on the eight-wave 256 x 256 kernel, the others on the 12-wave one
+            assert fwd[4][1] == "k_conv_ws_bf16<5>" and fwd[1][1] == "k_conv_ws_bf16<2>"
+            assert fwd[3][1] == "k_conv_ws_bf16<2>" and fwd[2][1] == "k_conv_ws8<2, bf16, 256, 256>"
             prev = lib.sel_tune(37, 1)
             try:
-                assert DC.kernel(DC._fwd_desc(specs[4], Bs, *geo[4], 0.1), torch.bfloat16)[1] == "k_conv_ws_bf16<5>"
+                assert DC.kernel(DC._fwd_desc(specs[2], Bs, *geo[2], 0.1), torch.bfloat16)[1] == "k_conv_ws_bf16<2>"
             finally:
                 lib.sel_tune(37, prev)
             prev = lib.sel_tune(22, 1)

@@ -13,7 +13,7 @@ for cfg in "$@"; do
   tune=${cfg%%|*}
   envs=""
   [[ "$cfg" == *"|"* ]] && envs=${cfg#*|} && envs=${envs//|/ }
-  tag=${cfg//[,|=]/_}
+  tag=${cfg//[,|=\/]/_}; tag=${tag:0:60}
   env SEL_TUNE=$tune $envs timeout -k 10 300 python bench.py $ARGS --no-cpu-baseline --no-fp32-companion > gpurun_out/ab_${i}_$tag.log 2>&1 || exit 1
   echo "cfg=$cfg $(tail -1 gpurun_out/ab_${i}_$tag.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print("mean", d["ms_per_step"], "median", d["median_ms_per_step"], d["value"], d["roofline"]["kernel"], d["roofline"]["frac"])')"
 done
