@@ -939,7 +939,11 @@ struct Ws8 {
   static constexpr int NB = 3;                      // ring slots
   static constexpr int BUF = (XROWS + KT * BN) * WS_CK;  // bf16 elements per slot
   static constexpr int EP = BN + 4;                 // fp32 epilogue pitch (conflict-free 16-B writes)
-  static constexpr size_t RING = size_t(NB) * BUF * 2, EPI = size_t(128) * EP * 4;
+  static constexpr size_t RING = size_t(NB) * BUF * 2;
+  // epilogue pass rows: 256 where that fp32 tile fits over the ring (the 512 x
+  // 128 tiles: 2 passes instead of 4, half the exposed aux / res load latency)
+  static constexpr int PR = (BM >= 256 && size_t(256) * EP * 4 <= RING) ? 256 : 128;
+  static constexpr size_t EPI = size_t(PR) * EP * 4;
   static constexpr size_t LDS = RING > EPI ? RING : EPI;
   static_assert(XROWS % WS_RPI == 0 && WI * WS_RPI == KT * BN && LDS <= 160 * 1024, "LDS");
   static_assert(2 * PW < 64, "vmcnt range");
@@ -1078,19 +1082,19 @@ __global__ __launch_bounds__(512) void k_conv_ws8(Args a, const __bf16* __restri
   }
   if (dbg & 8) return;
 
-  // epilogue in BM / 128 passes of 128 rows: the waves whose rows fall in pass p
-  // write their accumulators into an fp32 [128][BN + 4] tile over the (drained)
+  // epilogue in BM / PR passes of PR rows: the waves whose rows fall in pass p
+  // write their accumulators into an fp32 [PR][BN + 4] tile over the (drained)
   // ring, then all 8 waves run row-contiguous 16-B accesses (the 12-wave
   // kernel's epilogue)
   struct alignas(16) V8 { TO v[8]; };
-  constexpr int BNV = BN / 8, EV = 128 * BNV / 512, NP = BM / 128;
+  constexpr int PR = G::PR, BNV = BN / 8, EV = PR * BNV / 512, NP = BM / PR;
   float* const tile = reinterpret_cast<float*>(smem);
 #pragma unroll
   for (int p = 0; p < NP; ++p) {
-    if (wm * G::WTM / 128 == p) {
+    if (wm * G::WTM / PR == p) {
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        const int r = wm * G::WTM % 128 + i * 32 + (lane & 31);
+        const int r = wm * G::WTM % PR + i * 32 + (lane & 31);
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -1103,7 +1107,7 @@ __global__ __launch_bounds__(512) void k_conv_ws8(Args a, const __bf16* __restri
       }
     }
     __syncthreads();
-    const int prow = p * 128;
+    const int prow = p * PR;
 #pragma unroll
     for (int u = 0; u < EV; ++u) {
       const int v = tid + u * 512;
