@@ -13,8 +13,12 @@ form.  Autograd runs each chain's backward on the stream of its forward and
 synchronises the streams where gradients cross them (torch's stream semantics
 of backward passes).
 
-SEL_D_STREAMS = number of side streams (default 4, one per hardware queue:
-GPU_MAX_HW_QUEUES); 0 = everything on the current stream.
+SEL_D_STREAMS = number of side streams (default 8: one per chain; 0 =
+everything on the current stream).  Measured at C5, alternating in one call:
+8 streams 35.2 / 35.4 ms median, 4 streams 36.1 / 35.8, 2 streams 35.8 / 35.8,
+serial 41.8 (an earlier call); raising GPU_MAX_HW_QUEUES from the box's 4 to 8 made the step
+48-54 ms.  Launching D(target) on the side streams before the generator
+forward (it needs neither) measured neutral (35.8 vs 35.9-36.1 ms median).
 """
 import os
 
@@ -24,7 +28,7 @@ _POOL = {}
 
 
 def side_streams(device):
-    n = int(os.environ.get("SEL_D_STREAMS", "4"))
+    n = int(os.environ.get("SEL_D_STREAMS", "8"))
     if n <= 0 or device.type != "cuda":
         return []
     key = (device.index, n)
