@@ -554,9 +554,18 @@ def main():
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knobs for the multi-rank path on a box with fewer GPUs than
+    # ranks (tests only): SEL_BENCH_BACKEND=gloo, SEL_BENCH_SHARE_GPU=1 (rank r
+    # on GPU r mod count); the driver's runs use RCCL, one rank per GPU
+    backend = os.environ.get("SEL_BENCH_BACKEND", "nccl")
+    if os.environ.get("SEL_BENCH_SHARE_GPU", "0") == "1":
+        local = local % torch.cuda.device_count()
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
 
     from sel import _lib

@@ -29,6 +29,10 @@ class ResidualVQFn(torch.autograd.Function):
         ctx.save_for_backward(x, embeds, idx)
         ctx.commitment = float(commitment)
         ctx.mark_non_differentiable(ppl, idx)
+        # the perplexities / indices (and an unused loss) take no gradient:
+        # None in backward instead of materialised zero tensors (two fill
+        # launches per step)
+        ctx.set_materialize_grads(False)
         ctx.counts = counts
         return out, loss, ppl, idx
 

@@ -19,7 +19,9 @@ def timed(fn, iters=20):
     return e0.elapsed_time(e1) * 1e3 / iters
 
 gpu = torch.device("cuda")
-B, T, C = 64, 24000, 32
+# RU_C=64: the 64-channel units at their C3 length (T = 8000)
+C = int(os.environ.get("RU_C", "32"))
+B, T = 64, (24000 if C == 32 else 8000)
 x = (0.5 * torch.randn(B * T, C, device=gpu)).to(torch.bfloat16)
 h = (0.5 * torch.randn(B * T, C, device=gpu)).to(torch.bfloat16)
 g = (0.5 * torch.randn(B * T, C, device=gpu)).to(torch.bfloat16)
