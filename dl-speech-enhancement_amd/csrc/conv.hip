@@ -310,6 +310,23 @@ __global__ __launch_bounds__(256) void k_conv_fwd(Args a, const TI* __restrict__
 // ---------------------------------------------------------------------------
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 constexpr int F4_HALOMAX = 64;
+// residual-unit kernels' occupancy targets (waves per SIMD the register
+// allocation must allow)
+#ifndef SEL_W_RU32F
+#define SEL_W_RU32F 3
+#endif
+#ifndef SEL_W_RU32B
+#define SEL_W_RU32B 1
+#endif
+#ifndef SEL_W_RU32W
+#define SEL_W_RU32W 2
+#endif
+#ifndef SEL_W_RU64F
+#define SEL_W_RU64F 2
+#endif
+#ifndef SEL_W_RU64B
+#define SEL_W_RU64B 2
+#endif
 constexpr int F4_P = 40;  // staged row pitch (bf16 elements) = 80 B
 
 // XCD-aware block order for multi-column-tile launches (1-D grid of
@@ -1723,7 +1740,7 @@ __device__ __forceinline__ void ru_wfrags(const __bf16* __restrict__ wp, bf16x8 
 }
 
 template <int R>
-__global__ __launch_bounds__(256) void k_ru32_fwd(Args a, const __bf16* __restrict__ x,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU32F))) void k_ru32_fwd(Args a, const __bf16* __restrict__ x,
                                                   const __bf16* __restrict__ w1p, const float* __restrict__ b1,
                                                   const __bf16* __restrict__ w2p, const float* __restrict__ b2,
                                                   __bf16* __restrict__ hout, __bf16* __restrict__ out,
@@ -1836,7 +1853,7 @@ struct Ru64 {
 };
 
 template <int R>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_ru64_fwd(Args a, const __bf16* __restrict__ x,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU64F))) void k_ru64_fwd(Args a, const __bf16* __restrict__ x,
                                                   const __bf16* __restrict__ w1p, const float* __restrict__ b1,
                                                   const __bf16* __restrict__ w2p, const float* __restrict__ b2,
                                                   __bf16* __restrict__ hout, __bf16* __restrict__ out,
@@ -2012,7 +2029,7 @@ struct Ru64B {
 };
 
 template <int R>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_ru64_bwd(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU64B))) void k_ru64_bwd(
     Args a, const __bf16* __restrict__ g, const __bf16* __restrict__ h, const __bf16* __restrict__ x,
     const __bf16* __restrict__ wd1, const __bf16* __restrict__ wd2, __bf16* __restrict__ ghout,
     __bf16* __restrict__ gx, int tiles_per_block) {
@@ -2193,7 +2210,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 // (and HBM when the weight gradient needs it); gx = conv1^T(gh) * ELU'(x) + g.
 // wd1 / wd2 are the dgrad-packed weights of the primitive path.
 template <int R>
-__global__ __launch_bounds__(256) void k_ru32_bwd(Args a, const __bf16* __restrict__ g,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU32B))) void k_ru32_bwd(Args a, const __bf16* __restrict__ g,
                                                   const __bf16* __restrict__ h, const __bf16* __restrict__ x,
                                                   const __bf16* __restrict__ wd1, const __bf16* __restrict__ wd2,
                                                   __bf16* __restrict__ ghout, __bf16* __restrict__ gx,
@@ -2695,7 +2712,7 @@ struct Ru32W {
 };
 
 template <int R>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_ru32_bwdw(Args a, const __bf16* __restrict__ g,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU32W))) void k_ru32_bwdw(Args a, const __bf16* __restrict__ g,
                                                    const __bf16* __restrict__ h, const __bf16* __restrict__ x,
                                                    const __bf16* __restrict__ wd1, const __bf16* __restrict__ wd2,
                                                    __bf16* __restrict__ gx, float* __restrict__ part1,

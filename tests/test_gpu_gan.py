@@ -372,3 +372,41 @@ def test_gan_step_reused_real_half_matches_concatenated(gpu, dt, monkeypatch):
     exact = all(torch.equal(a, b) for a, b in zip(res[1][1], res[0][1]))
     print(f"reuse vs concatenated ({dt}): grad rel {(num / den) ** 0.5:.3e}, bit-equal {exact}")
     assert (num / den) ** 0.5 <= tol, (num / den) ** 0.5
+
+
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+def test_gan_step_side_streams_bit_identical_to_serial(gpu, dt, monkeypatch):
+    """The sub-discriminator chains on side streams (sel.streams, SEL_D_STREAMS)
+    against everything on one stream: the same kernels in the same order per
+    chain, so the losses and the generator and discriminator gradients are
+    bit-identical (twice with streams on: a missing stream dependency would
+    show up as a difference from the serial run)."""
+    from models.autoencoder_without_PQC.AudioDec import Generator
+    from sel import configs
+    from sel.convops import precision
+    from train_denoise import DenoiseStep
+    g = golden("gan_step")
+    gp = dict(encode_channels=4, decode_channels=4, code_dim=64, codebook_num=2, codebook_size=64)
+    x, y = torch.from_numpy(g["x_noisy"]), torch.from_numpy(g["x_clean"])
+    res = []
+    for n_streams in ("0", "8", "2", "8"):
+        monkeypatch.setenv("SEL_D_STREAMS", n_streams)
+        G = Generator(**gp)
+        G.load_state_dict({k[3:]: torch.from_numpy(v) for k, v in golden("generator_nopqc").items()
+                           if k.startswith("sd.")})
+        G = G.to(gpu)
+        D, _ = _disc(gpu)
+        step = DenoiseStep(configs.get("symAD_vctk_48000_hop300"), gpu, generator=G, discriminator=D)
+        step.discriminator_enabled = True
+        step.optimizer["discriminator"].step = lambda *a, **k: None
+        step.optimizer["generator"].step = lambda *a, **k: None
+        with precision(torch.float32 if dt == "fp32" else torch.bfloat16):
+            gen, dis, frags = step.model_step(y, x)
+        torch.cuda.synchronize()
+        res.append(([gen.item(), dis.item()] + [float(v) for _, v in frags[:3]],
+                    [p.grad.detach().clone() for p in list(D.parameters()) + list(G.parameters())
+                     if p.grad is not None]))
+    for r in res[1:]:
+        assert r[0] == res[0][0], (r[0], res[0][0])
+        assert len(r[1]) == len(res[0][1]) > 0
+        assert all(torch.equal(a, b) for a, b in zip(r[1], res[0][1]))
