@@ -3175,6 +3175,10 @@ __global__ __launch_bounds__(256) void k_wgrad2_bf16(Args a, const __bf16* __res
   }
 }
 
+// rows of one k_wgrad3_bf16 X plane: the 128-row tile + this layer's halo,
+// rounded up to 16 rows (at most W2_BM + W2_HALO)
+__host__ __device__ constexpr int wgrad3_xrows(int K, int dil) { return W2_BM + (((K - 1) * dil + 15) & ~15); }
+
 // bf16 weight gradient, general tr-read path (C % 32 == 0, N % 32 == 0,
 // halo <= 64, K <= 8).  A block owns NB = 32*NT output channels x CB = 32*CT
 // input channels x ALL K taps over a contiguous range of 128-row tiles, so a
@@ -3196,7 +3200,7 @@ __global__ __launch_bounds__(256) void k_wgrad3_bf16(Args a, const __bf16* __res
   constexpr int XROWS = W2_BM + W2_HALO;
   constexpr int GV = W2_BM * NB / 8 / 256;   // 2*NT
   constexpr int XV = XROWS * CB / 8 / 256;   // 3*CT
-  constexpr int GS = NT * W2_BM * 32, XS = CT * XROWS * 32;
+  constexpr int GS = NT * W2_BM * 32;
   constexpr int WPN = 4 / NT;                // waves per 32-wide n subtile
   extern __shared__ __align__(16) unsigned char smem[];
   __bf16* const base = reinterpret_cast<__bf16*>(smem);  // [buf]{G[NT][128][32], X[CT][192][32]}
@@ -3209,6 +3213,10 @@ __global__ __launch_bounds__(256) void k_wgrad3_bf16(Args a, const __bf16* __res
   const int64_t te = tb + tiles_per_split < n_tiles ? tb + tiles_per_split : n_tiles;
   const int halo = (a.K - 1) * a.dil;
   const int span = W2_BM + halo;
+  // X planes sized for this layer's halo (wgrad3_xrows; the launch sizes the LDS
+  // the same way): a k1 / k3 layer's blocks need less LDS, more fit on a CU
+  const int xrows = wgrad3_xrows(a.K, a.dil);
+  const int XS = CT * xrows * 32;
   // wave -> (n subtile, (ct, k) pairs); too few pairs -> the waves split the rows
   const int P = CT * a.K;
   const int RG = P >= WPN ? 1 : WPN / P;     // P in {1, 2} when RG > 1
@@ -3259,11 +3267,12 @@ __global__ __launch_bounds__(256) void k_wgrad3_bf16(Args a, const __bf16* __res
       if (u * 256 / (CB / 8) >= span) continue;
       const int v = tid + u * 256;
       const int r = v / (CB / 8), c8 = v % (CB / 8);
+      if (r >= span) continue;  // the X planes end at xrows (no tap reads past span - 1)
       uint4 val = xok[u] ? xr[u] : make_uint4(0, 0, 0, 0);
       if (a.in_elu) {
         val = elu8(val);
       }
-      *reinterpret_cast<uint4*>(x + (c8 >> 2) * (XROWS * 32) + r * 32 + (c8 & 3) * 8) = val;
+      *reinterpret_cast<uint4*>(x + (c8 >> 2) * (xrows * 32) + r * 32 + (c8 & 3) * 8) = val;
     }
   };
 
@@ -3274,7 +3283,7 @@ __global__ __launch_bounds__(256) void k_wgrad3_bf16(Args a, const __bf16* __res
   for (int j = 0; j < MAXT; ++j) {
     int p = pw + WPP * j;
     p = p < P ? p : P - 1;
-    xoff[j] = (p / a.K) * (XROWS * 32) + (p % a.K) * a.dil * 32;
+    xoff[j] = (p / a.K) * (xrows * 32) + (p % a.K) * a.dil * 32;
   }
 
   floatx16 acc[MAXT];
@@ -4298,13 +4307,14 @@ WgPlan wgrad_plan(const sel_conv_desc* d, int mode) {
 template <int NT, int CT>
 hipError_t launch_wgrad3(const WgPlan& p, const Args& a, const __bf16* gout, const __bf16* in, float* part,
                          float* bpart, hipStream_t s) {
-  constexpr size_t lds = size_t(2) * (NT * W2_BM * 32 + CT * (W2_BM + W2_HALO) * 32) * sizeof(__bf16);
+  constexpr size_t lds_max = size_t(2) * (NT * W2_BM * 32 + CT * (W2_BM + W2_HALO) * 32) * sizeof(__bf16);
+  const size_t lds = size_t(2) * (NT * W2_BM * 32 + CT * wgrad3_xrows(a.K, a.dil) * 32) * sizeof(__bf16);
   dim3 grid(unsigned(p.nsplit), unsigned(a.N / (32 * NT)), unsigned(a.C / (32 * CT)));
 #define SEL_WG3(MT)                                                                                            \
   {                                                                                                            \
     auto kern = k_wgrad3_bf16<NT, CT, MT>;                                                                     \
-    if (lds > 64 * 1024) {                                                                                     \
-      hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)); \
+    if (lds_max > 64 * 1024) {                                                                                 \
+      hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds_max)); \
       if (e != hipSuccess) return e;                                                                           \
     }                                                                                                          \
     hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, a, gout, in, int(p.tiles_per_sample), p.n_tiles,          \
