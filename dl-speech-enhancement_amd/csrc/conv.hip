@@ -2089,7 +2089,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU64B
     __syncthreads();  // every wave is done with the previous tile's gs / ghs
     store();
     __syncthreads();
-    if (tile + 1 < tile_end) load(tile + 1);
     // h rows of a gh unit (the ELU'(h) factor), one unit ahead of its MFMAs
     auto load_h = [&](int unit, uint2 (&hq)[4]) {
       const int sb = unit >> 1, sl = unit & 1;
@@ -2162,6 +2161,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU64B
       }
     }
     __syncthreads();
+    // the next tile's g rows, requested after the gh phase: its h / x / weight
+    // loads then wait only for each other (memory counters retire in order),
+    // and this request has the gx phase to land
+    if (tile + 1 < tile_end) load(tile + 1);
     // gx = conv1^T(gh) * ELU'(x) + g (k_conv_thin_bf16 order: taps, chunks, sub-tiles)
     floatx16 acc[G::TM];
 #pragma unroll
@@ -2242,7 +2245,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU32B
     __syncthreads();  // every wave is done with the previous tile's g / gh rows
     st.store(gs, span, false);
     __syncthreads();
-    if (tile + 1 < tile_end) st.load(a, g, (tile + 1) / tps, int((tile + 1) % tps) * R, 0, span);
     // every global operand of this tile's MFMA phases is requested up front (L2-hot:
     // h and x rows of the tile): ELU'(h) for this wave's gh sub-tiles, ELU'(x) for its gx sub-tiles
     constexpr int NSUB_W = (G::SPAN / 32 + 3) / 4;  // gh sub-tiles per wave (max)
@@ -2298,6 +2300,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU32B
       }
     }
     __syncthreads();
+    // the next tile's g rows, requested after the gh phase (k_ru64_bwd)
+    if (tile + 1 < tile_end) st.load(a, g, (tile + 1) / tps, int((tile + 1) % tps) * R, 0, span);
 #pragma unroll
     for (int i = 0; i < G::TM; ++i) {
       const int lr = wave * (R / 4) + i * 32 + (lane & 31);
@@ -2766,10 +2770,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU32W
       st.store(gs, span, false);
       sx.store(xs, span, true, nullptr, 0, PW);
       __syncthreads();
-      if (tile + 1 < tile_end) {
-        st.load(a, g, (tile + 1) / tps, int((tile + 1) % tps) * R, 0, span);
-        sx.load(a, x, (tile + 1) / tps, int((tile + 1) % tps) * R, -halo, span);
-      }
       constexpr int NSUB_W = (G::SPAN / 32 + 3) / 4;
       uint2 hpre[NSUB_W][4], xpre[Ru32<R>::TM][4];
 #pragma unroll
@@ -2828,6 +2828,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU32W
         }
       }
       __syncthreads();
+      // the next tile's g and x rows, requested after the gh phase (k_ru64_bwd)
+      if (tile + 1 < tile_end) {
+        st.load(a, g, (tile + 1) / tps, int((tile + 1) % tps) * R, 0, span);
+        sx.load(a, x, (tile + 1) / tps, int((tile + 1) % tps) * R, -halo, span);
+      }
       // gx = conv1^T(gh) * ELU'(x) + g (k_ru32_bwd)
 #pragma unroll
       for (int i = 0; i < Ru32<R>::TM; ++i) {
