@@ -1684,22 +1684,38 @@ struct Ru32 {
   static_assert(R % 128 == 0, "ru32 tile rows");
 };
 
+// one sample's rows as a buffer resource (bytes < 2^31: the launchers check
+// T * C * 2) and a 16-B load from it; RU_OOB is past any sample's bytes, so a
+// load there returns zeros and touches no memory
+constexpr int RU_OOB = 0x7ffffff0;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t ru_rsrc(const __bf16* base, int64_t elems) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(base), 0, int(elems * 2), 0x00020000);
+}
+__device__ __forceinline__ uint4 ru_bload(__amdgpu_buffer_rsrc_t rs, int byte_off) {
+  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, byte_off, 0, 0));
+}
+
 // stage `span` rows of a 32-channel tensor starting at sample row t0 + off
 // (rows outside [0, T) -> zero) into registers / LDS (optionally ELU'd)
 template <int R>
 struct Ru32Stage {
   uint4 r[Ru32<R>::XV];
   bool ok[Ru32<R>::XV];
+  // Buffer loads over sample b: rows outside [0, T), past the span or of a
+  // dead request (live = false: no next tile) take an out-of-range offset and
+  // return zeros without touching memory.  No branch around any load, so the
+  // compiler counts this request exactly and later waits in the tile loop do
+  // not fall back to vmcnt(0) behind it.
   __device__ __forceinline__ void load(const Args& a, const __bf16* __restrict__ src, int64_t b, int t0, int off,
-                                       int span) {
+                                       int span, bool live = true) {
+    const __amdgpu_buffer_rsrc_t rs = ru_rsrc(src + b * a.T * RU_C, a.T * RU_C);
 #pragma unroll
     for (int u = 0; u < Ru32<R>::XV; ++u) {
       const int v = threadIdx.x + u * 256;
       const int row = v >> 2, c = (v & 3) * 8;
-      int ti = t0 + off + row;
+      const int ti = t0 + off + row;
       ok[u] = row < span && ti >= 0 && ti < a.T;
-      ti = ti < 0 ? 0 : (ti >= a.T ? a.T - 1 : ti);
-      if ((u * 256) / 4 < span) r[u] = *reinterpret_cast<const uint4*>(src + (b * a.T + ti) * RU_C + c);
+      r[u] = ru_bload(rs, live && ok[u] ? (ti * RU_C + c) * 2 : RU_OOB);
     }
   }
   // raw != nullptr: rows [raw_off, raw_off + R) are also stored un-ELU'd into raw
@@ -1760,7 +1776,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU32F
   bf16x8 wf[RU_K][2], w2f[1][2];
   ru_wfrags<RU_K>(w1p, wf);
   ru_wfrags<1>(w2p, w2f);
+  ws_wait_vm<0>();  // weights landed: the tile loop's waits then count only its own loads
 
+  // both biases staged in LDS once (k_ru64_fwd)
+  __shared__ __align__(16) float bsm[2][RU_C];
+  if (threadIdx.x < 2 * RU_C) {
+    const int i = threadIdx.x;
+    const float* bp = i < RU_C ? b1 : b2;
+    bsm[i / RU_C][i % RU_C] = bp ? bp[i % RU_C] : 0.f;
+  }
   Ru32Stage<R> st;
   st.load(a, x, tile0 / tps, int(tile0 % tps) * R, -a.pad, span);
   for (int64_t tile = tile0; tile < tile_end; ++tile) {
@@ -1770,7 +1794,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU32F
     __syncthreads();  // every wave is done with the previous tile's rows
     st.store(xs, span, true, xr, a.pad);
     __syncthreads();
-    if (tile + 1 < tile_end) st.load(a, x, (tile + 1) / tps, int((tile + 1) % tps) * R, -a.pad, span);
+    {  // unconditional (a dead request loads nothing): exact counts
+      const bool live = tile + 1 < tile_end;
+      const int64_t nt = live ? tile + 1 : tile;
+      st.load(a, x, nt / tps, int(nt % tps) * R, -a.pad, span, live);
+    }
 #pragma unroll
     for (int i = 0; i < G::TM; ++i) {
       const int lr = wave * (R / 4) + i * 32 + (lane & 31);  // this lane's row in the tile
@@ -1792,7 +1820,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU32F
       float v[16];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const floatx4 bq = b1 ? *reinterpret_cast<const floatx4*>(b1 + 8 * q + 4 * hl) : floatx4{0.f, 0.f, 0.f, 0.f};
+        const floatx4 bq = *reinterpret_cast<const floatx4*>(&bsm[0][8 * q + 4 * hl]);
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[4 * q + e] = acc[4 * q + e] + bq[e];
       }
@@ -1815,7 +1843,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU32F
       for (int q = 0; q < 4; ++q) {
         const uint2 xres = *reinterpret_cast<const uint2*>(xr + lr * P + 8 * q + 4 * hl);
         const __bf16* rv = reinterpret_cast<const __bf16*>(&xres);
-        const floatx4 bq = b2 ? *reinterpret_cast<const floatx4*>(b2 + 8 * q + 4 * hl) : floatx4{0.f, 0.f, 0.f, 0.f};
+        const floatx4 bq = *reinterpret_cast<const floatx4*>(&bsm[1][8 * q + 4 * hl]);
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[4 * q + e] = acc2[4 * q + e] + bq[e] + float(rv[e]);
       }
@@ -1882,25 +1910,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU64F
 #pragma unroll
     for (int g = 0; g < C / 16; ++g) wf2[g] = *reinterpret_cast<const bf16x8*>(wrow2 + 16 * g);
   }
+  ws_wait_vm<0>();  // weights landed: the tile loop's waits then count only its own loads
   // biases in accumulator order (element group q = channels ns*32 + 8q + 4hl .. +4),
   // read where used (L1-hot; registers are what bounds this kernel's occupancy)
-  auto bias_q = [&](const float* bp, int q) {
-    return bp ? *reinterpret_cast<const floatx4*>(bp + ns * 32 + 8 * q + 4 * hl) : floatx4{0.f, 0.f, 0.f, 0.f};
-  };
+  // both biases staged in LDS once (zeros when absent): a global bias load in
+  // the tile loop would wait behind the next tile's prefetch (memory counters
+  // retire in order)
+  __shared__ __align__(16) float bsm[2][C];
+  for (int i = tid; i < 2 * C; i += 256) {
+    const float* bp = i < C ? b1 : b2;
+    bsm[i / C][i % C] = bp ? bp[i % C] : 0.f;
+  }
+  auto bias_q = [&](int which, int q) { return *reinterpret_cast<const floatx4*>(&bsm[which][ns * 32 + 8 * q + 4 * hl]); };
 
   uint4 xr[G::XV];
   bool xok[G::XV];
-  auto load = [&](int64_t tile) {
+  auto load = [&](int64_t tile, bool live) {
     const int64_t b = tile / tps;
     const int t0 = int(tile % tps) * R;
+    const __amdgpu_buffer_rsrc_t rs = ru_rsrc(x + b * a.T * C, int64_t(a.T) * C);
 #pragma unroll
     for (int u = 0; u < G::XV; ++u) {
       const int v = tid + u * 256;
       const int r = v / CV, c = (v % CV) * 8;
-      int ti = t0 - a.pad + r;
+      const int ti = t0 - a.pad + r;
       xok[u] = r < span && ti >= 0 && ti < a.T;
-      ti = ti < 0 ? 0 : (ti >= a.T ? a.T - 1 : ti);
-      if ((u * 256) / CV < span) xr[u] = *reinterpret_cast<const uint4*>(x + (b * a.T + ti) * C + c);
+      xr[u] = ru_bload(rs, live && xok[u] ? (ti * C + c) * 2 : RU_OOB);  // Ru32Stage::load
     }
   };
   auto store = [&]() {
@@ -1914,7 +1949,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU64F
     }
   };
 
-  load(tile0);
+  load(tile0, true);
   for (int64_t tile = tile0; tile < tile_end; ++tile) {
     const int64_t b = tile / tps;
     const int t0 = int(tile % tps) * R;
@@ -1922,7 +1957,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU64F
     __syncthreads();  // every wave is done with the previous tile's xs / hs
     store();
     __syncthreads();
-    if (tile + 1 < tile_end) load(tile + 1);
 
     // conv1 (k_conv_thin_bf16 order: taps, 16-channel chunks, sub-tiles)
     floatx16 acc[G::TM];
@@ -1952,6 +1986,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU64F
 #pragma unroll
       for (int q = 0; q < 4; ++q) xres[i][q] = in ? *reinterpret_cast<const uint2*>(x + orow + 8 * q) : make_uint2(0, 0);
     }
+    // the next tile's rows, requested after the residual rows (which the out
+    // epilogue then waits for alone: memory counters retire in order) and
+    // unconditionally (a dead request loads nothing): exact counts
+    load(tile + 1 < tile_end ? tile + 1 : tile, tile + 1 < tile_end);
     // h = conv1 + b1 -> bf16 -> HBM; ELU(h) -> the 1x1's LDS tile (plane ns)
 #pragma unroll
     for (int i = 0; i < G::TM; ++i) {
@@ -1959,7 +1997,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU64F
       float v[16];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const floatx4 bq = bias_q(b1, q);
+        const floatx4 bq = bias_q(0, q);
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[4 * q + e] = acc[i][4 * q + e] + bq[e];
       }
@@ -1992,7 +2030,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU64F
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const __bf16* rv = reinterpret_cast<const __bf16*>(&xres[i][q]);
-        const floatx4 bq = bias_q(b2, q);
+        const floatx4 bq = bias_q(1, q);
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[4 * q + e] = __fadd_rn(acc2[4 * q + e] + bq[e], float(rv[e]));
       }
@@ -2056,19 +2094,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU64B
 #pragma unroll
       for (int q = 0; q < C / 16; ++q) wf[k][q] = *reinterpret_cast<const bf16x8*>(wrow + k * C + 16 * q);
   }
+  // the 1x1 adjoint's weights [C][C] in LDS (rows padded to W2P: 16-B reads of
+  // 32 rows x 2 lane halves spread over the banks); a per-unit global load in
+  // the gh phase waited behind every request before it (memory counters
+  // retire in order)
+  constexpr int W2P = C + 8;
+  __shared__ __align__(16) __bf16 w2s[C * W2P];
+  for (int i = tid; i < C * C / 8; i += 256) {
+    const int n = i / (C / 8), c8 = (i % (C / 8)) * 8;
+    *reinterpret_cast<bf16x8*>(w2s + n * W2P + c8) = *reinterpret_cast<const bf16x8*>(wd2 + int64_t(n) * C + c8);
+  }
+  ws_wait_vm<0>();  // weights landed: the tile loop's waits then count only its own loads
 
   uint4 xr[G::XV];
   bool xok[G::XV];
-  auto load = [&](int64_t tile) {  // g rows t0 .. t0 + span (rows >= T: zero)
+  auto load = [&](int64_t tile, bool live) {  // g rows t0 .. t0 + span (rows >= T: zero; Ru32Stage::load)
     const int64_t b = tile / tps;
     const int t0 = int(tile % tps) * R;
+    const __amdgpu_buffer_rsrc_t rs = ru_rsrc(g + b * a.T * C, int64_t(a.T) * C);
 #pragma unroll
     for (int u = 0; u < G::XV; ++u) {
       const int v = tid + u * 256;
       const int r = v / CV, c = (v % CV) * 8;
       const int ti = t0 + r;
       xok[u] = r < span && ti < a.T;
-      if ((u * 256) / CV < span) xr[u] = *reinterpret_cast<const uint4*>(g + (b * a.T + (xok[u] ? ti : 0)) * C + c);
+      xr[u] = ru_bload(rs, live && xok[u] ? (ti * C + c) * 2 : RU_OOB);
     }
   };
   auto store = [&]() {
@@ -2081,7 +2131,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU64B
     }
   };
 
-  load(tile0);
+  load(tile0, true);
   for (int64_t tile = tile0; tile < tile_end; ++tile) {
     const int64_t b = tile / tps;
     const int t0 = int(tile % tps) * R;
@@ -2099,8 +2149,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU64B
       for (int q = 0; q < 4; ++q)
         hq[q] = inside ? *reinterpret_cast<const uint2*>(h + orow + 8 * q + 4 * hl) : make_uint2(0, 0);
     };
-    uint2 hnext[4];
-    load_h(wave, hnext);
+    // every gh unit's h rows requested up front (one latency per tile, not one per unit)
+    uint2 hall[G::UPW][4];
+#pragma unroll
+    for (int uu = 0; uu < G::UPW; ++uu) load_h(wave + 4 * uu, hall[uu]);
     // x rows of this wave's gx sub-tiles (the ELU'(x) factor), requested before
     // the gh phase so their HBM latency hides behind it
     uint2 xpre[G::TM][4];
@@ -2125,12 +2177,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU64B
       const int64_t orow = (b * a.T + (inside ? ti : 0)) * C + sl * 32;
       uint2 hq[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) hq[q] = hnext[q];
-      if (uu + 1 < G::UPW) load_h(unit + 4, hnext);
-      // the slice-sl weights of the 1x1 adjoint: rows n = sl*32 + (lane & 31)
+      for (int q = 0; q < 4; ++q) hq[q] = hall[uu][q];
+      // the slice-sl weights of the 1x1 adjoint: rows n = sl*32 + (lane & 31), from LDS
       bf16x8 w2q[C / 16];
       {
-        const __bf16* wr2 = wd2 + int64_t(sl * 32 + (lane & 31)) * C + 8 * hl;
+        const __bf16* wr2 = w2s + (sl * 32 + (lane & 31)) * W2P + 8 * hl;
 #pragma unroll
         for (int q = 0; q < C / 16; ++q) w2q[q] = *reinterpret_cast<const bf16x8*>(wr2 + 16 * q);
       }
@@ -2164,7 +2215,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU64B
     // the next tile's g rows, requested after the gh phase: its h / x / weight
     // loads then wait only for each other (memory counters retire in order),
     // and this request has the gx phase to land
-    if (tile + 1 < tile_end) load(tile + 1);
+    load(tile + 1 < tile_end ? tile + 1 : tile, tile + 1 < tile_end);  // unconditional: exact counts
     // gx = conv1^T(gh) * ELU'(x) + g (k_conv_thin_bf16 order: taps, chunks, sub-tiles)
     floatx16 acc[G::TM];
 #pragma unroll
@@ -2235,6 +2286,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU32B
   bf16x8 wf[RU_K][2], w2f[1][2];
   ru_wfrags<RU_K>(wd1, wf);
   ru_wfrags<1>(wd2, w2f);
+  ws_wait_vm<0>();  // weights landed: the tile loop's waits then count only its own loads
 
   Ru32Stage<R> st;
   st.load(a, g, tile0 / tps, int(tile0 % tps) * R, 0, span);
@@ -2301,7 +2353,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU32B
     }
     __syncthreads();
     // the next tile's g rows, requested after the gh phase (k_ru64_bwd)
-    if (tile + 1 < tile_end) st.load(a, g, (tile + 1) / tps, int((tile + 1) % tps) * R, 0, span);
+    {  // unconditional (a dead request loads nothing): exact counts
+      const bool live = tile + 1 < tile_end;
+      const int64_t nt = live ? tile + 1 : tile;
+      st.load(a, g, nt / tps, int(nt % tps) * R, 0, span, live);
+    }
 #pragma unroll
     for (int i = 0; i < G::TM; ++i) {
       const int lr = wave * (R / 4) + i * 32 + (lane & 31);
@@ -2758,6 +2814,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU32W
     bf16x8 wf[RU_K][2], w2f[1][2];
     ru_wfrags<RU_K>(wd1, wf);
     ru_wfrags<1>(wd2, w2f);
+    ws_wait_vm<0>();  // weights landed: the tile loop's waits then count only its own loads
 
     Ru32Stage<R> st, sx;
     st.load(a, g, tile0 / tps, int(tile0 % tps) * R, 0, span);
@@ -2829,9 +2886,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU32W
       }
       __syncthreads();
       // the next tile's g and x rows, requested after the gh phase (k_ru64_bwd)
-      if (tile + 1 < tile_end) {
-        st.load(a, g, (tile + 1) / tps, int((tile + 1) % tps) * R, 0, span);
-        sx.load(a, x, (tile + 1) / tps, int((tile + 1) % tps) * R, -halo, span);
+      {  // unconditional (a dead request loads nothing): exact counts
+        const bool live = tile + 1 < tile_end;
+        const int64_t nt = live ? tile + 1 : tile;
+        st.load(a, g, nt / tps, int(nt % tps) * R, 0, span, live);
+        sx.load(a, x, nt / tps, int(nt % tps) * R, -halo, span, live);
       }
       // gx = conv1^T(gh) * ELU'(x) + g (k_ru32_bwd)
 #pragma unroll
