@@ -594,6 +594,17 @@ __device__ __forceinline__ void ws_wait_vm() {
   __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
 }
 
+// one sample's rows as a buffer resource (bytes < 2^31: thin_index and
+// ru_fused_ok check T * C * 2) and a 16-B load from it; RU_OOB is past any sample's bytes, so a
+// load there returns zeros and touches no memory
+constexpr int RU_OOB = 0x7ffffff0;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t ru_rsrc(const __bf16* base, int64_t elems) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(base), 0, int(elems * 2), 0x00020000);
+}
+__device__ __forceinline__ uint4 ru_bload(__amdgpu_buffer_rsrc_t rs, int byte_off) {
+  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, byte_off, 0, 0));
+}
+
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 // DMA piece of producer wave pw's u-th slot: q = 4u + pw, clamped to the last piece
@@ -1271,12 +1282,16 @@ __global__ __launch_bounds__(256) void k_conv_thin_bf16(Args a, const __bf16* __
 #pragma unroll
       for (int g = 0; g < C / 16; ++g) wf[k][g] = *reinterpret_cast<const bf16x8*>(wrow + k * C + 16 * g);
   }
+  ws_wait_vm<0>();  // weights landed: the tile loop's MFMAs then wait on no request of the loop
 
   uint4 xr[G::XV];
   bool xok[G::XV];
-  auto load = [&](int64_t tile) {
+  // branch-free buffer loads (Ru32Stage::load): rows past the span, zero-padded
+  // rows and a dead request (live = false) read nothing and return zeros
+  auto load = [&](int64_t tile, bool live) {
     const int64_t b = tile / tps;
     const int t0 = int(tile % tps) * R;
+    const __amdgpu_buffer_rsrc_t rs = ru_rsrc(in + b * a.T * C, int64_t(a.T) * C);
 #pragma unroll
     for (int u = 0; u < G::XV; ++u) {
       const int v = tid + u * 256;
@@ -1285,8 +1300,7 @@ __global__ __launch_bounds__(256) void k_conv_thin_bf16(Args a, const __bf16* __
       const bool inside = ti >= 0 && ti < a.T;
       xok[u] = r < span && (inside || a.pad_mode == SEL_PAD_REPLICATE);
       ti = ti < 0 ? 0 : (ti >= a.T ? a.T - 1 : ti);
-      if ((u * 256) / CV < span)  // block-uniform: batches wholly past the halo are never fetched
-        xr[u] = *reinterpret_cast<const uint4*>(in + (b * a.T + ti) * C + c);  // masked in store()
+      xr[u] = ru_bload(rs, live && xok[u] ? (ti * C + c) * 2 : RU_OOB);
     }
   };
   auto store = [&]() {
@@ -1303,19 +1317,23 @@ __global__ __launch_bounds__(256) void k_conv_thin_bf16(Args a, const __bf16* __
     }
   };
 
-  const bool bias_vec = bias && a.bias_period && (a.bias_period % 8) == 0;
-  load(tile0);
+  // the bias over this kernel's N output channels in LDS (bs[n] = bias[n % period]):
+  // a global bias load in the epilogue would wait behind the next tile's request
+  __shared__ __align__(16) float bs[N];
+  const bool has_bias = bias && a.bias_period;
+  if (has_bias && tid < N) bs[tid] = bias[tid % a.bias_period];
+  load(tile0, true);
   if (split) {
     store();
     __syncthreads();
-    if (tile0 + 1 < tile_end) load(tile0 + 1);
+    if (tile0 + 1 < tile_end) load(tile0 + 1, true);
   }
   for (int64_t tile = tile0; tile < tile_end; ++tile) {
     if (!split) {
       __syncthreads();  // the previous tile's epilogue is done with ot (= xs)
       store();
       __syncthreads();
-      if (tile + 1 < tile_end) load(tile + 1);
+      load(tile + 1 < tile_end ? tile + 1 : tile, tile + 1 < tile_end);  // unconditional: exact counts
     }
 
     // this tile's epilogue operands (ELU'(aux), residual), fetched before the
@@ -1373,7 +1391,7 @@ __global__ __launch_bounds__(256) void k_conv_thin_bf16(Args a, const __bf16* __
     // tile costs two barriers and its epilogue overlaps the next MFMA phase
     if (split && tile + 1 < tile_end) store();
     __syncthreads();
-    if (split && tile + 2 < tile_end) load(tile + 2);
+    if (split && tile + 2 < tile_end) load(tile + 2, true);
 
     // coalesced epilogue: a sample-aligned tile's output rows are contiguous in HBM
     const int64_t b = tile / tps;
@@ -1386,14 +1404,11 @@ __global__ __launch_bounds__(256) void k_conv_thin_bf16(Args a, const __bf16* __
       const floatx4 lo = *reinterpret_cast<const floatx4*>(ot + r * G::OP + n);
       const floatx4 hi = *reinterpret_cast<const floatx4*>(ot + r * G::OP + n + 4);
       float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      if (bias_vec) {
-        const float4 b0 = *reinterpret_cast<const float4*>(bias + (n % a.bias_period));
-        const float4 b1 = *reinterpret_cast<const float4*>(bias + (n % a.bias_period) + 4);
-        v[0] += b0.x, v[1] += b0.y, v[2] += b0.z, v[3] += b0.w;
-        v[4] += b1.x, v[5] += b1.y, v[6] += b1.z, v[7] += b1.w;
-      } else if (bias && a.bias_period) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] += bias[(n + e) % a.bias_period];
+      if (has_bias) {
+        const floatx4 b0 = *reinterpret_cast<const floatx4*>(bs + n);
+        const floatx4 b1 = *reinterpret_cast<const floatx4*>(bs + n + 4);
+        v[0] += b0[0], v[1] += b0[1], v[2] += b0[2], v[3] += b0[3];
+        v[4] += b1[0], v[5] += b1[1], v[6] += b1[2], v[7] += b1[3];
       }
       const int64_t o = obase + int64_t(r) * N + n;
       // explicit roundings (no FMA contraction): every instance, and the fused
@@ -1683,17 +1698,6 @@ struct Ru32 {
   static constexpr size_t LDS_BWD = 2 * size_t(SPAN) * P * 2;  // g tile + gh tile
   static_assert(R % 128 == 0, "ru32 tile rows");
 };
-
-// one sample's rows as a buffer resource (bytes < 2^31: the launchers check
-// T * C * 2) and a 16-B load from it; RU_OOB is past any sample's bytes, so a
-// load there returns zeros and touches no memory
-constexpr int RU_OOB = 0x7ffffff0;
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t ru_rsrc(const __bf16* base, int64_t elems) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(base), 0, int(elems * 2), 0x00020000);
-}
-__device__ __forceinline__ uint4 ru_bload(__amdgpu_buffer_rsrc_t rs, int byte_off) {
-  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, byte_off, 0, 0));
-}
 
 // stage `span` rows of a 32-channel tensor starting at sample row t0 + off
 // (rows outside [0, T) -> zero) into registers / LDS (optionally ELU'd)
@@ -4026,7 +4030,8 @@ int launch_thin(const Args& a, const void* in, const void* wp, const float* bias
   X(3, 64, 64, 1, 128, 64) X(4, 96, 64, 3, 128, 64) X(5, 96, 64, 2, 128, 64) X(6, 128, 128, 1, 64, 32)
 
 int thin_index(const Args& a) {
-  if (tune(4) == 1 || (a.K - 1) * a.dil > F4_HALOMAX) return -1;
+  // (one sample's rows must fit a 2^31-byte buffer resource: ru_rsrc)
+  if (tune(4) == 1 || (a.K - 1) * a.dil > F4_HALOMAX || int64_t(a.T) * a.C * 2 >= (int64_t(1) << 31)) return -1;
 #define SEL_THIN_IDX(I_, C_, N_, K_, R_, R2_) \
   if (a.C == C_ && a.N == N_ && a.K == K_) return (tune(7) >> I_) & 1 ? -1 : I_;
   SEL_THIN_SHAPES(SEL_THIN_IDX)
@@ -4227,7 +4232,7 @@ int launch_ru32_bwdw(const Args& a, const void* g, const void* h, const void* x,
 bool ru_fused_ok(const Args& a) {
   return (a.C == 32 || a.C == 64) && a.N == a.C && a.K == 7 && a.pad == (a.K - 1) * a.dil &&
          a.pad_mode == SEL_PAD_ZERO && a.in_elu == 1 && (a.K - 1) * a.dil <= F4_HALOMAX &&
-         (a.bias_period == 0 || a.bias_period == a.N);
+         (a.bias_period == 0 || a.bias_period == a.N) && int64_t(a.T) * a.C * 2 < (int64_t(1) << 31);
 }
 
 template <typename TI, typename TO>
