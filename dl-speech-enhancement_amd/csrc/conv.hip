@@ -2771,7 +2771,8 @@ struct Ru32W {
   static constexpr int PW = 32;    // ELU(x) / ELU(h) rows (64 B: conflict-free transposing reads)
   static constexpr int SPAN = R + F4_HALOMAX;
   static constexpr int NW1 = RU_C * RU_K * RU_C, NW2 = RU_C * RU_C;  // packed weight elements
-  static constexpr size_t LDS = size_t(2) * SPAN * P * 2 + size_t(SPAN + R) * PW * 2;
+  // g, gh and h planes (pitch P) + ELU(x) span and ELU(h) tile planes (pitch PW)
+  static constexpr size_t LDS = size_t(3) * SPAN * P * 2 + size_t(SPAN + R) * PW * 2;
   static_assert(R % 128 == 0, "ru32 tile rows");
 };
 
@@ -2788,6 +2789,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU32W
   __bf16* const ghs = gs + G::SPAN * P;                // [SPAN][P]: gh rows t0 ..
   __bf16* const xs = ghs + G::SPAN * P;                // [SPAN][PW]: ELU(x) rows t0 - halo ..
   __bf16* const es = xs + G::SPAN * PW;                // [R][PW]: ELU(h) rows t0 ..
+  __bf16* const hs = es + R * PW;                      // [SPAN][P]: h rows t0 .. (the ELU'(h) factor)
   const int lane = threadIdx.x & 63, hl = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int halo = (RU_K - 1) * a.dil;
@@ -2820,9 +2822,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU32W
     ru_wfrags<1>(wd2, w2f);
     ws_wait_vm<0>();  // weights landed: the tile loop's waits then count only its own loads
 
-    Ru32Stage<R> st, sx;
+    // g, x and h rows staged one tile ahead (branch-free buffer loads): the gh
+    // phase then reads h from LDS instead of waiting on a request made at the
+    // top of the tile
+    Ru32Stage<R> st, sx, sh;
     st.load(a, g, tile0 / tps, int(tile0 % tps) * R, 0, span);
     sx.load(a, x, tile0 / tps, int(tile0 % tps) * R, -halo, span);
+    sh.load(a, h, tile0 / tps, int(tile0 % tps) * R, 0, span);
     for (int64_t tile = tile0; tile < tile_end; ++tile) {
       const int64_t b = tile / tps;
       const int t0 = int(tile % tps) * R;
@@ -2830,18 +2836,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU32W
       __syncthreads();  // every wave is done with the previous tile's rows
       st.store(gs, span, false);
       sx.store(xs, span, true, nullptr, 0, PW);
+      sh.store(hs, span, false);
       __syncthreads();
       constexpr int NSUB_W = (G::SPAN / 32 + 3) / 4;
-      uint2 hpre[NSUB_W][4], xpre[Ru32<R>::TM][4];
-#pragma unroll
-      for (int j = 0; j < NSUB_W; ++j) {
-        const int ti = t0 + (wave + 4 * j) * 32 + (lane & 31);
-        const bool in = wave + 4 * j < nsub && ti < a.T;
-        const int64_t orow = (b * a.T + (in ? ti : 0)) * RU_C;
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          hpre[j][q] = in ? *reinterpret_cast<const uint2*>(h + orow + 8 * q + 4 * hl) : make_uint2(0, 0);
-      }
+      uint2 xpre[Ru32<R>::TM][4];
 #pragma unroll
       for (int i = 0; i < Ru32<R>::TM; ++i) {
         const int lr = wave * (R / 4) + i * 32 + (lane & 31);
@@ -2865,10 +2863,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU32W
         for (int c = 0; c < 2; ++c)
           acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w2f[0][c], *reinterpret_cast<const bf16x8*>(gw + 16 * c), acc, 0,
                                                         0, 0);
+        uint2 hq[4];  // h rows (zero past T), as staged
+#pragma unroll
+        for (int q = 0; q < 4; ++q) hq[q] = *reinterpret_cast<const uint2*>(hs + lr * P + 8 * q + 4 * hl);
         float v[16];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const __bf16* hv = reinterpret_cast<const __bf16*>(&hpre[j][q]);
+          const __bf16* hv = reinterpret_cast<const __bf16*>(&hq[q]);
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[4 * q + e] = acc[4 * q + e] * elu_grad_fast(float(hv[e]));
         }
@@ -2881,8 +2882,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU32W
         if (sb < R / 32) {  // wave-uniform: a tile sub-tile (rows past T hold h = 0 -> ELU = 0)
 #pragma unroll
           for (int qq = 0; qq < 2; ++qq) {
-            const uint4 e8 = elu8(make_uint4(hpre[j][2 * qq].x, hpre[j][2 * qq].y, hpre[j][2 * qq + 1].x,
-                                             hpre[j][2 * qq + 1].y));
+            const uint4 e8 = elu8(make_uint4(hq[2 * qq].x, hq[2 * qq].y, hq[2 * qq + 1].x, hq[2 * qq + 1].y));
             *reinterpret_cast<uint2*>(es + lr * PW + 16 * qq + 4 * hl) = make_uint2(e8.x, e8.y);
             *reinterpret_cast<uint2*>(es + lr * PW + 16 * qq + 8 + 4 * hl) = make_uint2(e8.z, e8.w);
           }
@@ -2895,6 +2895,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU32W
         const int64_t nt = live ? tile + 1 : tile;
         st.load(a, g, nt / tps, int(nt % tps) * R, 0, span, live);
         sx.load(a, x, nt / tps, int(nt % tps) * R, -halo, span, live);
+        sh.load(a, h, nt / tps, int(nt % tps) * R, 0, span, live);
       }
       // gx = conv1^T(gh) * ELU'(x) + g (k_ru32_bwd)
 #pragma unroll
