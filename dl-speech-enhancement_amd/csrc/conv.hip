@@ -3297,16 +3297,21 @@ __global__ __launch_bounds__(256) void k_wgrad3_bf16(Args a, const __bf16* __res
 
   uint4 gr[GV], xr[XV];
   bool gok[GV], xok[XV];
-  auto load = [&](int64_t tile) {
+  // branch-free buffer loads over one sample (ru_bload: rows past T / the span,
+  // padded rows and a dead request read nothing): the compiler then counts the
+  // request exactly, and the MFMA phase no longer waits on it with vmcnt(0)
+  auto load = [&](int64_t tile, bool live) {
     const int64_t b = tile / tiles_per_sample;
     const int t0 = int(tile % tiles_per_sample) * W2_BM;
     const int64_t rb = b * a.T;
+    const __amdgpu_buffer_rsrc_t rg = ru_rsrc(gout + rb * a.N, int64_t(a.T) * a.N);
+    const __amdgpu_buffer_rsrc_t rx = ru_rsrc(in + rb * a.C, int64_t(a.T) * a.C);
 #pragma unroll
     for (int u = 0; u < GV; ++u) {
       const int v = tid + u * 256;
       const int t = t0 + v / (NB / 8);
       gok[u] = t < a.T;
-      gr[u] = *reinterpret_cast<const uint4*>(gout + (rb + (gok[u] ? t : 0)) * a.N + n0 + (v % (NB / 8)) * 8);
+      gr[u] = ru_bload(rg, live && gok[u] ? (t * a.N + n0 + (v % (NB / 8)) * 8) * 2 : RU_OOB);
     }
 #pragma unroll
     for (int u = 0; u < XV; ++u) {
@@ -3316,8 +3321,7 @@ __global__ __launch_bounds__(256) void k_wgrad3_bf16(Args a, const __bf16* __res
       const bool inside = ti >= 0 && ti < a.T;
       xok[u] = r < span && (inside || a.pad_mode == SEL_PAD_REPLICATE);
       ti = ti < 0 ? 0 : (ti >= a.T ? a.T - 1 : ti);
-      if (u * 256 / (CB / 8) < span)  // block-uniform: rows past the halo are never fetched
-        xr[u] = *reinterpret_cast<const uint4*>(in + (rb + ti) * a.C + c0 + (v % (CB / 8)) * 8);
+      xr[u] = ru_bload(rx, live && xok[u] ? (ti * a.C + c0 + (v % (CB / 8)) * 8) * 2 : RU_OOB);
     }
   };
   // zero-fill happens here, after the wait (see the v4 forward kernel's store())
@@ -3368,12 +3372,12 @@ __global__ __launch_bounds__(256) void k_wgrad3_bf16(Args a, const __bf16* __res
   const int q = (lane & 15) >> 2;
   const int lrow = (4 * h + q) * 32 + col;
 
-  if (tb < te) load(tb);
+  if (tb < te) load(tb, true);
   int buf = 0;
   for (int64_t tile = tb; tile < te; ++tile, buf ^= 1) {
     store(buf);
     __syncthreads();
-    if (tile + 1 < te) load(tile + 1);
+    load(tile + 1 < te ? tile + 1 : tile, tile + 1 < te);  // unconditional: exact counts
     const __bf16* g = base + buf * (GS + XS) + nt * (W2_BM * 32);
     const __bf16* x = base + buf * (GS + XS) + GS;
     if (do_bias) {
@@ -4303,7 +4307,9 @@ struct WgPlan {
 };
 
 bool wgrad_tr_ok(const sel_conv_desc* d) {
-  return d->C % 32 == 0 && d->N % 32 == 0 && (d->K - 1) * d->dil <= W2_HALO && d->K <= 8;
+  // (one sample's gout / input rows must fit a 2^31-byte buffer resource: ru_rsrc)
+  return d->C % 32 == 0 && d->N % 32 == 0 && (d->K - 1) * d->dil <= W2_HALO && d->K <= 8 &&
+         int64_t(d->T) * std::max(d->C, d->N) * 2 < (int64_t(1) << 31);
 }
 
 // tune key 1: 0 = k_wgrad3 where legal, 1 = generic, 2 = k_wgrad2 (32x32 blocks)
