@@ -594,17 +594,6 @@ __device__ __forceinline__ void ws_wait_vm() {
   __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
 }
 
-// one sample's rows as a buffer resource (bytes < 2^31: thin_index and
-// ru_fused_ok check T * C * 2) and a 16-B load from it; RU_OOB is past any sample's bytes, so a
-// load there returns zeros and touches no memory
-constexpr int RU_OOB = 0x7ffffff0;
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t ru_rsrc(const __bf16* base, int64_t elems) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(base), 0, int(elems * 2), 0x00020000);
-}
-__device__ __forceinline__ uint4 ru_bload(__amdgpu_buffer_rsrc_t rs, int byte_off) {
-  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, byte_off, 0, 0));
-}
-
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 // DMA piece of producer wave pw's u-th slot: q = 4u + pw, clamped to the last piece

@@ -1034,19 +1034,23 @@ __global__ __launch_bounds__(256) void k_dwgrad_w3(D d, const __bf16* __restrict
 
   uint4 gr[GV], xr[XV];
   bool gok[GV], xok[XV];
-  auto load = [&](int64_t tile) {
+  // branch-free buffer loads (sel_common.h ru_bload): invalid rows and a dead
+  // request (live = false) read nothing, so the request is counted exactly and
+  // the MFMA phase does not wait on it
+  auto load = [&](int64_t tile, bool live) {
     // flat_p > 0: one row space over all sequences (pitch flat_p, zero gaps; see
     // conv.hip dconv_ws_fwd), rows valid by their position in their sequence
     const int b = int(tile / tiles_per_seq);
     const int j0 = int(tile % tiles_per_seq) * W3_BM;
     const int nflat = flat_p * d.B;
+    const __amdgpu_buffer_rsrc_t rg = ru_rsrc(gout + int64_t(b) * d.Tvo * d.ldo, int64_t(d.B - b) * d.Tvo * d.ldo);
+    const __amdgpu_buffer_rsrc_t rx = ru_rsrc(x + int64_t(b) * d.Tvs * d.ldx, int64_t(d.B - b) * d.Tvs * d.ldx);
 #pragma unroll
     for (int u = 0; u < GV; ++u) {
       const int v = tid + u * 256;
       const int j = j0 + v / (NB / 8);
       gok[u] = flat_p ? j < nflat && j % flat_p < d.Tvalid : j < d.Tvalid;
-      gr[u] = *reinterpret_cast<const uint4*>(gout + (int64_t(b) * d.Tvo + (gok[u] ? j : 0)) * d.ldo + n0 +
-                                              (v % (NB / 8)) * 8);
+      gr[u] = ru_bload(rg, live && gok[u] ? (j * d.ldo + n0 + (v % (NB / 8)) * 8) * 2 : RU_OOB);
     }
 #pragma unroll
     for (int u = 0; u < XV; ++u) {
@@ -1054,9 +1058,7 @@ __global__ __launch_bounds__(256) void k_dwgrad_w3(D d, const __bf16* __restrict
       const int r = v / (CB / 8);
       const int t = j0 + d.q0 + r;
       xok[u] = r < span && t >= 0 && (flat_p ? t < nflat && t % flat_p < d.Tv : t < d.Tv);
-      if (u * 256 / (CB / 8) < span)
-        xr[u] = *reinterpret_cast<const uint4*>(x + (int64_t(b) * d.Tvs + (xok[u] ? t : 0)) * d.ldx + c0 +
-                                                (v % (CB / 8)) * 8);
+      xr[u] = ru_bload(rx, live && xok[u] ? (t * d.ldx + c0 + (v % (CB / 8)) * 8) * 2 : RU_OOB);
     }
   };
   auto store = [&](int buf) {
@@ -1097,12 +1099,12 @@ __global__ __launch_bounds__(256) void k_dwgrad_w3(D d, const __bf16* __restrict
   const int q = (lane & 15) >> 2;
   const int lrow = (4 * h + q) * 32 + col;
 
-  if (tb < te) load(tb);
+  if (tb < te) load(tb, true);
   int buf = 0;
   for (int64_t tile = tb; tile < te; ++tile, buf ^= 1) {
     store(buf);
     __syncthreads();
-    if (tile + 1 < te) load(tile + 1);
+    load(tile + 1 < te ? tile + 1 : tile, tile + 1 < te);  // unconditional: exact counts
     const __bf16* g = base + buf * (GS + XS) + nt * (W3_BM * 32);
     const __bf16* xx = base + buf * (GS + XS) + GS;
     for (int kh = 0; kh < RROWS / 16; ++kh) {
@@ -2145,7 +2147,9 @@ WgPlanD wg_plan(const sel_dconv_desc* d, int dtype) {
     return p;
   }
   p.w3 = p.mfma && d->G == 1 && d->So == 1 && (d->S == 1 || d->Cs == d->Cg) && d->K <= 8 && width % 32 == 0 &&
-         nred % 32 == 0 && d->ldo % 8 == 0 && tune(16) != 1;
+         nred % 32 == 0 && d->ldo % 8 == 0 && tune(16) != 1 &&
+         // gout and x as buffer resources (ru_rsrc): < 2^31 bytes each
+         int64_t(d->B) * d->Tvo * d->ldo * 2 < (int64_t(1) << 31) && int64_t(d->B) * d->Tvs * d->ldx * 2 < (int64_t(1) << 31);
   if (p.w3) {
     p.w3_nt = width % 64 == 0 ? 2 : 1;
     p.w3_ct = nred % 64 == 0 ? 2 : 1;

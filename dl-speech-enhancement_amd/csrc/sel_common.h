@@ -43,6 +43,21 @@ __device__ __forceinline__ T block_sum(T v, T* red) {
   return s;  // valid in thread 0 (and the whole first wave)
 }
 
+// Branch-free staging loads for the persistent tile loops: a bf16 tensor
+// region as a buffer resource (bytes < 2^31: the dispatch predicates check)
+// and a 16-B load from it.  RU_OOB is past any region's bytes, so a load there
+// returns zeros and touches no memory: rows outside the sample / span and a
+// dead next-tile request take it instead of a branch around the load, and the
+// compiler then counts the request exactly (a conditional request makes every
+// later wait on an earlier load fall back to vmcnt(0) behind it).
+constexpr int RU_OOB = 0x7ffffff0;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t ru_rsrc(const __bf16* base, int64_t elems) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(base), 0, int(elems * 2), 0x00020000);
+}
+__device__ __forceinline__ uint4 ru_bload(__amdgpu_buffer_rsrc_t rs, int byte_off) {
+  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, byte_off, 0, 0));
+}
+
 }  // namespace sel
 
 #define SEL_REQUIRE(cond, code, ...)      \
