@@ -316,7 +316,7 @@ constexpr int F4_HALOMAX = 64;
 #define SEL_W_RU32F 3
 #endif
 #ifndef SEL_W_RU32B
-#define SEL_W_RU32B 1
+#define SEL_W_RU32B 3
 #endif
 #ifndef SEL_W_RU32W
 #define SEL_W_RU32W 2
@@ -1684,7 +1684,7 @@ struct Ru32 {
   static constexpr int XV = (SPAN * 4 + 255) / 256;
   static constexpr int TM = R / 128;            // 32-row sub-tiles per wave
   static constexpr size_t LDS_FWD = size_t(SPAN + R) * P * 2;  // ELU(x) span + raw tile rows
-  static constexpr size_t LDS_BWD = 2 * size_t(SPAN) * P * 2;  // g tile + gh tile
+  static constexpr size_t LDS_BWD = 3 * size_t(SPAN) * P * 2;  // g, gh and h tiles
   static_assert(R % 128 == 0, "ru32 tile rows");
 };
 
@@ -2257,7 +2257,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU64B
 // (and HBM when the weight gradient needs it); gx = conv1^T(gh) * ELU'(x) + g.
 // wd1 / wd2 are the dgrad-packed weights of the primitive path.
 template <int R>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU32B))) void k_ru32_bwd(Args a, const __bf16* __restrict__ g,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 128 ? SEL_W_RU32B : 1))) void k_ru32_bwd(Args a, const __bf16* __restrict__ g,
                                                   const __bf16* __restrict__ h, const __bf16* __restrict__ x,
                                                   const __bf16* __restrict__ wd1, const __bf16* __restrict__ wd2,
                                                   __bf16* __restrict__ ghout, __bf16* __restrict__ gx,
@@ -2267,6 +2267,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU32B
   extern __shared__ __align__(16) unsigned char smem[];
   __bf16* const gs = reinterpret_cast<__bf16*>(smem);  // [SPAN][P]: g rows t0 ..
   __bf16* const ghs = gs + G::SPAN * P;                // [SPAN][P]: gh rows t0 ..
+  __bf16* const hs = ghs + G::SPAN * P;                // [SPAN][P]: h rows t0 .. (the ELU'(h) factor)
   const int lane = threadIdx.x & 63, hl = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int halo = (RU_K - 1) * a.dil;
@@ -2281,27 +2282,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU32B
   ru_wfrags<1>(wd2, w2f);
   ws_wait_vm<0>();  // weights landed: the tile loop's waits then count only its own loads
 
-  Ru32Stage<R> st;
+  // g and h rows staged one tile ahead (k_ru32_bwdw): the gh phase reads h from
+  // LDS instead of waiting on a request made at the top of the tile
+  Ru32Stage<R> st, sh;
   st.load(a, g, tile0 / tps, int(tile0 % tps) * R, 0, span);
+  sh.load(a, h, tile0 / tps, int(tile0 % tps) * R, 0, span);
   for (int64_t tile = tile0; tile < tile_end; ++tile) {
     const int64_t b = tile / tps;
     const int t0 = int(tile % tps) * R;
     const int mrows = a.T - t0 < R ? a.T - t0 : R;
     __syncthreads();  // every wave is done with the previous tile's g / gh rows
     st.store(gs, span, false);
+    sh.store(hs, span, false);
     __syncthreads();
-    // every global operand of this tile's MFMA phases is requested up front (L2-hot:
-    // h and x rows of the tile): ELU'(h) for this wave's gh sub-tiles, ELU'(x) for its gx sub-tiles
+    // the x rows of this wave's gx sub-tiles (ELU'(x)), requested up front (their
+    // latency hides behind the gh phase)
     constexpr int NSUB_W = (G::SPAN / 32 + 3) / 4;  // gh sub-tiles per wave (max)
-    uint2 hpre[NSUB_W][4], xpre[G::TM][4];
-#pragma unroll
-    for (int j = 0; j < NSUB_W; ++j) {
-      const int ti = t0 + (wave + 4 * j) * 32 + (lane & 31);
-      const bool in = wave + 4 * j < nsub && ti < a.T;
-      const int64_t orow = (b * a.T + (in ? ti : 0)) * RU_C;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) hpre[j][q] = in ? *reinterpret_cast<const uint2*>(h + orow + 8 * q + 4 * hl) : make_uint2(0, 0);
-    }
+    uint2 xpre[G::TM][4];
 #pragma unroll
     for (int i = 0; i < G::TM; ++i) {
       const int lr = wave * (R / 4) + i * 32 + (lane & 31);
@@ -2326,10 +2323,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU32B
       const int ti = t0 + lr;
       const bool inside = ti < a.T;
       const int64_t orow = (b * a.T + (inside ? ti : 0)) * RU_C;
+      uint2 hq[4];  // h rows (zero past T), as staged
+#pragma unroll
+      for (int q = 0; q < 4; ++q) hq[q] = *reinterpret_cast<const uint2*>(hs + lr * P + 8 * q + 4 * hl);
       float v[16];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const __bf16* hv = reinterpret_cast<const __bf16*>(&hpre[j][q]);
+        const __bf16* hv = reinterpret_cast<const __bf16*>(&hq[q]);
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[4 * q + e] = acc[4 * q + e] * elu_grad_fast(float(hv[e]));
       }
@@ -2350,6 +2350,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU32B
       const bool live = tile + 1 < tile_end;
       const int64_t nt = live ? tile + 1 : tile;
       st.load(a, g, nt / tps, int(nt % tps) * R, 0, span, live);
+      sh.load(a, h, nt / tps, int(nt % tps) * R, 0, span, live);
     }
 #pragma unroll
     for (int i = 0; i < G::TM; ++i) {
