@@ -1869,7 +1869,8 @@ struct Ru64 {
   static constexpr int XV = (SPAN * CV + 255) / 256;
   static constexpr int WR = R / 2;  // rows per row group
   static constexpr int TM = WR / 32;
-  static constexpr size_t LDS = size_t(2) * (SPAN + R) * P * 2;  // ELU(x) span planes + ELU(h) planes
+  // ELU(x) span planes + ELU(h) planes + raw x tile planes (the residual)
+  static constexpr size_t LDS = size_t(2) * (SPAN + 2 * R) * P * 2;
   static_assert(R % 64 == 0, "ru64 tile rows");
 };
 
@@ -1884,6 +1885,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU64F
   extern __shared__ __align__(16) unsigned char smem[];
   __bf16* const xs = reinterpret_cast<__bf16*>(smem);  // [2][SPAN][P]: ELU(x) rows t0 - pad ..
   __bf16* const hs = xs + 2 * G::SPAN * P;             // [2][R][P]: ELU(h) rows t0 ..
+  __bf16* const xraw = hs + 2 * R * P;                 // [2][R][P]: raw x rows t0 .. (the residual)
   const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int ns = wave & 1, rg = wave >> 1;
@@ -1937,8 +1939,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU64F
       const int v = tid + u * 256;
       const int r = v / CV, c = (v % CV) * 8;
       if (r >= span) continue;
-      const uint4 val = elu8(xok[u] ? xr[u] : make_uint4(0, 0, 0, 0));
-      *reinterpret_cast<uint4*>(xs + ((c >> 5) * G::SPAN + r) * P + (c & 31)) = val;
+      const uint4 raw = xok[u] ? xr[u] : make_uint4(0, 0, 0, 0);
+      if (r >= a.pad && r < a.pad + R) *reinterpret_cast<uint4*>(xraw + ((c >> 5) * R + r - a.pad) * P + (c & 31)) = raw;
+      *reinterpret_cast<uint4*>(xs + ((c >> 5) * G::SPAN + r) * P + (c & 31)) = elu8(raw);
     }
   };
 
@@ -1950,6 +1953,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU64F
     __syncthreads();  // every wave is done with the previous tile's xs / hs
     store();
     __syncthreads();
+    // the next tile's rows (no other global load in the tile loop: the
+    // residual rows come from the staged raw planes)
+    load(tile + 1 < tile_end ? tile + 1 : tile, tile + 1 < tile_end);  // unconditional: exact counts
 
     // conv1 (k_conv_thin_bf16 order: taps, 16-channel chunks, sub-tiles)
     floatx16 acc[G::TM];
@@ -1968,21 +1974,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU64F
           acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[k][g], *reinterpret_cast<const bf16x8*>(xb + i * 32 * P),
                                                            acc[i], 0, 0, 0);
       }
-    // residual rows of this wave's sub-tiles and slice in accumulator order
-    // (L2-hot), requested before the h epilogue and the barrier
-    uint2 xres[G::TM][4];
-#pragma unroll
-    for (int i = 0; i < G::TM; ++i) {
-      const int lr = rg * G::WR + i * 32 + (lane & 31);
-      const bool in = lr < mrows;
-      const int64_t orow = (b * a.T + t0 + (in ? lr : 0)) * C + ns * 32 + 4 * hl;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) xres[i][q] = in ? *reinterpret_cast<const uint2*>(x + orow + 8 * q) : make_uint2(0, 0);
-    }
-    // the next tile's rows, requested after the residual rows (which the out
-    // epilogue then waits for alone: memory counters retire in order) and
-    // unconditionally (a dead request loads nothing): exact counts
-    load(tile + 1 < tile_end ? tile + 1 : tile, tile + 1 < tile_end);
     // h = conv1 + b1 -> bf16 -> HBM; ELU(h) -> the 1x1's LDS tile (plane ns)
 #pragma unroll
     for (int i = 0; i < G::TM; ++i) {
@@ -2022,7 +2013,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU64F
       float v[16];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const __bf16* rv = reinterpret_cast<const __bf16*>(&xres[i][q]);
+        const uint2 xres = *reinterpret_cast<const uint2*>(xraw + (ns * R + lr) * P + 8 * q + 4 * hl);
+        const __bf16* rv = reinterpret_cast<const __bf16*>(&xres);
         const floatx4 bq = bias_q(1, q);
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[4 * q + e] = __fadd_rn(acc2[4 * q + e] + bq[e], float(rv[e]));
