@@ -593,7 +593,7 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    timer = _lib.KernelTimer([dom] + (["sel_resunit_fwd", "sel_resunit_bwd"] if cfg == "c3" else [])
+    timer = _lib.KernelTimer([dom] + (["sel_resunit_fwd", "sel_resunit_bwd", "sel_resunit_bwd_wgrad"] if cfg == "c3" else [])
                              + (["sel_dconv_fwd"] if cfg == "c5" else []))
     elapsed, per_step = _timed_steps(step, args.steps, world, dev, timer)
 

@@ -2955,6 +2955,350 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU32W
   if (wave == 3 && lane < 32) part2[int64_t(nb) * G::NW2 + int64_t(blockIdx.x) * RU_C + lane] = bsum;
 }
 
+// ---------------------------------------------------------------------------
+// Residual unit at 64 channels: backward AND both weight gradients in one
+// launch (round 4; the encoder's units, residual_unit.py:43-46 and the wgrad of
+// conv_layer.py:139-142).  The weight-gradient accumulators (28 conv1 tiles +
+// 4 1x1 tiles of 32x32 fp32 = 128 registers per lane over four waves) do not
+// fit beside k_ru64_bwd's register-resident k7 adjoint (112 VGPRs), so the
+// workgroup has eight waves in two roles that share every LDS plane:
+//  * all eight stage the next tile's g, h and x span rows (registers, one
+//    tile ahead, branch-free buffer loads) and compute gh = (W2^T g) * ELU'(h)
+//    over the tile + its anti-causal halo (k_ru64_bwd's gh units) into LDS,
+//    plus ELU(bf16 h) of the tile rows;
+//  * waves 0-3 compute gx = conv1^T(gh) * ELU'(x) + g exactly as k_ru64_bwd
+//    (same MFMA order, rounding points and epilogue: same bits);
+//  * waves 4-7 accumulate the weight gradients over the tile rows with
+//    transposing LDS reads (the k_ru32_bwdw / k_wgrad3_bf16 operand scheme):
+//    wave 4 + v owns h-channel slice v & 1 and, for v < 2, conv1 taps 0-3, for
+//    v >= 2 taps 4-6 and the 1x1 (A = g, B = ELU(h)), both input-channel
+//    slices, plus the bias column sums of gh (v < 2) or g (v >= 2).
+// A workgroup's waves are dealt to the SIMDs cyclically, so each SIMD runs one
+// gx wave beside one weight-gradient wave.  The roles' tile loops are separate
+// code (so neither role's registers are live in the other) with the same
+// barrier sequence.  One workgroup per CU (the planes take 159 KB of LDS);
+// one fp32 partial per workgroup of every weight, in the packed layouts that
+// sel_wgrad_finish_many reduces in block order (deterministic).
+// HBM per row: reads g, h, x and writes gx; k_ru64_bwd with gh plus the two
+// k_wgrad3 launches moved 9 tensors.
+// ---------------------------------------------------------------------------
+template <int R>
+struct Ru64W {
+  static constexpr int C = 64, K = 7, P = F4_P, PW = 32;
+  static constexpr int SPAN = R + F4_HALOMAX;
+  static constexpr int CV = C / 8;
+  static constexpr int XV = (SPAN * CV + 511) / 512;  // staged 16-B pieces per thread and tensor
+  static constexpr int UPW = (2 * (SPAN / 32) + 7) / 8;  // gh (sub-tile, slice) units per wave
+  static constexpr int NW1 = C * K * C, NW2 = C * C;
+  static constexpr int W2P = C + 8;
+  // planes (bf16 elements): g, gh, h [2][SPAN][P]; ELU(x) span [2][SPAN][PW];
+  // raw x tile [2][R][P] (ELU'(x)); ELU(h) tile [2][R][PW]; the 1x1 adjoint [C][W2P]
+  static constexpr size_t OFF_GH = size_t(2) * SPAN * P;
+  static constexpr size_t OFF_H = 2 * OFF_GH;
+  static constexpr size_t OFF_XS = 3 * OFF_GH;
+  static constexpr size_t OFF_XR = OFF_XS + size_t(2) * SPAN * PW;
+  static constexpr size_t OFF_ES = OFF_XR + size_t(2) * R * P;
+  static constexpr size_t OFF_W2 = OFF_ES + size_t(2) * R * PW;
+  static constexpr size_t LDS = (OFF_W2 + size_t(C) * W2P) * 2;
+  static_assert(R % 64 == 0 && LDS <= 160 * 1024, "ru64w tile rows / LDS");
+  static_assert(SPAN * CV % 512 == 0, "ru64w staging pieces");
+};
+
+template <int R>
+struct Ru64WStage {
+  uint4 g[Ru64W<R>::XV], h[Ru64W<R>::XV], x[Ru64W<R>::XV];
+};
+
+// one tile's g, h (rows t0 .. t0 + span) and x (rows t0 - halo .. t0 + R) into
+// registers: branch-free buffer loads (rows outside [0, T), past the span or of
+// a dead request read nothing and return zeros; Ru32Stage::load)
+template <int R>
+__device__ __forceinline__ void ru64w_load(Ru64WStage<R>& st, const Args& a, const __bf16* __restrict__ g,
+                                           const __bf16* __restrict__ h, const __bf16* __restrict__ x, int64_t tile,
+                                           int tps, int halo, bool live) {
+  using G = Ru64W<R>;
+  const int64_t b = tile / tps;
+  const int t0 = int(tile % tps) * R;
+  const int64_t base = b * a.T * G::C;
+  const __amdgpu_buffer_rsrc_t rg = ru_rsrc(g + base, int64_t(a.T) * G::C);
+  const __amdgpu_buffer_rsrc_t rh = ru_rsrc(h + base, int64_t(a.T) * G::C);
+  const __amdgpu_buffer_rsrc_t rx = ru_rsrc(x + base, int64_t(a.T) * G::C);
+  const int span = R + halo;
+#pragma unroll
+  for (int u = 0; u < G::XV; ++u) {
+    const int v = threadIdx.x + u * 512;
+    const int r = v / G::CV, c = (v % G::CV) * 8;
+    const int tg = t0 + r, tx = t0 - halo + r;
+    const bool gok = live && r < span && tg < a.T;
+    const bool xok = live && r < span && tx >= 0 && tx < a.T;
+    st.g[u] = ru_bload(rg, gok ? (tg * G::C + c) * 2 : RU_OOB);
+    st.h[u] = ru_bload(rh, gok ? (tg * G::C + c) * 2 : RU_OOB);
+    st.x[u] = ru_bload(rx, xok ? (tx * G::C + c) * 2 : RU_OOB);
+  }
+}
+
+// the staged tile -> LDS planes (out-of-range rows were loaded as zeros)
+template <int R>
+__device__ __forceinline__ void ru64w_store(const Ru64WStage<R>& st, __bf16* smem_bf, int span, int halo) {
+  using G = Ru64W<R>;
+  constexpr int P = G::P, PW = G::PW, SPAN = G::SPAN;
+  __bf16* const gs = smem_bf;
+  __bf16* const hs = smem_bf + G::OFF_H;
+  __bf16* const xs = smem_bf + G::OFF_XS;
+  __bf16* const xr = smem_bf + G::OFF_XR;
+#pragma unroll
+  for (int u = 0; u < G::XV; ++u) {
+    const int v = threadIdx.x + u * 512;
+    const int r = v / G::CV, c = (v % G::CV) * 8;
+    if (r >= span) continue;
+    const int pl = c >> 5, cc = c & 31;
+    *reinterpret_cast<uint4*>(gs + (pl * SPAN + r) * P + cc) = st.g[u];
+    *reinterpret_cast<uint4*>(hs + (pl * SPAN + r) * P + cc) = st.h[u];
+    *reinterpret_cast<uint4*>(xs + (pl * SPAN + r) * PW + cc) = elu8(st.x[u]);
+    if (r >= halo && r < halo + R) *reinterpret_cast<uint4*>(xr + (pl * R + r - halo) * P + cc) = st.x[u];
+  }
+}
+
+// gh = (W2^T g) * ELU'(h) over rows t0 .. t0 + span (k_ru64_bwd's units, round
+// robin over the eight waves) -> ghs; ELU(bf16 h) of the tile rows -> es
+template <int R>
+__device__ __forceinline__ void ru64w_gh(__bf16* smem_bf, int wave, int lane, int nsub, int span) {
+  using G = Ru64W<R>;
+  constexpr int P = G::P, PW = G::PW, SPAN = G::SPAN, C = G::C;
+  const __bf16* const gs = smem_bf;
+  __bf16* const ghs = smem_bf + G::OFF_GH;
+  const __bf16* const hs = smem_bf + G::OFF_H;
+  __bf16* const es = smem_bf + G::OFF_ES;
+  const __bf16* const w2s = smem_bf + G::OFF_W2;
+  const int hl = lane >> 5;
+#pragma unroll
+  for (int uu = 0; uu < G::UPW; ++uu) {
+    const int unit = wave + 8 * uu;
+    if (unit >= 2 * nsub) break;  // wave-uniform
+    const int sb = unit >> 1, sl = unit & 1;
+    const int lr = sb * 32 + (lane & 31);
+    bf16x8 w2q[C / 16];
+    {
+      const __bf16* wr2 = w2s + (sl * 32 + (lane & 31)) * G::W2P + 8 * hl;
+#pragma unroll
+      for (int q = 0; q < C / 16; ++q) w2q[q] = *reinterpret_cast<const bf16x8*>(wr2 + 16 * q);
+    }
+    floatx16 acc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+    const __bf16* gw = gs + lr * P + 8 * hl;
+#pragma unroll
+    for (int q = 0; q < C / 16; ++q)
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w2q[q], *reinterpret_cast<const bf16x8*>(gw + (q >> 1) * SPAN * P + 16 * (q & 1)),
+                                                    acc, 0, 0, 0);
+    uint2 hq[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) hq[q] = *reinterpret_cast<const uint2*>(hs + (sl * SPAN + lr) * P + 8 * q + 4 * hl);
+    float v[16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const __bf16* hv = reinterpret_cast<const __bf16*>(&hq[q]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[4 * q + e] = __fmul_rn(acc[4 * q + e], elu_grad_fast(float(hv[e])));
+    }
+    bf16x8 ghf[2];
+    ru_acc_to_frags(v, ghf);
+    if (lr < span) {
+      *reinterpret_cast<bf16x8*>(ghs + (sl * SPAN + lr) * P + 8 * hl) = ghf[0];
+      *reinterpret_cast<bf16x8*>(ghs + (sl * SPAN + lr) * P + 16 + 8 * hl) = ghf[1];
+    }
+    if (sb < R / 32) {  // wave-uniform: a tile sub-tile (rows past T hold h = 0 -> ELU = 0)
+#pragma unroll
+      for (int qq = 0; qq < 2; ++qq) {
+        const uint4 e8 = elu8(make_uint4(hq[2 * qq].x, hq[2 * qq].y, hq[2 * qq + 1].x, hq[2 * qq + 1].y));
+        *reinterpret_cast<uint2*>(es + (sl * R + lr) * PW + 16 * qq + 4 * hl) = make_uint2(e8.x, e8.y);
+        *reinterpret_cast<uint2*>(es + (sl * R + lr) * PW + 16 * qq + 8 + 4 * hl) = make_uint2(e8.z, e8.w);
+      }
+    }
+  }
+}
+
+template <int R>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k_ru64_bwdw(
+    Args a, const __bf16* __restrict__ g, const __bf16* __restrict__ h, const __bf16* __restrict__ x,
+    const __bf16* __restrict__ wd1, const __bf16* __restrict__ wd2, __bf16* __restrict__ gx,
+    float* __restrict__ part1, float* __restrict__ part2, int tiles_per_block) {
+  using G = Ru64W<R>;
+  constexpr int P = G::P, PW = G::PW, C = G::C, K = G::K, SPAN = G::SPAN;
+  extern __shared__ __align__(16) unsigned char smem[];
+  __bf16* const sb = reinterpret_cast<__bf16*>(smem);
+  const __bf16* const gs = sb;
+  const __bf16* const ghs = sb + G::OFF_GH;
+  const __bf16* const xs = sb + G::OFF_XS;
+  const __bf16* const xr = sb + G::OFF_XR;
+  const __bf16* const es = sb + G::OFF_ES;
+  const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int halo = (K - 1) * a.dil;
+  const int span = R + halo;
+  const int nsub = (span + 31) / 32;
+  const int tps = (a.T + R - 1) / R;
+  int64_t tile0 = 0, tile_end = 0;
+  const bool any = ru_tiles((a.rows / a.T) * tps, tiles_per_block, tile0, tile_end);
+
+  // the 1x1 adjoint's weights [C][C] -> LDS (rows padded to W2P; k_ru64_bwd)
+  if (any) {
+    __bf16* const w2s = sb + G::OFF_W2;
+    for (int i = tid; i < C * C / 8; i += 512) {
+      const int n = i / (C / 8), c8 = (i % (C / 8)) * 8;
+      *reinterpret_cast<bf16x8*>(w2s + n * G::W2P + c8) = *reinterpret_cast<const bf16x8*>(wd2 + int64_t(n) * C + c8);
+    }
+  }
+
+  if (wave < 4) {
+    // ---- gx role: k_ru64_bwd's gx phase (row group rg, output slice ns) ----
+    if (!any) return;  // workgroup-uniform: a block without tiles has no barriers
+    const int ns = wave & 1, rg = wave >> 1;
+    constexpr int WR = R / 2, TM = WR / 32;
+    bf16x8 wf[K][C / 16];
+    {
+      const __bf16* wrow = wd1 + int64_t(ns * 32 + (lane & 31)) * K * C + 8 * hl;
+#pragma unroll
+      for (int k = 0; k < K; ++k)
+#pragma unroll
+        for (int q = 0; q < C / 16; ++q) wf[k][q] = *reinterpret_cast<const bf16x8*>(wrow + k * C + 16 * q);
+    }
+    ws_wait_vm<0>();  // weights landed: the tile loop's waits then count only its own loads
+    Ru64WStage<R> st;
+    ru64w_load<R>(st, a, g, h, x, tile0, tps, halo, true);
+    for (int64_t tile = tile0; tile < tile_end; ++tile) {
+      const int64_t b = tile / tps;
+      const int t0 = int(tile % tps) * R;
+      const int mrows = a.T - t0 < R ? a.T - t0 : R;
+      __syncthreads();  // B1: every wave is done with the previous tile's planes
+      ru64w_store<R>(st, sb, span, halo);
+      __syncthreads();  // B2
+      ru64w_load<R>(st, a, g, h, x, tile + 1 < tile_end ? tile + 1 : tile, tps, halo, tile + 1 < tile_end);
+      ru64w_gh<R>(sb, wave, lane, nsub, span);
+      __syncthreads();  // B3: gh planes complete
+      floatx16 acc[TM];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
+      const __bf16* hw = ghs + (rg * WR + (lane & 31)) * P + 8 * hl;
+#pragma unroll
+      for (int k = 0; k < K; ++k)
+#pragma unroll
+        for (int q = 0; q < C / 16; ++q) {
+          const __bf16* hb = hw + ((q >> 1) * SPAN + k * a.dil) * P + 16 * (q & 1);
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+            acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[k][q], *reinterpret_cast<const bf16x8*>(hb + i * 32 * P),
+                                                             acc[i], 0, 0, 0);
+        }
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int lr = rg * WR + i * 32 + (lane & 31);
+        if (__builtin_amdgcn_readfirstlane(rg * WR + i * 32) >= mrows) break;
+        const bool valid = lr < mrows;
+        const int64_t orow = (b * a.T + t0 + (valid ? lr : 0)) * C + ns * 32;
+        float v[16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint2 graw = *reinterpret_cast<const uint2*>(gs + (ns * SPAN + lr) * P + 8 * q + 4 * hl);
+          const uint2 xraw = *reinterpret_cast<const uint2*>(xr + (ns * R + lr) * P + 8 * q + 4 * hl);
+          const __bf16* xv = reinterpret_cast<const __bf16*>(&xraw);
+          const __bf16* gv = reinterpret_cast<const __bf16*>(&graw);
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            v[4 * q + e] = __fadd_rn(__fmul_rn(acc[i][4 * q + e], elu_grad_fast(float(xv[e]))), float(gv[e]));
+        }
+        bf16x8 of[2];
+        ru_acc_to_frags(v, of);
+        if (valid) {
+          ru_store(gx + orow + 8 * hl, of[0]);
+          ru_store(gx + orow + 16 + 8 * hl, of[1]);
+        }
+      }
+    }
+    return;
+  }
+
+  // ---- weight-gradient role ----
+  const int v = wave - 4;
+  const int wn = v & 1;     // h-channel (output) slice of the weight gradients
+  const int upper = v >> 1;  // 0: conv1 taps 0-3; 1: taps 4-6 + the 1x1
+  floatx16 wacc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) wacc[j][e] = 0.f;
+  float bsum = 0.f;  // column sums of gh (upper = 0: conv1 bias) or g (upper = 1: the 1x1's)
+  if (any) {
+    const int tq = (lane & 15) >> 2;
+    const int tcol = ((lane >> 4) & 1) * 16 + 4 * (lane & 3);
+    auto trfrag = [&](const __bf16* base, int pitch, int r0) {
+      const v4i16 lo = tr_read(base + (r0 + 4 * hl + tq) * pitch + tcol);
+      const v4i16 hi = tr_read(base + (r0 + 8 + 4 * hl + tq) * pitch + tcol);
+      return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+    };
+    // wave-uniform operand bases: A0 = gh slice wn; jobs 0-5 = taps kb + j/2 over
+    // ELU(x) input slice j & 1; jobs 6-7: A1 (gh again / g) against tap 3 of
+    // ELU(x) (upper = 0) or ELU(h) (upper = 1), input slice j & 1
+    const int kb = upper ? 4 : 0;
+    const __bf16* const a0p = ghs + wn * SPAN * P;
+    const __bf16* const a1p = upper ? gs + wn * SPAN * P : a0p;
+    const __bf16* const b67 = upper ? es : xs + 3 * a.dil * PW;
+    const int b67s = upper ? R * PW : SPAN * PW;
+    Ru64WStage<R> st;
+    ru64w_load<R>(st, a, g, h, x, tile0, tps, halo, true);
+    for (int64_t tile = tile0; tile < tile_end; ++tile) {
+      __syncthreads();  // B1
+      ru64w_store<R>(st, sb, span, halo);
+      __syncthreads();  // B2
+      ru64w_load<R>(st, a, g, h, x, tile + 1 < tile_end ? tile + 1 : tile, tps, halo, tile + 1 < tile_end);
+      ru64w_gh<R>(sb, wave, lane, nsub, span);
+      __syncthreads();  // B3
+      // rows past T hold g = 0 -> gh = 0: no masks
+#pragma unroll 1
+      for (int kh = 0; kh < R / 16; ++kh) {
+        const bf16x8 A0 = trfrag(a0p, P, kh * 16);
+        const bf16x8 A1 = trfrag(a1p, P, kh * 16);
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+          const bf16x8 B = trfrag(xs + ((j & 1) * SPAN + (kb + (j >> 1)) * a.dil) * PW, PW, kh * 16);
+          wacc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0, B, wacc[j], 0, 0, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const bf16x8 B = trfrag(b67 + j * b67s, PW, kh * 16);
+          wacc[6 + j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1, B, wacc[6 + j], 0, 0, 0);
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bsum += float(A1[e]);
+      }
+    }
+  }
+  // this block's partials (zeros from a block without tiles): accumulator
+  // element r of lane l -> n = wn*32 + (r & 3) + 8 (r >> 2) + 4 hl, c = slice*32 + (l & 31)
+  const int nb = gridDim.x;
+  float* const p1 = part1 + int64_t(blockIdx.x) * G::NW1;
+  float* const p2 = part2 + int64_t(blockIdx.x) * G::NW2;
+  const int kb = upper ? 4 : 0;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int n = wn * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl, c = lane & 31;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) p1[(n * K + kb + (j >> 1)) * C + (j & 1) * 32 + c] = wacc[j][r];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      if (upper) p2[n * C + j * 32 + c] = wacc[6 + j][r];
+      else p1[(n * K + 3) * C + j * 32 + c] = wacc[6 + j][r];
+    }
+  }
+  bsum += __shfl_xor(bsum, 32, 64);
+  if (lane < 32) {
+    if (upper) part2[int64_t(nb) * G::NW2 + int64_t(blockIdx.x) * C + wn * 32 + lane] = bsum;
+    else part1[int64_t(nb) * G::NW1 + int64_t(blockIdx.x) * C + wn * 32 + lane] = bsum;
+  }
+}
+
 constexpr int WB_BM = 64;
 constexpr int WB_BC = 32;
 constexpr int WB_MAXJ = 16;
@@ -4018,7 +4362,7 @@ int launch_thin(const Args& a, const void* in, const void* wp, const float* bias
 
 int thin_index(const Args& a) {
   // (one sample's rows must fit a 2^31-byte buffer resource: ru_rsrc)
-  if (tune(4) == 1 || (a.K - 1) * a.dil > F4_HALOMAX || int64_t(a.T) * a.C * 2 >= (int64_t(1) << 31)) return -1;
+  if (tune(4) == 1 || (a.K - 1) * a.dil > F4_HALOMAX || !ru_region_ok(int64_t(a.T) * a.C * 2)) return -1;
 #define SEL_THIN_IDX(I_, C_, N_, K_, R_, R2_) \
   if (a.C == C_ && a.N == N_ && a.K == K_) return (tune(7) >> I_) & 1 ? -1 : I_;
   SEL_THIN_SHAPES(SEL_THIN_IDX)
@@ -4216,10 +4560,45 @@ int launch_ru32_bwdw(const Args& a, const void* g, const void* h, const void* x,
   return SEL_OK;
 }
 
+// fused 64-channel backward with the weight gradients: one 512-thread block per
+// CU (its LDS planes), one partial per block
+template <int R>
+int ru64w_blocks(int64_t ntiles, int64_t& tpb) {
+  static const int64_t slots = [] {
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipFuncSetAttribute((const void*)k_ru64_bwdw<R>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            int(Ru64W<R>::LDS)) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_ru64_bwdw<R>, 512, Ru64W<R>::LDS) != hipSuccess)
+      return int64_t(0);
+    return int64_t(cus) * per_cu / 8 * 8;
+  }();
+  const int64_t target = tune(40) > 0 ? tune(40) : (slots > 0 ? slots : 256);
+  tpb = std::max<int64_t>(1, (ntiles + target - 1) / target);
+  return int(((ntiles + tpb - 1) / tpb + 7) / 8 * 8);
+}
+
+template <int R>
+int launch_ru64_bwdw(const Args& a, const void* g, const void* h, const void* x, const void* wd1, const void* wd2,
+                     void* gx, float* part1, float* part2, int nsplit, hipStream_t s) {
+  const int64_t ntiles = (a.rows / a.T) * ((a.T + R - 1) / R);
+  int64_t tpb = 1;
+  const int nb = ru64w_blocks<R>(ntiles, tpb);
+  SEL_REQUIRE(nb == nsplit, SEL_ERR_ARG, "sel_resunit_bwd_wgrad: nsplit %d, this shape needs %d", nsplit, nb);
+  SEL_HIP(hipFuncSetAttribute((const void*)k_ru64_bwdw<R>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              int(Ru64W<R>::LDS)));
+  hipLaunchKernelGGL(k_ru64_bwdw<R>, dim3(unsigned(nb)), dim3(512), Ru64W<R>::LDS, s, a, static_cast<const __bf16*>(g),
+                     static_cast<const __bf16*>(h), static_cast<const __bf16*>(x), static_cast<const __bf16*>(wd1),
+                     static_cast<const __bf16*>(wd2), static_cast<__bf16*>(gx), part1, part2, int(tpb));
+  SEL_LAUNCH_CHECK();
+  return SEL_OK;
+}
+
 bool ru_fused_ok(const Args& a) {
   return (a.C == 32 || a.C == 64) && a.N == a.C && a.K == 7 && a.pad == (a.K - 1) * a.dil &&
          a.pad_mode == SEL_PAD_ZERO && a.in_elu == 1 && (a.K - 1) * a.dil <= F4_HALOMAX &&
-         (a.bias_period == 0 || a.bias_period == a.N) && int64_t(a.T) * a.C * 2 < (int64_t(1) << 31);
+         (a.bias_period == 0 || a.bias_period == a.N) && ru_region_ok(int64_t(a.T) * a.C * 2);
 }
 
 template <typename TI, typename TO>
@@ -4291,7 +4670,7 @@ struct WgPlan {
 bool wgrad_tr_ok(const sel_conv_desc* d) {
   // (one sample's gout / input rows must fit a 2^31-byte buffer resource: ru_rsrc)
   return d->C % 32 == 0 && d->N % 32 == 0 && (d->K - 1) * d->dil <= W2_HALO && d->K <= 8 &&
-         int64_t(d->T) * std::max(d->C, d->N) * 2 < (int64_t(1) << 31);
+         ru_region_ok(int64_t(d->T) * std::max(d->C, d->N) * 2);
 }
 
 // tune key 1: 0 = k_wgrad3 where legal, 1 = generic, 2 = k_wgrad2 (32x32 blocks)
@@ -4541,10 +4920,11 @@ int sel_resunit_bwd(const sel_conv_desc* d1, int dtype, const void* g, const voi
 int sel_resunit_wgrad_splits(const sel_conv_desc* d1, int dtype) {
   if (int rc = check_desc(d1)) return rc;
   const Args a = to_args(d1);
-  SEL_REQUIRE(dtype == SEL_BF16 && ru_fused_ok(a) && a.C == 32 && a.rows > 0, SEL_ERR_UNSUPPORTED,
-              "sel_resunit_bwd_wgrad: needs bf16, C = N = 32, K = 7, causal zero pad, ELU prologue");
+  SEL_REQUIRE(dtype == SEL_BF16 && ru_fused_ok(a) && a.rows > 0, SEL_ERR_UNSUPPORTED,
+              "sel_resunit_bwd_wgrad: needs bf16, C = N in {32, 64}, K = 7, causal zero pad, ELU prologue");
   int64_t tpb = 1;
-  return ru32w_blocks<128>((a.rows / a.T) * ((a.T + 127) / 128), tpb);
+  const int64_t ntiles = (a.rows / a.T) * ((a.T + 127) / 128);
+  return a.C == 64 ? ru64w_blocks<128>(ntiles, tpb) : ru32w_blocks<128>(ntiles, tpb);
 }
 
 int sel_resunit_bwd_wgrad(const sel_conv_desc* d1, int dtype, const void* g, const void* h, const void* x,
@@ -4552,9 +4932,12 @@ int sel_resunit_bwd_wgrad(const sel_conv_desc* d1, int dtype, const void* g, con
                           sel_stream_t stream) {
   if (int rc = check_desc(d1)) return rc;
   const Args a = to_args(d1);
-  SEL_REQUIRE(dtype == SEL_BF16 && ru_fused_ok(a) && a.C == 32 && a.rows > 0, SEL_ERR_UNSUPPORTED,
-              "sel_resunit_bwd_wgrad: needs bf16, C = N = 32, K = 7, causal zero pad, ELU prologue");
+  SEL_REQUIRE(dtype == SEL_BF16 && ru_fused_ok(a) && a.rows > 0, SEL_ERR_UNSUPPORTED,
+              "sel_resunit_bwd_wgrad: needs bf16, C = N in {32, 64}, K = 7, causal zero pad, ELU prologue");
   SEL_REQUIRE(g && h && x && wd1pack && wd2pack && gx && part1 && part2, SEL_ERR_ARG, "null pointer");
+  if (a.C == 64)
+    return launch_ru64_bwdw<128>(a, g, h, x, wd1pack, wd2pack, gx, part1, part2, nsplit,
+                                 reinterpret_cast<hipStream_t>(stream));
   return launch_ru32_bwdw<128>(a, g, h, x, wd1pack, wd2pack, gx, part1, part2, nsplit,
                                reinterpret_cast<hipStream_t>(stream));
 }

@@ -2148,8 +2148,8 @@ WgPlanD wg_plan(const sel_dconv_desc* d, int dtype) {
   }
   p.w3 = p.mfma && d->G == 1 && d->So == 1 && (d->S == 1 || d->Cs == d->Cg) && d->K <= 8 && width % 32 == 0 &&
          nred % 32 == 0 && d->ldo % 8 == 0 && tune(16) != 1 &&
-         // gout and x as buffer resources (ru_rsrc): < 2^31 bytes each
-         int64_t(d->B) * d->Tvo * d->ldo * 2 < (int64_t(1) << 31) && int64_t(d->B) * d->Tvs * d->ldx * 2 < (int64_t(1) << 31);
+         // gout and x as buffer resources (ru_rsrc): ru_region_ok
+         ru_region_ok(int64_t(d->B) * d->Tvo * d->ldo * 2) && ru_region_ok(int64_t(d->B) * d->Tvs * d->ldx * 2);
   if (p.w3) {
     p.w3_nt = width % 64 == 0 ? 2 : 1;
     p.w3_ct = nred % 64 == 0 ? 2 : 1;

@@ -44,7 +44,7 @@ __device__ __forceinline__ T block_sum(T v, T* red) {
 }
 
 // Branch-free staging loads for the persistent tile loops: a bf16 tensor
-// region as a buffer resource (bytes < 2^31: the dispatch predicates check)
+// region as a buffer resource (bytes <= RU_OOB: ru_region_ok, checked by the dispatch predicates)
 // and a 16-B load from it.  RU_OOB is past any region's bytes, so a load there
 // returns zeros and touches no memory: rows outside the sample / span and a
 // dead next-tile request take it instead of a branch around the load, and the
@@ -57,6 +57,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t ru_rsrc(const __bf16* base, in
 __device__ __forceinline__ uint4 ru_bload(__amdgpu_buffer_rsrc_t rs, int byte_off) {
   return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, byte_off, 0, 0));
 }
+// Host-side predicate of every dispatch that builds such a resource: the
+// region's bytes must end at or before RU_OOB, so an RU_OOB request lies past
+// it (a region reaching into [RU_OOB, 2^31) would turn a dead request into a
+// real load).
+inline bool ru_region_ok(int64_t bytes) { return bytes >= 0 && bytes <= RU_OOB; }
 
 }  // namespace sel
 

@@ -63,10 +63,19 @@ class Discriminator(nn.Module):
         x = self._flat(x)
         return self._chains(x, self.msd._scales(x, lambda f, v: v), "stash_first_half")
 
+    def clear_stash(self):
+        """Drop every sub-discriminator's stash_first_half buffers (sized for 2B
+        clips): called whenever the generator step will not be followed by a
+        forward_second_half that consumes them."""
+        for f in list(self.msd.discriminators) + list(self.mpd.discriminators):
+            f._stash = None
+
     def forward_second_half(self, x):
         """forward(torch.cat([stashed clips, x])) without recomputing the stashed
-        half: the same outputs (the kernels compute every output row the same
-        way for any batch), one autograd graph over all 2B clips."""
+        half, as one autograd graph over all 2B clips.  Each output row runs the
+        same kernels as in the concatenated pass, but the flat tiling may put a
+        clip in another tile: tests/test_gpu_gan.py holds the two paths to 1e-6
+        (fp32) / 1e-3 (bf16) norm-wise, not to bit equality."""
         x = self._flat(x)
         with torch.no_grad():  # the waveform (a detached prediction) takes no gradient
             pooled = self.msd._scales(x, lambda f, v: v)

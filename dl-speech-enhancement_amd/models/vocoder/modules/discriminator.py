@@ -142,8 +142,7 @@ class HiFiGANPeriodDiscriminator(nn.Module):
 
     def forward_second_half(self, x):
         """forward(cat[stashed clips, x]) with the stashed half not recomputed."""
-        x0, bufs, n, Lv = self._stash
-        self._stash = None
+        x0, bufs, n, Lv = _take_stash(self)
         x0[n:] = self._x0(x)[0].detach()
         return self._outs(DC.ChainFn.apply(x0, Lv, self.plan(), self.slope, self.use_weight_norm, "period",
                                            2 * x.shape[0], self.period, getattr(self, "_frozen", False),
@@ -158,6 +157,16 @@ class HiFiGANPeriodDiscriminator(nn.Module):
 
     def apply_spectral_norm(self):
         raise NotImplementedError("spectral norm is not lowered to the HIP path")
+
+
+def _take_stash(f):
+    """The stash_first_half state of sub-discriminator f, consumed (a clear error
+    instead of an unpacking failure when there is none)."""
+    st = getattr(f, "_stash", None)
+    if st is None:
+        raise RuntimeError(f"{type(f).__name__}.forward_second_half needs a stash_first_half of the same step")
+    f._stash = None
+    return st
 
 
 class HiFiGANMultiPeriodDiscriminator(nn.Module):
@@ -267,8 +276,7 @@ class HiFiGANScaleDiscriminator(nn.Module):
         return [DC._view(y[:b], "scale", b, g[2], 1) for y, g in zip(bufs, geo)]
 
     def forward_second_half(self, x):
-        x0, bufs, b, t = self._stash
-        self._stash = None
+        x0, bufs, b, t = _take_stash(self)
         x0[b:] = self._x0(x).detach()
         return list(DC.ChainFn.apply(x0, t, self.plan(), self.slope, False, "scale", 2 * b, 1,
                                      getattr(self, "_frozen", False), (b, bufs), *self._params()))

@@ -408,13 +408,19 @@ def _flush_deferred():
                 raise L.SelError("sel: a deferred weight gradient did not become the parameter's .grad "
                                  "(set SEL_WGRAD_DEFER=0 for this use)")
     # one launch per stream the partial kernels ran on (normally one)
+    cur = torch.cuda.current_stream()
     for st in dict.fromkeys(e[3] for e in pending):
         group = [e[0] for e in pending if e[3] == st]
         jobs = (_WgradJob * len(group))(*group)
         L.call("sel_wgrad_finish_many", ctypes.cast(jobs, ctypes.c_void_p), len(group), ctypes.c_void_p(st))
-        side = next((s for s in _WG_STREAMS.values() if s.cuda_stream == st), None)
-        if side is not None:  # the gradients are read on the current stream from here on
-            torch.cuda.current_stream(side.device).wait_stream(side)
+        if (st or 0) != cur.cuda_stream:  # (a null-stream handle reads as None)
+            # the gradients are read on the current stream from here on (the
+            # optimizer): order it after this finish on ANY other stream, not
+            # only the SEL_WGRAD_STREAM side streams
+            side = next((s for s in _WG_STREAMS.values() if s.cuda_stream == st), None)
+            if side is None:
+                side = torch.cuda.ExternalStream(st, device=cur.device)
+            cur.wait_stream(side)
     # the workspaces are released here; the finish kernel is already enqueued on
     # this stream ahead of any later use of that memory
 
@@ -586,17 +592,24 @@ def _ru_bwd_meta(d1, xf, want_gh, wgrad=False):
     nbytes = (4 + int(want_gh)) * d1.rows * d1.C * es
     flops = 2.0 * d1.rows * d1.N * d1.C * (d1.K + 1) * (2 if wgrad else 1)
     if wgrad:
-        return "k_ru32_bwdw<128>", nbytes, flops
+        return ("k_ru32_bwdw<128>" if d1.C == 32 else "k_ru64_bwdw<128>"), nbytes, flops
     return ("k_ru32_bwd<128>" if d1.C == 32 else "k_ru64_bwd<128>"), nbytes, flops
 
 
-# fused 32-channel backward with both weight gradients (SEL_RU_WGRAD=0: off)
-RU_WGRAD = os.environ.get("SEL_RU_WGRAD", "1") != "0"
+# fused backward with both weight gradients (k_ru32_bwdw / k_ru64_bwdw);
+# SEL_RU_WGRAD=0: off, =32: the 32-channel unit only (A/B of the 64-channel kernel)
+RU_WGRAD = os.environ.get("SEL_RU_WGRAD", "1")
+
+
+def ru_wgrad_fused_ok(d1, dtype):
+    """Fused residual-unit backward with both weight gradients for this conv1?"""
+    return (RU_WGRAD != "0" and ru_bwd_fused_ok(d1, dtype) and (d1.C == 32 or RU_WGRAD != "32"))
 
 
 def resunit_bwd_wgrad(d1, gf, h, xf, wd1, wd2, s1, s2, want_b1, want_b2, params1, params2):
-    """gx and both weight gradients of a 32-channel residual unit: ONE launch
-    (k_ru32_bwdw: gh, gx, and per-block partials of conv1 and the 1x1), then the
+    """gx and both weight gradients of a 32- or 64-channel residual unit: ONE
+    launch (k_ru32_bwdw / k_ru64_bwdw: gh, gx, and per-block partials of conv1
+    and the 1x1), then the
     block-order reduction into the torch layouts, deferred to the end of the
     backward like wgrad_torch's when the parameters allow it (params1 / params2:
     the (weight, bias) leaves receiving gw1, gb1 / gw2, gb2, or None)."""
@@ -690,9 +703,8 @@ class ResidualUnitFn(torch.autograd.Function):
         need_w2 = ctx.needs_input_grad[3] or ctx.needs_input_grad[4]
         gx = None
         pr = ctx.prefs
-        if (RU_WGRAD and ctx.needs_input_grad[0] and need_w1 and need_w2 and d1.C == 32
-                and ru_bwd_fused_ok(d1, x.dtype)):
-            # one launch: gx and both weight gradients (k_ru32_bwdw)
+        if ctx.needs_input_grad[0] and need_w1 and need_w2 and ru_wgrad_fused_ok(d1, x.dtype):
+            # one launch: gx and both weight gradients (k_ru32_bwdw / k_ru64_bwdw)
             want_b1 = d1.bias_period > 0 and ctx.needs_input_grad[2]
             want_b2 = d2.bias_period > 0 and ctx.needs_input_grad[4]
             p1 = _live(pr[0], pr[1] if want_b1 else None) if ctx.needs_input_grad[1] else None

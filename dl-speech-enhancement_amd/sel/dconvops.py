@@ -290,9 +290,10 @@ def chain_forward(x0, T0, specs, slope, wn, params, lo=0, hi=None, bufs=None):
     """The layers of one sub-discriminator over the sequences [lo, hi) of x0
     (Bs, T0_alloc, 1) into the per-layer buffers `bufs` (allocated for all Bs
     sequences when None; other sequences are left as they are).  Returns
-    (bufs, geo).  The kernels compute each output row the same way whatever
-    the launch's sequence count, so a chain run in two halves gives the bits of
-    one run over the whole batch."""
+    (bufs, geo).  Each output row runs the same kernels whatever the launch's
+    sequence count; the flat tiling may put a sequence in another tile, so a
+    chain run in two halves is held to the concatenated run at 1e-6 (fp32) /
+    1e-3 (bf16) norm-wise by tests/test_gpu_gan.py, not to bit equality."""
     dtype = x0.dtype
     Bs = x0.shape[0]
     hi = Bs if hi is None else hi

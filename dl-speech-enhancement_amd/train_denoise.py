@@ -103,6 +103,11 @@ class DenoiseStep:
                 dkw.setdefault("fused", True)
             self.optimizer["discriminator"] = (disc_optimizer if disc_optimizer is not None
                                                else torch.optim.Adam(discriminator.parameters(), **dkw))
+            self._d_opt_steps = 0
+
+            def _d_stepped(*_):
+                self._d_opt_steps += 1
+            self.optimizer["discriminator"].register_step_post_hook(_d_stepped)
         self.measures = {"MAE": nn.L1Loss(), "SNR": SignalNoiseRatio(),
                          "Mel-loss": MultiMelSpectrogramLoss(**config["mel_loss_params"]).to(device)}
         # :123-131 (note: FeatureMatchLoss() with its DEFAULT averaging, as the reference builds it)
@@ -132,13 +137,14 @@ class DenoiseStep:
             Dm = _unwrap(self.model["discriminator"])
             with frozen_parameters(Dm) as D:
                 p_ = D(pred)
-            self._stashed = None
+            self._drop_stash()
             if self._reuse_real():
                 # D(target) is also the real half of the D step (:160): D's weights
                 # change only in that step's Adam update.  Computed once, into the
-                # D step's buffers (Discriminator.stash_first_half)
+                # D step's buffers (Discriminator.stash_first_half); valid for
+                # exactly this target tensor and these D parameters (_stash_key)
                 p = Dm.stash_first_half(target)
-                self._stashed = target.shape[0]
+                self._stashed = self._stash_key(target)
             else:
                 with torch.no_grad():
                     p = Dm(target)
@@ -153,16 +159,34 @@ class DenoiseStep:
         forward under DDP)."""
         D = self.model["discriminator"]
         B = target.shape[0]
-        if getattr(self, "_stashed", None) == B:
-            # the real half was computed in the generator step: only D(pred) runs
+        st = getattr(self, "_stashed", None)
+        if st is not None and st[0] is target and st[1:] == self._stash_key(target)[1:]:
+            # the real half was computed in the generator step from this same
+            # target and the same D weights: only D(pred) runs
             self._stashed = None
             outs = _unwrap(D).forward_second_half(pred)
         else:
+            self._drop_stash()
             outs = D(torch.cat([target, pred], 0))
         p = [[t[:B] for t in o] for o in outs]
         p_ = [[t[B:] for t in o] for o in outs]
         real_loss, fake_loss = self.criterion["dis_adv"](p_, p)
         return (real_loss + fake_loss) * self.config["lambda_adv"]
+
+    def _stash_key(self, target):
+        """What a stashed D(target) is valid for: the target tensor itself (and
+        its version), the D parameters' versions and the D optimizer's step count
+        (torch's fused Adam writes the parameters without bumping _version)."""
+        Dm = _unwrap(self.model["discriminator"])
+        return (target, target._version, tuple(p._version for p in Dm.parameters()),
+                getattr(self, "_d_opt_steps", 0))
+
+    def _drop_stash(self):
+        """Forget a stashed real half (and free its 2B-clip buffers)."""
+        self._stashed = None
+        Dm = _unwrap(self.model["discriminator"]) if self.model.get("discriminator") is not None else None
+        if Dm is not None and hasattr(Dm, "clear_stash"):
+            Dm.clear_stash()
 
     def _reuse_real(self):
         """Reuse the generator step's D(target) as the D step's real half: one

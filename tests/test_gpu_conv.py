@@ -487,6 +487,60 @@ def test_resunit32_bwd_wgrad_fused(gpu, shape):
         assert rel(gb1, ghd.sum((0, 1))) <= 1e-5 and rel(gb2, g.double().sum(0)) <= 1e-5
 
 
+RU64_WGRAD_SHAPES = [(1, 1, 2, 500), (3, 1, 3, 333), (9, 0, 2, 40), (9, 1, 1, 130), (9, 1, 8, 8000),
+                     (1, 0, 64, 8000), (3, 1, 64, 8000), (9, 1, 64, 8000)]
+
+
+@pytest.mark.parametrize("shape", RU64_WGRAD_SHAPES, ids=lambda s: "d{}b{}B{}T{}".format(*s))
+def test_resunit64_bwd_wgrad_fused(gpu, shape):
+    """sel_resunit_bwd_wgrad at 64 channels (k_ru64_bwdw: eight waves, gx waves
+    beside weight-gradient waves, per-block partials reduced by
+    sel_wgrad_finish_many) against the unfused path on the same bf16 operands:
+    gx bit-identical to k_ru64_bwd (same gx phase), the four weight / bias
+    gradients against the two k_wgrad3 launches (another fp32 row-summation
+    order: <= 1e-5 norm-wise) and against fp64 of the same bf16 operands
+    (<= 1e-5).  Ragged tails, T < halo, one tile, empty blocks and the C3 RU64
+    size (B = 64 x 8000) at the three dilations."""
+    from sel import convops as CO
+    dil, bias, B, T = shape
+    C = 64
+    torch.manual_seed(dil + T + B + 64)
+    x = (0.5 * torch.randn(B * T, C, device=gpu)).to(torch.bfloat16)
+    h = (0.5 * torch.randn(B * T, C, device=gpu)).to(torch.bfloat16)
+    g = (0.5 * torch.randn(B * T, C, device=gpu)).to(torch.bfloat16)
+    w1 = 0.1 * torch.randn(C, C, 7, device=gpu)
+    w2 = 0.2 * torch.randn(C, C, 1, device=gpu)
+    d1 = CO.ConvDesc(B * T, T, C, C, 7, dil, 6 * dil, CO.PAD_ZERO, 1, C if bias else 0)
+    d2 = CO.ConvDesc(B * T, T, C, C, 1, 1, 0, CO.PAD_ZERO, 1, C if bias else 0)
+    wp1, wd1 = CO.PACKS.get(CO.PACK_FWD, w1, 1, torch.bfloat16)
+    wp2, wd2 = CO.PACKS.get(CO.PACK_FWD, w2, 1, torch.bfloat16)
+    assert CO.ru_wgrad_fused_ok(d1, torch.bfloat16)
+    gx, gw1, gb1, gw2, gb2 = CO.resunit_bwd_wgrad(d1, g, h, x, wd1, wd2, (C, C, 7), (C, C, 1), bool(bias),
+                                                  bool(bias), None, None)
+    gx_ref, gh_ref = CO.resunit_bwd(d1, g, h, x, wd1, wd2, True)
+    assert torch.equal(gx, gx_ref), (gx.float() - gx_ref.float()).abs().max().item()
+    gw2_ref, gb2_ref = CO.wgrad_torch(d2, g, h, CO.PACK_FWD, (C, C, 1), 1, bool(bias))
+    gw1_ref, gb1_ref = CO.wgrad_torch(d1, gh_ref, x, CO.PACK_FWD, (C, C, 7), 1, bool(bias))
+    torch.cuda.synchronize()
+    rel = lambda a, b: ((a.double() - b.double()).norm() / b.double().norm()).item()  # noqa: E731
+    for name, a_, b_ in (("gw1", gw1, gw1_ref), ("gw2", gw2, gw2_ref)) + \
+            ((("gb1", gb1, gb1_ref), ("gb2", gb2, gb2_ref)) if bias else ()):
+        assert rel(a_, b_) <= 1e-5, (name, rel(a_, b_))
+    elu = lambda v: torch.where(v > 0, v, torch.expm1(v)).to(torch.bfloat16).double()  # noqa: E731
+    ghd = gh_ref.double().view(B, T, C)
+    xe = elu(x.double()).view(B, T, C)
+    ref1 = torch.zeros(C, C, 7, dtype=torch.float64, device=gpu)
+    for k in range(7):
+        s = (6 - k) * dil
+        if s < T:
+            ref1[:, :, k] = torch.einsum("btn,btc->nc", ghd[:, s:], xe[:, :T - s])
+    ref2 = torch.einsum("tn,tc->nc", g.double(), elu(h.double()))[:, :, None]
+    assert rel(gw1, ref1) <= 1e-5, rel(gw1, ref1)
+    assert rel(gw2, ref2) <= 1e-5, rel(gw2, ref2)
+    if bias:
+        assert rel(gb1, ghd.sum((0, 1))) <= 1e-5 and rel(gb2, g.double().sum(0)) <= 1e-5
+
+
 def _ulp_close(a, b, frac=1e-3):
     """bf16 tensors equal up to one ulp on at most `frac` of the elements: the
     ELU'(x) factor's hardware exp rounds differently in the fused kernel on a

@@ -15,9 +15,10 @@ OUT=$R/gpurun_out
 mkdir -p $OUT
 case $CMD in
   tests)
-    ARGS=${@:-tests}
+    ARGS=("$@")
+    [ ${#ARGS[@]} -eq 0 ] && ARGS=(tests)
     cd $R && timeout -k 10 ${GPU_TIMEOUT:-900} python -u -m pytest -x -v -m gpu --timeout ${TEST_TIMEOUT:-300} \
-      --timeout-method thread $ARGS > $OUT/${TAG}_tests.log 2>&1
+      --timeout-method thread "${ARGS[@]}" > $OUT/${TAG}_tests.log 2>&1
     RC=$?; echo "tests rc=$RC"; grep -E "passed|failed|error" $OUT/${TAG}_tests.log | tail -3
     exit $RC ;;
   bench)
