@@ -49,6 +49,9 @@ for dil in (1, 3, 9):
     bw = timed(lambda: CO.resunit_bwd(d1, g, h, x, wd1, wd2, True))
     bw0 = timed(lambda: CO.resunit_bwd(d1, g, h, x, wd1, wd2, False))
     b2c = timed(lambda: CO.prim(d1.adjoint(), CO.prim(d2.adjoint(), g, wd2, aux=h), wd1, aux=x, res=g))
+    # gx + both weight gradients (k_ru32_bwdw / k_ru64_bwdw), with the finish reduction
+    bww = timed(lambda: CO.resunit_bwd_wgrad(d1, g, h, x, wd1, wd2, (C, C, 7), (C, C, 1), True, True, None, None))
     print(f"dil {dil}: fwd fused {f:.1f} us ({3 * MB / f:.2f} TB/s) vs two calls {f2:.1f}; "
-          f"bwd fused {bw:.1f} ({5 * MB / bw:.2f} TB/s) / no-gh {bw0:.1f} ({4 * MB / bw0:.2f} TB/s) vs two calls {b2c:.1f}",
+          f"bwd fused {bw:.1f} ({5 * MB / bw:.2f} TB/s) / no-gh {bw0:.1f} ({4 * MB / bw0:.2f} TB/s) vs two calls {b2c:.1f}; "
+          f"bwd+wgrad {bww:.1f} ({4 * MB / bww:.2f} TB/s incl. finish)",
           flush=True)
