@@ -136,11 +136,11 @@ def c3_setup(dev, B, world, local, graph=False, dtype=torch.bfloat16):
     G = Generator(**cfg["generator_params"]).to(dev)
     model = {"generator": G, "discriminator": None}
     if world > 1:
-        from torch.nn.parallel import DistributedDataParallel as DDP
+        from sel.dist import wrap_ddp
         # freeze first so DDP only buckets the trainable (encoder + projector) grads
         for p in list(G.quantizer.parameters()) + list(G.decoder.parameters()):
             p.requires_grad = False
-        model["generator"] = DDP(G, device_ids=[local], broadcast_buffers=False, bucket_cap_mb=16)
+        model["generator"] = wrap_ddp(G, dev)  # 4 MB buckets + the sel comm hook (deferred wgrad per bucket)
     mel = MultiMelSpectrogramLoss(**cfg["mel_loss_params"]).to(dev)
     opt_kw = dict(cfg["generator_optimizer_params"])
     if graph:

@@ -1660,6 +1660,16 @@ __device__ __forceinline__ void ru_store(__bf16* p, bf16x8 v) {
   else *reinterpret_cast<bf16x8*>(p) = v;
 }
 
+// branch-free output store into a buffer resource (ru_rsrc): a row outside the
+// tile's valid rows takes RU_OOB and is dropped by the hardware.  Every wave
+// then issues the same number of stores per tile, so the compiler counts the
+// next tile's prefetch exactly (a conditional store made the staging wait at
+// the top of the next tile fall back to vmcnt(0), i.e. wait for these stores'
+// completion too).
+__device__ __forceinline__ void ru_bstore(__amdgpu_buffer_rsrc_t rs, int byte_off, bf16x8 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, byte_off, 0, 0);
+}
+
 __device__ __forceinline__ void ru_acc_to_frags(const float (&v)[16], bf16x8 (&frag)[2]) {
   unsigned pk[8];
 #pragma unroll
@@ -3031,9 +3041,15 @@ __device__ __forceinline__ void ru64w_load(Ru64WStage<R>& st, const Args& a, con
     const int tg = t0 + r, tx = t0 - halo + r;
     const bool gok = live && r < span && tg < a.T;
     const bool xok = live && r < span && tx >= 0 && tx < a.T;
+    // program order pinned (sched_barrier): the loads leave in the same order
+    // from the prologue and from the tile loop, so the waits of the staging
+    // store count them exactly on both paths into it
     st.g[u] = ru_bload(rg, gok ? (tg * G::C + c) * 2 : RU_OOB);
+    __builtin_amdgcn_sched_barrier(0);
     st.h[u] = ru_bload(rh, gok ? (tg * G::C + c) * 2 : RU_OOB);
+    __builtin_amdgcn_sched_barrier(0);
     st.x[u] = ru_bload(rx, xok ? (tx * G::C + c) * 2 : RU_OOB);
+    __builtin_amdgcn_sched_barrier(0);
   }
 }
 
@@ -3166,6 +3182,17 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
     ws_wait_vm<0>();  // weights landed: the tile loop's waits then count only its own loads
     Ru64WStage<R> st;
     ru64w_load<R>(st, a, g, h, x, tile0, tps, halo, true);
+    {
+      // the tile loop issues 2 TM stores after each prefetch; the same number of
+      // dropped stores here makes both paths into the staging waits identical,
+      // so the compiler's count leaves the previous tile's gx stores pending
+      // (a zero-byte region: every offset is out of range; distinct offsets so
+      // that the compiler does not merge them)
+      const __amdgpu_buffer_rsrc_t rz = ru_rsrc(gx, 0);
+      const bf16x8 z = {};
+#pragma unroll
+      for (int i = 0; i < 2 * TM; ++i) ru_bstore(rz, 16 * i, z);
+    }
     for (int64_t tile = tile0; tile < tile_end; ++tile) {
       const int64_t b = tile / tps;
       const int t0 = int(tile % tps) * R;
@@ -3192,12 +3219,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
             acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[k][q], *reinterpret_cast<const bf16x8*>(hb + i * 32 * P),
                                                              acc[i], 0, 0, 0);
         }
+      // every sub-tile is stored (rows past T to RU_OOB): a fixed count of
+      // stores per tile keeps the next tile's staging wait exact (ru_bstore)
+      const __amdgpu_buffer_rsrc_t rgx = ru_rsrc(gx + b * a.T * C, int64_t(a.T) * C);
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int lr = rg * WR + i * 32 + (lane & 31);
-        if (__builtin_amdgcn_readfirstlane(rg * WR + i * 32) >= mrows) break;
         const bool valid = lr < mrows;
-        const int64_t orow = (b * a.T + t0 + (valid ? lr : 0)) * C + ns * 32;
         float v[16];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -3211,10 +3239,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
         }
         bf16x8 of[2];
         ru_acc_to_frags(v, of);
-        if (valid) {
-          ru_store(gx + orow + 8 * hl, of[0]);
-          ru_store(gx + orow + 16 + 8 * hl, of[1]);
-        }
+        const int off = ((t0 + lr) * C + ns * 32 + 8 * hl) * 2;
+        ru_bstore(rgx, valid ? off : RU_OOB, of[0]);
+        ru_bstore(rgx, valid ? off + 32 : RU_OOB, of[1]);
       }
     }
     return;

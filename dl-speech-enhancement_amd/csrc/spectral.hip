@@ -1232,7 +1232,10 @@ __global__ __launch_bounds__(256) void k_finish_partials(const double* __restric
 }
 
 // {sc, mag} from sums (stft_loss.py:56, :77)
+// inv_n == 0: the element count is sums[3] (the data-parallel exchange's
+// all-reduced count, kept on device: no host sync)
 __global__ void k_stft_loss_finish(const double* __restrict__ sums, double inv_n, float* out2) {
+  if (inv_n == 0.0) inv_n = 1.0 / sums[3];
   const float n1 = sqrtf(float(sums[0])), n2 = sqrtf(float(sums[1]));
   out2[0] = n1 / n2;
   out2[1] = float(sums[2] * inv_n);
@@ -1242,6 +1245,7 @@ __global__ void k_stft_loss_finish(const double* __restrict__ sums, double inv_n
 __global__ void k_stft_loss_coef(const double* __restrict__ sums, double inv_n,
                                  const float* __restrict__ g_sc, const float* __restrict__ g_mag,
                                  float* coef) {
+  if (inv_n == 0.0) inv_n = 1.0 / sums[3];  // k_stft_loss_finish
   const float n1 = sqrtf(float(sums[0])), n2 = sqrtf(float(sums[1]));
   const float gsc = g_sc ? g_sc[0] : 0.f, gmag = g_mag ? g_mag[0] : 0.f;
   // d||y-x||/dx = (x-y)/||y-x|| (0 when the norm is 0), then /n2
@@ -1532,18 +1536,18 @@ int sel_stft_loss_bwd(const float* x, const float* y, int64_t B, int64_t T, int 
 }
 
 int sel_stft_loss_finish(const double* sums, int64_t n, float* out2, sel_stream_t stream) {
-  SEL_REQUIRE(n > 0, SEL_ERR_ARG, "n must be > 0");
+  SEL_REQUIRE(n >= 0 && sums && out2, SEL_ERR_ARG, "n must be >= 0 (0: the count is sums[3])");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(k_stft_loss_finish, dim3(1), dim3(1), 0, s, sums, 1.0 / double(n), out2);
+  hipLaunchKernelGGL(k_stft_loss_finish, dim3(1), dim3(1), 0, s, sums, n ? 1.0 / double(n) : 0.0, out2);
   SEL_LAUNCH_CHECK();
   return SEL_OK;
 }
 
 int sel_stft_loss_coef(const double* sums, int64_t n, const float* g_sc, const float* g_mag,
                        float* coef, sel_stream_t stream) {
-  SEL_REQUIRE(n > 0, SEL_ERR_ARG, "n must be > 0");
+  SEL_REQUIRE(n >= 0 && sums && coef, SEL_ERR_ARG, "n must be >= 0 (0: the count is sums[3])");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(k_stft_loss_coef, dim3(1), dim3(1), 0, s, sums, 1.0 / double(n), g_sc, g_mag,
+  hipLaunchKernelGGL(k_stft_loss_coef, dim3(1), dim3(1), 0, s, sums, n ? 1.0 / double(n) : 0.0, g_sc, g_mag,
                      coef);
   SEL_LAUNCH_CHECK();
   return SEL_OK;

@@ -331,10 +331,14 @@ class _WgradJob(ctypes.Structure):
 # tensor in between: the parameter is a leaf whose .grad is None (AccumulateGrad
 # then takes the returned tensor itself, no copy or add) and has no tensor or
 # post-accumulate hook (a hook that reads .grad early should set
-# SEL_WGRAD_DEFER=0 if it is attached some other way), no create_graph, no
-# multi-rank process group (DDP copies gradients into its buckets from hooks as
-# they arrive).  The flush checks that every deferred tensor is still the one
-# AccumulateGrad kept and raises otherwise.
+# SEL_WGRAD_DEFER=0 if it is attached some other way), no create_graph.  Under
+# a multi-rank process group DDP copies each gradient into its bucket as it
+# arrives, so a layer defers only when every parameter it feeds is in a DDP
+# module carrying ddp_comm_hook (install_ddp_hook): that hook runs the pending
+# reductions of its bucket's parameters into the bucket's own gradient views
+# before the all-reduce (one launch per bucket instead of one per layer).  The
+# flush checks that every deferred tensor is still the one AccumulateGrad kept
+# and raises otherwise.
 WGRAD_DEFER = os.environ.get("SEL_WGRAD_DEFER", "1") != "0"
 _DEFERRED = []
 _DEFER_LOCK = threading.Lock()
@@ -362,7 +366,11 @@ def _can_defer(params):
     try:
         import torch.distributed as dist
         if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-            return False
+            # DDP reads each gradient from its hook as it arrives: only parameters
+            # of a module whose buckets run ddp_comm_hook may wait for the flush
+            if not DDP_DEFER or not all(p is not None and _DDP_HOOKED.get(id(p)) is not None
+                                        and _DDP_HOOKED[id(p)]() is p for p in params):
+                return False
         for p in params:
             if p is None or not p.is_leaf or p.grad is not None:
                 return False
@@ -391,14 +399,103 @@ def _queue_flush():
 def _defer(job, ws, params, gw, gb, st):
     refs = [(weakref.ref(params[0]), gw.data_ptr())] + \
         ([(weakref.ref(params[1]), gb.data_ptr())] if gb is not None else [])
+    # (no reference to gw / gb here: AccumulateGrad takes the returned tensor
+    # itself as .grad only while nothing else holds it)
     with _DEFER_LOCK:
         _DEFERRED.append((job, ws, refs, st.value))
+
+
+# ---------------------------------------------------------------------------
+# DDP: deferred reductions flushed per gradient bucket (install_ddp_hook)
+# ---------------------------------------------------------------------------
+DDP_DEFER = os.environ.get("SEL_DDP_DEFER", "1") != "0"
+_DDP_HOOKED = {}   # id(param) -> weakref(param): parameters of a hooked DDP module
+_DDP_READY = {}    # id(param) -> finished gradient waiting for its (later) bucket
+DDP_STATS = {"bucket_flushes": 0, "jobs": 0}
+
+
+def _run_jobs(entries):
+    """sel_wgrad_finish_many over deferred entries, one launch per stream."""
+    cur = torch.cuda.current_stream()
+    for st in dict.fromkeys(e[3] for e in entries):
+        group = [e[0] for e in entries if e[3] == st]
+        jobs = (_WgradJob * len(group))(*group)
+        L.call("sel_wgrad_finish_many", ctypes.cast(jobs, ctypes.c_void_p), len(group), ctypes.c_void_p(st))
+        if (st or 0) != cur.cuda_stream:  # (a null-stream handle reads as None)
+            # the gradients are read on the current stream from here on (the
+            # optimizer / the all-reduce): order it after this finish on ANY
+            # other stream, not only the SEL_WGRAD_STREAM side streams
+            side = next((s for s in _WG_STREAMS.values() if s.cuda_stream == st), None)
+            if side is None:
+                side = torch.cuda.ExternalStream(st, device=cur.device)
+            cur.wait_stream(side)
+
+
+def flush_bucket(params, grads):
+    """Inside DDP's communication hook, before the bucket's all-reduce: the
+    deferred reductions of every layer with a parameter in this bucket run
+    now, writing that parameter's result straight into its bucket gradient
+    view (DDP copied the not-yet-reduced tensor there when AccumulateGrad
+    fired).  A layer's other parameter in another bucket gets its result in a
+    fresh tensor, copied into that bucket's view when its hook runs (a later
+    bucket: an earlier one would have run this layer already).  The layer's
+    own gradient tensors are never written here: with gradient_as_bucket_view
+    DDP has already replaced .grad by the bucket view and released them."""
+    views = {id(p): g for p, g in zip(params, grads)}
+    for p in params:
+        r = _DDP_READY.pop(id(p), None)
+        if r is not None:
+            views[id(p)].copy_(r.view_as(views[id(p)]))
+    with _DEFER_LOCK:
+        mine = [e for e in _DEFERRED if any(id(ref()) in views for ref, _ in e[2] if ref() is not None)]
+        if mine:
+            ids = {id(e) for e in mine}
+            _DEFERRED[:] = [e for e in _DEFERRED if id(e) not in ids]
+    if not mine:
+        return
+    run = []
+    for job, ws, refs, st in mine:
+        j = _WgradJob.from_buffer_copy(job)
+        for slot, (ref, _ptr) in enumerate(refs):
+            p_ = ref()
+            if p_ is None:
+                raise L.SelError("sel: a parameter with a deferred weight gradient was released mid-backward")
+            v = views.get(id(p_))
+            if v is None or not v.is_contiguous() or v.dtype != torch.float32 or v.numel() != p_.numel():
+                v = torch.empty(p_.shape, dtype=torch.float32, device=p_.device)
+                _DDP_READY[id(p_)] = v  # finished here, copied at its own bucket's hook
+            if slot == 0:
+                j.gw = v.data_ptr()
+            else:
+                j.gb = v.data_ptr()
+        run.append((j, ws, refs, st))
+    _run_jobs(run)
+    DDP_STATS["bucket_flushes"] += 1
+    DDP_STATS["jobs"] += len(run)
+
+
+def ddp_comm_hook(process_group, bucket):
+    """DDP communication hook: the bucket's deferred weight-gradient reductions
+    (flush_bucket), then DDP's default all-reduce of the bucket (average)."""
+    from torch.distributed.algorithms.ddp_comm_hooks import default_hooks
+    flush_bucket(bucket.parameters(), bucket.gradients())
+    return default_hooks.allreduce_hook(process_group, bucket)
+
+
+def install_ddp_hook(ddp_module, process_group=None):
+    """Register ddp_comm_hook on a DistributedDataParallel module and let its
+    parameters' weight-gradient reductions be deferred (see _can_defer)."""
+    ddp_module.register_comm_hook(process_group, ddp_comm_hook)
+    for p in ddp_module.module.parameters():
+        _DDP_HOOKED[id(p)] = weakref.ref(p)
+    return ddp_module
 
 
 def _flush_deferred():
     with _DEFER_LOCK:
         pending = list(_DEFERRED)
         _DEFERRED.clear()
+    _DDP_READY.clear()
     if not pending:
         return
     for _job, _ws, refs, _st in pending:
@@ -408,19 +505,7 @@ def _flush_deferred():
                 raise L.SelError("sel: a deferred weight gradient did not become the parameter's .grad "
                                  "(set SEL_WGRAD_DEFER=0 for this use)")
     # one launch per stream the partial kernels ran on (normally one)
-    cur = torch.cuda.current_stream()
-    for st in dict.fromkeys(e[3] for e in pending):
-        group = [e[0] for e in pending if e[3] == st]
-        jobs = (_WgradJob * len(group))(*group)
-        L.call("sel_wgrad_finish_many", ctypes.cast(jobs, ctypes.c_void_p), len(group), ctypes.c_void_p(st))
-        if (st or 0) != cur.cuda_stream:  # (a null-stream handle reads as None)
-            # the gradients are read on the current stream from here on (the
-            # optimizer): order it after this finish on ANY other stream, not
-            # only the SEL_WGRAD_STREAM side streams
-            side = next((s for s in _WG_STREAMS.values() if s.cuda_stream == st), None)
-            if side is None:
-                side = torch.cuda.ExternalStream(st, device=cur.device)
-            cur.wait_stream(side)
+    _run_jobs(pending)
     # the workspaces are released here; the finish kernel is already enqueued on
     # this stream ahead of any later use of that memory
 

@@ -72,13 +72,17 @@ def global_loss_sums(sums, n):
     every rank; DDP then AVERAGES the parameter gradients over the W ranks, so
     each rank back-propagates W x d(global loss)/d(local sums) (grad_scale = W):
     the average is then exactly the single-device gradient on the global batch
-    (the SC ratio is not a mean over shards)."""
+    (the SC ratio is not a mean over shards).  Data parallel, the
+    global count stays on device as the 4th element of the returned sums and
+    the returned n is 0 (sel_stft_loss_finish / _coef then read it there): no
+    host sync per resolution and step."""
     if not (GLOBAL_BATCH_LOSSES and is_dist()) or dist.get_world_size() == 1:
         return sums, n, 1.0
-    t = torch.cat([sums.detach().to(torch.float64), torch.tensor([float(n)], dtype=torch.float64,
-                                                                  device=sums.device)])
+    t = torch.empty(4, dtype=torch.float64, device=sums.device)
+    t[:3] = sums.detach()
+    t[3] = float(n)
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    return t[:3].contiguous(), int(round(t[3].item())), float(dist.get_world_size())
+    return t, 0, float(dist.get_world_size())
 
 
 def allreduce_sum_(t):
@@ -115,16 +119,23 @@ def add_noise_global(speech, noise, snr):
     return _mix(a, b, sums, snr)
 
 
-def wrap_ddp(module, device=None, bucket_cap_mb=16):
+DDP_BUCKET_MB = 4
+
+
+def wrap_ddp(module, device=None, bucket_cap_mb=DDP_BUCKET_MB):
     """DistributedDataParallel over the trainable parameters only (frozen
     decoder/quantizer of trainer/denoise.py are skipped).  Gradient buckets are
-    all-reduced by RCCL while the backward is still running.  16 MB buckets:
-    the denoise trainer's 15.6 MB of fp32 encoder grads become ~1-2 ring
-    all-reduces per step on the per-link-bound xGMI mesh."""
+    all-reduced by RCCL while the backward is still running.  4 MB buckets:
+    the denoise trainer's 15.6 MB of fp32 encoder grads span 4-5 ring
+    all-reduces, the first of which start while the encoder's earlier layers
+    are still in their backward (one 16 MB bucket would only start after the
+    last of them).  The sel communication hook (convops.install_ddp_hook)
+    keeps the weight-gradient reductions batched per bucket."""
     from torch.nn.parallel import DistributedDataParallel as DDP
     if not is_dist() or dist.get_world_size() == 1:
         return module
     kw = dict(broadcast_buffers=False, bucket_cap_mb=bucket_cap_mb, gradient_as_bucket_view=True)
     if device is not None and device.type == "cuda":
         kw["device_ids"] = [device.index]
-    return DDP(module, **kw)
+    from .convops import install_ddp_hook
+    return install_ddp_hook(DDP(module, **kw))

@@ -94,7 +94,10 @@ int sel_stft_loss_bwd(const float* x, const float* y, int64_t B, int64_t T, int 
                       float* g_x, void* ws, size_t ws_bytes, sel_stream_t stream);
 /* Finishing arithmetic on device (no host sync): from sums -> out2 = {sc, mag}
  * and, for the backward, coef = {a, b, c, d} (see sel_mag_pair_bwd) given the
- * upstream grads *g_sc, *g_mag (device scalars; NULL = zero). */
+ * upstream grads *g_sc, *g_mag (device scalars; NULL = zero).  n = the
+ * element count of the log-magnitude mean, or 0: read it from sums[3] (a
+ * 4-element sums array whose count was all-reduced on device by a
+ * data-parallel caller). */
 int sel_stft_loss_finish(const double* sums, int64_t n, float* out2, sel_stream_t stream);
 int sel_stft_loss_coef(const double* sums, int64_t n, const float* g_sc, const float* g_mag,
                        float* coef, sel_stream_t stream);

@@ -5,7 +5,8 @@
 Runs the product's own training step under a gloo process group on CUDA
 tensors — RCCL cannot put two ranks on one device, gloo can, and the code paths
 above the backend (DDP buckets and hooks, sel.dist exchanges, the
-deferred-wgrad opt-out) are the ones RCCL runs on 8 GPUs — and saves the
+deferred weight-gradient reductions flushed by the sel comm hook per bucket)
+are the ones RCCL runs on 8 GPUs — and saves the
 per-step loss values and the final weights.  `run_case` is also what the test
 calls in-process (no process group) for the single-device reference on the
 concatenated global batch.
@@ -16,6 +17,11 @@ Cases:
         use_stft_loss on, so the spectral-convergence exchange
         (losses/stft_loss.py:56 over the global batch) runs through the real
         autograd op; add_noise over the global batch (data_utils.py:12-22).
+  c3  — the bench's C3 step at full width: trainer/denoise.Trainer._train_step
+        on the symAD_libritts_24000_hop300 PQC generator in bf16 (mel + vq,
+        the fused 32/64-channel residual-unit kernels with their weight
+        gradients), 4 global clips of 1 s, DDP with the sel comm hook (the
+        deferred weight-gradient reductions run per gradient bucket).
   gan — train_denoise.DenoiseStep.model_step in GAN mode (:138-165, :213-263)
         on a reduced-width without-PQC generator + HiFi-GAN discriminator, with
         lambda_snr_loss = 1 so the global SNR surrogate runs; generator and
@@ -73,16 +79,17 @@ def _floats(d):
     return {k: float(v) for k, v in d.items()}
 
 
-def run_pqc(dev):
+def run_pqc(dev, full=False):
     from dataloader.data_utils import add_noise  # noqa: F401
     from losses import MultiMelSpectrogramLoss, MultiResolutionSTFTLoss
     from models.autoencoder.AudioDec import Generator
     from sel import configs
     from sel import dist as D
+    from sel.convops import precision
     from trainer.denoise import Trainer
     cfg = configs.get("symAD_libritts_24000_hop300")
-    cfg.update(outdir=None, train_max_steps=1 << 40, use_stft_loss=True)
-    gp = dict(cfg["generator_params"], **GP)
+    cfg.update(outdir=None, train_max_steps=1 << 40, use_stft_loss=not full)
+    gp = dict(cfg["generator_params"], **({} if full else GP))
     torch.manual_seed(0)
     G = Generator(**gp).to(dev)
     # frozen before wrapping (trainer/denoise.py:43-49): DDP buckets the trainable grads only
@@ -95,10 +102,11 @@ def run_pqc(dev):
     sched = torch.optim.lr_scheduler.StepLR(opt, **cfg["generator_scheduler_params"])
     tr = Trainer(steps=0, epochs=0, data_loader={}, model=model, criterion=crit, optimizer={"generator": opt},
                  scheduler={"generator": sched}, config=cfg, device=dev)
-    clean, mixed = _mix(*_global_batch(4800), dev)
+    clean, mixed = _mix(*_global_batch(24000 if full else 4800), dev)
     steps = []
     for _ in range(STEPS):
-        tr._train_step((mixed, clean))
+        with precision(torch.bfloat16 if full else torch.float32):
+            tr._train_step((mixed, clean))
         tot = tr.total_train_loss
         steps.append(_floats({k: tot[k] for k in list(tot.keys()) if "loss" in k}))
     return {"steps": steps, "params": {k: p.detach().cpu().clone() for k, p in G.named_parameters()
@@ -137,7 +145,7 @@ def run_gan(dev):
 
 
 def run_case(case, dev):
-    return {"pqc": run_pqc, "gan": run_gan}[case](dev)
+    return {"pqc": run_pqc, "c3": lambda d: run_pqc(d, full=True), "gan": run_gan}[case](dev)
 
 
 def main():
@@ -152,6 +160,7 @@ def main():
     res["rank_world"] = D.rank_world()
     from sel import convops as CO
     res["deferred_pending"] = len(CO._DEFERRED)
+    res["ddp_stats"] = dict(CO.DDP_STATS)  # deferred reductions flushed by the DDP comm hook
     torch.save(res, out)
     dist.barrier()
     dist.destroy_process_group()

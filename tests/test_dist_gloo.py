@@ -157,7 +157,11 @@ def _sc_case(rank):
     x, y = D.shard(xm), D.shard(ym)
     sums = torch.stack([((y - x) ** 2).sum(), (y ** 2).sum(), (torch.log(y) - torch.log(x)).abs().sum()])
     sums_g, n_g, scale = D.global_loss_sums(sums, x.numel())
-    assert n_g == xm.numel() and scale == WORLD
+    # the global count stays on device (sums_g[3]); n = 0 tells the finishing
+    # kernels to read it there (no host sync)
+    assert n_g == 0 and sums_g.shape == (4,) and scale == WORLD
+    assert sums_g[3].item() == xm.numel()
+    n_g = sums_g[3]
     n1, n2 = sums_g[0].sqrt(), sums_g[1].sqrt()
     sc, mag = n1 / n2, sums_g[2] / n_g
     # d/dx of sc and mag w.r.t. this shard, times grad_scale (stft_loss_coef + mag_pair_bwd)

@@ -5,7 +5,8 @@ process is never exec'ed) in a world-size-2 gloo process group over CUDA
 tensors.  RCCL cannot place two ranks on one device; gloo can, and everything
 above the backend is what bench.py / train_denoise.py run over RCCL on 8 GPUs:
 DDP's bucket hooks on the HIP autograd ops, the deferred weight-gradient
-opt-out under a multi-rank group (sel/convops.py _can_defer), the packed-weight
+reductions run per bucket by the sel DDP comm hook (sel/convops.py
+flush_bucket; asserted to have run), the packed-weight
 refresh after the DDP-averaged Adam step, the batch-global add_noise exchange
 (sel.dist.add_noise_global), the spectral-convergence exchange through the real
 STFT-loss autograd op (sel.dist.global_loss_sums, losses/stft_loss.py:56), the
@@ -76,12 +77,17 @@ def _update_check(p0, ref, got, lr):
             (du_ref ** 2).sum().item())
 
 
-@pytest.mark.parametrize("case", ["pqc", "gan"])
+@pytest.mark.parametrize("case", ["pqc", "c3", "gan"])
 def test_ddp_product_step_matches_single_process(gpu, case, tmp_path):
     import ddp_product_worker as W
     ranks = _run_ranks(case, tmp_path)
     assert [tuple(r["rank_world"]) for r in ranks] == [(0, 2), (1, 2)]
     assert all(r["deferred_pending"] == 0 for r in ranks)
+    if case in ("pqc", "c3"):
+        # the generator's weight-gradient reductions were deferred under the
+        # process group and run by the sel DDP comm hook, per bucket
+        for r in ranks:
+            assert r["ddp_stats"]["jobs"] > 0 and r["ddp_stats"]["bucket_flushes"] > 0, r["ddp_stats"]
     # DDP keeps the replicas identical
     for k, v in ranks[0]["params"].items():
         assert torch.equal(v, ranks[1]["params"][k]), k
@@ -119,10 +125,10 @@ def _initial_params(case, dev):
     import ddp_product_worker as W
     from sel import configs
     torch.manual_seed(0)
-    if case == "pqc":
+    if case in ("pqc", "c3"):
         from models.autoencoder.AudioDec import Generator
         cfg = configs.get("symAD_libritts_24000_hop300")
-        G = Generator(**dict(cfg["generator_params"], **W.GP))
+        G = Generator(**dict(cfg["generator_params"], **(W.GP if case == "pqc" else {})))
         return {k: p.detach().clone() for k, p in G.named_parameters()}
     from models.autoencoder_without_PQC.AudioDec import Generator
     from models.vocoder.HiFiGAN import Discriminator
