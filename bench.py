@@ -121,6 +121,13 @@ def c2_cpu_baseline(B_sample=4, steps=20):
 C3_CONFIG = "symAD_libritts_24000_hop300"
 
 
+# rehearsal knob (not a driver configuration): SEL_BENCH_FORCE_DDP=1 runs the
+# N = 1 step DDP-wrapped under a one-rank process group, i.e. the data-parallel
+# schedule (bucket copies, the sel comm hook's per-bucket weight-gradient
+# reductions, the all-reduce calls) without the interconnect
+FORCE_DDP = os.environ.get("SEL_BENCH_FORCE_DDP", "0") == "1"
+
+
 def c3_setup(dev, B, world, local, graph=False, dtype=torch.bfloat16):
     from sel import configs
     from sel.convops import precision
@@ -135,12 +142,13 @@ def c3_setup(dev, B, world, local, graph=False, dtype=torch.bfloat16):
     torch.manual_seed(93)
     G = Generator(**cfg["generator_params"]).to(dev)
     model = {"generator": G, "discriminator": None}
-    if world > 1:
+    if world > 1 or FORCE_DDP:
         from sel.dist import wrap_ddp
         # freeze first so DDP only buckets the trainable (encoder + projector) grads
         for p in list(G.quantizer.parameters()) + list(G.decoder.parameters()):
             p.requires_grad = False
-        model["generator"] = wrap_ddp(G, dev)  # 4 MB buckets + the sel comm hook (deferred wgrad per bucket)
+        # sel.ddp: 4 MB buckets, the deferred weight-gradient reductions per bucket
+        model["generator"] = wrap_ddp(G, dev, force=FORCE_DDP)
     mel = MultiMelSpectrogramLoss(**cfg["mel_loss_params"]).to(dev)
     opt_kw = dict(cfg["generator_optimizer_params"])
     if graph:
@@ -560,12 +568,17 @@ def main():
     backend = os.environ.get("SEL_BENCH_BACKEND", "nccl")
     if os.environ.get("SEL_BENCH_SHARE_GPU", "0") == "1":
         local = local % torch.cuda.device_count()
-    if world > 1:
+    if world > 1 or FORCE_DDP:
         torch.cuda.set_device(local)
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 1000))
+            os.environ.setdefault("RANK", "0")
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), rank=int(os.environ.get("RANK", "0")),
+                                    world_size=world)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, rank=int(os.environ.get("RANK", "0")), world_size=world)
     dev = torch.device("cuda", local)
 
     from sel import _lib
@@ -641,7 +654,7 @@ def main():
             "roofline": roof, "cpu_baseline": cpu, "fp32_companion": fp32, "stft_kernel": stft_roof,
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

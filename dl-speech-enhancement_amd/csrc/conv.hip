@@ -4877,7 +4877,7 @@ int dconv_ws_fwd(const sel_dconv_desc* d, const void* x, const void* wp, const f
 extern "C" {
 
 int sel_conv_fwd_kernel_id(const sel_conv_desc* d, int in_dtype, int out_dtype, int has_epilogue) {
-  if (!d || in_dtype != SEL_BF16) return -1;
+  if (!d || in_dtype != SEL_BF16 || check_desc(d) != SEL_OK) return -1;
   const Args a = to_args(d);
   if (out_dtype == SEL_BF16 && thin_ok(a)) {  // thin: 1e9 + E*5e8 + ((R/32*1000 + C)*1000 + N)*10 + K
     int r = 0;
@@ -4970,7 +4970,8 @@ int sel_resunit_bwd_wgrad(const sel_conv_desc* d1, int dtype, const void* g, con
 }
 
 size_t sel_conv_wgrad_workspace(const sel_conv_desc* d) {
-  if (!d || d->rows <= 0 || d->T <= 0) return 16;
+  // (an invalid descriptor sizes nothing: sel_conv_wgrad* rejects it itself)
+  if (!d || d->rows <= 0 || check_desc(d) != SEL_OK) return 16;
   int ns = wgrad_plan(d, 0).nsplit;
   if (wgrad_tr_ok(d)) ns = std::max(ns, std::max(wgrad_plan(d, 2).nsplit, wgrad_plan(d, 3).nsplit));
   if (wgrad_c1_ok(d)) ns = std::max(ns, wgrad_plan(d, 4).nsplit);

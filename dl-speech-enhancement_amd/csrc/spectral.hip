@@ -1403,7 +1403,9 @@ int ola(const float* slab, const FrameArgs& a, float* gx, hipStream_t s) {
   return SEL_OK;
 }
 
+// (0 for an invalid shape: the call it sizes fails its own check_frame)
 size_t slab_bytes(int64_t B, int64_t T, int hop, int win) {
+  if (B < 0 || T < 0 || hop <= 0 || win <= 0) return 0;
   return size_t(B) * size_t(1 + T / hop) * size_t(win) * sizeof(float);
 }
 
@@ -1495,7 +1497,7 @@ int sel_mag_pair_bwd(const float* x_mag, const float* y_mag, int64_t n, const fl
 size_t sel_stft_loss_workspace(int64_t B, int64_t T, int n_fft, int hop, int win_length) {
   int logn = 0;
   while ((1 << logn) < n_fft) ++logn;
-  if (logn < kMinLog || logn > kMaxLog - 1) return 0;
+  if (logn < kMinLog || logn > kMaxLog - 1 || B < 0 || T < 0 || hop <= 0 || win_length <= 0) return 0;
   const int64_t nf = B * (1 + T / hop);
   const size_t part = size_t(n_blocks(logn, nf)) * 3 * sizeof(double);
   const size_t slab = slab_bytes(B, T, hop, win_length);

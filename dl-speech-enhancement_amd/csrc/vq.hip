@@ -665,6 +665,7 @@ extern "C" {
 size_t sel_rvq_workspace(int64_t N, int S, int K) {
   // per-block SSE partials, then |e|^2 per (stage, code) for the matrix-core variant
   // + the B-fragment-ordered codebook copy for the matrix-core variant (any D <= 64)
+  if (N < 0 || S < 0 || K < 0) return 0;  // (sel_rvq_fwd rejects the shape itself)
   return ep_offset(N, S, K) + size_t(S) * size_t(MfmaGeo(DM, K).stage_floats()) * sizeof(float);
 }
 

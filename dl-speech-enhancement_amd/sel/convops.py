@@ -332,13 +332,13 @@ class _WgradJob(ctypes.Structure):
 # then takes the returned tensor itself, no copy or add) and has no tensor or
 # post-accumulate hook (a hook that reads .grad early should set
 # SEL_WGRAD_DEFER=0 if it is attached some other way), no create_graph.  Under
-# a multi-rank process group DDP copies each gradient into its bucket as it
-# arrives, so a layer defers only when every parameter it feeds is in a DDP
-# module carrying ddp_comm_hook (install_ddp_hook): that hook runs the pending
-# reductions of its bucket's parameters into the bucket's own gradient views
-# before the all-reduce (one launch per bucket instead of one per layer).  The
-# flush checks that every deferred tensor is still the one AccumulateGrad kept
-# and raises otherwise.
+# a multi-rank process group a layer defers only when every parameter it feeds
+# belongs to a sel.ddp.GradBuckets reducer: the returned gradient is then a
+# view of the parameter's slot in the reducer's flat buffer, and the reducer
+# runs the pending reductions of a bucket (flush_params) when the bucket's last
+# gradient has arrived, right before its all-reduce.  The flush checks that
+# every deferred tensor is still the one AccumulateGrad kept and raises
+# otherwise.
 WGRAD_DEFER = os.environ.get("SEL_WGRAD_DEFER", "1") != "0"
 _DEFERRED = []
 _DEFER_LOCK = threading.Lock()
@@ -365,18 +365,21 @@ def _can_defer(params):
         return False
     try:
         import torch.distributed as dist
-        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-            # DDP reads each gradient from its hook as it arrives: only parameters
-            # of a module whose buckets run ddp_comm_hook may wait for the flush
-            if not DDP_DEFER or not all(p is not None and _DDP_HOOKED.get(id(p)) is not None
-                                        and _DDP_HOOKED[id(p)]() is p for p in params):
-                return False
+        # data parallel: only parameters of a sel.ddp reducer, which runs the
+        # pending reductions of a bucket before its all-reduce, may wait
+        owned = all(p is not None and _owner(p) is not None for p in params)
+        if owned and not DDP_DEFER:
+            return False
+        if not owned and dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            return False
         for p in params:
             if p is None or not p.is_leaf or p.grad is not None:
                 return False
             # a tensor hook or a post-accumulate hook (e.g. an optimizer-in-backward)
-            # would read the gradient before the final callback computes it
-            if getattr(p, "_backward_hooks", None) or getattr(p, "_post_accumulate_grad_hooks", None):
+            # would read the gradient before the final callback computes it (the
+            # reducer's own arrival hook reads no values)
+            if getattr(p, "_backward_hooks", None) or (getattr(p, "_post_accumulate_grad_hooks", None)
+                                                       and not owned):
                 return False
             # the engine accumulates into .grad in this backward (not autograd.grad(inputs=...))
             if not torch._C._will_engine_execute_node(torch.autograd.graph.get_gradient_edge(p).node):
@@ -406,12 +409,30 @@ def _defer(job, ws, params, gw, gb, st):
 
 
 # ---------------------------------------------------------------------------
-# DDP: deferred reductions flushed per gradient bucket (install_ddp_hook)
+# data parallel: the deferred reductions run per gradient bucket (sel.ddp)
 # ---------------------------------------------------------------------------
 DDP_DEFER = os.environ.get("SEL_DDP_DEFER", "1") != "0"
-_DDP_HOOKED = {}   # id(param) -> weakref(param): parameters of a hooked DDP module
-_DDP_READY = {}    # id(param) -> finished gradient waiting for its (later) bucket
+_REDUCERS = []     # weakrefs to sel.ddp.GradBuckets
 DDP_STATS = {"bucket_flushes": 0, "jobs": 0}
+
+
+def register_grad_buckets(reducer):
+    _REDUCERS.append(weakref.ref(reducer))
+
+
+def _owner(p):
+    for ref in _REDUCERS:
+        r = ref()
+        if r is not None and r.owns(p):
+            return r
+    return None
+
+
+def _grad_out(p, shape, device):
+    """Gradient tensor of a deferred reduction for parameter p: a view of its
+    slot when a data-parallel reducer owns p, else a fresh tensor."""
+    r = _owner(p) if p is not None else None
+    return r.view(p) if r is not None else torch.empty(shape, dtype=torch.float32, device=device)
 
 
 def _run_jobs(entries):
@@ -431,71 +452,27 @@ def _run_jobs(entries):
             cur.wait_stream(side)
 
 
-def flush_bucket(params, grads):
-    """Inside DDP's communication hook, before the bucket's all-reduce: the
-    deferred reductions of every layer with a parameter in this bucket run
-    now, writing that parameter's result straight into its bucket gradient
-    view (DDP copied the not-yet-reduced tensor there when AccumulateGrad
-    fired).  A layer's other parameter in another bucket gets its result in a
-    fresh tensor, copied into that bucket's view when its hook runs (a later
-    bucket: an earlier one would have run this layer already).  The layer's
-    own gradient tensors are never written here: with gradient_as_bucket_view
-    DDP has already replaced .grad by the bucket view and released them."""
-    views = {id(p): g for p, g in zip(params, grads)}
-    for p in params:
-        r = _DDP_READY.pop(id(p), None)
-        if r is not None:
-            views[id(p)].copy_(r.view_as(views[id(p)]))
+def flush_params(params):
+    """Run now (one launch) the pending reductions of every layer with a
+    parameter in `params` (a data-parallel bucket about to be all-reduced);
+    a layer's parameters in other buckets get their values too, before their
+    own bucket's all-reduce."""
+    ids = {id(p) for p in params}
     with _DEFER_LOCK:
-        mine = [e for e in _DEFERRED if any(id(ref()) in views for ref, _ in e[2] if ref() is not None)]
+        mine = [e for e in _DEFERRED if any(id(ref()) in ids for ref, _ in e[2] if ref() is not None)]
         if mine:
-            ids = {id(e) for e in mine}
-            _DEFERRED[:] = [e for e in _DEFERRED if id(e) not in ids]
-    if not mine:
-        return
-    run = []
-    for job, ws, refs, st in mine:
-        j = _WgradJob.from_buffer_copy(job)
-        for slot, (ref, _ptr) in enumerate(refs):
-            p_ = ref()
-            if p_ is None:
-                raise L.SelError("sel: a parameter with a deferred weight gradient was released mid-backward")
-            v = views.get(id(p_))
-            if v is None or not v.is_contiguous() or v.dtype != torch.float32 or v.numel() != p_.numel():
-                v = torch.empty(p_.shape, dtype=torch.float32, device=p_.device)
-                _DDP_READY[id(p_)] = v  # finished here, copied at its own bucket's hook
-            if slot == 0:
-                j.gw = v.data_ptr()
-            else:
-                j.gb = v.data_ptr()
-        run.append((j, ws, refs, st))
-    _run_jobs(run)
-    DDP_STATS["bucket_flushes"] += 1
-    DDP_STATS["jobs"] += len(run)
-
-
-def ddp_comm_hook(process_group, bucket):
-    """DDP communication hook: the bucket's deferred weight-gradient reductions
-    (flush_bucket), then DDP's default all-reduce of the bucket (average)."""
-    from torch.distributed.algorithms.ddp_comm_hooks import default_hooks
-    flush_bucket(bucket.parameters(), bucket.gradients())
-    return default_hooks.allreduce_hook(process_group, bucket)
-
-
-def install_ddp_hook(ddp_module, process_group=None):
-    """Register ddp_comm_hook on a DistributedDataParallel module and let its
-    parameters' weight-gradient reductions be deferred (see _can_defer)."""
-    ddp_module.register_comm_hook(process_group, ddp_comm_hook)
-    for p in ddp_module.module.parameters():
-        _DDP_HOOKED[id(p)] = weakref.ref(p)
-    return ddp_module
+            keep = {id(e) for e in mine}
+            _DEFERRED[:] = [e for e in _DEFERRED if id(e) not in keep]
+    if mine:
+        _run_jobs(mine)
+        DDP_STATS["bucket_flushes"] += 1
+        DDP_STATS["jobs"] += len(mine)
 
 
 def _flush_deferred():
     with _DEFER_LOCK:
         pending = list(_DEFERRED)
         _DEFERRED.clear()
-    _DDP_READY.clear()
     if not pending:
         return
     for _job, _ws, refs, _st in pending:
@@ -517,13 +494,13 @@ def wgrad_torch(desc, gout, x, kind, w_shape, stride, want_bias, params=None):
     returned gradients (enables the deferred, batched reduction; WGRAD_DEFER)."""
     lib = L.lib()
     ws = L.workspace(lib.sel_conv_wgrad_workspace(ctypes.byref(desc)), x.device)
-    gw = torch.empty(w_shape, dtype=torch.float32, device=x.device)
-    gb = torch.empty(desc.bias_period, dtype=torch.float32, device=x.device) if want_bias else None
     if kind == PACK_CONVT:
         cin, cout, k = w_shape
     else:
         cout, cin, k = w_shape
-    if params is not None and len(params) == 1 + int(gb is not None) and _can_defer(params) and _queue_flush():
+    if params is not None and len(params) == 1 + int(want_bias) and _can_defer(params) and _queue_flush():
+        gw = _grad_out(params[0], w_shape, x.device)
+        gb = _grad_out(params[1], (desc.bias_period,), x.device) if want_bias else None
         ns = ctypes.c_int()
         st = L.stream()
         if WGRAD_STREAM:
@@ -539,6 +516,8 @@ def wgrad_torch(desc, gout, x, kind, w_shape, stride, want_bias, params=None):
                         stride)
         _defer(job, ws, params, gw, gb, st)
         return gw, gb
+    gw = torch.empty(w_shape, dtype=torch.float32, device=x.device)
+    gb = torch.empty(desc.bias_period, dtype=torch.float32, device=x.device) if want_bias else None
     L.call("sel_conv_wgrad_unpacked", ctypes.byref(desc), _code(x.dtype), L.ptr(gout), L.ptr(x), kind, cout, cin,
            k, stride, L.ptr(gw), L.ptr(gb), L.ptr(ws), ws.numel(), L.stream())
     return gw, gb
@@ -713,11 +692,16 @@ def resunit_bwd_wgrad(d1, gf, h, xf, wd1, wd2, s1, s2, want_b1, want_b2, params1
            meta=lambda: _ru_bwd_meta(d1, xf, False, wgrad=True))
     out, jobs = [], []
     for (shape, want_b, params, off, nw, k) in ((s1, want_b1, params1, 0, nw1, d1.K), (s2, want_b2, params2, n1, nw2, 1)):
-        gw = torch.empty(shape, dtype=torch.float32, device=xf.device)
-        gb = torch.empty(N, dtype=torch.float32, device=xf.device) if want_b else None
+        defer = params is not None and len(params) == 1 + int(want_b) and _can_defer(params) and _queue_flush()
+        if defer:
+            gw = _grad_out(params[0], shape, xf.device)
+            gb = _grad_out(params[1], (N,), xf.device) if want_b else None
+        else:
+            gw = torch.empty(shape, dtype=torch.float32, device=xf.device)
+            gb = torch.empty(N, dtype=torch.float32, device=xf.device) if want_b else None
         job = _WgradJob(ws.data_ptr() + 4 * off, gw.data_ptr(), gb.data_ptr() if gb is not None else None, nw, ns, N,
                         N, PACK_FWD, shape[0], shape[1], k, 1)
-        if params is not None and len(params) == 1 + int(want_b) and _can_defer(params) and _queue_flush():
+        if defer:
             _defer(job, ws, params, gw, gb, st)
         else:
             jobs.append(job)

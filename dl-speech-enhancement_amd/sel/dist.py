@@ -119,23 +119,30 @@ def add_noise_global(speech, noise, snr):
     return _mix(a, b, sums, snr)
 
 
-DDP_BUCKET_MB = 4
+DDP_BUCKET_MB = float(os.environ.get("SEL_DDP_BUCKET_MB", "4"))
 
 
-def wrap_ddp(module, device=None, bucket_cap_mb=DDP_BUCKET_MB):
+def wrap_ddp(module, device=None, bucket_cap_mb=DDP_BUCKET_MB, force=False):
     """DistributedDataParallel over the trainable parameters only (frozen
     decoder/quantizer of trainer/denoise.py are skipped).  Gradient buckets are
     all-reduced by RCCL while the backward is still running.  4 MB buckets:
     the denoise trainer's 15.6 MB of fp32 encoder grads span 4-5 ring
     all-reduces, the first of which start while the encoder's earlier layers
     are still in their backward (one 16 MB bucket would only start after the
-    last of them).  The sel communication hook (convops.install_ddp_hook)
-    keeps the weight-gradient reductions batched per bucket."""
-    from torch.nn.parallel import DistributedDataParallel as DDP
-    if not is_dist() or dist.get_world_size() == 1:
+    last of them).  The sel reducer (sel.ddp.SelDDP)
+    keeps the weight-gradient reductions batched per bucket and writes them
+    straight into the buckets (sel.ddp).  SEL_DDP=torch: torch's
+    DistributedDataParallel instead (its own bucket copies; the weight-gradient
+    reductions then run per layer).  force: wrap under a one-rank group too
+    (bench.py's SEL_BENCH_FORCE_DDP rehearsal of the data-parallel schedule on
+    one GPU)."""
+    if not is_dist() or (dist.get_world_size() == 1 and not force):
         return module
-    kw = dict(broadcast_buffers=False, bucket_cap_mb=bucket_cap_mb, gradient_as_bucket_view=True)
-    if device is not None and device.type == "cuda":
-        kw["device_ids"] = [device.index]
-    from .convops import install_ddp_hook
-    return install_ddp_hook(DDP(module, **kw))
+    if os.environ.get("SEL_DDP", "sel") == "torch":
+        from torch.nn.parallel import DistributedDataParallel as DDP
+        kw = dict(broadcast_buffers=False, bucket_cap_mb=bucket_cap_mb, gradient_as_bucket_view=True)
+        if device is not None and device.type == "cuda":
+            kw["device_ids"] = [device.index]
+        return DDP(module, **kw)
+    from .ddp import SelDDP
+    return SelDDP(module, bucket_cap_mb=bucket_cap_mb)

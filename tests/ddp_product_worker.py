@@ -5,7 +5,7 @@
 Runs the product's own training step under a gloo process group on CUDA
 tensors — RCCL cannot put two ranks on one device, gloo can, and the code paths
 above the backend (DDP buckets and hooks, sel.dist exchanges, the
-deferred weight-gradient reductions flushed by the sel comm hook per bucket)
+deferred weight-gradient reductions flushed by the sel reducer per bucket)
 are the ones RCCL runs on 8 GPUs — and saves the
 per-step loss values and the final weights.  `run_case` is also what the test
 calls in-process (no process group) for the single-device reference on the
@@ -20,8 +20,9 @@ Cases:
   c3  — the bench's C3 step at full width: trainer/denoise.Trainer._train_step
         on the symAD_libritts_24000_hop300 PQC generator in bf16 (mel + vq,
         the fused 32/64-channel residual-unit kernels with their weight
-        gradients), 4 global clips of 1 s, DDP with the sel comm hook (the
-        deferred weight-gradient reductions run per gradient bucket).
+        gradients), 4 global clips of 1 s, data parallel through sel.ddp (the
+        deferred weight-gradient reductions run per gradient bucket, right
+        before its all-reduce).
   gan — train_denoise.DenoiseStep.model_step in GAN mode (:138-165, :213-263)
         on a reduced-width without-PQC generator + HiFi-GAN discriminator, with
         lambda_snr_loss = 1 so the global SNR surrogate runs; generator and
@@ -160,7 +161,7 @@ def main():
     res["rank_world"] = D.rank_world()
     from sel import convops as CO
     res["deferred_pending"] = len(CO._DEFERRED)
-    res["ddp_stats"] = dict(CO.DDP_STATS)  # deferred reductions flushed by the DDP comm hook
+    res["ddp_stats"] = dict(CO.DDP_STATS)  # deferred reductions flushed per bucket by sel.ddp
     torch.save(res, out)
     dist.barrier()
     dist.destroy_process_group()

@@ -123,6 +123,58 @@ def test_ddp_grad_equals_full_batch():
             torch.testing.assert_close(g, p.grad, rtol=1e-5, atol=1e-6)
 
 
+def _buckets_case(rank):
+    """sel.ddp with one-parameter buckets (bucket_cap_mb tiny), an unused
+    parameter and two backward passes: every bucket all-reduced in order,
+    the unused parameter's .grad left None."""
+    from sel.ddp import SelDDP
+
+    class WithUnused(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.net = _tiny_model()
+            self.extra = torch.nn.Linear(2, 2)  # never used: its bucket is launched by the final callback
+
+        def forward(self, x):
+            return self.net(x)
+    model = WithUnused()
+    m = SelDDP(model, bucket_cap_mb=1e-6)
+    assert len(m.reducer.buckets) == len(list(model.parameters()))
+    x, y = _batch()
+    out = []
+    for it in range(2):
+        for p in model.parameters():
+            p.grad = None
+        loss = torch.nn.functional.l1_loss(m(D_shard(x)), D_shard(y)) * (it + 1)
+        loss.backward()
+        assert model.extra.weight.grad is None and model.extra.bias.grad is None
+        out += [p.grad.clone() for p in model.parameters() if p.grad is not None]
+    assert m.reducer.stats["buckets"] == 2 * len(m.reducer.buckets)
+    # the state dict has the wrapped module's keys (no "module." prefix)
+    assert set(m.state_dict()) == set(model.state_dict())
+    return out
+
+
+def D_shard(t):
+    from sel import dist as D
+    return D.shard(t)
+
+
+def test_sel_ddp_buckets_average_like_full_batch():
+    out = _run(_buckets_case)
+    m = _tiny_model()
+    x, y = _batch()
+    ref = []
+    for it in range(2):
+        m.zero_grad(set_to_none=True)
+        (torch.nn.functional.l1_loss(m(x), y) * (it + 1)).backward()
+        ref += [p.grad.clone() for p in m.parameters()]
+    for r in range(WORLD):
+        assert len(out[r]) == len(ref)
+        for g, gr in zip(out[r], ref):
+            torch.testing.assert_close(g, gr, rtol=1e-5, atol=1e-6)
+
+
 def _shard_case(rank):
     from sel import dist as D
     t = torch.arange(8)

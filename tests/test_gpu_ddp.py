@@ -5,8 +5,8 @@ process is never exec'ed) in a world-size-2 gloo process group over CUDA
 tensors.  RCCL cannot place two ranks on one device; gloo can, and everything
 above the backend is what bench.py / train_denoise.py run over RCCL on 8 GPUs:
 DDP's bucket hooks on the HIP autograd ops, the deferred weight-gradient
-reductions run per bucket by the sel DDP comm hook (sel/convops.py
-flush_bucket; asserted to have run), the packed-weight
+reductions run per gradient bucket by the sel reducer (sel/ddp.py, convops
+flush_params; asserted to have run), the packed-weight
 refresh after the DDP-averaged Adam step, the batch-global add_noise exchange
 (sel.dist.add_noise_global), the spectral-convergence exchange through the real
 STFT-loss autograd op (sel.dist.global_loss_sums, losses/stft_loss.py:56), the
@@ -85,7 +85,7 @@ def test_ddp_product_step_matches_single_process(gpu, case, tmp_path):
     assert all(r["deferred_pending"] == 0 for r in ranks)
     if case in ("pqc", "c3"):
         # the generator's weight-gradient reductions were deferred under the
-        # process group and run by the sel DDP comm hook, per bucket
+        # process group and run by the sel reducer, per bucket
         for r in ranks:
             assert r["ddp_stats"]["jobs"] > 0 and r["ddp_stats"]["bucket_flushes"] > 0, r["ddp_stats"]
     # DDP keeps the replicas identical
