@@ -370,7 +370,8 @@ def _can_defer(params):
         owned = all(p is not None and _owner(p) is not None for p in params)
         if owned and not DDP_DEFER:
             return False
-        if not owned and dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        # (any process group: torch's DDP may wrap the module even at one rank)
+        if not owned and dist.is_available() and dist.is_initialized():
             return False
         for p in params:
             if p is None or not p.is_leaf or p.grad is not None:

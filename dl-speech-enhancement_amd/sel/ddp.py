@@ -78,6 +78,8 @@ class GradBuckets:
         return self.flat.narrow(0, off, n).view(p.shape)
 
     def _arrived(self, p):
+        if p.grad is None:  # an undefined gradient (e.g. a frozen pass): not an arrival
+            return
         if not self.armed:
             self.armed = True
             torch.autograd.Variable._execution_engine.queue_callback(self._finish)
