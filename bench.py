@@ -606,15 +606,36 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    timer = _lib.KernelTimer([dom] + (["sel_resunit_fwd", "sel_resunit_bwd", "sel_resunit_bwd_wgrad"] if cfg == "c3" else [])
-                             + (["sel_dconv_fwd"] if cfg == "c5" else []))
+    timer = (_lib.KernelTimer([dom] + (["sel_resunit_fwd", "sel_resunit_bwd", "sel_resunit_bwd_wgrad"]
+                                       if cfg == "c3" else []))
+             if cfg != "c5" else None)  # C5: a serialised extra step below
     elapsed, per_step = _timed_steps(step, args.steps, world, dev, timer)
 
     ms_per_step = 1e3 * elapsed / args.steps
     frames_per_step = world * B * sr / HOP
     value = frames_per_step * args.steps / elapsed
     med_ms = float(np.median(per_step))
-    roof = roofline(cfg, timer, dom, B, 1)  # the timer covered the last timed step
+    if cfg == "c5":
+        # the C5 step runs the 8 sub-discriminator chains on side streams: an
+        # event pair around one launch there also spans what the other streams
+        # run beside it, so the roofline comes from ONE extra step with the
+        # chains serialised (SEL_D_STREAMS=0: same kernels, same bits), after
+        # the timed region; each launch's events then bracket that launch alone
+        prev = os.environ.get("SEL_D_STREAMS")
+        os.environ["SEL_D_STREAMS"] = "0"
+        timer = _lib.KernelTimer([dom, "sel_dconv_fwd"])
+        torch.cuda.synchronize()
+        _lib.TIMER = timer
+        step()
+        torch.cuda.synchronize()
+        _lib.TIMER = None
+        if prev is None:
+            del os.environ["SEL_D_STREAMS"]
+        else:
+            os.environ["SEL_D_STREAMS"] = prev
+    roof = roofline(cfg, timer, dom, B, 1)  # the timer covered one step (C3: the last timed one)
+    if cfg == "c5":
+        roof["timing"] = "one extra step with the sub-discriminator chains serialised (SEL_D_STREAMS=0)"
 
     fp32 = None
     if cfg == "c3" and not args.no_fp32_companion:

@@ -1670,6 +1670,18 @@ __device__ __forceinline__ void ru_bstore(__amdgpu_buffer_rsrc_t rs, int byte_of
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, byte_off, 0, 0);
 }
 
+// N dropped stores (a zero-byte region; distinct offsets so that the compiler
+// keeps them apart) after a tile loop's first prefetch: the loop issues N
+// output stores after each later prefetch, so both paths into the staging
+// waits carry the same count and the compiler leaves those stores pending
+template <int N>
+__device__ __forceinline__ void ru_dummy_stores(const __bf16* base) {
+  const __amdgpu_buffer_rsrc_t rz = ru_rsrc(base, 0);
+  const bf16x8 z = {};
+#pragma unroll
+  for (int i = 0; i < N; ++i) ru_bstore(rz, 16 * i, z);
+}
+
 __device__ __forceinline__ void ru_acc_to_frags(const float (&v)[16], bf16x8 (&frag)[2]) {
   unsigned pk[8];
 #pragma unroll
@@ -1719,6 +1731,9 @@ struct Ru32Stage {
       const int ti = t0 + off + row;
       ok[u] = row < span && ti >= 0 && ti < a.T;
       r[u] = ru_bload(rs, live && ok[u] ? (ti * RU_C + c) * 2 : RU_OOB);
+      // program order pinned: the same order from the prologue and the tile
+      // loop, so the staging waits count both paths into them exactly
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
   // raw != nullptr: rows [raw_off, raw_off + R) are also stored un-ELU'd into raw
@@ -1790,6 +1805,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU32F
   }
   Ru32Stage<R> st;
   st.load(a, x, tile0 / tps, int(tile0 % tps) * R, -a.pad, span);
+  ru_dummy_stores<4 * G::TM>(out);  // the loop's h / out stores after each prefetch
   for (int64_t tile = tile0; tile < tile_end; ++tile) {
     const int64_t b = tile / tps;
     const int t0 = int(tile % tps) * R;
@@ -1802,12 +1818,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU32F
       const int64_t nt = live ? tile + 1 : tile;
       st.load(a, x, nt / tps, int(nt % tps) * R, -a.pad, span, live);
     }
+    // every sub-tile computes and stores (rows past T to RU_OOB): a fixed count
+    // of stores per tile keeps the next tile's staging wait exact (ru_bstore)
+    const __amdgpu_buffer_rsrc_t rh = ru_rsrc(hout + b * a.T * RU_C, int64_t(a.T) * RU_C);
+    const __amdgpu_buffer_rsrc_t ro = ru_rsrc(out + b * a.T * RU_C, int64_t(a.T) * RU_C);
 #pragma unroll
     for (int i = 0; i < G::TM; ++i) {
       const int lr = wave * (R / 4) + i * 32 + (lane & 31);  // this lane's row in the tile
-      if (__builtin_amdgcn_readfirstlane(wave * (R / 4) + i * 32) >= mrows) break;  // wave-uniform
       const bool valid = lr < mrows;
-      const int64_t orow = (b * a.T + t0 + lr) * RU_C;
+      const int off = ((t0 + lr) * RU_C + 8 * hl) * 2;
       floatx16 acc;
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[e] = 0.f;
@@ -1829,10 +1848,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU32F
       }
       bf16x8 hf[2];
       ru_acc_to_frags(v, hf);
-      if (valid && !(dbg & 1)) {  // tune key 15 bit 0: diagnostic without the h store
-        ru_store(hout + orow + 8 * hl, hf[0]);
-        ru_store(hout + orow + 16 + 8 * hl, hf[1]);
-      }
+      const bool hst = valid && !(dbg & 1);  // tune key 15 bit 0: diagnostic without the h store
+      ru_bstore(rh, hst ? off : RU_OOB, hf[0]);
+      ru_bstore(rh, hst ? off + 32 : RU_OOB, hf[1]);
       floatx16 acc2;
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc2[e] = 0.f;
@@ -1852,10 +1870,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU32F
       }
       bf16x8 of[2];
       ru_acc_to_frags(v, of);
-      if (valid && !(dbg & 2)) {  // bit 1: diagnostic without the out store
-        ru_store(out + orow + 8 * hl, of[0]);
-        ru_store(out + orow + 16 + 8 * hl, of[1]);
-      }
+      const bool ost = valid && !(dbg & 2);  // bit 1: diagnostic without the out store
+      ru_bstore(ro, ost ? off : RU_OOB, of[0]);
+      ru_bstore(ro, ost ? off + 32 : RU_OOB, of[1]);
     }
   }
 }
@@ -1941,6 +1958,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU64F
       const int ti = t0 - a.pad + r;
       xok[u] = r < span && ti >= 0 && ti < a.T;
       xr[u] = ru_bload(rs, live && xok[u] ? (ti * C + c) * 2 : RU_OOB);  // Ru32Stage::load
+      __builtin_amdgcn_sched_barrier(0);  // program order pinned (Ru32Stage::load)
     }
   };
   auto store = [&]() {
@@ -1956,6 +1974,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU64F
   };
 
   load(tile0, true);
+  ru_dummy_stores<4 * G::TM>(out);  // the loop's h / out stores after each prefetch
   for (int64_t tile = tile0; tile < tile_end; ++tile) {
     const int64_t b = tile / tps;
     const int t0 = int(tile % tps) * R;
@@ -1984,6 +2003,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU64F
           acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[k][g], *reinterpret_cast<const bf16x8*>(xb + i * 32 * P),
                                                            acc[i], 0, 0, 0);
       }
+    // every sub-tile stores (rows past T to RU_OOB): a fixed count of stores per
+    // tile keeps the next tile's staging wait exact (ru_bstore)
+    const __amdgpu_buffer_rsrc_t rh = ru_rsrc(hout + b * a.T * C, int64_t(a.T) * C);
+    const __amdgpu_buffer_rsrc_t ro = ru_rsrc(out + b * a.T * C, int64_t(a.T) * C);
     // h = conv1 + b1 -> bf16 -> HBM; ELU(h) -> the 1x1's LDS tile (plane ns)
 #pragma unroll
     for (int i = 0; i < G::TM; ++i) {
@@ -1997,11 +2020,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU64F
       }
       bf16x8 hf[2];
       ru_acc_to_frags(v, hf);
-      if (lr < mrows) {
-        const int64_t orow = (b * a.T + t0 + lr) * C + ns * 32 + 8 * hl;
-        ru_store(hout + orow, hf[0]);
-        ru_store(hout + orow + 16, hf[1]);
-      }
+      const int off = ((t0 + lr) * C + ns * 32 + 8 * hl) * 2;
+      ru_bstore(rh, lr < mrows ? off : RU_OOB, hf[0]);
+      ru_bstore(rh, lr < mrows ? off + 32 : RU_OOB, hf[1]);
 #pragma unroll
       for (int g = 0; g < 2; ++g)
         *reinterpret_cast<uint4*>(hs + (ns * R + lr) * P + 16 * g + 8 * hl) = elu8(__builtin_bit_cast(uint4, hf[g]));
@@ -2011,7 +2032,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU64F
 #pragma unroll
     for (int i = 0; i < G::TM; ++i) {
       const int lr = rg * G::WR + i * 32 + (lane & 31);
-      if (__builtin_amdgcn_readfirstlane(rg * G::WR + i * 32) >= mrows) break;  // wave-uniform
       floatx16 acc2;
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc2[e] = 0.f;
@@ -2031,11 +2051,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU64F
       }
       bf16x8 of[2];
       ru_acc_to_frags(v, of);
-      if (lr < mrows) {
-        const int64_t orow = (b * a.T + t0 + lr) * C + ns * 32 + 8 * hl;
-        ru_store(out + orow, of[0]);
-        ru_store(out + orow + 16, of[1]);
-      }
+      const int off = ((t0 + lr) * C + ns * 32 + 8 * hl) * 2;
+      ru_bstore(ro, lr < mrows ? off : RU_OOB, of[0]);
+      ru_bstore(ro, lr < mrows ? off + 32 : RU_OOB, of[1]);
     }
   }
 }
@@ -2289,6 +2307,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 128 ? 
   Ru32Stage<R> st, sh;
   st.load(a, g, tile0 / tps, int(tile0 % tps) * R, 0, span);
   sh.load(a, h, tile0 / tps, int(tile0 % tps) * R, 0, span);
+  ru_dummy_stores<2 * G::TM>(gx);  // the loop's gx stores after each prefetch
   for (int64_t tile = tile0; tile < tile_end; ++tile) {
     const int64_t b = tile / tps;
     const int t0 = int(tile % tps) * R;
@@ -2354,10 +2373,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 128 ? 
       st.load(a, g, nt / tps, int(nt % tps) * R, 0, span, live);
       sh.load(a, h, nt / tps, int(nt % tps) * R, 0, span, live);
     }
+    // every sub-tile stores (rows past T to RU_OOB): a fixed count of stores per
+    // tile keeps the next tile's staging waits exact (ru_bstore)
+    const __amdgpu_buffer_rsrc_t rgx = ru_rsrc(gx + b * a.T * RU_C, int64_t(a.T) * RU_C);
 #pragma unroll
     for (int i = 0; i < G::TM; ++i) {
       const int lr = wave * (R / 4) + i * 32 + (lane & 31);
-      if (__builtin_amdgcn_readfirstlane(wave * (R / 4) + i * 32) >= mrows) break;
       floatx16 acc;
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[e] = 0.f;
@@ -2369,7 +2390,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 128 ? 
           acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[k][c], *reinterpret_cast<const bf16x8*>(hw + k * a.dil * P + 16 * c),
                                                         acc, 0, 0, 0);
       const bool valid = lr < mrows;
-      const int64_t orow = (b * a.T + t0 + (valid ? lr : 0)) * RU_C;
       float v[16];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -2382,10 +2402,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 128 ? 
       }
       bf16x8 of[2];
       ru_acc_to_frags(v, of);
-      if (valid) {
-        ru_store(gx + orow + 8 * hl, of[0]);
-        ru_store(gx + orow + 16 + 8 * hl, of[1]);
-      }
+      const int off = ((t0 + lr) * RU_C + 8 * hl) * 2;
+      ru_bstore(rgx, valid ? off : RU_OOB, of[0]);
+      ru_bstore(rgx, valid ? off + 32 : RU_OOB, of[1]);
     }
   }
 }
@@ -2821,6 +2840,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU32W
     st.load(a, g, tile0 / tps, int(tile0 % tps) * R, 0, span);
     sx.load(a, x, tile0 / tps, int(tile0 % tps) * R, -halo, span);
     sh.load(a, h, tile0 / tps, int(tile0 % tps) * R, 0, span);
+    ru_dummy_stores<2 * Ru32<R>::TM>(gx);  // the loop's gx stores after each prefetch
     for (int64_t tile = tile0; tile < tile_end; ++tile) {
       const int64_t b = tile / tps;
       const int t0 = int(tile % tps) * R;
@@ -2889,11 +2909,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU32W
         sx.load(a, x, nt / tps, int(nt % tps) * R, -halo, span, live);
         sh.load(a, h, nt / tps, int(nt % tps) * R, 0, span, live);
       }
-      // gx = conv1^T(gh) * ELU'(x) + g (k_ru32_bwd)
+      // gx = conv1^T(gh) * ELU'(x) + g (k_ru32_bwd); every sub-tile stores
+      // (rows past T to RU_OOB): a fixed count of stores per tile keeps the
+      // next tile's staging waits exact (ru_bstore)
+      const __amdgpu_buffer_rsrc_t rgx = ru_rsrc(gx + b * a.T * RU_C, int64_t(a.T) * RU_C);
 #pragma unroll
       for (int i = 0; i < Ru32<R>::TM; ++i) {
         const int lr = wave * (R / 4) + i * 32 + (lane & 31);
-        if (__builtin_amdgcn_readfirstlane(wave * (R / 4) + i * 32) >= mrows) break;
         floatx16 acc;
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[e] = 0.f;
@@ -2906,7 +2928,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU32W
                                                           *reinterpret_cast<const bf16x8*>(hw + k * a.dil * P + 16 * c),
                                                           acc, 0, 0, 0);
         const bool valid = lr < mrows;
-        const int64_t orow = (b * a.T + t0 + (valid ? lr : 0)) * RU_C;
         float v[16];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -2919,10 +2940,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU32W
         }
         bf16x8 of[2];
         ru_acc_to_frags(v, of);
-        if (valid) {
-          ru_store(gx + orow + 8 * hl, of[0]);
-          ru_store(gx + orow + 16 + 8 * hl, of[1]);
-        }
+        const int off = ((t0 + lr) * RU_C + 8 * hl) * 2;
+        ru_bstore(rgx, valid ? off : RU_OOB, of[0]);
+        ru_bstore(rgx, valid ? off + 32 : RU_OOB, of[1]);
       }
       // weight gradients over the tile rows (rows past T: g = 0 -> gh = 0)
       const __bf16* b0p = xs + k0 * a.dil * PW;
@@ -3134,7 +3154,10 @@ __device__ __forceinline__ void ru64w_gh(__bf16* smem_bf, int wave, int lane, in
   }
 }
 
-template <int R>
+// WG = false: the same kernel without the weight-gradient role (the decoder's
+// units, whose weights are frozen): all eight waves compute gx, one 32-row
+// sub-tile and 32-channel slice each (part1 / part2 unused).
+template <int R, bool WG = true>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k_ru64_bwdw(
     Args a, const __bf16* __restrict__ g, const __bf16* __restrict__ h, const __bf16* __restrict__ x,
     const __bf16* __restrict__ wd1, const __bf16* __restrict__ wd2, __bf16* __restrict__ gx,
@@ -3166,11 +3189,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
     }
   }
 
-  if (wave < 4) {
+  if (!WG || wave < 4) {
     // ---- gx role: k_ru64_bwd's gx phase (row group rg, output slice ns) ----
     if (!any) return;  // workgroup-uniform: a block without tiles has no barriers
     const int ns = wave & 1, rg = wave >> 1;
-    constexpr int WR = R / 2, TM = WR / 32;
+    constexpr int WR = WG ? R / 2 : R / 4, TM = WR / 32;
     bf16x8 wf[K][C / 16];
     {
       const __bf16* wrow = wd1 + int64_t(ns * 32 + (lane & 31)) * K * C + 8 * hl;
@@ -3182,17 +3205,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
     ws_wait_vm<0>();  // weights landed: the tile loop's waits then count only its own loads
     Ru64WStage<R> st;
     ru64w_load<R>(st, a, g, h, x, tile0, tps, halo, true);
-    {
-      // the tile loop issues 2 TM stores after each prefetch; the same number of
-      // dropped stores here makes both paths into the staging waits identical,
-      // so the compiler's count leaves the previous tile's gx stores pending
-      // (a zero-byte region: every offset is out of range; distinct offsets so
-      // that the compiler does not merge them)
-      const __amdgpu_buffer_rsrc_t rz = ru_rsrc(gx, 0);
-      const bf16x8 z = {};
-#pragma unroll
-      for (int i = 0; i < 2 * TM; ++i) ru_bstore(rz, 16 * i, z);
-    }
+    ru_dummy_stores<2 * TM>(gx);  // the loop's gx stores after each prefetch
     for (int64_t tile = tile0; tile < tile_end; ++tile) {
       const int64_t b = tile / tps;
       const int t0 = int(tile % tps) * R;
@@ -3246,7 +3259,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
     }
     return;
   }
-
+  if constexpr (WG) {
   // ---- weight-gradient role ----
   const int v = wave - 4;
   const int wn = v & 1;     // h-channel (output) slice of the weight gradients
@@ -3324,6 +3337,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
     if (upper) part2[int64_t(nb) * G::NW2 + int64_t(blockIdx.x) * C + wn * 32 + lane] = bsum;
     else part1[int64_t(nb) * G::NW1 + int64_t(blockIdx.x) * C + wn * 32 + lane] = bsum;
   }
+  }  // WG
 }
 
 constexpr int WB_BM = 64;
@@ -4589,15 +4603,15 @@ int launch_ru32_bwdw(const Args& a, const void* g, const void* h, const void* x,
 
 // fused 64-channel backward with the weight gradients: one 512-thread block per
 // CU (its LDS planes), one partial per block
-template <int R>
+template <int R, bool WG = true>
 int ru64w_blocks(int64_t ntiles, int64_t& tpb) {
   static const int64_t slots = [] {
     int dev = 0, cus = 0, per_cu = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipFuncSetAttribute((const void*)k_ru64_bwdw<R>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        hipFuncSetAttribute((const void*)k_ru64_bwdw<R, WG>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             int(Ru64W<R>::LDS)) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_ru64_bwdw<R>, 512, Ru64W<R>::LDS) != hipSuccess)
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_ru64_bwdw<R, WG>, 512, Ru64W<R>::LDS) != hipSuccess)
       return int64_t(0);
     return int64_t(cus) * per_cu / 8 * 8;
   }();
@@ -4606,18 +4620,20 @@ int ru64w_blocks(int64_t ntiles, int64_t& tpb) {
   return int(((ntiles + tpb - 1) / tpb + 7) / 8 * 8);
 }
 
-template <int R>
+template <int R, bool WG = true>
 int launch_ru64_bwdw(const Args& a, const void* g, const void* h, const void* x, const void* wd1, const void* wd2,
                      void* gx, float* part1, float* part2, int nsplit, hipStream_t s) {
   const int64_t ntiles = (a.rows / a.T) * ((a.T + R - 1) / R);
+  if (ntiles == 0 && !WG) return SEL_OK;
   int64_t tpb = 1;
-  const int nb = ru64w_blocks<R>(ntiles, tpb);
-  SEL_REQUIRE(nb == nsplit, SEL_ERR_ARG, "sel_resunit_bwd_wgrad: nsplit %d, this shape needs %d", nsplit, nb);
-  SEL_HIP(hipFuncSetAttribute((const void*)k_ru64_bwdw<R>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  const int nb = ru64w_blocks<R, WG>(ntiles, tpb);
+  SEL_REQUIRE(!WG || nb == nsplit, SEL_ERR_ARG, "sel_resunit_bwd_wgrad: nsplit %d, this shape needs %d", nsplit, nb);
+  SEL_HIP(hipFuncSetAttribute((const void*)k_ru64_bwdw<R, WG>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               int(Ru64W<R>::LDS)));
-  hipLaunchKernelGGL(k_ru64_bwdw<R>, dim3(unsigned(nb)), dim3(512), Ru64W<R>::LDS, s, a, static_cast<const __bf16*>(g),
-                     static_cast<const __bf16*>(h), static_cast<const __bf16*>(x), static_cast<const __bf16*>(wd1),
-                     static_cast<const __bf16*>(wd2), static_cast<__bf16*>(gx), part1, part2, int(tpb));
+  hipLaunchKernelGGL((k_ru64_bwdw<R, WG>), dim3(unsigned(nb)), dim3(512), Ru64W<R>::LDS, s, a,
+                     static_cast<const __bf16*>(g), static_cast<const __bf16*>(h), static_cast<const __bf16*>(x),
+                     static_cast<const __bf16*>(wd1), static_cast<const __bf16*>(wd2), static_cast<__bf16*>(gx), part1,
+                     part2, int(tpb));
   SEL_LAUNCH_CHECK();
   return SEL_OK;
 }
@@ -4939,6 +4955,12 @@ int sel_resunit_bwd(const sel_conv_desc* d1, int dtype, const void* g, const voi
   SEL_REQUIRE(dtype == SEL_BF16 && ru_fused_ok(a), SEL_ERR_UNSUPPORTED,
               "sel_resunit_bwd: fused path needs bf16, C = N in {32, 64}, K = 7, causal zero pad, ELU prologue");
   SEL_REQUIRE(g && h && x && wd1pack && wd2pack && gx, SEL_ERR_ARG, "null pointer");
+  // tune key 41 = 1 (without gh): the eight-wave LDS-staged form, k_ru64_bwdw's
+  // gx role on all waves (one workgroup per CU: measured slower than two
+  // four-wave k_ru64_bwd workgroups, 82-83 vs 72 us per unit at C3)
+  if (a.C == 64 && gh == nullptr && tune(41) == 1)
+    return launch_ru64_bwdw<128, false>(a, g, h, x, wd1pack, wd2pack, gx, nullptr, nullptr, 0,
+                                        reinterpret_cast<hipStream_t>(stream));
   if (a.C == 64)
     return launch_ru64_bwd<128>(a, g, h, x, wd1pack, wd2pack, gh, gx, reinterpret_cast<hipStream_t>(stream));
   return launch_ru32_bwd<128>(a, g, h, x, wd1pack, wd2pack, gh, gx, reinterpret_cast<hipStream_t>(stream));

@@ -650,6 +650,14 @@ def resunit_bwd(d1, gf, h, xf, wd1, wd2, want_gh):
     return gx, gh
 
 
+def _tune_value(key):
+    """Current value of a sel_tune knob (sel_tune sets and returns the previous one)."""
+    lib = L.lib()
+    v = lib.sel_tune(key, 0)
+    lib.sel_tune(key, v)
+    return v
+
+
 def _ru_bwd_meta(d1, xf, want_gh, wgrad=False):
     """Algorithmic bytes: read g, h, x once, write gx (and gh); flops of the two
     adjoints (and of the two weight gradients)."""
@@ -658,6 +666,8 @@ def _ru_bwd_meta(d1, xf, want_gh, wgrad=False):
     flops = 2.0 * d1.rows * d1.N * d1.C * (d1.K + 1) * (2 if wgrad else 1)
     if wgrad:
         return ("k_ru32_bwdw<128>" if d1.C == 32 else "k_ru64_bwdw<128>"), nbytes, flops
+    if d1.C == 64 and not want_gh and _tune_value(41) == 1:
+        return "k_ru64_bwdw<128, false>", nbytes, flops
     return ("k_ru32_bwd<128>" if d1.C == 32 else "k_ru64_bwd<128>"), nbytes, flops
 
 

@@ -8,7 +8,10 @@ own layer shapes.  Knobs covered elsewhere: 0 (tile variants, test_gpu_c3),
 * generator (C3 widths, B = 2 x 1 s @ 24 kHz, bf16, full fwd + bwd): 6 (thin
   kernel instances on their alternative tile rows), 7 (thin kernel off: tiled
   kernels), 8 (plain 2-D grid instead of the XCD-aware order), 12 (epilogue
-  prefetch flipped on every thin instance), 20 (two-pass split reduction);
+  prefetch flipped on every thin instance), 20 (two-pass split reduction),
+  40 (k_ru64_bwdw workgroup target: another split of the weight-gradient
+  rows), 41 (the 64-channel backward without gh on the eight-wave kernel
+  instead of k_ru64_bwd: bit-identical);
 * discriminator (C5 widths, B = 2 x 1 s @ 48 kHz, bf16, fwd + bwd incl.
   weight-norm grads): 16 (no prefetching kernels: k_dconv_mfma tiles and the
   generic weight gradient), 25 (scalar bias partials), 28 (128-row tiles for
@@ -24,7 +27,8 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-GEN_KNOBS = [(6, 0xFFFF, False), (7, 0xFFFF, False), (8, 1, True), (12, 0xFFFF, False), (20, 1, True)]
+GEN_KNOBS = [(6, 0xFFFF, False), (7, 0xFFFF, False), (8, 1, True), (12, 0xFFFF, False), (20, 1, True),
+             (40, 64, False), (41, 1, True)]
 DISC_KNOBS = [(16, 1, False), (25, 1, False), (28, 1, False), (31, 1, False)]
 
 
