@@ -24,7 +24,7 @@
 namespace sel {
 namespace spec {
 
-__device__ float2 g_tw[kTwTotal];
+__constant__ float2 g_tw[kTwTotal];  // constant address space: lane-uniform reads are scalar loads
 
 hipError_t upload_twiddles(const float2* host, size_t count) {
   return hipMemcpyToSymbol(HIP_SYMBOL(g_tw), host, count * sizeof(float2));
@@ -684,27 +684,45 @@ __device__ __forceinline__ void fetch_frame_vm(const float* __restrict__ x, __am
                                                const FrameArgs& a, int b, int f, int l, bool active,
                                                v2f_t (&raw)[8]) {
   using G = Geo<LOGN>;
-  static_assert(G::PPL == 8 && G::LPF * 8 * 7 < 4096, "immediate offsets");
+  static_assert(G::PPL == 8 && G::LPF * 8 * 3 < 4096, "immediate offsets");
   constexpr int S = G::LPF * 8;  // bytes between a lane's consecutive points
   const int T = int(a.T);
   const int base = f * a.hop - a.P;
   const int sig = b * T;
   const float* xs = x + sig + base;
   if (active && base >= 0 && base + G::N <= T && (reinterpret_cast<uintptr_t>(xs) & 7) == 0) {
-    const float2* p = reinterpret_cast<const float2*>(xs) + l;
-    asm volatile(
-        "global_load_dwordx2 %0, %8, off\n\t"
-        "global_load_dwordx2 %1, %8, off offset:%9\n\t"
-        "global_load_dwordx2 %2, %8, off offset:%10\n\t"
-        "global_load_dwordx2 %3, %8, off offset:%11\n\t"
-        "global_load_dwordx2 %4, %8, off offset:%12\n\t"
-        "global_load_dwordx2 %5, %8, off offset:%13\n\t"
-        "global_load_dwordx2 %6, %8, off offset:%14\n\t"
-        "global_load_dwordx2 %7, %8, off offset:%15"
-        : "=&v"(raw[0]), "=&v"(raw[1]), "=&v"(raw[2]), "=&v"(raw[3]), "=&v"(raw[4]), "=&v"(raw[5]),
-          "=&v"(raw[6]), "=&v"(raw[7])
-        : "v"(p), "i"(S), "i"(2 * S), "i"(3 * S), "i"(4 * S), "i"(5 * S), "i"(6 * S), "i"(7 * S)
-        : "memory");
+    if constexpr (G::LPF * 8 * 7 >= 4096) {  // n_fft 2048: points 4-7 off a second base address
+      const float2* p = reinterpret_cast<const float2*>(xs) + l;
+      const float2* p4 = p + 4 * G::LPF;
+      asm volatile(
+          "global_load_dwordx2 %0, %8, off\n\t"
+          "global_load_dwordx2 %1, %8, off offset:%10\n\t"
+          "global_load_dwordx2 %2, %8, off offset:%11\n\t"
+          "global_load_dwordx2 %3, %8, off offset:%12\n\t"
+          "global_load_dwordx2 %4, %9, off\n\t"
+          "global_load_dwordx2 %5, %9, off offset:%10\n\t"
+          "global_load_dwordx2 %6, %9, off offset:%11\n\t"
+          "global_load_dwordx2 %7, %9, off offset:%12"
+          : "=&v"(raw[0]), "=&v"(raw[1]), "=&v"(raw[2]), "=&v"(raw[3]), "=&v"(raw[4]), "=&v"(raw[5]),
+            "=&v"(raw[6]), "=&v"(raw[7])
+          : "v"(p), "v"(p4), "i"(S), "i"(2 * S), "i"(3 * S)
+          : "memory");
+    } else {
+      const float2* p = reinterpret_cast<const float2*>(xs) + l;
+      asm volatile(
+          "global_load_dwordx2 %0, %8, off\n\t"
+          "global_load_dwordx2 %1, %8, off offset:%9\n\t"
+          "global_load_dwordx2 %2, %8, off offset:%10\n\t"
+          "global_load_dwordx2 %3, %8, off offset:%11\n\t"
+          "global_load_dwordx2 %4, %8, off offset:%12\n\t"
+          "global_load_dwordx2 %5, %8, off offset:%13\n\t"
+          "global_load_dwordx2 %6, %8, off offset:%14\n\t"
+          "global_load_dwordx2 %7, %8, off offset:%15"
+          : "=&v"(raw[0]), "=&v"(raw[1]), "=&v"(raw[2]), "=&v"(raw[3]), "=&v"(raw[4]), "=&v"(raw[5]),
+            "=&v"(raw[6]), "=&v"(raw[7])
+          : "v"(p), "i"(S), "i"(2 * S), "i"(3 * S), "i"(4 * S), "i"(5 * S), "i"(6 * S), "i"(7 * S)
+          : "memory");
+    }
   } else if (active) {
     unsigned o[16];
 #pragma unroll
@@ -1064,33 +1082,127 @@ struct MelArgs {
   int log_kind;
 };
 
+// The filterbank's nonzero band staged in LDS once per block: mel m's weights
+// over its bins [kr_m.x, kr_m.y) at wl[m * wmax + (k - kr_m.x)], wmax = the
+// widest filter.  The per-frame mel sums then read LDS instead of one global
+// load per (bin, mel) — at n_fft 2048 the top filters span ~70 bins, and that
+// chain of L2 round trips was most of the log-mel kernels' time (the same
+// fmaf order and weights: bit-identical results).  Needs nm * wmax <= cap
+// floats (kMelCap, or the host's smaller grant); otherwise the block keeps
+// reading melmat from global (returns 0).
+constexpr int kMelCap = 6144;  // 24 KB: 80 filters x 76 bins (n_fft 2048) fit
+__device__ __forceinline__ int stage_mel(const float* __restrict__ melmat, const int2* __restrict__ krange, int nm,
+                                         int2* kr_l, float* wl, int cap) {
+  __shared__ int s_wmax;
+  const int tid = threadIdx.x;
+  if (tid == 0) s_wmax = 0;
+  __syncthreads();
+  int w = 0;
+  for (int m = tid; m < nm; m += blockDim.x) {
+    const int2 r = krange[m];
+    kr_l[m] = r;
+    w = max(w, r.y - r.x);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) w = max(w, __shfl_xor(w, o, 64));
+  if ((tid & 63) == 0) atomicMax(&s_wmax, w);
+  __syncthreads();
+  const int wmax = s_wmax;
+  if (wmax <= 0 || int64_t(nm) * wmax > cap) return 0;
+  const int total = nm * wmax;
+  for (int i0 = 0; i0 < total; i0 += 8 * int(blockDim.x)) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {  // eight loads in flight per lane
+      const int i = i0 + u * int(blockDim.x) + tid;
+      const int m = i / wmax, j = i - m * wmax;
+      const int2 r = i < total ? kr_l[m] : make_int2(0, 0);
+      v[u] = r.x + j < r.y ? melmat[int64_t(r.x + j) * nm + m] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + u * int(blockDim.x) + tid;
+      if (i < total) wl[i] = v[u];
+    }
+  }
+  __syncthreads();
+  return wmax;
+}
+
+// LDS bytes of the staged filterbank after the frame slots
+inline size_t mel_lds_bytes(int nm) { return (size_t(nm) * sizeof(int2) + 15) / 16 * 16 + size_t(kMelCap) * 4; }
+
 // log-mel forward (mel_loss.py:84-94): stft -> |X| (floor eps) -> melmat -> floor eps -> log.
+// Frame loop on the |X| kernel's memory schedule: the next frame's samples are
+// requested through inline asm (fetch_frame_vm, invisible to hipcc's counter
+// model) and waited for by hand with vmcnt(MS), MS = the fixed number of log-mel
+// stores each lane issues per frame after that request (one per mel slot m = l +
+// LPF*i, i < MS; slots past n_mels or of an inactive frame go to RU_OOB and are
+// dropped).  hipcc's own wait there was vmcnt(0): every frame also waited for
+// the previous frame's stores to reach memory.
 template <int LOGN>
 __global__ __launch_bounds__(256) SEL_FFT_OCC void k_logmel_fwd(const float* __restrict__ x, FrameArgs a,
                                                     const float* __restrict__ window, MelArgs ma,
                                                     float* __restrict__ out, int iters) {
   FRAME_PROLOGUE(LOGN, 0)
+  constexpr int MS = (G::M + 12 + G::LPF - 1) / G::LPF;  // mel slots per lane (n_mels <= n_fft/2 + 12)
   float* magb = reinterpret_cast<float*>(z);
-  FRAME_LOOP_BEGIN(x, raw, SEL_PF)
-  (void)fr;
-  float pwr[G::PPL], pmid;
-  fft_pairs<LOGN>(v, z, l, tw, pwr, pmid);
+  int2* kr_l = reinterpret_cast<int2*>(lds_dyn + G::FPB * G::PADN);
+  float* wl = reinterpret_cast<float*>(kr_l) + (ma.nm * 2 + 3) / 4 * 4;
+  const int wmax = stage_mel(ma.melmat, ma.range, ma.nm, kr_l, wl, kMelCap);
+  const __amdgpu_buffer_rsrc_t xr = signal_rsrc(x, a);
+  // the host keeps B * n_mels * F * 4 <= RU_OOB (ru_region_ok)
+  const __amdgpu_buffer_rsrc_t orr =
+      __builtin_amdgcn_make_buffer_rsrc(out, 0, int(a.B * ma.nm * a.F * 4), 0x00020000);
+  v2f_t raw[8];
+  FramePos P;
+  P.init(fr0, nframes, a.F);
+  fetch_frame_vm<LOGN>(x, xr, a, P.b, P.f, l, P.active, raw);
+  vm_wait_raw<0>(raw);
+  for (int it = 0; it < iters; ++it) {
+    float2 v[G::PPL];
 #pragma unroll
-  for (int q = 0; q < G::PPL / 2; ++q) {
-    magb[l + G::LPF * q] = clamp_sqrt(pwr[q], ma.eps);
-    magb[G::M - l - G::LPF * q] = clamp_sqrt(pwr[G::PPL / 2 + q], ma.eps);
-  }
-  if (l == 0) magb[G::M / 2] = clamp_sqrt(pmid, ma.eps);
-  frame_fence<LOGN>();
-  if (active) {
-    for (int m = l; m < ma.nm; m += G::LPF) {
-      const int2 r = ma.range[m];
-      const float s = mel_dot(magb, ma.melmat, ma.nm, m, r.x, r.y);
-      out[(b * ma.nm + m) * a.F + f] = log_k(fmaxf(s, ma.eps), ma.log_kind);
+    for (int q = 0; q < G::PPL; ++q) {
+      const float2 w = wn.get(q);
+      v[q] = make_float2(raw[q].x * w.x, raw[q].y * w.y);
     }
+    const FramePos cur = P;
+    const bool pf = it + 1 < iters;
+    if (pf) {
+      P.advance(G::FPB, nframes, a.F);
+      fetch_frame_vm<LOGN>(x, xr, a, P.b, P.f, l, P.active, raw);
+    }
+    float pwr[G::PPL], pmid;
+    fft_pairs<LOGN>(v, z, l, tw, pwr, pmid);
+#pragma unroll
+    for (int q = 0; q < G::PPL / 2; ++q) {
+      magb[l + G::LPF * q] = clamp_sqrt(pwr[q], ma.eps);
+      magb[G::M - l - G::LPF * q] = clamp_sqrt(pwr[G::PPL / 2 + q], ma.eps);
+    }
+    if (l == 0) magb[G::M / 2] = clamp_sqrt(pmid, ma.eps);
+    frame_fence<LOGN>();
+#pragma unroll
+    for (int i = 0; i < MS; ++i) {
+      const int m = l + G::LPF * i;
+      const bool ok = cur.active && m < ma.nm;
+      float val = 0.f;
+      if (ok) {
+        float s;
+        if (wmax) {
+          const int2 r = kr_l[m];
+          s = mel_dot(magb, wl + m * wmax - r.x, 1, 0, r.x, r.y);
+        } else {
+          const int2 r = ma.range[m];
+          s = mel_dot(magb, ma.melmat, ma.nm, m, r.x, r.y);
+        }
+        val = log_k(fmaxf(s, ma.eps), ma.log_kind);
+      }
+      const int off = ok ? int(((int64_t(cur.b) * ma.nm + m) * a.F + cur.f) * 4) : RU_OOB;
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, val), orr, off, 0, 0);
+    }
+    frame_fence<LOGN>();
+    if (pf) vm_wait_raw<MS>(raw);
   }
-  frame_fence<LOGN>();
-  FRAME_LOOP_END
 }
 
 // log-mel backward. gsel: if ref != nullptr, upstream = g_scale * sign(gout - ref)
@@ -1105,8 +1217,22 @@ __global__ __launch_bounds__(256) SEL_FFT_OCC void k_logmel_bwd(const float* __r
   FRAME_PROLOGUE(LOGN, glin_floats)
   float* magb = reinterpret_cast<float*>(z);
   float* glin = reinterpret_cast<float*>(z + G::PADN);
+  int2* kr_l = reinterpret_cast<int2*>(lds_dyn + G::FPB * (G::PADN + glin_floats / 2));
+  float* wl = reinterpret_cast<float*>(kr_l) + (ma.nm * 2 + 3) / 4 * 4;
+  const int wmax = stage_mel(ma.melmat, krange, ma.nm, kr_l, wl, kMelCap);
   const float gs = ref ? gscale[0] * gmul : 0.f;
   FRAME_LOOP_BEGIN(x, raw, false)
+  // upstream gradient of mel m of this frame
+  auto upstream = [&](int m) {
+    const int64_t o = (b * ma.nm + m) * a.F + f;
+    if (ref) {
+      const float d = gout[o] - ref[o];
+      return d > 0.f ? gs : (d < 0.f ? -gs : 0.f);
+    }
+    return gout[o];
+  };
+  // the first mel of this lane: loaded here, in flight across the transform
+  const float up0 = active && l < ma.nm ? upstream(l) : 0.f;
   fft_half<LOGN>(v, z, l, tw);
   float2 X[G::PPL + 1];
   real_split<LOGN>(z, l, tw, reinterpret_cast<float2(&)[G::PPL]>(X), X[G::PPL]);
@@ -1117,16 +1243,15 @@ __global__ __launch_bounds__(256) SEL_FFT_OCC void k_logmel_bwd(const float* __r
   for (int m = l; m < ma.nm; m += G::LPF) {
     float gv = 0.f;
     if (active) {
-      const int2 r = krange[m];
-      const float s = mel_dot(magb, ma.melmat, ma.nm, m, r.x, r.y);
-      const int64_t o = (b * ma.nm + m) * a.F + f;
-      float up;
-      if (ref) {
-        const float d = gout[o] - ref[o];
-        up = d > 0.f ? gs : (d < 0.f ? -gs : 0.f);
+      float s;
+      if (wmax) {
+        const int2 r = kr_l[m];
+        s = mel_dot(magb, wl + m * wmax - r.x, 1, 0, r.x, r.y);
       } else {
-        up = gout[o];
+        const int2 r = krange[m];
+        s = mel_dot(magb, ma.melmat, ma.nm, m, r.x, r.y);
       }
+      const float up = m == l ? up0 : upstream(m);
       const float mel = fmaxf(s, ma.eps);
       gv = (s >= ma.eps) ? up / (mel * dlog_k(ma.log_kind)) : 0.f;
     }
@@ -1138,7 +1263,15 @@ __global__ __launch_bounds__(256) SEL_FFT_OCC void k_logmel_bwd(const float* __r
     const int k = q < G::PPL ? l + G::LPF * q : G::M;
     const int2 r = ma.range[k];
     float gmag = 0.f;
-    for (int m = r.x; m < r.y; ++m) gmag = fmaf(ma.melmat[k * ma.nm + m], glin[m], gmag);
+    if (wmax) {
+      for (int m = r.x; m < r.y; ++m) {  // melmat[k][m] is 0 outside mel m's band
+        const int2 km = kr_l[m];
+        const float wv = k >= km.x && k < km.y ? wl[m * wmax + k - km.x] : 0.f;
+        gmag = fmaf(wv, glin[m], gmag);
+      }
+    } else {
+      for (int m = r.x; m < r.y; ++m) gmag = fmaf(ma.melmat[k * ma.nm + m], glin[m], gmag);
+    }
     const float p = pw(X[q]);
     const bool ok = active && p >= ma.eps && (q < G::PPL || l == 0);
     const float s = ok ? gmag * rsqrt_(p) : 0.f;
@@ -1148,6 +1281,111 @@ __global__ __launch_bounds__(256) SEL_FFT_OCC void k_logmel_bwd(const float* __r
   c2r_grad<LOGN>(reinterpret_cast<float2(&)[G::PPL]>(X), X[G::PPL], z, l, tw, v);
   store_frame_grad<LOGN>(v, a, wn, slab + (active ? fr : 0) * a.win, l, active);
   FRAME_LOOP_END
+}
+
+// Fused log-mel L1 (mel_loss.py:151-154): loss = mean |logmel(x) - logmel(y)|
+// and, with slab != nullptr, its gradient w.r.t. x for a unit upstream, in one
+// pass per frame position: y's FFT and log-mels (parked in the frame's
+// dL/dmel LDS slots), then x's FFT and log-mels, |d| into the loss partial, and
+// the adjoint of x's path (sign(d) / n through log, the mel projection, |X|
+// and the FFT) into the frame-gradient slab, as k_logmel_bwd does from stored
+// log-mels.  The separate path ran three frame transforms per position (x and y
+// forward, x again in the backward) and stored and re-read both log-mel
+// tensors; this one runs three in one launch (y, x, x's adjoint) with no
+// log-mel tensor in memory, and the backward is one scale by the upstream.
+template <int LOGN>
+__global__ __launch_bounds__(256) SEL_FFT_OCC void k_mel_l1(const float* __restrict__ x, const float* __restrict__ y,
+                                                FrameArgs a, const float* __restrict__ window, MelArgs ma,
+                                                const int2* __restrict__ krange, float inv_n,
+                                                double* __restrict__ partials, float* __restrict__ slab, int iters,
+                                                int glin_floats) {
+  FRAME_PROLOGUE(LOGN, glin_floats)
+  __shared__ double red[16];
+  float* magb = reinterpret_cast<float*>(z);
+  float* glin = reinterpret_cast<float*>(z + G::PADN);
+  int2* kr_l = reinterpret_cast<int2*>(lds_dyn + G::FPB * (G::PADN + glin_floats / 2));
+  float* wl = reinterpret_cast<float*>(kr_l) + (ma.nm * 2 + 3) / 4 * 4;
+  const int wmax = stage_mel(ma.melmat, krange, ma.nm, kr_l, wl, kMelCap);
+  const __amdgpu_buffer_rsrc_t y_rsrc = signal_rsrc(y, a);
+  const float dl = dlog_k(ma.log_kind);
+  auto mel_of = [&](int m) {  // sum_k melmat[k][m] |X_k| from magb
+    if (wmax) {
+      const int2 r = kr_l[m];
+      return mel_dot(magb, wl + m * wmax - r.x, 1, 0, r.x, r.y);
+    }
+    const int2 r = krange[m];
+    return mel_dot(magb, ma.melmat, ma.nm, m, r.x, r.y);
+  };
+  float lsum = 0.f;
+  FRAME_LOOP_BEGIN(x, raw, false)
+  (void)fr;
+  (void)f;
+  // y: log-mels of this lane's slots, parked in the frame's dL/dmel slots
+  // (glin[m]: read back and overwritten by the same lane in x's pass)
+  {
+    Y_FRAME(vy)
+    float pwr[G::PPL], pmid;
+    fft_pairs<LOGN, false>(vy, z, l, tw, pwr, pmid);
+#pragma unroll
+    for (int q = 0; q < G::PPL / 2; ++q) {
+      magb[l + G::LPF * q] = clamp_sqrt(pwr[q], ma.eps);
+      magb[G::M - l - G::LPF * q] = clamp_sqrt(pwr[G::PPL / 2 + q], ma.eps);
+    }
+    if (l == 0) magb[G::M / 2] = clamp_sqrt(pmid, ma.eps);
+    frame_fence<LOGN>();
+    for (int m = l; m < ma.nm; m += G::LPF) glin[m] = active ? log_k(fmaxf(mel_of(m), ma.eps), ma.log_kind) : 0.f;
+    frame_fence<LOGN>();  // magb reads done before x's transform overwrites the slots
+  }
+  // x: log-mels, |d|, and dL/dmel = sign(d) / n through the log
+  fft_half<LOGN>(v, z, l, tw);
+  float2 X[G::PPL + 1];
+  real_split<LOGN>(z, l, tw, reinterpret_cast<float2(&)[G::PPL]>(X), X[G::PPL]);
+#pragma unroll
+  for (int q = 0; q < G::PPL; ++q) magb[l + G::LPF * q] = clamp_sqrt(pw(X[q]), ma.eps);
+  if (l == 0) magb[G::M] = clamp_sqrt(pw(X[G::PPL]), ma.eps);
+  frame_fence<LOGN>();
+  for (int m = l; m < ma.nm; m += G::LPF) {
+    float gv = 0.f;
+    if (active) {
+      const float sm = mel_of(m);
+      const float mel = fmaxf(sm, ma.eps);
+      const float d = log_k(mel, ma.log_kind) - glin[m];
+      lsum += fabsf(d);
+      const float up = d > 0.f ? inv_n : (d < 0.f ? -inv_n : 0.f);
+      gv = (sm >= ma.eps) ? up / (mel * dl) : 0.f;
+    }
+    glin[m] = gv;
+  }
+  if (slab) {  // the gradient (launch-uniform)
+    frame_fence<LOGN>();
+#pragma unroll
+    for (int q = 0; q <= G::PPL; ++q) {
+      const int k = q < G::PPL ? l + G::LPF * q : G::M;
+      const int2 r = ma.range[k];
+      float gmag = 0.f;
+      if (wmax) {
+        for (int m = r.x; m < r.y; ++m) {  // melmat[k][m] is 0 outside mel m's band
+          const int2 km = kr_l[m];
+          const float wv = k >= km.x && k < km.y ? wl[m * wmax + k - km.x] : 0.f;
+          gmag = fmaf(wv, glin[m], gmag);
+        }
+      } else {
+        for (int m = r.x; m < r.y; ++m) gmag = fmaf(ma.melmat[k * ma.nm + m], glin[m], gmag);
+      }
+      const float p = pw(X[q]);
+      const bool ok = active && p >= ma.eps && (q < G::PPL || l == 0);
+      const float sc = ok ? gmag * rsqrt_(p) : 0.f;
+      X[q] = make_float2(sc * X[q].x, sc * X[q].y);
+    }
+    frame_fence<LOGN>();  // magb / glin reads done before c2r overwrites the slots
+    c2r_grad<LOGN>(reinterpret_cast<float2(&)[G::PPL]>(X), X[G::PPL], z, l, tw, v);
+    store_frame_grad<LOGN>(v, a, wn, slab + (active ? cur.fr : 0) * a.win, l, active);
+  } else {
+    frame_fence<LOGN>();  // glin / magb reads done before the next frame's transform
+  }
+  FRAME_LOOP_END
+  const double r = block_sum<double>(double(lsum), red);
+  if (threadIdx.x == 0) partials[blockIdx.x] = r;
 }
 
 // Overlap-add of frame-gradient slabs + adjoint of the reflect pad -> g_x (B,T).
@@ -1560,13 +1798,34 @@ int sel_logmel_fwd(const float* x, int64_t B, int64_t T, int n_fft, int hop, int
                    float eps, int log_kind, float* out, sel_stream_t stream) {
   int logn;
   if (int rc = check_frame(B, T, n_fft, hop, win_length, logn)) return rc;
-  SEL_REQUIRE(n_mels > 0, SEL_ERR_ARG, "n_mels must be > 0");
+  SEL_REQUIRE(n_mels > 0 && n_mels <= n_fft / 2 + 12, SEL_ERR_UNSUPPORTED,
+              "n_mels=%d must be in (0, n_fft/2 + 12]", n_mels);
   SEL_REQUIRE(log_kind >= SEL_LOG_E && log_kind <= SEL_LOG_10, SEL_ERR_ARG, "bad log kind");
   const FrameArgs a = frame_args(B, T, n_fft, hop, win_length);
+  SEL_REQUIRE(ru_region_ok(B * int64_t(n_mels) * a.F * 4), SEL_ERR_UNSUPPORTED,
+              "log-mel output of %lld bytes past the 32-bit store range", (long long)(B * int64_t(n_mels) * a.F * 4));
   MelArgs ma{melmat, reinterpret_cast<const int2*>(krange), n_mels, eps, log_kind};
   const int64_t nf = B * a.F;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  SEL_FRAME_DISPATCH(logn, nf, s, k_logmel_fwd, x, a, window, ma, out);
+  switch (logn) {
+#define SEL_LOGMEL_FWD_CASE(L)                                                                          \
+    case L: {                                                                                           \
+      using G = Geo<L>;                                                                                 \
+      int iters;                                                                                        \
+      const size_t lds = size_t(G::FPB) * G::PADN * sizeof(float2) + mel_lds_bytes(n_mels);             \
+      const unsigned grid = frame_grid<L>(nf, iters, frame_slots(k_logmel_fwd<L>, lds));               \
+      if (grid) hipLaunchKernelGGL(k_logmel_fwd<L>, dim3(grid), dim3(256), lds, s, x, a, window, ma, out, iters); \
+    } break;
+    SEL_LOGMEL_FWD_CASE(8)
+    SEL_LOGMEL_FWD_CASE(9)
+    SEL_LOGMEL_FWD_CASE(10)
+    SEL_LOGMEL_FWD_CASE(11)
+#undef SEL_LOGMEL_FWD_CASE
+    default:
+      ::sel::set_error("unsupported log2(n_fft)=%d", logn);
+      return SEL_ERR_UNSUPPORTED;
+  }
+  SEL_LAUNCH_CHECK();
   return SEL_OK;
 }
 
@@ -1588,6 +1847,64 @@ int sel_l1_mean(const float* a, const float* b, int64_t n, float* out, void* ws,
                      1.0 / double(n));
   SEL_LAUNCH_CHECK();
   return SEL_OK;
+}
+
+size_t sel_mel_l1_workspace(int64_t B, int64_t T, int n_fft, int hop, int win_length) {
+  int logn = 0;
+  while ((1 << logn) < n_fft) ++logn;
+  if (logn < kMinLog || logn > kFftMaxLog || B < 0 || T < 0 || hop <= 0 || win_length <= 0) return 0;
+  const size_t part = (size_t(n_blocks(logn, B * (1 + T / hop))) * sizeof(double) + 255) & ~size_t(255);
+  return part + slab_bytes(B, T, hop, win_length);
+}
+
+int sel_mel_l1_fwd_grad(const float* x, const float* y, int64_t B, int64_t T, int n_fft, int hop, int win_length,
+                        const float* window, const float* melmat, const int32_t* krange, const int32_t* mrange,
+                        int n_mels, float eps, int log_kind, float* loss, float* g_x, void* ws, size_t ws_bytes,
+                        sel_stream_t stream) {
+  int logn;
+  if (int rc = check_frame(B, T, n_fft, hop, win_length, logn)) return rc;
+  SEL_REQUIRE(B > 0 && x && y && loss, SEL_ERR_ARG, "mel L1 needs a non-empty batch, x, y and loss");
+  SEL_REQUIRE(n_mels > 0 && n_mels <= n_fft / 2 + 12, SEL_ERR_UNSUPPORTED,
+              "n_mels=%d must be in (0, n_fft/2 + 12]", n_mels);
+  SEL_REQUIRE(log_kind >= SEL_LOG_E && log_kind <= SEL_LOG_10, SEL_ERR_ARG, "bad log kind");
+  SEL_REQUIRE(ws_bytes >= sel_mel_l1_workspace(B, T, n_fft, hop, win_length), SEL_ERR_WORKSPACE,
+              "workspace too small");
+  const FrameArgs a = frame_args(B, T, n_fft, hop, win_length);
+  MelArgs ma{melmat, reinterpret_cast<const int2*>(mrange), n_mels, eps, log_kind};
+  const int64_t nf = B * a.F;
+  const double n = double(nf) * n_mels;  // elements of each log-mel tensor
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  double* part = static_cast<double*>(ws);
+  float* slab = g_x ? reinterpret_cast<float*>(static_cast<char*>(ws) +
+                                               ((size_t(n_blocks(logn, nf)) * sizeof(double) + 255) & ~size_t(255)))
+                    : nullptr;
+  const int glin = (n_mels + 3) / 4 * 4;
+  unsigned grid = 0;
+  switch (logn) {
+#define SEL_MEL_L1_CASE(L)                                                                              \
+    case L: {                                                                                           \
+      using G = Geo<L>;                                                                                 \
+      int iters;                                                                                        \
+      const size_t lds = size_t(G::FPB) * (G::PADN * sizeof(float2) + size_t(glin) * sizeof(float)) +   \
+                         mel_lds_bytes(n_mels);                                                         \
+      grid = frame_grid<L>(nf, iters, frame_slots(k_mel_l1<L>, lds));                                   \
+      if (grid)                                                                                         \
+        hipLaunchKernelGGL(k_mel_l1<L>, dim3(grid), dim3(256), lds, s, x, y, a, window, ma,             \
+                           reinterpret_cast<const int2*>(krange), float(1.0 / n), part, slab, iters, glin); \
+    } break;
+    SEL_MEL_L1_CASE(8)
+    SEL_MEL_L1_CASE(9)
+    SEL_MEL_L1_CASE(10)
+    SEL_MEL_L1_CASE(11)
+#undef SEL_MEL_L1_CASE
+    default:
+      ::sel::set_error("unsupported log2(n_fft)=%d", logn);
+      return SEL_ERR_UNSUPPORTED;
+  }
+  SEL_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_finish_partials, dim3(1), dim3(256), 0, s, part, int(grid), 1, nullptr, loss, 1.0 / n);
+  SEL_LAUNCH_CHECK();
+  return g_x ? ola(slab, a, g_x, s) : SEL_OK;
 }
 
 size_t sel_logmel_bwd_workspace(int64_t B, int64_t T, int n_fft, int hop, int win_length) {
@@ -1619,7 +1936,8 @@ int sel_logmel_bwd(const float* x, int64_t B, int64_t T, int n_fft, int hop, int
     case L: {                                                                                           \
       using G = Geo<L>;                                                                                 \
       int iters;                                                                                        \
-      const size_t lds = size_t(G::FPB) * (G::PADN * sizeof(float2) + size_t(glin) * sizeof(float));    \
+      const size_t lds = size_t(G::FPB) * (G::PADN * sizeof(float2) + size_t(glin) * sizeof(float)) +   \
+                         mel_lds_bytes(n_mels);                                                         \
       const unsigned grid = frame_grid<L>(nf, iters, frame_slots(k_logmel_bwd<L>, lds));               \
       if (grid)                                                                                         \
         hipLaunchKernelGGL(k_logmel_bwd<L>, dim3(grid), dim3(256), lds, s, x, a, window, ma,           \

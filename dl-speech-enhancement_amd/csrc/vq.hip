@@ -6,8 +6,8 @@
 // picks the code, and the row update (straight-through value r + (q - r), next
 // residual, running sum) is done in LDS.  Cross-row quantities (commitment SSE,
 // code histogram for the perplexity) go to deterministic per-block partials and
-// integer atomics.  Three kernels with one arithmetic (bit-identical results,
-// tune key 2): k_rvq_mfma (default, f32-input matrix cores), k_rvq_fwd2
+// integer atomics.  Three kernel families with one arithmetic (bit-identical
+// results, tune key 2): k_rvq_mfma (default, f32-input matrix cores), k_rvq_fwd2
 // (codebook staged through LDS, fp32 VALU) and k_rvq_fwd (direct, any D).
 #include <algorithm>
 
@@ -367,8 +367,9 @@ constexpr int DM = 64;
 using f32x4 = __attribute__((ext_vector_type(4))) float;
 
 struct MfmaGeo {
-  int ntile, nj4;  // 16-code tiles; groups of four k-steps (4 dims each)
-  __host__ __device__ MfmaGeo(int D, int K) : ntile((K + 15) / 16), nj4((D / 4 + 3) / 4) {}
+  int ntile, nj4;  // 16-code tiles; groups of four k-steps (4 dims each), always DM / 16:
+                   // fragments past D are zeros, so the tile loads have no runtime bound
+  __host__ __device__ MfmaGeo(int D, int K) : ntile((K + 15) / 16), nj4(DM / 16) { (void)D; }
   __host__ __device__ int64_t tile_floats() const { return int64_t(nj4) * 256; }
   __host__ __device__ int64_t stage_floats() const { return int64_t(ntile) * tile_floats(); }
 };
@@ -408,12 +409,28 @@ __global__ __launch_bounds__(256) void k_rvq_prep(const float* __restrict__ embe
 
 constexpr int SM = 16;  // max stages of the matrix-core variant (per-stage state in LDS)
 
+// timing ablations of the matrix-core kernel (diagnostic builds only, wrong
+// results): 1 no tile loop, 4 no codebook gather in the row update, 8 no |e|^2
+// staging; 0 in every product build
+#ifndef SEL_RVQ_ABL
+#define SEL_RVQ_ABL 0
+#endif
+
 // RG row groups of 16 rows per block share every codebook tile: each wave's
 // B operands (4 KB per 16-code tile, read from L2) feed RG independent MFMA
 // chains.  RG = 2 halves the codebook reads per row (the hypothesis: the L2 ->
 // CU rate binds at C3, 320 blocks x 8 stages x 256 KB) at the same busiest-CU
 // MFMA work, but measured slower (160 blocks, one per CU, at 2 waves per SIMD:
 // 169 -> 193 us per forward), so RG = 1 is the default (tune key 39 = 2: RG = 2).
+// Tile-loop schedule: the next tile's B operands are requested one tile ahead
+// with branch-free addresses (past the last tile of a stage: the next stage's
+// first tile; past the last stage: this tile again), |e|^2 of the stage is read
+// from LDS (staged at the stage start), and operands past D are zeros (resT is
+// zero-padded to DM dims, k_rvq_prep zero-pads the B fragments), so the loads
+// and the MFMA chain have no runtime bound: a zero product on a zero-based accumulator
+// (never -0) adds exactly nothing, so results equal the chain over d < D.  The
+// earlier form waited for vmcnt(0) in every tile's epilogue (a global |e|^2
+// load issued after the prefetch): each tile exposed the prefetch's L2 latency.
 template <int RG>
 __global__ __launch_bounds__(TM) __attribute__((amdgpu_waves_per_eu(RG == 1 ? 4 : 2))) void k_rvq_mfma(
     const float* __restrict__ x, int64_t N, int D, const float* __restrict__ embeds, int S, int K,
@@ -428,17 +445,17 @@ __global__ __launch_bounds__(TM) __attribute__((amdgpu_waves_per_eu(RG == 1 ? 4 
   __shared__ int sel_k[SM][RB];    // chosen codes, written to idx after the last stage
   __shared__ float sq_t[SM][TM];   // per-thread SSE per stage, reduced after the last stage
   __shared__ double red[16];
+  extern __shared__ float en_l[];  // |e|^2 of the current stage (K floats, dynamic)
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int col = lane & 15, h = lane >> 4;
   const int64_t r0 = int64_t(blockIdx.x) * RB;
-  for (int i = tid; i < RB * D; i += TM) {
-    const int r = i / D, d = i % D;
+  for (int i = tid; i < RB * DM; i += TM) {
+    const int r = i / DM, d = i % DM;
     const int64_t row = r0 + r;
-    resT[d * RB + r] = row < N ? x[row * D + d] : 0.f;
-    acc_o[r * D + d] = 0.f;
+    resT[d * RB + r] = row < N && d < D ? x[row * D + d] : 0.f;
+    if (d < D) acc_o[r * D + d] = 0.f;
   }
-  const int ns = D / 4;
   const MfmaGeo g(D, K);
   const int ntile = g.ntile, nj4 = g.nj4;
   const int rot = int((blockIdx.x * 4u) % unsigned(ntile));  // L2 de-synchronisation across blocks
@@ -449,12 +466,15 @@ __global__ __launch_bounds__(TM) __attribute__((amdgpu_waves_per_eu(RG == 1 ? 4 
     const int t = p + rot;
     return t >= ntile ? t - ntile : t;
   };
+  // wave w scores tiles w, w + 8, ... in a block-rotated order with the next
+  // tile's operands in flight (one tile keeps the kernel at 4 waves/SIMD); the
+  // last tile of a stage prefetches the next stage's first one
   float4 cur[DM / 16], nxt[DM / 16];
   auto load = [&](int st, int p, float4 (&b)[DM / 16]) {
     const float4* src = reinterpret_cast<const float4*>(ep_all + int64_t(st) * g.stage_floats()) +
                         int64_t(tile_of(p)) * (nj4 * 64) + lane;
 #pragma unroll
-    for (int j4 = 0; j4 < DM / 16; ++j4) b[j4] = j4 < nj4 ? src[j4 * 64] : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int j4 = 0; j4 < DM / 16; ++j4) b[j4] = src[j4 * 64];
   };
   if (wave < ntile) load(0, wave, cur);
   __syncthreads();
@@ -462,18 +482,20 @@ __global__ __launch_bounds__(TM) __attribute__((amdgpu_waves_per_eu(RG == 1 ? 4 
   for (int s = 0; s < S; ++s) {
     const float* __restrict__ E = embeds + int64_t(s) * D * K;
     const float* __restrict__ enS = en_all + int64_t(s) * K;
+    if constexpr (!(SEL_RVQ_ABL & 8))
+      for (int k = tid; k < K; k += TM) en_l[k] = enS[k];
     for (int r = wave; r < RB; r += NWM) {
       float v = 0.f;
       for (int d = lane; d < D; d += 64) v = fmaf(resT[d * RB + r], resT[d * RB + r], v);
       v = wave_sum(v);
       if (lane == 0) xn[r] = v;
     }
+    __syncthreads();
     float a[RG][DM / 4];
 #pragma unroll
     for (int q = 0; q < RG; ++q)
 #pragma unroll
-      for (int j = 0; j < DM / 4; ++j) a[q][j] = j < ns ? resT[(4 * j + h) * RB + RM * q + col] : 0.f;
-    __syncthreads();
+      for (int j = 0; j < DM / 4; ++j) a[q][j] = resT[(4 * j + h) * RB + RM * q + col];
     float xr[RG][4];
 #pragma unroll
     for (int q = 0; q < RG; ++q)
@@ -488,26 +510,26 @@ __global__ __launch_bounds__(TM) __attribute__((amdgpu_waves_per_eu(RG == 1 ? 4 
         bd[q][i] = __builtin_inff();
         bk[q][i] = 0x7fffffff;
       }
-    for (int p = wave; p < ntile; p += NWM) {
-      if (p + NWM < ntile)
-        load(s, p + NWM, nxt);
-      else if (s + 1 < S)
-        load(s + 1, wave, nxt);
+    // one tile: request the next one into `fill`, score this one from `use`
+    // (the loop alternates the two buffers: a register copy between them
+    // would make every tile wait for its own prefetch)
+    auto tile = [&](int p, const float4 (&use)[DM / 16], float4 (&fill)[DM / 16]) {
+      const bool more = p + NWM < ntile;
+      load(more || s + 1 >= S ? s : s + 1, more ? p + NWM : (s + 1 < S ? wave : p), fill);
+      __builtin_amdgcn_sched_barrier(0);  // the requests go out before this tile's MFMAs
       f32x4 c[RG];
 #pragma unroll
       for (int q = 0; q < RG; ++q) c[q] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int j = 0; j < DM / 4; ++j) {
-        if (j < ns) {
-          const float4 bv = cur[j >> 2];
-          const float bj = (j & 3) == 0 ? bv.x : (j & 3) == 1 ? bv.y : (j & 3) == 2 ? bv.z : bv.w;
+        const float4 bv = use[j >> 2];
+        const float bj = (j & 3) == 0 ? bv.x : (j & 3) == 1 ? bv.y : (j & 3) == 2 ? bv.z : bv.w;
 #pragma unroll
-          for (int q = 0; q < RG; ++q) c[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[q][j], bj, c[q], 0, 0, 0);
-        }
+        for (int q = 0; q < RG; ++q) c[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[q][j], bj, c[q], 0, 0, 0);
       }
       const int k = tile_of(p) * 16 + col;
       const bool kin = k < K;
-      const float ek = kin ? enS[k] : 0.f;
+      const float ek = en_l[kin ? k : 0];
 #pragma unroll
       for (int q = 0; q < RG; ++q)
 #pragma unroll
@@ -517,9 +539,22 @@ __global__ __launch_bounds__(TM) __attribute__((amdgpu_waves_per_eu(RG == 1 ? 4 
           bd[q][i] = take ? dist : bd[q][i];
           bk[q][i] = take ? k : bk[q][i];
         }
-#pragma unroll
-      for (int j4 = 0; j4 < DM / 16; ++j4) cur[j4] = nxt[j4];
-    }
+    };
+    // the buffer holding this stage's first tile alternates with the parity of
+    // the tiles scored so far (no register copies)
+    const int tpw = wave < ntile ? (ntile - wave + NWM - 1) / NWM : 0;
+    auto stage_tiles = [&](float4 (&X)[DM / 16], float4 (&Y)[DM / 16]) {
+      int p = (SEL_RVQ_ABL & 1) ? ntile : wave;
+      for (; p + NWM < ntile; p += 2 * NWM) {
+        tile(p, X, Y);
+        tile(p + NWM, Y, X);
+      }
+      if (p < ntile) tile(p, X, Y);
+    };
+    if (((s * tpw) & 1) == 0)
+      stage_tiles(cur, nxt);
+    else
+      stage_tiles(nxt, cur);
 #pragma unroll
     for (int q = 0; q < RG; ++q)
 #pragma unroll
@@ -549,6 +584,7 @@ __global__ __launch_bounds__(TM) __attribute__((amdgpu_waves_per_eu(RG == 1 ? 4 
           d0 = red_d[w][tid];
           k0 = red_k[w][tid];
         }
+      if constexpr (SEL_RVQ_ABL != 0) k0 = min(max(k0, 0), K - 1);  // ablations leave rows unscored
       sel_k[s][tid] = k0;
     }
     __syncthreads();
@@ -556,8 +592,8 @@ __global__ __launch_bounds__(TM) __attribute__((amdgpu_waves_per_eu(RG == 1 ? 4 
     for (int i = tid; i < RB * D; i += TM) {
       const int r = i / D, d = i % D;
       if (r0 + r >= N) continue;
-      const float q = E[int64_t(d) * K + sel_k[s][r]];
       const float rv = resT[d * RB + r];
+      const float q = (SEL_RVQ_ABL & 4) ? rv : E[int64_t(d) * K + sel_k[s][r]];
       const float diff = q - rv;
       sq = fmaf(diff, diff, sq);
       const float qst = rv + diff;
@@ -683,7 +719,8 @@ int sel_rvq_fwd(const float* x, int64_t N, int D, const float* embeds, int S, in
   // matrix-core rows per block: one 16-row group (tune key 39 = 2: two groups
   // sharing each codebook tile, measured slower at C3: 169 -> 193 us per RVQ
   // forward with its prep / histogram / finish, alternating in one call)
-  const int rows = mfma ? ((N + 2 * RM - 1) / (2 * RM) >= 128 && tune(39) == 2 ? 2 * RM : RM) : staged ? R2 : ROWS;
+  const int mrows = tune(39) == 2 && (N + 2 * RM - 1) / (2 * RM) >= 128 ? 2 * RM : RM;
+  const int rows = mfma ? mrows : staged ? R2 : ROWS;
   const int nb = int((N + rows - 1) / rows);
   double* part = static_cast<double*>(ws);
   if (nb > 0 && mfma) {
@@ -692,10 +729,14 @@ int sel_rvq_fwd(const float* x, int64_t N, int D, const float* embeds, int S, in
     const int64_t nprep = std::max<int64_t>(int64_t(S) * MfmaGeo(D, K).stage_floats() / 4, int64_t(S) * K);
     hipLaunchKernelGGL(k_rvq_prep, dim3(unsigned((nprep + 255) / 256)), dim3(256), 0, s, embeds, S, D, K, ep, en);
     SEL_LAUNCH_CHECK();
-    if (rows == 2 * RM)
-      hipLaunchKernelGGL(k_rvq_mfma<2>, dim3(nb), dim3(TM), 0, s, x, N, D, embeds, S, K, ep, en, out, idx, part);
-    else
-      hipLaunchKernelGGL(k_rvq_mfma<1>, dim3(nb), dim3(TM), 0, s, x, N, D, embeds, S, K, ep, en, out, idx, part);
+    const size_t lds = size_t(K) * sizeof(float);  // |e|^2 of one stage
+    if (rows == 2 * RM) {
+      SEL_HIP(hipFuncSetAttribute((const void*)k_rvq_mfma<2>, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
+      hipLaunchKernelGGL(k_rvq_mfma<2>, dim3(nb), dim3(TM), lds, s, x, N, D, embeds, S, K, ep, en, out, idx, part);
+    } else {
+      SEL_HIP(hipFuncSetAttribute((const void*)k_rvq_mfma<1>, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
+      hipLaunchKernelGGL(k_rvq_mfma<1>, dim3(nb), dim3(TM), lds, s, x, N, D, embeds, S, K, ep, en, out, idx, part);
+    }
     SEL_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_rvq_hist, dim3(unsigned((N + kHistRows - 1) / kHistRows), unsigned(S)), dim3(512), 0, s,
                        idx, N, K, counts);

@@ -41,6 +41,8 @@ SIGNATURES = {
     "sel_logmel_fwd": (I32, [P, I64, I64, I32, I32, I32, P, P, P, I32, F32, I32, P, P]),
     "sel_l1_workspace": (SZ, [I64]),
     "sel_l1_mean": (I32, [P, P, I64, P, P, SZ, P]),
+    "sel_mel_l1_workspace": (SZ, [I64, I64, I32, I32, I32]),
+    "sel_mel_l1_fwd_grad": (I32, [P, P, I64, I64, I32, I32, I32, P, P, P, P, I32, F32, I32, P, P, P, SZ, P]),
     "sel_logmel_bwd_workspace": (SZ, [I64, I64, I32, I32, I32]),
     "sel_logmel_bwd": (I32, [P, I64, I64, I32, I32, I32, P, P, P, P, I32, F32, I32,
                              P, P, P, F32, P, P, SZ, P]),

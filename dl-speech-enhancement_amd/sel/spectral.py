@@ -197,10 +197,17 @@ class LogMel(torch.autograd.Function):
 
 # SEL_MEL_PAIR=0: the two log-mel forwards of the L1 loss as two launches
 MEL_PAIR_ONE_LAUNCH = os.environ.get("SEL_MEL_PAIR", "1") != "0"
+# SEL_MEL_FUSED=0: the loss as log-mel forwards + L1 + a log-mel backward
+# instead of the fused forward-with-gradient launch (sel_mel_l1_fwd_grad)
+MEL_FUSED = os.environ.get("SEL_MEL_FUSED", "1") != "0"
 
 
 class MelL1(torch.autograd.Function):
-    """mean |logmel(x) - logmel(y)| with grad w.r.t. x (mel_loss.py:151-154)."""
+    """mean |logmel(x) - logmel(y)| with grad w.r.t. x (mel_loss.py:151-154).
+
+    When x needs a gradient the forward is the fused launch: it returns the
+    loss and keeps d loss / d x for a unit upstream (one (B, T) fp32 tensor),
+    and the backward scales it by the upstream gradient."""
 
     @staticmethod
     def forward(ctx, x, y, n_fft, hop, win_length, window, melmat, krange, mrange, eps, log_kind):
@@ -210,6 +217,16 @@ class MelL1(torch.autograd.Function):
         M = melmat.shape[1]
         F = _frames(T, hop)
         s = L.stream()
+        ctx.fused = MEL_FUSED and ctx.needs_input_grad[0]
+        if ctx.fused:
+            loss = torch.empty((), device=x.device, dtype=torch.float32)
+            gx1 = torch.empty_like(x)
+            ws = L.workspace(lib.sel_mel_l1_workspace(B, T, n_fft, hop, win_length), x.device)
+            L.call("sel_mel_l1_fwd_grad", L.ptr(x), L.ptr(y), B, T, n_fft, hop, win_length, L.ptr(window),
+                   L.ptr(melmat), L.ptr(krange), L.ptr(mrange), M, float(eps), log_kind, L.ptr(loss), L.ptr(gx1),
+                   L.ptr(ws), ws.numel(), s)
+            ctx.save_for_backward(gx1)
+            return loss
         if MEL_PAIR_ONE_LAUNCH:
             # both signals' log-mels in ONE launch over the (2B, T) pair: one frame
             # grid of twice the frames instead of two launches with their tails
@@ -235,6 +252,9 @@ class MelL1(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
+        if ctx.fused:
+            (gx1,) = ctx.saved_tensors
+            return gx1 * g, None, None, None, None, None, None, None, None, None, None
         x, window, melmat, krange, mrange, a, b = ctx.saved_tensors
         n_fft, hop, win, eps, log_kind = ctx.cfg
         lib = L.lib()

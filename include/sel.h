@@ -105,7 +105,8 @@ int sel_stft_loss_coef(const double* sums, int64_t n, const float* g_sc, const f
 /* ---- log-mel: losses/mel_loss.py:74-94 (MelSpectrogram.forward) -------
  * x (B,T) -> out (B, n_mels, F).  melmat (K, n_mels) is the module buffer;
  * krange (n_mels int2) = nonzero bin range [lo,hi) of each filter, mrange (K int2)
- * = filters touching each bin, both derived from melmat by the host. */
+ * = filters touching each bin, both derived from melmat by the host.
+ * 0 < n_mels <= n_fft/2 + 12 (SEL_ERR_UNSUPPORTED otherwise, as the backward). */
 int sel_logmel_fwd(const float* x, int64_t B, int64_t T, int n_fft, int hop,
                    int win_length, const float* window, const float* melmat,
                    const int32_t* krange, int n_mels, float eps, int log_kind,
@@ -127,6 +128,17 @@ int sel_l1_mean(const float* a, const float* b, int64_t n, float* out, void* ws,
  * With ref != NULL: g_out is logmel(x) from the forward and the upstream of each
  * element is (*g_scale) * g_mul * sign(g_out - ref)  (g_mul = 1/N for a mean).
  * Overwrites g_x. */
+/* Fused log-mel L1 (mel_loss.py:151-154): *loss = mean |logmel(x) - logmel(y)|
+ * over (B, n_mels, F), and, when g_x != NULL, g_x = d loss / d x for a unit
+ * upstream (the backward scales it by the upstream gradient): one launch per
+ * resolution computes y's and x's log-mels per frame position and x's adjoint
+ * (k_mel_l1), then the overlap-add.  mrange / krange as for sel_logmel_bwd.
+ * 0 < n_mels <= n_fft/2 + 12.  ws >= sel_mel_l1_workspace(...). */
+size_t sel_mel_l1_workspace(int64_t B, int64_t T, int n_fft, int hop, int win_length);
+int sel_mel_l1_fwd_grad(const float* x, const float* y, int64_t B, int64_t T, int n_fft, int hop,
+                        int win_length, const float* window, const float* melmat, const int32_t* krange,
+                        const int32_t* mrange, int n_mels, float eps, int log_kind, float* loss, float* g_x,
+                        void* ws, size_t ws_bytes, sel_stream_t stream);
 size_t sel_logmel_bwd_workspace(int64_t B, int64_t T, int n_fft, int hop, int win_length);
 int sel_logmel_bwd(const float* x, int64_t B, int64_t T, int n_fft, int hop,
                    int win_length, const float* window, const float* melmat,

@@ -65,7 +65,8 @@ for args in ((None, 1, 100, 1000, 10, 100), (None, 0, 0, 0, 0, 0), (None, -1, -5
              (None, 2, 24000, 3000, 120, 600)):
     assert call(stft, *args, None, 1e-7, None, None) < 0
     assert call(last)
-for name in ("sel_stft_bwd_workspace", "sel_stft_loss_workspace", "sel_logmel_bwd_workspace"):
+for name in ("sel_stft_bwd_workspace", "sel_stft_loss_workspace", "sel_logmel_bwd_workspace",
+             "sel_mel_l1_workspace"):
     f = fn(name, SZ, I64, I64, I32, I32, I32)
     for B, T, n, h, w in ((1, 24000, 1024, 120, 600), (64, 24000, 2048, 300, 2048), (0, 0, 512, 50, 240),
                           (-3, 100, 0, 0, 0), (2, 7, 4096, 1, 4096)):
@@ -74,6 +75,11 @@ for name in ("sel_mag_pair_workspace", "sel_l1_workspace", "sel_add_noise_worksp
     f = fn(name, SZ, I64)
     for n in (0, 1, 7, 1 << 20, -5):
         call(f, n)
+mell1 = fn("sel_mel_l1_fwd_grad", I32, P, P, I64, I64, I32, I32, I32, P, P, P, P, I32, F32, I32, P, P, P, SZ, P)
+for args in ((1, 24000, 2048, 300, 2048, 80), (0, 24000, 2048, 300, 2048, 80), (2, 9000, 1024, 256, 1024, 0),
+             (2, 9000, 1024, 256, 1024, 600), (2, 100, 1000, 10, 100, 80), (-1, 5, 256, 0, 0, 10)):
+    B, T, n, h, w, nm = args
+    assert call(mell1, None, None, B, T, n, h, w, None, None, None, None, nm, 1e-10, 0, None, None, None, 0, None) < 0
 fin = fn("sel_stft_loss_finish", I32, P, I64, P, P)
 assert call(fin, None, -1, None, None) < 0 and call(fin, None, 0, None, None) < 0
 

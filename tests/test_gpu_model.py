@@ -228,11 +228,12 @@ def test_full_width_generator_bf16_vs_oracle(gpu):
 
 @pytest.mark.parametrize("N,D,K,S", [(5120, 64, 1024, 8), (333, 64, 1000, 3), (40, 16, 64, 2), (77, 12, 40, 3)])
 def test_rvq_kernels_bit_identical(gpu, N, D, K, S):
-    """The matrix-core RVQ kernel (default, tune key 2 = 0), the direct one (= 1)
-    and the staged-codebook one (= 2) evaluate every distance with the same fp32
-    operation order (the f32-input MFMA is a k-ordered fmaf chain), so indices
-    and outputs must be bit-identical (the fp64 SSE partials are grouped by block
-    size, 16 vs 20 rows: losses agree to 1e-6)."""
+    """The matrix-core RVQ kernel (default, tune key 2 = 0; key 39 = 2: two 16-row
+    groups per block), the direct one (key 2 = 1) and the staged-codebook one
+    (= 2) evaluate every distance with the same fp32 operation order (the
+    f32-input MFMA is a k-ordered fmaf chain), so indices and outputs must be
+    bit-identical (the fp64 SSE partials are grouped by block size, 16 vs 20
+    rows: losses agree to 1e-6)."""
     from sel import _lib as L
     from sel.vqops import ResidualVQFn
     torch.manual_seed(N + K)

@@ -267,6 +267,40 @@ def test_mel_loss_large_batch_vs_oracle(gpu):
     cond_close(yd.grad, yr.grad, _mel_grad64(yh, y, [(2048, 300, 2048)], [mt.melmat.cpu()], None))
 
 
+@pytest.mark.parametrize("res,log_base", [((2048, 300, 2048), None), ((1024, 256, 1024), 10.0),
+                                          ((512, 128, 400), 2.0), ((256, 64, 256), None)])
+def test_mel_l1_fused_matches_separate_path(gpu, res, log_base):
+    """The fused log-mel L1 (sel_mel_l1_fwd_grad: one launch computes both
+    log-mels per frame and x's adjoint for a unit upstream, the backward scales
+    it) against the separate path (log-mel forwards + L1 + log-mel backward):
+    same per-element arithmetic, different summation order of the loss and one
+    more rounding of the gradient (unit gradient x upstream)."""
+    from losses import MultiMelSpectrogramLoss
+    from sel import spectral as SP
+    n, h, w = res
+    ml = MultiMelSpectrogramLoss(fs=24000, fft_sizes=[n], hop_sizes=[h], win_lengths=[w], window="hann_window",
+                                 num_mels=80, fmin=0, fmax=12000, log_base=log_base).to(gpu)
+    g = torch.Generator().manual_seed(n + h)
+    yh = (0.1 * torch.randn(5, 1, 9000, generator=g)).to(gpu)
+    y = (0.1 * torch.randn(5, 1, 9000, generator=g)).to(gpu)
+    out = {}
+    for fused in (True, False):
+        prev = SP.MEL_FUSED
+        SP.MEL_FUSED = fused
+        try:
+            x = yh.clone().requires_grad_(True)
+            loss = ml(x, y)
+            (3.0 * loss).backward()
+            out[fused] = (loss.detach(), x.grad)
+        finally:
+            SP.MEL_FUSED = prev
+    torch.testing.assert_close(out[True][0], out[False][0], rtol=2e-6, atol=0)
+    ga, gb = out[True][1], out[False][1]
+    assert float((ga - gb).norm() / gb.norm()) < 1e-5
+    with torch.no_grad():  # no gradient wanted: the log-mel forwards + L1
+        torch.testing.assert_close(ml(yh, y), out[False][0], rtol=0, atol=0)
+
+
 def test_stft_loss_full_size_properties(gpu):
     """At B=512 (beyond the 256 MB Infinity Cache for the magnitudes): the fused
     loss equals the modular (magnitudes materialised) path, and the backward is

@@ -18,8 +18,12 @@ def main():
     x = torch.randn(N, D, device=dev)
     emb = torch.randn(S, D, K, device=dev)
     lib = L.lib()
-    for v in (int(v) for v in os.environ.get("RVQ_VARIANTS", "0,2,1").split(",")):  # 0 matrix-core, 2 staged, 1 direct
+    # "v" or "v:g": tune key 2 = v (0 matrix-core, 2 staged, 1 direct), key 39 = g
+    # (matrix-core rows per block: 0 = 16, 2 = 2 x 16)
+    for vg in os.environ.get("RVQ_VARIANTS", "0,0:2,2,1").split(","):
+        v, g = (int(t) for t in (vg.split(":") + ["0"])[:2])
         lib.sel_tune(2, v)
+        lib.sel_tune(39, g)
         for _ in range(3):
             ResidualVQFn.apply(x, emb, 1.0)
         torch.cuda.synchronize()
@@ -29,8 +33,10 @@ def main():
             ResidualVQFn.apply(x, emb, 1.0)
         e1.record()
         torch.cuda.synchronize()
-        print(f"{(N, D, K, S)} variant {v}: {e0.elapsed_time(e1) / 20 * 1e3:.1f} us per RVQ forward (+finish)", flush=True)
+        print(f"{(N, D, K, S)} variant {vg}: {e0.elapsed_time(e1) / 20 * 1e3:.1f} us per RVQ forward (+finish)",
+              flush=True)
     lib.sel_tune(2, 0)
+    lib.sel_tune(39, 0)
 
 
 if __name__ == "__main__":
