@@ -1305,7 +1305,12 @@ __global__ __launch_bounds__(256) SEL_FFT_OCC void k_mel_l1(const float* __restr
   float* glin = reinterpret_cast<float*>(z + G::PADN);
   int2* kr_l = reinterpret_cast<int2*>(lds_dyn + G::FPB * (G::PADN + glin_floats / 2));
   float* wl = reinterpret_cast<float*>(kr_l) + (ma.nm * 2 + 3) / 4 * 4;
-  const int wmax = stage_mel(ma.melmat, krange, ma.nm, kr_l, wl, kMelCap);
+  // per-bin mel ranges (mrange) after the filterbank: the adjoint's per-bin
+  // loop reads them from LDS, not one global load per bin and frame
+  int2* mr_l = reinterpret_cast<int2*>(wl + kMelCap);
+  for (int k = threadIdx.x; k <= G::M; k += blockDim.x) mr_l[k] = ma.range[k];
+  const int wmax = stage_mel(ma.melmat, krange, ma.nm, kr_l, wl, kMelCap);  // (its barriers cover mr_l)
+  const __amdgpu_buffer_rsrc_t x_rsrc = signal_rsrc(x, a);
   const __amdgpu_buffer_rsrc_t y_rsrc = signal_rsrc(y, a);
   const float dl = dlog_k(ma.log_kind);
   auto mel_of = [&](int m) {  // sum_k melmat[k][m] |X_k| from magb
@@ -1317,13 +1322,22 @@ __global__ __launch_bounds__(256) SEL_FFT_OCC void k_mel_l1(const float* __restr
     return mel_dot(magb, ma.melmat, ma.nm, m, r.x, r.y);
   };
   float lsum = 0.f;
-  FRAME_LOOP_BEGIN(x, raw, false)
-  (void)fr;
-  (void)f;
+  FramePos P;
+  P.init(fr0, nframes, a.F);
+  for (int it = 0; it < iters; ++it) {
+  const FramePos cur = P;
+  if (it + 1 < iters) P.advance(G::FPB, nframes, a.F);
+  const bool active = cur.active;
+  // both frames requested together (one exposed latency per position)
+  float2 raw[G::PPL], rawy[G::PPL];
+  fetch_frame<LOGN>(x, x_rsrc, a, cur.b, cur.f, l, cur.active, raw);
+  fetch_frame<LOGN>(y, y_rsrc, a, cur.b, cur.f, l, cur.active, rawy);
+  float2 v[G::PPL];
   // y: log-mels of this lane's slots, parked in the frame's dL/dmel slots
   // (glin[m]: read back and overwritten by the same lane in x's pass)
   {
-    Y_FRAME(vy)
+    float2 vy[G::PPL];
+    window_frame<LOGN>(rawy, wn, vy);
     float pwr[G::PPL], pmid;
     fft_pairs<LOGN, false>(vy, z, l, tw, pwr, pmid);
 #pragma unroll
@@ -1337,6 +1351,7 @@ __global__ __launch_bounds__(256) SEL_FFT_OCC void k_mel_l1(const float* __restr
     frame_fence<LOGN>();  // magb reads done before x's transform overwrites the slots
   }
   // x: log-mels, |d|, and dL/dmel = sign(d) / n through the log
+  window_frame<LOGN>(raw, wn, v);
   fft_half<LOGN>(v, z, l, tw);
   float2 X[G::PPL + 1];
   real_split<LOGN>(z, l, tw, reinterpret_cast<float2(&)[G::PPL]>(X), X[G::PPL]);
@@ -1361,7 +1376,7 @@ __global__ __launch_bounds__(256) SEL_FFT_OCC void k_mel_l1(const float* __restr
 #pragma unroll
     for (int q = 0; q <= G::PPL; ++q) {
       const int k = q < G::PPL ? l + G::LPF * q : G::M;
-      const int2 r = ma.range[k];
+      const int2 r = mr_l[k];
       float gmag = 0.f;
       if (wmax) {
         for (int m = r.x; m < r.y; ++m) {  // melmat[k][m] is 0 outside mel m's band
@@ -1383,7 +1398,7 @@ __global__ __launch_bounds__(256) SEL_FFT_OCC void k_mel_l1(const float* __restr
   } else {
     frame_fence<LOGN>();  // glin / magb reads done before the next frame's transform
   }
-  FRAME_LOOP_END
+  }
   const double r = block_sum<double>(double(lsum), red);
   if (threadIdx.x == 0) partials[blockIdx.x] = r;
 }
@@ -1886,7 +1901,7 @@ int sel_mel_l1_fwd_grad(const float* x, const float* y, int64_t B, int64_t T, in
       using G = Geo<L>;                                                                                 \
       int iters;                                                                                        \
       const size_t lds = size_t(G::FPB) * (G::PADN * sizeof(float2) + size_t(glin) * sizeof(float)) +   \
-                         mel_lds_bytes(n_mels);                                                         \
+                         mel_lds_bytes(n_mels) + size_t(G::M + 1) * sizeof(int2);                       \
       grid = frame_grid<L>(nf, iters, frame_slots(k_mel_l1<L>, lds));                                   \
       if (grid)                                                                                         \
         hipLaunchKernelGGL(k_mel_l1<L>, dim3(grid), dim3(256), lds, s, x, y, a, window, ma,             \
