@@ -1519,14 +1519,53 @@ __device__ __forceinline__ void dpack_channel(const PackGeo& pg, int mode, const
 // One block per output channel n; the partials are walked in their packed
 // (tap, phase, channel) order, so each split's slice is one coalesced read, and
 // scattered once into the torch (channel, tap) positions.
+__device__ __forceinline__ void dwgrad_finish_channel(const PackGeo& pg, const float* __restrict__ part, int nsplit,
+                                                      const float* __restrict__ bpart, int bsplit,
+                                                      const float* __restrict__ v, const float* __restrict__ wg,
+                                                      float* __restrict__ gw, float* __restrict__ gg,
+                                                      float* __restrict__ gb, int n);
+
 __global__ __launch_bounds__(256) void k_dwgrad_finish(PackGeo pg, const float* __restrict__ part, int nsplit,
                                                        const float* __restrict__ bpart, int bsplit,
                                                        const float* __restrict__ v, const float* __restrict__ wg,
                                                        float* __restrict__ gw, float* __restrict__ gg,
                                                        float* __restrict__ gb) {
+  dwgrad_finish_channel(pg, part, nsplit, bpart, bsplit, v, wg, gw, gg, gb, blockIdx.x);
+}
+
+// batched form (sel_dconv_wgrad_finish_many): the final reductions of several
+// layers in one launch, block ranges per job in the kernel argument (a
+// sub-discriminator's layers finish together after its chain backward instead
+// of one launch per layer)
+constexpr int DWF_MAXJ = 24;
+struct DwgradJobs {
+  PackGeo pg[DWF_MAXJ];
+  const float* part[DWF_MAXJ];
+  const float* bpart[DWF_MAXJ];
+  const float* v[DWF_MAXJ];
+  const float* wg[DWF_MAXJ];
+  float* gw[DWF_MAXJ];
+  float* gg[DWF_MAXJ];
+  float* gb[DWF_MAXJ];
+  int nsplit[DWF_MAXJ], bsplit[DWF_MAXJ];
+  int bstart[DWF_MAXJ + 1];
+  int njobs;
+};
+
+__global__ __launch_bounds__(256) void k_dwgrad_finish_many(DwgradJobs dj) {
+  int j = 0;
+  while (j + 1 < dj.njobs && int(blockIdx.x) >= dj.bstart[j + 1]) ++j;  // block-uniform
+  dwgrad_finish_channel(dj.pg[j], dj.part[j], dj.nsplit[j], dj.bpart[j], dj.bsplit[j], dj.v[j], dj.wg[j], dj.gw[j],
+                        dj.gg[j], dj.gb[j], int(blockIdx.x) - dj.bstart[j]);
+}
+
+__device__ __forceinline__ void dwgrad_finish_channel(const PackGeo& pg, const float* __restrict__ part, int nsplit,
+                                                      const float* __restrict__ bpart, int bsplit,
+                                                      const float* __restrict__ v, const float* __restrict__ wg,
+                                                      float* __restrict__ gw, float* __restrict__ gg,
+                                                      float* __restrict__ gb, int n) {
   __shared__ float red[16];
   __shared__ float bc[2];
-  const int n = blockIdx.x;
   const int per = pg.Cg * pg.Kt;
   const int Ng = pg.N / pg.G, g = n / Ng, nl = n - g * Ng;
   const int nred = pg.s * pg.Cg;
@@ -2354,6 +2393,58 @@ size_t sel_dconv_wgrad_workspace(const sel_dconv_desc* d, int dtype) {
 int sel_dconv_wgrad(const sel_dconv_desc* d, int dtype, const void* gout, const void* x, int N, int Cg, int Kt,
                     int stride, int pad, const float* v, const float* wg, float* gw, float* gg, float* gb, void* ws,
                     size_t ws_bytes, sel_stream_t stream) {
+  sel_dwgrad_job job;
+  if (int rc = sel_dconv_wgrad_partials(d, dtype, gout, x, N, Cg, Kt, stride, pad, v, wg, gw, gg, gb, ws, ws_bytes,
+                                        &job, stream))
+    return rc;
+  const PackGeo pg = pack_geo(job.N, job.Cg, job.Kt, job.stride, job.pad, job.G);
+  hipLaunchKernelGGL(k_dwgrad_finish, dim3(job.N), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), pg,
+                     job.part, job.nsplit, job.bpart, job.bsplit, job.v, job.wg, job.gw, job.gg, job.gb);
+  SEL_LAUNCH_CHECK();
+  return SEL_OK;
+}
+
+int sel_dconv_wgrad_finish_many(const sel_dwgrad_job* jobs, int njobs, sel_stream_t stream) {
+  SEL_REQUIRE(njobs >= 0 && (njobs == 0 || jobs), SEL_ERR_ARG, "bad wgrad finish job list");
+  for (int j = 0; j < njobs; ++j) {
+    const sel_dwgrad_job& J = jobs[j];
+    SEL_REQUIRE(J.part && J.gw && J.N > 0 && J.Cg > 0 && J.Kt > 0 && J.stride > 0 && J.pad >= 0 && J.G > 0 &&
+                    J.N % J.G == 0 && J.nsplit > 0 && J.nsplit <= PRESUM && (!J.gb || (J.bpart && J.bsplit > 0)) &&
+                    (!J.v || (J.wg && J.gg)),
+                SEL_ERR_ARG, "bad wgrad finish job %d", j);
+  }
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  int j = 0;
+  while (j < njobs) {
+    DwgradJobs dj{};
+    int n = 0, blocks = 0;
+    for (; j < njobs && n < DWF_MAXJ; ++j, ++n) {
+      const sel_dwgrad_job& J = jobs[j];
+      dj.pg[n] = pack_geo(J.N, J.Cg, J.Kt, J.stride, J.pad, J.G);
+      dj.part[n] = J.part;
+      dj.bpart[n] = J.bpart;
+      dj.nsplit[n] = J.nsplit;
+      dj.bsplit[n] = J.bsplit;
+      dj.v[n] = J.v;
+      dj.wg[n] = J.wg;
+      dj.gw[n] = J.gw;
+      dj.gg[n] = J.gg;
+      dj.gb[n] = J.gb;
+      dj.bstart[n] = blocks;
+      blocks += J.N;
+    }
+    dj.bstart[n] = blocks;
+    dj.njobs = n;
+    hipLaunchKernelGGL(k_dwgrad_finish_many, dim3(unsigned(blocks)), dim3(256), 0, s, dj);
+    SEL_LAUNCH_CHECK();
+  }
+  return SEL_OK;
+}
+
+int sel_dconv_wgrad_partials(const sel_dconv_desc* d, int dtype, const void* gout, const void* x, int N, int Cg,
+                             int Kt, int stride, int pad, const float* v, const float* wg, float* gw, float* gg,
+                             float* gb, void* ws, size_t ws_bytes, sel_dwgrad_job* job, sel_stream_t stream) {
+  SEL_REQUIRE(job != nullptr, SEL_ERR_ARG, "sel_dconv_wgrad_partials: job is NULL");
   if (int rc = check(d)) return rc;
   SEL_REQUIRE(dtype == SEL_BF16 || dtype == SEL_F32, SEL_ERR_UNSUPPORTED, "dtype %d", dtype);
   SEL_REQUIRE(d->So == 1 && d->S == stride && d->G * d->Ng == N && d->Cg == Cg, SEL_ERR_ARG,
@@ -2384,9 +2475,7 @@ int sel_dconv_wgrad(const sel_dconv_desc* d, int dtype, const void* gout, const 
     }
     part = src;
   }
-  hipLaunchKernelGGL(k_dwgrad_finish, dim3(N), dim3(256), 0, s, pg, part, nsplit, bpart, bsplit, v, wg, gw, gg,
-                     gb);
-  SEL_LAUNCH_CHECK();
+  *job = sel_dwgrad_job{part, bpart, v, wg, gw, gg, gb, N, Cg, Kt, stride, pad, d->G, nsplit, bsplit};
   return SEL_OK;
 }
 

@@ -88,6 +88,8 @@ SIGNATURES = {
     "sel_dconv_pack_many": (I32, [P, I32, I32, P]),
     "sel_dconv_wgrad_workspace": (SZ, [P, I32]),
     "sel_dconv_wgrad": (I32, [P, I32, P, P, I32, I32, I32, I32, I32, P, P, P, P, P, P, SZ, P]),
+    "sel_dconv_wgrad_partials": (I32, [P, I32, P, P, I32, I32, I32, I32, I32, P, P, P, P, P, P, SZ, P, P]),
+    "sel_dconv_wgrad_finish_many": (I32, [P, I32, P]),
     "sel_avgpool1d_fwd": (I32, [P, I32, I32, I32, I32, I32, I32, I32, I32, P, P]),
     "sel_avgpool1d_bwd": (I32, [P, I32, I32, I32, I32, I32, I32, I32, I32, P, P]),
     "sel_mpd_fold": (I32, [P, I32, I32, I32, I32, I32, P, P]),

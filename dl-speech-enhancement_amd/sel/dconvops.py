@@ -15,6 +15,7 @@ Reference layouts returned (views, no copies):
                         final (B, L*p)    (a copy, as torch.flatten in :134)
 """
 import ctypes
+import os
 import weakref
 
 import torch
@@ -257,8 +258,21 @@ def _meta(d, x, out, tag):
     return (kernel(d, x.dtype)[1], nbytes, flops)
 
 
-def wgrad(sp, desc, gout, x, w_or_v, wg, want_w, want_b):
-    """(gw or gv, gg, gb) of one layer (fp32, torch layouts)."""
+class _DwgradJob(ctypes.Structure):
+    """sel_dwgrad_job (include/sel.h)."""
+    _fields_ = [(n, ctypes.c_void_p) for n in ("part", "bpart", "v", "wg", "gw", "gg", "gb")] + \
+               [(n, ctypes.c_int32) for n in ("N", "Cg", "Kt", "stride", "pad", "G", "nsplit", "bsplit")]
+
+
+# SEL_DWGRAD_MERGE=0: one final-reduction launch per layer (sel_dconv_wgrad)
+# instead of one per sub-discriminator chain (sel_dconv_wgrad_finish_many)
+DWGRAD_MERGE = os.environ.get("SEL_DWGRAD_MERGE", "1") != "0"
+
+
+def wgrad(sp, desc, gout, x, w_or_v, wg, want_w, want_b, pending=None):
+    """(gw or gv, gg, gb) of one layer (fp32, torch layouts).  With a `pending`
+    list the final reduction is left to finish_pending(pending): the tensors
+    are written when it has run (stream order)."""
     lib = L.lib()
     ws = L.workspace(lib.sel_dconv_wgrad_workspace(ctypes.byref(desc), _code(x.dtype)), x.device)
     gw = torch.empty(w_or_v.shape, dtype=torch.float32, device=x.device)
@@ -266,10 +280,23 @@ def wgrad(sp, desc, gout, x, w_or_v, wg, want_w, want_b):
     gb = torch.empty(sp.cout, dtype=torch.float32, device=x.device) if want_b else None
     v = w_or_v.detach().contiguous().float() if wg is not None else None
     g = wg.detach().contiguous().float() if wg is not None else None
-    L.call("sel_dconv_wgrad", ctypes.byref(desc), _code(x.dtype), L.ptr(gout), L.ptr(x), sp.cout,
-           sp.cin // sp.groups, sp.Kt, sp.stride, sp.pad, L.ptr(v), L.ptr(g), L.ptr(gw), L.ptr(gg), L.ptr(gb),
-           L.ptr(ws), ws.numel(), L.stream())
+    args = (ctypes.byref(desc), _code(x.dtype), L.ptr(gout), L.ptr(x), sp.cout, sp.cin // sp.groups, sp.Kt, sp.stride,
+            sp.pad, L.ptr(v), L.ptr(g), L.ptr(gw), L.ptr(gg), L.ptr(gb), L.ptr(ws), ws.numel())
+    if pending is None:
+        L.call("sel_dconv_wgrad", *args, L.stream())
+    else:
+        job = _DwgradJob()
+        L.call("sel_dconv_wgrad_partials", *args, ctypes.byref(job), L.stream())
+        pending.append((job, ws, v, g))  # the finish reads ws, v and g
     return (gw if want_w else None), gg, gb
+
+
+def finish_pending(pending):
+    """The final weight-gradient reductions of the layers in `pending`, one launch."""
+    if pending:
+        jobs = (_DwgradJob * len(pending))(*[p[0] for p in pending])
+        L.call("sel_dconv_wgrad_finish_many", ctypes.cast(jobs, ctypes.c_void_p), len(pending), L.stream())
+        pending.clear()
 
 
 def _cast(x, dtype):
@@ -362,6 +389,7 @@ class ChainFn(torch.autograd.Function):
         top = max((li for li in range(nl) if gviews[li] is not None), default=None)
         if top is None:
             return (None,) * (npre + len(params))
+        pending = [] if DWGRAD_MERGE else None  # the chain's final reductions: one launch at the end
         g = ext(top)
         gpre = _lrelu_bwd(g, bufs[top], slope) if specs[top].leaky else g
         gx0 = None
@@ -376,7 +404,7 @@ class ChainFn(torch.autograd.Function):
             need_b = b is not None and ctx.needs_input_grad[base + per - 1] and not frozen
             if need_w or need_g or need_b:
                 d_f = _fwd_desc(sp, Bs, T_in, T_alloc_in, T_out, T_out_alloc, slope)
-                gw, gg, gb = wgrad(sp, d_f, gpre, x_in, w, wg, True, need_b)
+                gw, gg, gb = wgrad(sp, d_f, gpre, x_in, w, wg, True, need_b, pending)
                 pgrads[per * li] = gw if need_w else None
                 if wn:
                     pgrads[per * li + 1] = gg if need_g else None
@@ -399,6 +427,7 @@ class ChainFn(torch.autograd.Function):
             if li == 0:
                 gx0 = gin
             gpre = gin
+        finish_pending(pending)
         return (gx0, None, None, None, None, None, None, None, None, None, *pgrads)
 
 

@@ -404,6 +404,25 @@ size_t sel_dconv_wgrad_workspace(const sel_dconv_desc* d, int dtype);
 int sel_dconv_wgrad(const sel_dconv_desc* d, int dtype, const void* gout, const void* x, int N, int Cg, int Kt,
                     int stride, int pad, const float* v, const float* wg, float* gw, float* gg, float* gb, void* ws,
                     size_t ws_bytes, sel_stream_t stream);
+/* sel_dconv_wgrad in two phases, so that several layers' final reductions run
+ * as one launch: _partials writes the split partials into ws (which must stay
+ * allocated, in stream order, until the finish) and describes the reduction
+ * in *job; _finish_many runs the reductions of njobs layers (gw / gg / gb as
+ * sel_dconv_wgrad writes them). */
+typedef struct {
+  const float* part;   /* folded split partials (in the layer's ws) */
+  const float* bpart;  /* bias partials or NULL */
+  const float* v;      /* weight_v or NULL */
+  const float* wg;     /* weight_g or NULL */
+  float* gw;
+  float* gg;
+  float* gb;
+  int32_t N, Cg, Kt, stride, pad, G, nsplit, bsplit;
+} sel_dwgrad_job;
+int sel_dconv_wgrad_partials(const sel_dconv_desc* d, int dtype, const void* gout, const void* x, int N, int Cg,
+                             int Kt, int stride, int pad, const float* v, const float* wg, float* gw, float* gg,
+                             float* gb, void* ws, size_t ws_bytes, sel_dwgrad_job* job, sel_stream_t stream);
+int sel_dconv_wgrad_finish_many(const sel_dwgrad_job* jobs, int njobs, sel_stream_t stream);
 /* AvgPool1d(kernel, stride, padding, count_include_pad) between MSD scales
  * (discriminator.py:428-447): (B, T) rows of pitch ldx -> (B, To) rows of pitch ldo
  * (positions >= To zero-filled); backward overwrites gx. */

@@ -118,6 +118,26 @@ assert call(finish, C.cast(jobs, P), 30, None) < 0
 jobs[0].nsplit, jobs[0].N, jobs[0].nw = 1 << 20, 4, 16
 assert call(finish, C.cast(jobs, P), 1, None) < 0
 
+# batched discriminator weight-gradient reductions: bad job lists fail before any launch
+dfin = fn("sel_dconv_wgrad_finish_many", I32, P, I32, P)
+assert call(dfin, None, 2, None) < 0
+assert call(dfin, None, 0, None) == 0
+
+
+class DwgradJob(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in ("part", "bpart", "v", "wg", "gw", "gg", "gb")] + \
+               [(n, C.c_int32) for n in ("N", "Cg", "Kt", "stride", "pad", "G", "nsplit", "bsplit")]
+
+
+djobs = (DwgradJob * 3)()
+for jb in djobs:
+    jb.N, jb.Cg, jb.Kt, jb.stride, jb.G, jb.nsplit = 4, 2, 3, 1, 1, 1
+assert call(dfin, C.cast(djobs, P), 3, None) < 0  # null partials / outputs
+djobs[0].part, djobs[0].gw, djobs[0].nsplit = 16, 16, 99
+assert call(dfin, C.cast(djobs, P), 1, None) < 0  # nsplit past the presum bound
+dpart = fn("sel_dconv_wgrad_partials", I32, P, I32, P, P, I32, I32, I32, I32, I32, P, P, P, P, P, P, SZ, P, P)
+assert call(dpart, None, 1, None, None, 4, 2, 3, 1, 0, None, None, None, None, None, None, 0, None, None) < 0
+
 # discriminator geometry, dispatch decision and kernel names (short buffers)
 geo = fn("sel_dconv_geometry", I32, I32, I32, I32, C.POINTER(I32), C.POINTER(I32))
 Kp, q0 = I32(), I32()

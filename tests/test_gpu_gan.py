@@ -380,17 +380,22 @@ def test_gan_step_side_streams_bit_identical_to_serial(gpu, dt, monkeypatch):
     against everything on one stream: the same kernels in the same order per
     chain, so the losses and the generator and discriminator gradients are
     bit-identical (twice with streams on: a missing stream dependency would
-    show up as a difference from the serial run)."""
+    show up as a difference from the serial run), and with the chains' final
+    weight-gradient reductions as one launch per layer instead of one per chain
+    (sel_dconv_wgrad vs sel_dconv_wgrad_finish_many: the same per-channel
+    reduction)."""
     from models.autoencoder_without_PQC.AudioDec import Generator
     from sel import configs
+    from sel import dconvops
     from sel.convops import precision
     from train_denoise import DenoiseStep
     g = golden("gan_step")
     gp = dict(encode_channels=4, decode_channels=4, code_dim=64, codebook_num=2, codebook_size=64)
     x, y = torch.from_numpy(g["x_noisy"]), torch.from_numpy(g["x_clean"])
     res = []
-    for n_streams in ("0", "8", "2", "8"):
+    for n_streams, merge in (("0", True), ("8", True), ("2", True), ("8", True), ("0", False), ("8", False)):
         monkeypatch.setenv("SEL_D_STREAMS", n_streams)
+        monkeypatch.setattr(dconvops, "DWGRAD_MERGE", merge)
         G = Generator(**gp)
         G.load_state_dict({k[3:]: torch.from_numpy(v) for k, v in golden("generator_nopqc").items()
                            if k.startswith("sd.")})
