@@ -5170,9 +5170,9 @@ namespace conv {
 // of k_split_sum1 + k_split_sum2_unpack / k_split_sum2 (and of k_split_finish1,
 // the one-group case of the same formula): group sums of 32 splits
 // (split_group_sum), then the groups in order, four at a time.  A weight block
-// owns 64 consecutive PACKED elements of one job (coalesced partial reads): its
-// 4 waves compute the group sums of groups w, w + 4, ... into LDS, wave 0 adds
-// them in order and scatters to the torch layout.  A bias block owns one bias
+// owns 256 consecutive PACKED elements of one job (coalesced partial reads),
+// one per thread: the thread adds its element's group sums in order and
+// scatters to the torch layout.  A bias block owns one bias
 // element: its threads compute the (group, column) sums, thread 0 adds them in
 // order.  Block ranges per job come in the kernel argument.
 constexpr int FM_MAXJ = 24;
@@ -5220,15 +5220,21 @@ __global__ __launch_bounds__(256) void k_wgrad_finish_many(FinishJobs fj) {
     return split_group_sum(p + int64_t(s0) * n, cnt, n);
   };
   if (lb < fj.wblocks[jb]) {
-    const int64_t j = int64_t(lb) * 64 + lane;
-    if (j < J.nw)
-      for (int g = wave; g < ng; g += 4) gs[g][lane] = group(J.part + j, g, J.nw);
-    __syncthreads();
-    if (wave == 0 && j < J.nw) {
+    // one packed element per thread, its group sums in order (the reduction
+    // needs no LDS: all 256 threads stream partials, where the 64-element
+    // blocks left three of four waves idle for the common one-group jobs)
+    (void)lane;
+    (void)wave;
+    const int64_t j = int64_t(lb) * 256 + tid;
+    if (j < J.nw) {
       float acc = 0.f;
       int g = 0;
-      for (; g + 4 <= ng; g += 4) acc += (gs[g][lane] + gs[g + 1][lane]) + (gs[g + 2][lane] + gs[g + 3][lane]);
-      for (; g < ng; ++g) acc += gs[g][lane];
+      for (; g + 4 <= ng; g += 4) {
+        const float g0 = group(J.part + j, g, J.nw), g1 = group(J.part + j, g + 1, J.nw);
+        const float g2 = group(J.part + j, g + 2, J.nw), g3 = group(J.part + j, g + 3, J.nw);
+        acc += (g0 + g1) + (g2 + g3);
+      }
+      for (; g < ng; ++g) acc += group(J.part + j, g, J.nw);
       const int64_t i = pack_dst(J.kind, j, J.cout, J.cin, J.k, J.stride);
       if (i >= 0) J.gw[i] = acc;
     }
@@ -5279,7 +5285,7 @@ int sel_wgrad_finish_many(const sel_wgrad_job* jobs, int njobs, sel_stream_t str
                                                FM_MAXG * 65)),
                   SEL_ERR_ARG, "bad wgrad job %d", j0 + j);
       fj.j[j] = J;
-      fj.wblocks[j] = int((J.nw + 63) / 64);
+      fj.wblocks[j] = int((J.nw + 255) / 256);
       fj.bstart[j] = int(blocks);
       blocks += fj.wblocks[j] + (J.gb ? J.bias_period : 0);
     }
