@@ -157,7 +157,10 @@ def c3_setup(dev, B, world, local, graph=False, dtype=torch.bfloat16):
         # one fused multi-tensor Adam launch instead of torch's 7 foreach passes
         # (128 us/step at C3, profiles/r1_c3_v22_kernel_stats.md); same update rule
         opt_kw.setdefault("fused", True)
-    opt = torch.optim.Adam(G.parameters(), **opt_kw)
+    # sel.optim.Adam (one sel_adam_step_many launch) unless SEL_ADAM=torch or a
+    # HIP-graph replay needs torch's capturable form
+    from sel import optim as sel_optim
+    opt = sel_optim.adam(G.parameters(), **opt_kw)
     sched = torch.optim.lr_scheduler.StepLR(opt, **cfg["generator_scheduler_params"])
     tr = Trainer(steps=0, epochs=0, data_loader={}, model=model, criterion={"mel": mel},
                  optimizer={"generator": opt}, scheduler={"generator": sched}, config=cfg, device=dev)

@@ -114,6 +114,64 @@ __global__ __launch_bounds__(256) void k_snr_bwd(const float* __restrict__ p, co
   }
 }
 
+
+// Adam update of many fp32 tensors in one launch (torch.optim.Adam semantics,
+// L2 weight decay, no amsgrad / maximize; the arithmetic of torch's fused
+// kernel: m = b1 m + (1 - b1) g, v = b2 v + (1 - b2) g g, p -= step_size m /
+// (sqrt(v) / bc2_sqrt + eps)).  Block b of the launch -> tensor j by the block
+// ranges in the argument; four elements per thread (16-B accesses where the
+// tensor allows them).
+constexpr int ADAM_MAXT = 48;
+constexpr int ADAM_EPB = 1024;  // elements per block
+struct AdamJobs {
+  float* p[ADAM_MAXT];
+  const float* g[ADAM_MAXT];
+  float* m[ADAM_MAXT];
+  float* v[ADAM_MAXT];
+  int64_t n[ADAM_MAXT];
+  int bstart[ADAM_MAXT + 1];
+  int nt;
+};
+
+struct AdamConst {
+  float b1, omb1, b2, omb2, eps, wd, step_size, bc2_sqrt;  // omb = 1 - beta, rounded once from double
+};
+
+__device__ __forceinline__ void adam_one(float& p, float g, float& m, float& v, const AdamConst& c) {
+  const float b1 = c.b1, omb1 = c.omb1, b2 = c.b2, omb2 = c.omb2, eps = c.eps, wd = c.wd,
+              step_size = c.step_size, bc2_sqrt = c.bc2_sqrt;
+  if (wd != 0.f) g = g + wd * p;
+  m = b1 * m + omb1 * g;
+  v = b2 * v + omb2 * g * g;
+  const float denom = sqrtf(v) / bc2_sqrt + eps;
+  p = p - step_size * m / denom;
+}
+
+__global__ __launch_bounds__(256) void k_adam_many(AdamJobs aj, AdamConst c) {
+  int j = 0;
+  while (j + 1 < aj.nt && int(blockIdx.x) >= aj.bstart[j + 1]) ++j;  // block-uniform
+  const int64_t n = aj.n[j];
+  const int64_t i0 = int64_t(int(blockIdx.x) - aj.bstart[j]) * ADAM_EPB + 4 * threadIdx.x;
+  float* __restrict__ P = aj.p[j];
+  const float* __restrict__ G = aj.g[j];
+  float* __restrict__ M = aj.m[j];
+  float* __restrict__ V = aj.v[j];
+  const bool vec = ((reinterpret_cast<uintptr_t>(P) | reinterpret_cast<uintptr_t>(G) | reinterpret_cast<uintptr_t>(M) |
+                     reinterpret_cast<uintptr_t>(V)) & 15) == 0;
+  if (vec && i0 + 4 <= n) {
+    float4 p = *reinterpret_cast<const float4*>(P + i0), g = *reinterpret_cast<const float4*>(G + i0);
+    float4 m = *reinterpret_cast<const float4*>(M + i0), v = *reinterpret_cast<const float4*>(V + i0);
+    adam_one(p.x, g.x, m.x, v.x, c);
+    adam_one(p.y, g.y, m.y, v.y, c);
+    adam_one(p.z, g.z, m.z, v.z, c);
+    adam_one(p.w, g.w, m.w, v.w, c);
+    *reinterpret_cast<float4*>(P + i0) = p;
+    *reinterpret_cast<float4*>(M + i0) = m;
+    *reinterpret_cast<float4*>(V + i0) = v;
+  } else {
+    for (int64_t i = i0; i < i0 + 4 && i < n; ++i) adam_one(P[i], G[i], M[i], V[i], c);
+  }
+}
 }  // namespace glue
 }  // namespace sel
 
@@ -183,6 +241,48 @@ int sel_snr_bwd(const float* pred, const float* target, int64_t B, int64_t T, co
   const int nb = int(std::min<int64_t>(4096, (B * T + 255) / 256));
   hipLaunchKernelGGL(k_snr_bwd, dim3(nb), dim3(256), 0, s, pred, target, B, T, sums, g_out, g_pred);
   SEL_LAUNCH_CHECK();
+  return SEL_OK;
+}
+
+int sel_adam_step_many(const sel_adam_tensor* ts, int nt, double beta1, double beta2, double eps, double weight_decay,
+                       double step_size, double bc2_sqrt, sel_stream_t stream) {
+  using namespace sel::glue;
+  SEL_REQUIRE(nt >= 0 && (nt == 0 || ts), SEL_ERR_ARG, "bad Adam tensor list");
+  SEL_REQUIRE(bc2_sqrt > 0.0 && eps >= 0.0, SEL_ERR_ARG, "bad Adam constants");
+  // (1 - beta) rounded once from the double, as torch's kernels receive it:
+  // 1 - float(0.999) is 1.3e-5 away from 0.001
+  const AdamConst c{float(beta1), float(1.0 - beta1), float(beta2),     float(1.0 - beta2),
+                    float(eps),   float(weight_decay), float(step_size), float(bc2_sqrt)};
+  for (int j = 0; j < nt; ++j)
+    SEL_REQUIRE(ts[j].n >= 0 && (ts[j].n == 0 || (ts[j].p && ts[j].g && ts[j].m && ts[j].v)) &&
+                    (ts[j].n + ADAM_EPB - 1) / ADAM_EPB < (int64_t(1) << 30),
+                SEL_ERR_ARG, "bad Adam tensor %d", j);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  int j = 0;
+  while (j < nt) {
+    AdamJobs aj{};
+    int64_t blocks = 0;
+    int k = 0;
+    for (; j < nt && k < ADAM_MAXT; ++j) {
+      if (ts[j].n == 0) continue;
+      const int64_t nb = (ts[j].n + ADAM_EPB - 1) / ADAM_EPB;
+      if (k > 0 && blocks + nb >= (int64_t(1) << 31)) break;
+      aj.p[k] = ts[j].p;
+      aj.g[k] = ts[j].g;
+      aj.m[k] = ts[j].m;
+      aj.v[k] = ts[j].v;
+      aj.n[k] = ts[j].n;
+      aj.bstart[k] = int(blocks);
+      blocks += nb;
+      ++k;
+    }
+    aj.bstart[k] = int(blocks);
+    aj.nt = k;
+    if (blocks > 0) {
+      hipLaunchKernelGGL(k_adam_many, dim3(unsigned(blocks)), dim3(256), 0, s, aj, c);
+      SEL_LAUNCH_CHECK();
+    }
+  }
   return SEL_OK;
 }
 

@@ -17,6 +17,7 @@ P = ctypes.c_void_p
 I64 = ctypes.c_int64
 I32 = ctypes.c_int
 F32 = ctypes.c_float
+F64 = ctypes.c_double
 SZ = ctypes.c_size_t
 
 # name -> (restype, argtypes); must cover every function declared in include/sel.h
@@ -90,6 +91,7 @@ SIGNATURES = {
     "sel_dconv_wgrad": (I32, [P, I32, P, P, I32, I32, I32, I32, I32, P, P, P, P, P, P, SZ, P]),
     "sel_dconv_wgrad_partials": (I32, [P, I32, P, P, I32, I32, I32, I32, I32, P, P, P, P, P, P, SZ, P, P]),
     "sel_dconv_wgrad_finish_many": (I32, [P, I32, P]),
+    "sel_adam_step_many": (I32, [P, I32, F64, F64, F64, F64, F64, F64, P]),
     "sel_avgpool1d_fwd": (I32, [P, I32, I32, I32, I32, I32, I32, I32, I32, P, P]),
     "sel_avgpool1d_bwd": (I32, [P, I32, I32, I32, I32, I32, I32, I32, I32, P, P]),
     "sel_mpd_fold": (I32, [P, I32, I32, I32, I32, I32, P, P]),

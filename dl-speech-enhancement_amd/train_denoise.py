@@ -42,6 +42,7 @@ from models.vocoder.HiFiGAN import Discriminator as DiscriminatorHiFiGAN
 from models.vocoder.modules.discriminator import frozen_parameters
 from sel import configs as sel_configs
 from sel import dist as D
+from sel import optim as sel_optim
 from sel.metrics import SignalNoiseRatio
 from trainer.trainerGAN import ScalarWriter
 
@@ -91,18 +92,19 @@ class DenoiseStep:
                       "discriminator": discriminator}
         gen = self.model["generator"]
         on_gpu = next(gen.parameters()).is_cuda
-        # on the GPU: torch's fused multi-tensor Adam (one launch per step, same update rule)
+        # on the GPU: sel.optim.Adam (every tensor's update in one launch; SEL_ADAM=torch:
+        # torch's fused multi-tensor Adam), the same update rule and state layout
         opt_kw = dict(config["generator_optimizer_params"])
         if on_gpu:
             opt_kw.setdefault("fused", True)
         self.optimizer = {"generator": optimizer if optimizer is not None
-                          else torch.optim.Adam(gen.parameters(), **opt_kw)}
+                          else sel_optim.adam(gen.parameters(), **opt_kw)}
         if discriminator is not None:
             dkw = dict(config.get("discriminator_optimizer_params", {}))
             if on_gpu:
                 dkw.setdefault("fused", True)
             self.optimizer["discriminator"] = (disc_optimizer if disc_optimizer is not None
-                                               else torch.optim.Adam(discriminator.parameters(), **dkw))
+                                               else sel_optim.adam(discriminator.parameters(), **dkw))
             self._d_opt_steps = 0
 
             def _d_stepped(*_):

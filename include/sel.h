@@ -301,6 +301,22 @@ int sel_sumsq2(const float* speech, const float* noise, int64_t n, double* sums2
 int sel_mix_noise(const float* speech, const float* noise, int64_t n, const double* sums2, float snr,
                   float* out, sel_stream_t stream);
 
+/* ---- optimizer step (trainer/trainerGAN.py:271-281 optimizer.step()) ---- */
+/* Adam update (torch.optim.Adam semantics: L2 weight decay, no amsgrad /
+ * maximize) of nt fp32 tensors in one launch: per element, g += wd p;
+ * m = b1 m + (1 - b1) g; v = b2 v + (1 - b2) g g;
+ * p -= step_size m / (sqrt(v) / bc2_sqrt + eps), step_size = lr / (1 - b1^t),
+ * bc2_sqrt = sqrt(1 - b2^t) (computed by the caller from the step count t). */
+typedef struct {
+  float* p;
+  const float* g;
+  float* m;  /* exp_avg */
+  float* v;  /* exp_avg_sq */
+  int64_t n;
+} sel_adam_tensor;
+int sel_adam_step_many(const sel_adam_tensor* ts, int nt, double beta1, double beta2, double eps,
+                       double weight_decay, double step_size, double bc2_sqrt, sel_stream_t stream);
+
 /* ---- SNR term of train_denoise.py:140 (torchmetrics 1.2.0 SignalNoiseRatio,
  * zero_mean=False): snr_b = 10 log10((sum t^2 + eps) / (sum (t-p)^2 + eps)) over the
  * last dim, out[0] = mean_b snr_b.  bwd: g_p = g * 20/ln10 * (t-p) / (D_b + eps) / B. */

@@ -138,6 +138,13 @@ assert call(dfin, C.cast(djobs, P), 1, None) < 0  # nsplit past the presum bound
 dpart = fn("sel_dconv_wgrad_partials", I32, P, I32, P, P, I32, I32, I32, I32, I32, P, P, P, P, P, P, SZ, P, P)
 assert call(dpart, None, 1, None, None, 4, 2, 3, 1, 0, None, None, None, None, None, None, 0, None, None) < 0
 
+# Adam over a tensor list: bad lists / constants fail before any launch
+F64 = C.c_double
+adam = fn("sel_adam_step_many", I32, P, I32, F64, F64, F64, F64, F64, F64, P)
+assert call(adam, None, 3, 0.9, 0.999, 1e-8, 0.0, 1e-3, 0.5, None) < 0
+assert call(adam, None, 0, 0.9, 0.999, 1e-8, 0.0, 1e-3, 0.5, None) == 0
+assert call(adam, None, 0, 0.9, 0.999, 1e-8, 0.0, 1e-3, 0.0, None) < 0
+
 # discriminator geometry, dispatch decision and kernel names (short buffers)
 geo = fn("sel_dconv_geometry", I32, I32, I32, I32, C.POINTER(I32), C.POINTER(I32))
 Kp, q0 = I32(), I32()

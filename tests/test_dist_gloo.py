@@ -238,3 +238,14 @@ def test_spectral_convergence_is_global_under_dp():
     # rank-local SC (no exchange) differs: the exchange is load-bearing
     loc = R.spectral_convergence(xm[:2], ym[:2])
     assert abs(loc.item() - sc.item()) > 1e-4
+
+
+def test_adam_factory_falls_back_to_torch_off_gpu():
+    """sel.optim.adam builds torch's Adam for CPU parameters (and for the options
+    sel.optim.Adam refuses); on the GPU path it is sel.optim.Adam."""
+    import torch
+    from sel import optim as O
+    p = [torch.zeros(3, requires_grad=True)]
+    assert type(O.adam(p, lr=1e-3, fused=False)) is torch.optim.Adam
+    with pytest.raises(NotImplementedError):
+        O.Adam(p, lr=1e-3, amsgrad=True)
