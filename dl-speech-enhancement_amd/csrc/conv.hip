@@ -1209,6 +1209,8 @@ __global__ __launch_bounds__(512) void k_conv_ws8(Args a, const __bf16* __restri
 template <int C, int N, int K, int R, bool E = false>
 struct Thin {
   static constexpr int PLANES = C / 32;
+  // NS output slices of 32 channels, RG row groups; at N = 96 the fourth
+  // wave has no slice (it stages and runs the epilogue only)
   static constexpr int NS = N / 32, RG = 4 / NS;
   static constexpr int WR = R / RG, TM = WR / 32;
   static constexpr int SPAN = R + F4_HALOMAX;
@@ -1226,7 +1228,7 @@ struct Thin {
   static constexpr bool EPF = E && EJ <= 8;
   static constexpr bool SPLIT = EPF && LDS_STAGE + LDS_OUT <= 64 * 1024;
   static constexpr size_t LDS_TOTAL = SPLIT ? LDS_STAGE + LDS_OUT : LDS;
-  static_assert(N == 32 || N == 64 || N == 128, "thin kernel: N in {32, 64, 128}");
+  static_assert(N == 32 || N == 64 || N == 96 || N == 128, "thin kernel: N in {32, 64, 96, 128}");
   static_assert(C % 32 == 0 && WR % 32 == 0, "thin kernel tiling");
   static_assert(LDS <= 64 * 1024, "thin kernel LDS");
 };
@@ -1345,35 +1347,40 @@ __global__ __launch_bounds__(256) void k_conv_thin_bf16(Args a, const __bf16* __
       }
     }
 
+    const bool mma_wave = G::NS * G::RG == 4 || rg < G::RG;  // wave-uniform
     floatx16 acc[G::TM];
 #pragma unroll
     for (int i = 0; i < G::TM; ++i)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
-    const __bf16* xw = xs + (rg * G::WR + (lane & 31)) * P + 8 * (lane >> 5);
+    const __bf16* xw = xs + ((mma_wave ? rg : 0) * G::WR + (lane & 31)) * P + 8 * (lane >> 5);
+    if (mma_wave) {
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
+      for (int k = 0; k < K; ++k) {
 #pragma unroll
-      for (int g = 0; g < C / 16; ++g) {
-        const __bf16* xb = xw + ((g >> 1) * G::SPAN + k * a.dil) * P + 16 * (g & 1);
+        for (int g = 0; g < C / 16; ++g) {
+          const __bf16* xb = xw + ((g >> 1) * G::SPAN + k * a.dil) * P + 16 * (g & 1);
 #pragma unroll
-        for (int i = 0; i < G::TM; ++i) {
-          const bf16x8 xf = *reinterpret_cast<const bf16x8*>(xb + i * 32 * P);
-          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[k][g], xf, acc[i], 0, 0, 0);
+          for (int i = 0; i < G::TM; ++i) {
+            const bf16x8 xf = *reinterpret_cast<const bf16x8*>(xb + i * 32 * P);
+            acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[k][g], xf, acc[i], 0, 0, 0);
+          }
         }
       }
     }
 
     // accumulators (out^T: lane -> row, element r -> channel) -> fp32 tile in LDS
     __syncthreads();  // every wave is done reading xs (split: and the last epilogue with ot)
+    if (mma_wave) {
 #pragma unroll
-    for (int i = 0; i < G::TM; ++i) {
-      const int row = rg * G::WR + i * 32 + (lane & 31);
+      for (int i = 0; i < G::TM; ++i) {
+        const int row = rg * G::WR + i * 32 + (lane & 31);
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int n = ns * 32 + 8 * g + 4 * (lane >> 5);
-        *reinterpret_cast<floatx4*>(ot + row * G::OP + n) =
-            floatx4{acc[i][4 * g], acc[i][4 * g + 1], acc[i][4 * g + 2], acc[i][4 * g + 3]};
+        for (int g = 0; g < 4; ++g) {
+          const int n = ns * 32 + 8 * g + 4 * (lane >> 5);
+          *reinterpret_cast<floatx4*>(ot + row * G::OP + n) =
+              floatx4{acc[i][4 * g], acc[i][4 * g + 1], acc[i][4 * g + 2], acc[i][4 * g + 3]};
+        }
       }
     }
     // split loop: the next tile is staged beside this tile's out tile, so a
@@ -1696,6 +1703,186 @@ __device__ __forceinline__ void ru_acc_to_frags(const float (&v)[16], bf16x8 (&f
     typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
     const u32x4 w = {r0[0], r1[0], r0[1], r1[1]};
     frag[pr] = __builtin_bit_cast(bf16x8, w);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Pointwise (1x1) conv for the 256-wide residual units at T = 400
+// (residual_unit.py:43-46's conv2 forward, out = x + W ELU(h), and its dgrad,
+// gh = ELU'(h) * W^T g).  The tiled kernel ran them as 8 dependent
+// 32-channel chunk steps per 64 x 128 tile (one global-load latency per
+// step): 19 us per launch for 39 MB, 2 TB/s.  Here one workgroup per CU owns
+// a contiguous range of rows:
+//   - N/32 waves; wave w holds the MFMA fragments of output columns
+//     [32w, 32w + 32) for all C input channels in VGPRs;
+//   - a pass over up to SUB 32-row sub-tiles requests everything up front,
+//     in use order: sub-tile 0's rows and epilogue operands, the weights,
+//     then the later sub-tiles (all row-contiguous 16-B pieces);
+//   - per sub-tile: wait for its own rows only, ELU them into its LDS slice,
+//     barrier, C/16 MFMAs per wave with every fragment read ahead,
+//     accumulators -> fp32 LDS tile, barrier, and a row-contiguous epilogue
+//     (bias, ELU'(aux), residual; 16-B stores), overlapping the arrival of
+//     the later sub-tiles;
+//   - every access is a buffer access over the block's own row range, so rows
+//     past it read zeros and their stores are dropped (no tail masking).
+// Same MFMA (32x32x16, weights as the first operand), same channel order and
+// the same epilogue roundings as k_conv_fwd_bf16: bit-identical outputs for
+// one epilogue operand (the residual-unit forms).
+// ---------------------------------------------------------------------------
+template <int C, int N>
+struct Pw {
+  static constexpr int WAVES = N / 32;
+  static constexpr int THREADS = WAVES * 64;
+  static constexpr int R = 32;                       // rows per sub-tile (one 32x32 MFMA tile)
+  static constexpr int SUB = 4;                      // sub-tiles per pass
+  static constexpr int RB = R * SUB;                 // rows per pass
+  static constexpr int PITCH = C + 8;                // LDS row pitch (bf16): conflict-free b128 reads
+  static constexpr int OP = N + 4;                   // fp32 out-tile pitch
+  static constexpr int XV = R * (C / 8) / THREADS;   // 16-B input pieces per thread per sub-tile
+  static constexpr int EV = R * (N / 8) / THREADS;   // 16-B output pieces per thread per sub-tile
+  static constexpr size_t LDS_X = size_t(RB) * PITCH * 2;
+  static constexpr size_t LDS = LDS_X + size_t(R) * OP * 4;
+  static_assert(XV >= 1 && R * (C / 8) % THREADS == 0 && EV >= 1 && R * (N / 8) % THREADS == 0, "pw pieces");
+};
+
+#ifndef SEL_W_PW
+#define SEL_W_PW 2
+#endif
+// timing ablations (diagnostic builds only, tools/pw_abl.sh): 1 no weight
+// loads, 2 no MFMAs, 4 no epilogue operand loads, 8 no output stores
+#ifndef SEL_PW_ABL
+#define SEL_PW_ABL 0
+#endif
+
+template <int C, int N, bool ELU, bool AUX, bool RES>
+__global__ __launch_bounds__((N / 32) * 64) __attribute__((amdgpu_waves_per_eu(SEL_W_PW))) void k_pw_bf16(
+    Args a, const __bf16* __restrict__ in, const __bf16* __restrict__ wp, const float* __restrict__ bias,
+    const __bf16* __restrict__ aux, const __bf16* __restrict__ res, __bf16* __restrict__ out, int rows_per_block) {
+  using G = Pw<C, N>;
+  constexpr int R = G::R, SUB = G::SUB, PITCH = G::PITCH, OP = G::OP, T = G::THREADS;
+  extern __shared__ __align__(16) unsigned char smem[];
+  __bf16* const xs = reinterpret_cast<__bf16*>(smem);             // [RB][PITCH]
+  float* const ot = reinterpret_cast<float*>(smem + G::LDS_X);    // [R][OP]
+  __shared__ __align__(16) float bs[N];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t r0 = int64_t(blockIdx.x) * rows_per_block;
+  if (r0 >= a.rows) return;  // block-uniform
+  const int nrows = int(a.rows - r0 < rows_per_block ? a.rows - r0 : rows_per_block);
+
+  const __amdgpu_buffer_rsrc_t rin = ru_rsrc(in + r0 * C, int64_t(nrows) * C);
+  const __amdgpu_buffer_rsrc_t rout = ru_rsrc(out + r0 * N, int64_t(nrows) * N);
+  const __amdgpu_buffer_rsrc_t raux = ru_rsrc(AUX ? aux + r0 * N : out, AUX ? int64_t(nrows) * N : 0);
+  const __amdgpu_buffer_rsrc_t rres = ru_rsrc(RES ? res + r0 * N : out, RES ? int64_t(nrows) * N : 0);
+
+  // the bias over the N columns (bs[n] = bias[n % period]) goes to LDS after
+  // the first sub-tile's requests; its value is requested here
+  const bool has_bias = bias && a.bias_period;
+  const float bval = has_bias && tid < N ? bias[tid % a.bias_period] : 0.f;
+
+  // input piece u of a sub-tile: row v / (C/8), channels (v % (C/8)) * 8;
+  // output piece j: row v / (N/8), channels (v % (N/8)) * 8 (v = tid + u*T)
+  uint4 xr[SUB][G::XV], ar[SUB][G::EV], rr[SUB][G::EV];
+  auto request = [&](int p0, int s) {
+#pragma unroll
+    for (int u = 0; u < G::XV; ++u) {
+      const int v = tid + u * T;
+      xr[s][u] = ru_bload(rin, ((p0 + s * R + v / (C / 8)) * C + (v % (C / 8)) * 8) * 2);
+    }
+#pragma unroll
+    for (int j = 0; j < G::EV; ++j) {
+      const int v = tid + j * T;
+      const int off = ((p0 + s * R + v / (N / 8)) * N + (v % (N / 8)) * 8) * 2;
+      if constexpr (SEL_PW_ABL & 4) {
+        ar[s][j] = make_uint4(off, 7u, 9u, 11u);
+        rr[s][j] = make_uint4(off ^ 5, 3u, 1u, 13u);
+      } else {
+        if constexpr (AUX) ar[s][j] = ru_bload(raux, off);
+        if constexpr (RES) rr[s][j] = ru_bload(rres, off);
+      }
+    }
+  };
+  // weight fragments of this wave's 32 output columns: wf[g] = Wp[n][16g + 8*(lane>>5) .. +8]
+  bf16x8 wf[C / 16];
+  const __bf16* const wrow = wp + int64_t(wave * 32 + (lane & 31)) * C + 8 * (lane >> 5);
+
+  for (int p0 = 0; p0 < nrows; p0 += G::RB) {
+    if (p0) __syncthreads();  // the previous pass is done with xs / ot
+    request(p0, 0);
+#pragma unroll
+    for (int g = 0; g < C / 16; ++g) {
+      if constexpr (SEL_PW_ABL & 1) wf[g] = __builtin_bit_cast(bf16x8, make_uint4(lane * 7u + g, g, lane, 3u));
+      else wf[g] = *reinterpret_cast<const bf16x8*>(wrow + 16 * g);
+    }
+#pragma unroll
+    for (int s = 1; s < SUB; ++s) request(p0, s);
+    if (tid < N) bs[tid] = bval;  // visible after the first sub-tile's barrier
+
+#pragma unroll
+    for (int s = 0; s < SUB; ++s) {
+      if (p0 + s * R >= nrows) break;  // block-uniform
+      // sub-tile s's rows -> its own LDS slice
+#pragma unroll
+      for (int u = 0; u < G::XV; ++u) {
+        const int v = tid + u * T;
+        const uint4 val = ELU ? elu8(xr[s][u]) : xr[s][u];
+        *reinterpret_cast<uint4*>(xs + (s * R + v / (C / 8)) * PITCH + (v % (C / 8)) * 8) = val;
+      }
+      __syncthreads();
+      // every fragment of the sub-tile requested before the first MFMA
+      const __bf16* xb = xs + (s * R + (lane & 31)) * PITCH + 8 * (lane >> 5);
+      bf16x8 xf[C / 16];
+#pragma unroll
+      for (int g = 0; g < C / 16; ++g) xf[g] = *reinterpret_cast<const bf16x8*>(xb + 16 * g);
+      __builtin_amdgcn_sched_barrier(0);
+      floatx16 acc;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+      if constexpr (SEL_PW_ABL & 2) {
+#pragma unroll
+        for (int g = 0; g < C / 16; ++g) acc[g] = float(xf[g][0]) + float(wf[g][1]);
+      } else {
+#pragma unroll
+        for (int g = 0; g < C / 16; ++g) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[g], xf[g], acc, 0, 0, 0);
+      }
+      // accumulators (out^T: lane -> row, element 4q + e -> channel 32w + 8q + 4*(lane>>5) + e)
+      // -> fp32 tile; the previous sub-tile's epilogue reads ended before this
+      // sub-tile's barrier
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        *reinterpret_cast<floatx4*>(ot + (lane & 31) * OP + wave * 32 + 8 * q + 4 * (lane >> 5)) =
+            floatx4{acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]};
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < G::EV; ++j) {
+        const int v = tid + j * T, r = v / (N / 8), n = (v % (N / 8)) * 8;
+        const floatx4 lo = *reinterpret_cast<const floatx4*>(ot + r * OP + n);
+        const floatx4 hi = *reinterpret_cast<const floatx4*>(ot + r * OP + n + 4);
+        float x[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        if (has_bias) {
+          const floatx4 b0 = *reinterpret_cast<const floatx4*>(bs + n);
+          const floatx4 b1 = *reinterpret_cast<const floatx4*>(bs + n + 4);
+          x[0] += b0[0], x[1] += b0[1], x[2] += b0[2], x[3] += b0[3];
+          x[4] += b1[0], x[5] += b1[1], x[6] += b1[2], x[7] += b1[3];
+        }
+        if constexpr (AUX) {
+          const __bf16* av = reinterpret_cast<const __bf16*>(&ar[s][j]);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) x[e] = __fmul_rn(x[e], elu_grad_fast(float(av[e])));
+        }
+        if constexpr (RES) {
+          const __bf16* rv = reinterpret_cast<const __bf16*>(&rr[s][j]);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) x[e] = __fadd_rn(x[e], float(rv[e]));
+        }
+        bf16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = __bf16(x[e]);
+        if (!(SEL_PW_ABL & 8) || x[0] == 1234.5f)
+          ru_bstore(rout, ((p0 + s * R + r) * N + n) * 2, o);
+      }
+    }
   }
 }
 
@@ -4394,12 +4581,16 @@ int launch_thin(const Args& a, const void* in, const void* wp, const float* bias
 
 // the (i, C, N, K) instances with their default / alternative tile rows:
 // residual-unit k7 / 1x1 at 32 and 64 channels, the first strided conv
-// (96 -> 64, 3 taps), the last transposed conv's dgrad (96 -> 64, 2 taps) and
-// the 128-channel residual-unit 1x1 (one 32-channel output slice per wave).
+// (96 -> 64, 3 taps), the last transposed conv's dgrad (96 -> 64, 2 taps),
+// the 128-channel residual-unit 1x1 (one 32-channel output slice per wave;
+// k_pw_bf16 by default), and the last transposed conv's forward (64 -> 96,
+// 2 taps, replicate pad) and the first strided conv's dgrad (64 -> 96, 3
+// taps): three output slices, the fourth wave stages and stores only.
 // A/B knobs: tune key 7 bit i = instance i off (tiled kernel instead),
 // key 6 bit i = instance i on its alternative tile rows
 #define SEL_THIN_SHAPES(X) X(0, 32, 32, 7, 256, 128) X(1, 32, 32, 1, 256, 128) X(2, 64, 64, 7, 128, 64) \
-  X(3, 64, 64, 1, 128, 64) X(4, 96, 64, 3, 128, 64) X(5, 96, 64, 2, 128, 64) X(6, 128, 128, 1, 64, 32)
+  X(3, 64, 64, 1, 128, 64) X(4, 96, 64, 3, 128, 64) X(5, 96, 64, 2, 128, 64) X(6, 128, 128, 1, 64, 32) \
+  X(7, 64, 96, 2, 128, 64) X(8, 64, 96, 3, 128, 64)
 
 int thin_index(const Args& a) {
   // (one sample's rows must fit a 2^31-byte buffer resource: ru_rsrc)
@@ -4638,6 +4829,62 @@ int launch_ru64_bwdw(const Args& a, const void* g, const void* h, const void* x,
   return SEL_OK;
 }
 
+
+// Pointwise kernel (k_pw_bf16) where it applies: 1x1, C = N in {128, 256}
+// (the RU128 / RU256 1x1 forwards and dgrads; rocprof on the C3 shapes:
+// 21.0 -> 19.6 us at 128 (thin kernel before), 19.1 -> 14.3 us at 256);
+// tune key 42: 1 = off; key 43 > 0: workgroup count
+bool pw_ok(const Args& a) {
+  if (a.K != 1 || a.C != a.N || a.pad != 0 || tune(42) == 1) return false;
+  if (!(a.N == 256 || a.N == 128)) return false;
+  // every block's row range is one buffer resource
+  return ru_region_ok(a.rows * int64_t(a.N) * 2);
+}
+
+template <int C, int N, bool ELU, bool AUX, bool RES>
+int launch_pw_t(const Args& a, const void* in, const void* wp, const float* bias, const void* aux, const void* res,
+                void* out, hipStream_t s) {
+  using G = Pw<C, N>;
+  if (a.rows == 0) return SEL_OK;
+  // one round of resident workgroups, each over an equal contiguous row range
+  static const int64_t slots = [] {
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_pw_bf16<C, N, ELU, AUX, RES>, G::THREADS, G::LDS) !=
+            hipSuccess)
+      return int64_t(256);
+    return std::max<int64_t>(1, int64_t(cus) * std::max(per_cu, 1));
+  }();
+  const int64_t target = tune(43) > 0 ? tune(43) : slots;
+  int64_t nb = std::min<int64_t>(target, (a.rows + G::R - 1) / G::R);
+  // (a pass covers RB rows: a range of more rows takes several passes)
+  const int64_t rpb = (a.rows + nb - 1) / nb;
+  nb = (a.rows + rpb - 1) / rpb;
+  hipLaunchKernelGGL((k_pw_bf16<C, N, ELU, AUX, RES>), dim3(unsigned(nb)), dim3(G::THREADS), G::LDS, s, a,
+                     static_cast<const __bf16*>(in), static_cast<const __bf16*>(wp), bias,
+                     static_cast<const __bf16*>(aux), static_cast<const __bf16*>(res), static_cast<__bf16*>(out),
+                     int(rpb));
+  SEL_LAUNCH_CHECK();
+  return SEL_OK;
+}
+
+template <int C, int N, bool ELU>
+int launch_pw_e(const Args& a, const void* in, const void* wp, const float* bias, const void* aux, const void* res,
+                void* out, hipStream_t s) {
+  if (aux && res) return launch_pw_t<C, N, ELU, true, true>(a, in, wp, bias, aux, res, out, s);
+  if (aux) return launch_pw_t<C, N, ELU, true, false>(a, in, wp, bias, aux, res, out, s);
+  if (res) return launch_pw_t<C, N, ELU, false, true>(a, in, wp, bias, aux, res, out, s);
+  return launch_pw_t<C, N, ELU, false, false>(a, in, wp, bias, aux, res, out, s);
+}
+
+template <int C, int N>
+int launch_pw(const Args& a, const void* in, const void* wp, const float* bias, const void* aux, const void* res,
+              void* out, hipStream_t s) {
+  return a.in_elu ? launch_pw_e<C, N, true>(a, in, wp, bias, aux, res, out, s)
+                  : launch_pw_e<C, N, false>(a, in, wp, bias, aux, res, out, s);
+}
+
 bool ru_fused_ok(const Args& a) {
   return (a.C == 32 || a.C == 64) && a.N == a.C && a.K == 7 && a.pad == (a.K - 1) * a.dil &&
          a.pad_mode == SEL_PAD_ZERO && a.in_elu == 1 && (a.K - 1) * a.dil <= F4_HALOMAX &&
@@ -4648,6 +4895,9 @@ template <typename TI, typename TO>
 int dispatch_fwd(const Args& a, const void* in, const void* wp, const float* bias, const void* aux,
                  const void* res, void* out, hipStream_t s) {
   if constexpr (sizeof(TI) == 2 && sizeof(TO) == 2) {
+    if (pw_ok(a))
+      return a.N == 256 ? launch_pw<256, 256>(a, in, wp, bias, aux, res, out, s)
+                        : launch_pw<128, 128>(a, in, wp, bias, aux, res, out, s);
     const int rc = dispatch_thin(a, in, wp, bias, aux, res, out, s);
     if (rc != kNotThin) return rc;
   }
@@ -4895,6 +5145,7 @@ extern "C" {
 int sel_conv_fwd_kernel_id(const sel_conv_desc* d, int in_dtype, int out_dtype, int has_epilogue) {
   if (!d || in_dtype != SEL_BF16 || check_desc(d) != SEL_OK) return -1;
   const Args a = to_args(d);
+  if (out_dtype == SEL_BF16 && pw_ok(a)) return 930000000 + a.N;  // pointwise: 9.3e8 + N
   if (out_dtype == SEL_BF16 && thin_ok(a)) {  // thin: 1e9 + E*5e8 + ((R/32*1000 + C)*1000 + N)*10 + K
     int r = 0;
     const bool e = thin_variant(a, has_epilogue != 0, r);

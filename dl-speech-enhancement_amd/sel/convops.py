@@ -280,6 +280,9 @@ def fwd_kernel_name(desc, in_dtype, out_dtype, has_epilogue=False):
         k, n, c, r = kid % 10, (kid // 10) % 1000, (kid // 10000) % 1000, 32 * (kid // 10000000)
         return f"k_conv_thin_bf16<{c}, {n}, {k}, {r}, {'true' if e else 'false'}>"
     to = "bf16" if out_dtype == torch.bfloat16 else "float"
+    if kid >= 93 * 10 ** 7:  # pointwise (1x1) weight-stationary kernel: 9.3e8 + N
+        n = kid - 93 * 10 ** 7
+        return f"k_pw_bf16<{n}, {n}"
     if kid >= 92 * 10 ** 7:  # eight-wave warp-specialised kernel, 256 x 128 tiles of 64 x 64 wave tiles: 9.2e8 + K
         return f"k_conv_ws8<{kid - 92 * 10 ** 7}, {to}, 256, 128, 64, 2>"
     if kid >= 91 * 10 ** 7:  # eight-wave warp-specialised kernel, 512 x 128 tiles: 9.1e8 + K

@@ -246,7 +246,9 @@ THIN_SHAPES = [(32, 32, 7, 9, 0, 1, 0, 0, 0, 3, 1000), (32, 32, 7, 9, 0, 0, 1, 1
                (64, 64, 7, 3, 0, 1, 0, 0, 0, 3, 800), (64, 64, 7, 1, 0, 0, 1, 1, 0, 2, 130),
                (64, 64, 1, 1, 0, 1, 0, 1, 0, 3, 800), (96, 64, 3, 1, 0, 0, 0, 0, 64, 4, 333),
                (96, 64, 2, 1, 0, 0, 0, 0, 0, 2, 500), (32, 32, 7, 9, 0, 1, 0, 0, 0, 2, 40),
-               (128, 128, 1, 1, 0, 1, 0, 1, 0, 3, 1000), (128, 128, 1, 1, 0, 0, 1, 0, 0, 2, 333)]
+               (128, 128, 1, 1, 0, 1, 0, 1, 0, 3, 1000), (128, 128, 1, 1, 0, 0, 1, 0, 0, 2, 333),
+               (64, 96, 2, 1, 1, 0, 0, 0, 96, 3, 1000), (64, 96, 3, 1, 0, 0, 0, 0, 0, 2, 777),
+               (64, 96, 2, 1, 1, 0, 0, 0, 96, 2, 61)]
 
 
 @pytest.mark.parametrize("shape", THIN_SHAPES, ids=lambda s: "C{}N{}K{}d{}e{}a{}r{}T{}".format(*s[:3], s[3], *s[5:8],
@@ -262,6 +264,14 @@ def test_thin_kernel_matches_tiled(gpu, shape):
     C, N, K, dil, mode, elu, aux, res, bias, B, T = shape
     torch.manual_seed(C + N + K + T)
     lib = L.lib()
+    prev42 = lib.sel_tune(42, 1)  # the 128-channel 1x1 on the thin kernel (k_pw_bf16 off)
+    try:
+        _thin_vs_tiled(lib, CO, C, N, K, dil, mode, elu, aux, res, bias, B, T, gpu)
+    finally:
+        lib.sel_tune(42, prev42)
+
+
+def _thin_vs_tiled(lib, CO, C, N, K, dil, mode, elu, aux, res, bias, B, T, gpu):
     for pad in ((K - 1) * dil, 0):
         d = CO.ConvDesc(B * T, T, C, N, K, dil, pad, mode, elu, bias)
         x = torch.randn(B * T, C, device=gpu).to(torch.bfloat16)
@@ -286,9 +296,12 @@ def test_thin_kernel_matches_tiled(gpu, shape):
         ref = torch.zeros(B, T, N, dtype=torch.float64, device=gpu)
         for k in range(K):
             idx = torch.arange(T, device=gpu) + k * dil - pad
-            ok = (idx >= 0) & (idx < T)
-            xs = torch.zeros(B, T, C, dtype=torch.float64, device=gpu)
-            xs[:, ok] = xa[:, idx[ok]]
+            if mode == CO.PAD_REPLICATE:
+                xs = xa[:, idx.clamp(0, T - 1)]
+            else:
+                ok = (idx >= 0) & (idx < T)
+                xs = torch.zeros(B, T, C, dtype=torch.float64, device=gpu)
+                xs[:, ok] = xa[:, idx[ok]]
             ref += torch.einsum("btc,nc->btn", xs, wp[:, k, :].double())
         ref = ref.view(B * T, N)
         if bias:
@@ -299,6 +312,62 @@ def test_thin_kernel_matches_tiled(gpu, shape):
             ref += r_.double()
         e = ((outs[0] - ref).norm() / ref.norm()).item()
         assert e < 4e-3, (pad, e)
+
+
+# (C, rows, T, in_elu, aux, res, bias): the RU256 1x1 forward (ELU'd h, residual x)
+# and dgrad (ELU'(h) epilogue) at C3 size, ragged row counts (tails of a block's
+# range and of a 32-row sub-tile), fewer rows than one sub-tile, bias, both
+# epilogue operands, and the 128-wide instance (tune key 42 = 2)
+PW_SHAPES = [(256, 25600, 400, 1, 0, 1, 0), (256, 25600, 400, 0, 1, 0, 0), (256, 6393, 6393, 1, 1, 1, 256),
+             (256, 5, 5, 0, 0, 0, 0), (256, 1000, 200, 0, 0, 1, 256), (256, 70001, 70001, 1, 0, 1, 0),
+             (128, 128000, 2000, 1, 0, 1, 0), (128, 777, 777, 0, 1, 0, 0)]
+
+
+@pytest.mark.parametrize("shape", PW_SHAPES, ids=lambda s: "C{}r{}e{}a{}r{}b{}".format(s[0], s[1], *s[3:]))
+def test_pointwise_kernel_matches_tiled(gpu, shape):
+    """k_pw_bf16 (weight-stationary 1x1, tune key 42) against the kernels it
+    replaces (key 42 = 1; k_conv_fwd_bf16<64, 128, 1, 1> at 256 channels, the
+    thin kernel at 128): the same 32x32x16 MFMA chain in the same channel
+    order and the same epilogue roundings -> bit-identical (the RU forms: one
+    epilogue operand);
+    against fp64 of the same bf16 operands within bf16 output rounding."""
+    from sel import _lib as L
+    from sel import convops as CO
+    C, rows, T, elu, aux, res, bias = shape
+    torch.manual_seed(C + rows)
+    lib = L.lib()
+    d = CO.ConvDesc(rows, T, C, C, 1, 1, 0, 0, elu, bias)
+    x = torch.randn(rows, C, device=gpu).to(torch.bfloat16)
+    wp = (0.1 * torch.randn(C, 1, C, device=gpu)).to(torch.bfloat16)
+    b = torch.randn(bias, device=gpu) if bias else None
+    a_ = torch.randn(rows, C, device=gpu).to(torch.bfloat16) if aux else None
+    r_ = torch.randn(rows, C, device=gpu).to(torch.bfloat16) if res else None
+    outs = []
+    for v in (2, 1):
+        prev = lib.sel_tune(42, v)
+        try:
+            name = CO.fwd_kernel_name(d, torch.bfloat16, torch.bfloat16, bool(aux or res))
+            assert name.startswith("k_pw_bf16") == (v == 2), name
+            outs.append(CO.prim(d, x, wp, bias=b, aux=a_, res=r_))
+        finally:
+            lib.sel_tune(42, prev)
+    if not (aux and res):
+        assert torch.equal(outs[0], outs[1])
+    else:  # with both epilogue operands the tiled kernel's ELU'(aux) * v + res may be contracted to an FMA
+        e = ((outs[0].double() - outs[1].double()).norm() / outs[1].double().norm()).item()
+        assert e < 4e-3, e
+    xa = x.double()
+    if elu:
+        xa = torch.where(xa > 0, xa, torch.expm1(xa)).to(torch.bfloat16).double()
+    ref = xa @ wp[:, 0, :].double().t()
+    if bias:
+        ref += b.double()
+    if aux:
+        ref *= torch.where(a_.double() > 0, 1.0, torch.exp(a_.double()))
+    if res:
+        ref += r_.double()
+    e = ((outs[0].double() - ref).norm() / ref.norm()).item()
+    assert e < 4e-3, e
 
 
 @pytest.mark.parametrize("epi", [0, 1, 2, 3])

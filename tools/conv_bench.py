@@ -30,6 +30,7 @@ SHAPES = [
     ("RU64 1x1 dgrad", 512000, 8000, 64, 64, 1, 1, 0, Z, 0, 1, 0, 0),
     ("up3 dgrad 96->64 k2", 512000, 8000, 96, 64, 2, 1, 0, Z, 0, 0, 0, 0),
     ("up3 64->96 k2 rep", 512000, 8000, 64, 96, 2, 1, 1, R, 0, 0, 0, 1),
+    ("down0 dgrad 64->96 k3", 512000, 8000, 64, 96, 3, 1, 0, Z, 0, 0, 0, 0),
     ("RU128 k7d9 fwd", 128000, 2000, 128, 128, 7, 9, 54, Z, 1, 0, 0, 0),
     ("RU128 k7d9 dgrad", 128000, 2000, 128, 128, 7, 9, 0, Z, 0, 1, 1, 0),
     ("RU128 1x1 fwd", 128000, 2000, 128, 128, 1, 1, 0, Z, 1, 0, 1, 0),
@@ -62,13 +63,15 @@ def run(shape, variant, iters=20):
     # every instance with epilogue operands (key 12 flips kThinEpfDefault =
     # 0b101, key 11 bit 0 = off); 36/37: the same with key 6 flipping every
     # instance's tile rows (kThinEpfAlt instances flip back under 34/36)
-    thin = 30 <= variant <= 37
+    # 41 / 42: the defaults with the pointwise kernel off / also at 128 channels (tune key 42)
+    thin = 30 <= variant <= 37 or variant in (41, 42)
+    L.lib().sel_tune(42, {41: 1, 42: 2}.get(variant, 0))
     L.lib().sel_tune(4, 0 if thin else 1)
     L.lib().sel_tune(5, 1 << 30 if variant in (31, 33) else 0)
     L.lib().sel_tune(6, 127 if variant in (32, 33, 36, 37) else 0)
     L.lib().sel_tune(12, 127 ^ 0b101 if variant in (34, 36) else 0)
     L.lib().sel_tune(11, 1 if variant in (35, 37) else 0)
-    L.lib().sel_tune(0, 0 if thin else variant)
+    L.lib().sel_tune(0, 0 if thin or variant == 0 else variant)
     try:
         for _ in range(3):
             y = CO.prim(d, x, wp, bias=b, aux=a_, res=r_)
@@ -104,7 +107,7 @@ def main():
         cells = " | ".join("-" if t is None else f"{t:.1f}" for t in times)
         print(f"| {name} | {cells} | v{best_v} | {nbytes / best_t / 1e3:.0f} | {flops / best_t / 1e6:.0f} |",
               flush=True)
-    for key in (0, 4, 5, 6, 7, 11, 12):
+    for key in (0, 4, 5, 6, 7, 11, 12, 42):
         L.lib().sel_tune(key, 0)
 
 
