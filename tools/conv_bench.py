@@ -43,6 +43,9 @@ SHAPES = [
     ("down3 1280->512 k3", 5120, 80, 1280, 512, 3, 1, 2, Z, 0, 0, 0, 1),
     ("dec conv1 64->512", 5120, 80, 64, 512, 7, 1, 6, Z, 0, 0, 0, 0),
     ("up0 512->1280 k2", 5120, 80, 512, 1280, 2, 1, 1, R, 0, 0, 0, 1),
+    ("up0 dgrad 1280->512 k2", 5120, 80, 1280, 512, 2, 1, 0, Z, 0, 0, 0, 0),
+    ("down3 dgrad 512->1280 k3", 5120, 80, 512, 1280, 3, 1, 0, Z, 0, 0, 0, 0),
+    ("dec conv1 dgrad 512->64 k7", 5120, 80, 512, 64, 7, 1, 0, Z, 0, 0, 0, 0),
 ]
 
 

@@ -24,14 +24,28 @@ def _meta(desc, x, out, wp, aux, res):
     return f"{shp} | {tag}", nb, fl
 
 
+_call = L.call
+
+
+def _call_tagged(name, *args, meta=None):
+    # the deferred weight-gradient partials (and the fused residual-unit calls) tagged by shape
+    if meta is None and name == "sel_conv_wgrad_partials":
+        d = args[0]._obj
+        tag = (f"wgrad r{d.rows} T{d.T} {d.C}->{d.N} k{d.K} d{d.dil} p{d.pad} e{d.in_elu}")
+        meta = (tag, 2 * (d.rows * d.C + d.rows * d.N), 2.0 * d.rows * d.N * d.K * d.C)
+    return _call(name, *args, meta=meta)
+
+
 def main():
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
     CO._fwd_meta = _meta
+    L.call = _call_tagged
     step = bench.c3_setup(torch.device("cuda"), 64, 1, 0)
     for _ in range(3):
         step()
     torch.cuda.synchronize()
-    L.TIMER = L.KernelTimer(["sel_conv_fwd"])
+    L.TIMER = L.KernelTimer(["sel_conv_fwd", "sel_conv_wgrad_partials", "sel_resunit_fwd", "sel_resunit_bwd",
+                             "sel_resunit_bwd_wgrad", "sel_wgrad_finish_many"])
     for _ in range(steps):
         step()
     summ = L.TIMER.summary()
