@@ -4835,7 +4835,8 @@ int launch_ru64_bwdw(const Args& a, const void* g, const void* h, const void* x,
 // 21.0 -> 19.6 us at 128 (thin kernel before), 19.1 -> 14.3 us at 256);
 // tune key 42: 1 = off; key 43 > 0: workgroup count
 bool pw_ok(const Args& a) {
-  if (a.K != 1 || a.C != a.N || a.pad != 0 || tune(42) == 1) return false;
+  // (a forced tiled variant, tune key 0, takes precedence)
+  if (a.K != 1 || a.C != a.N || a.pad != 0 || tune(42) == 1 || tune(0) != 0) return false;
   if (!(a.N == 256 || a.N == 128)) return false;
   // every block's row range is one buffer resource
   return ru_region_ok(a.rows * int64_t(a.N) * 2);

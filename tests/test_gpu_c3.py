@@ -106,6 +106,7 @@ def test_fwd4_tile_variants_on_c3_shapes(gpu, shape, form):
     ref = _ref(x, wp, d, B, b, a_, r_)
     lib = L.lib()
     p4 = lib.sel_tune(4, 1)  # the weight-stationary thin kernel would pre-empt the tiled one
+    p42 = lib.sel_tune(42, 1)  # and so would the pointwise kernel on the 1x1 shapes
     try:
         default_name = CO.fwd_kernel_name(d, torch.bfloat16, torch.bfloat16)
         assert default_name.startswith(("k_conv_fwd_bf16", "k_conv_ws_bf16", "k_conv_ws8")), default_name
@@ -134,6 +135,7 @@ def test_fwd4_tile_variants_on_c3_shapes(gpu, shape, form):
             assert torch.equal(got, first), (form, list(ws), name)
     finally:
         lib.sel_tune(4, p4)
+        lib.sel_tune(42, p42)
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "fp32"])
