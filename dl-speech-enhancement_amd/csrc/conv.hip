@@ -4110,12 +4110,18 @@ __global__ void k_pack_dgrad(const T* __restrict__ wp, int N, int K, int C, T* _
 
 // Multi-tensor pack: every job's fwd pack Wp and (optionally) its dgrad form Wd
 // in ONE launch (the per-layer launches of sel_pack_weight + sel_pack_dgrad were
-// ~120 x 4 us per training step).  Grid-stride over the concatenated packed
-// elements; a thread binary-searches its job in the device job table.
+// ~120 x 4 us per training step).  Grid-stride over TWO ranges of the
+// concatenated packed elements: [0, total) writes Wp in its own order, [total,
+// 2 total) writes Wd in ITS own order (gathering the source element), so both
+// write streams are coalesced (writing Wd as the transpose of the Wp walk made
+// every 2-B store its own partial line: 45 us per C3 step).  A thread
+// binary-searches its job in the device job table.
 template <typename TO>
 __global__ void k_pack_many(const sel_pack_job* __restrict__ jobs, int njobs, int64_t total) {
-  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
-       i += int64_t(gridDim.x) * blockDim.x) {
+  for (int64_t i2 = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i2 < 2 * total;
+       i2 += int64_t(gridDim.x) * blockDim.x) {
+    const bool dg = i2 >= total;  // dgrad-form range
+    const int64_t i = dg ? i2 - total : i2;
     int lo = 0, hi = njobs - 1;
     while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
@@ -4123,44 +4129,42 @@ __global__ void k_pack_many(const sel_pack_job* __restrict__ jobs, int njobs, in
       else hi = mid - 1;
     }
     const sel_pack_job& J = jobs[lo];
+    if (dg && !J.wdgrad) continue;
     // a layer's packed index fits 32 bits (host-checked): unsigned 32-bit
     // division instead of the 64-bit sequences (the per-step pack of the C3
     // weights took 105 us with them)
     const unsigned li = unsigned(i - J.offset);
     const unsigned s = unsigned(J.stride), cin = unsigned(J.cin), cout = unsigned(J.cout), K = unsigned(J.k);
-    float v = 0.f;
-    unsigned N, KP, n, kp, cp;
-    if (J.kind == SEL_PACK_FWD) {
-      N = cout, KP = K;
-      const unsigned q = li / cin;
-      cp = li - q * cin;
-      n = q / K;
-      kp = q - n * K;
-      v = J.w[(n * cin + cp) * K + kp];
-    } else if (J.kind == SEL_PACK_FWD_STRIDED) {
-      N = cout, KP = 3;
-      const unsigned CP = s * cin;
+    // packed geometry: Wp[n][kp][cp] (N rows, KP taps, CP channels per tap)
+    unsigned N, KP, CP;
+    if (J.kind == SEL_PACK_FWD) N = cout, KP = K, CP = cin;
+    else if (J.kind == SEL_PACK_FWD_STRIDED) N = cout, KP = 3, CP = s * cin;
+    else N = s * cout, KP = 2, CP = cin;
+    unsigned n, kp, cp;
+    if (!dg) {  // li = (n * KP + kp) * CP + cp
       const unsigned q = li / CP;
       cp = li - q * CP;
-      n = q / 3u;
-      kp = q - n * 3u;
+      n = q / KP;
+      kp = q - n * KP;
+    } else {  // Wd[c][j][n] = Wp[n][KP-1-j][c]: li = (cp * KP + j) * N + n
+      const unsigned r = li / N;
+      n = li - r * N;
+      cp = r / KP;
+      kp = KP - 1 - (r - cp * KP);
+    }
+    float v = 0.f;
+    if (J.kind == SEL_PACK_FWD) {
+      v = J.w[(n * cin + cp) * K + kp];
+    } else if (J.kind == SEL_PACK_FWD_STRIDED) {
       const unsigned ph = cp / cin, ci = cp - ph * cin;
       const int k = strided_k(int(kp), int(ph), int(s));
       v = k >= 0 ? J.w[(n * cin + ci) * (2 * s) + unsigned(k)] : 0.f;
     } else {
-      N = s * cout, KP = 2;
-      const unsigned q = li / cin;
-      cp = li - q * cin;
-      n = q >> 1;
-      kp = q & 1u;
       const unsigned ph = n / cout, co = n - ph * cout;
       const unsigned k = kp == 0 ? ph + s : ph;
       v = J.w[(cp * cout + co) * (2 * s) + k];
     }
-    const TO tv = from_f<TO>(v);
-    static_cast<TO*>(J.wpack)[li] = tv;
-    // Wd[c][j][n] = Wp[n][KP-1-j][c]
-    if (J.wdgrad) static_cast<TO*>(J.wdgrad)[(cp * KP + (KP - 1 - kp)) * N + n] = tv;
+    static_cast<TO*>(dg ? J.wdgrad : J.wpack)[li] = from_f<TO>(v);
   }
 }
 
@@ -5577,7 +5581,7 @@ int sel_pack_many(const sel_pack_job* jobs, int njobs, int64_t total, int dtype,
   // (the job table is device memory: each job's element count is checked < 2^31
   // by the host binding, sel/convops.py PackCache._refresh)
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  dim3 grid(unsigned(std::min<int64_t>(8192, (total + 255) / 256)));
+  dim3 grid(unsigned(std::min<int64_t>(8192, (2 * total + 255) / 256)));
   if (dtype == SEL_F32)
     hipLaunchKernelGGL(k_pack_many<float>, grid, dim3(256), 0, s, jobs, njobs, total);
   else

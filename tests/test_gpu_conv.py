@@ -696,3 +696,28 @@ def test_deferred_wgrad_reduction_bit_identical(gpu, monkeypatch):
     acc = run(True, accumulate=True)
     for a_, b_ in zip(acc, ref):
         assert torch.equal(a_, b_ + 1.0)
+
+
+def test_pack_many_matches_per_layer_pack(gpu):
+    """PackCache's one-launch refresh (sel_pack_many: Wp and the dgrad form Wd
+    written as two coalesced ranges) writes the same bytes as sel_pack_weight
+    + sel_pack_dgrad per layer, for the three packed kinds (causal conv,
+    phase-view strided conv, transposed conv) in both dtypes."""
+    from sel import convops as CO
+    torch.manual_seed(11)
+    layers = [(CO.PACK_FWD, (64, 32, 7), 1), (CO.PACK_FWD, (256, 256, 1), 1), (CO.PACK_FWD_STRIDED, (128, 64, 4), 2),
+              (CO.PACK_FWD_STRIDED, (512, 256, 10), 5), (CO.PACK_CONVT, (256, 128, 6), 3),
+              (CO.PACK_CONVT, (64, 96, 2), 1), (CO.PACK_FWD, (1, 32, 7), 1)]
+    for dt in (torch.bfloat16, torch.float32):
+        cache = CO.PackCache()
+        ws = [torch.randn(*shp, device=gpu) for _, shp, _ in layers]
+        for (kind, _, stride), w in zip(layers, ws):
+            cache.get(kind, w, stride, dt)  # registers the entry
+        with torch.no_grad():
+            for w in ws:
+                w.mul_(1.5)  # every entry stale: the next get refreshes all of them in one launch
+        for (kind, _, stride), w in zip(layers, ws):
+            wp, wd = cache.get(kind, w, stride, dt)
+            ref = CO.pack(kind, w, stride, dt)
+            assert torch.equal(wp, ref), (kind, tuple(w.shape), dt)
+            assert torch.equal(wd.contiguous(), CO.pack_dgrad(ref)), (kind, tuple(w.shape), dt)
