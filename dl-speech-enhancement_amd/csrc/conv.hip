@@ -2605,7 +2605,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 128 ? 
 // ---------------------------------------------------------------------------
 constexpr int C1_NMAX = 64;
 constexpr int C1_KMAX = 8;
-constexpr int C1_TR = 256;    // rows per sample-aligned tile
+constexpr int C1_TR = 256;    // rows per sample-aligned tile (weight gradient)
+constexpr int C1F_TR = 1024;  // rows per tile of the forward kernel
 constexpr int C1_HALO = 64;   // max (K-1)*dil
 
 // Stage act(x) for input times [t0 - pad, t0 - pad + C1_TR + halo) of sample b as
@@ -2626,12 +2627,13 @@ __device__ __forceinline__ void c1_stage(const Args& a, const __bf16* __restrict
 // Thread = (8-wide output group g, row lane rl): its 8 x K weights live in
 // registers; per row it reads K staged samples and writes one 16-B vector, the
 // NG lanes of a row together writing the row's contiguous N outputs.
-template <typename TO>
+template <typename TO, int TR>
 __global__ __launch_bounds__(256) void k_conv_c1_bf16(Args a, const __bf16* __restrict__ in,
                                                       const __bf16* __restrict__ wp, const float* __restrict__ bias,
                                                       const TO* __restrict__ aux, const TO* __restrict__ res,
                                                       TO* __restrict__ out) {
-  __shared__ float xs[C1_TR + C1_HALO];
+  __shared__ float xs[TR + C1_HALO];
+  constexpr int PV = (TR + C1_HALO + 255) / 256;  // staged samples per thread
   constexpr int V = Vec16<TO>::n;  // outputs per vector store (8 bf16 / 4 fp32)
   const int NG = a.N / V;
   const int tid = threadIdx.x, grp = tid % NG, rl = tid / NG, nrl = 256 / NG;
@@ -2643,17 +2645,17 @@ __global__ __launch_bounds__(256) void k_conv_c1_bf16(Args a, const __bf16* __re
 #pragma unroll
     for (int k = 0; k < C1_KMAX; ++k) w[e][k] = k < a.K ? float(wp[n * a.K + k]) : 0.f;
   }
-  const int tps = (a.T + C1_TR - 1) / C1_TR;
+  const int tps = (a.T + TR - 1) / TR;
   const int64_t ntiles = (a.rows / a.T) * tps;
   // the next tile's samples are fetched into registers while this tile is
   // computed and stored (one resident round of workgroups walks the tiles)
-  const int span = C1_TR + (a.K - 1) * a.dil;
-  float pre[2];
+  const int span = TR + (a.K - 1) * a.dil;
+  float pre[PV];
   auto fetch = [&](int64_t tile) {
     const int64_t b = tile / tps;
-    const int t0 = int(tile % tps) * C1_TR;
+    const int t0 = int(tile % tps) * TR;
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < PV; ++u) {
       const int r = threadIdx.x + 256 * u;
       int ti = t0 - a.pad + r;
       const bool ok = r < span && ((ti >= 0 && ti < a.T) || a.pad_mode == SEL_PAD_REPLICATE);
@@ -2665,14 +2667,14 @@ __global__ __launch_bounds__(256) void k_conv_c1_bf16(Args a, const __bf16* __re
   if (int64_t(blockIdx.x) < ntiles) fetch(blockIdx.x);
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int64_t b = tile / tps;
-    const int t0 = int(tile % tps) * C1_TR;
+    const int t0 = int(tile % tps) * TR;
     __syncthreads();
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+    for (int u = 0; u < PV; ++u)
       if (threadIdx.x + 256 * u < span) xs[threadIdx.x + 256 * u] = pre[u];
     __syncthreads();
     if (tile + gridDim.x < ntiles) fetch(tile + gridDim.x);
-    const int rows = a.T - t0 < C1_TR ? a.T - t0 : C1_TR;
+    const int rows = a.T - t0 < TR ? a.T - t0 : TR;
     for (int r = rl; r < rows; r += nrl) {
       float v[V];
 #pragma unroll
@@ -4896,6 +4898,29 @@ bool ru_fused_ok(const Args& a) {
          (a.bias_period == 0 || a.bias_period == a.N) && ru_region_ok(int64_t(a.T) * a.C * 2);
 }
 
+// single-input-channel forward (k_conv_c1_bf16): one resident round of
+// workgroups walking TR-row tiles (they prefetch their next tile); tune key
+// 44 = 1: the round-3 256-row tiles
+template <typename TO, int TR>
+int launch_c1(const Args& a, const void* in, const void* wp, const float* bias, const void* aux, const void* res,
+              void* out, hipStream_t s) {
+  static const int64_t slots = [] {
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_conv_c1_bf16<TO, TR>, 256, 0) != hipSuccess)
+      return int64_t(4096);
+    return std::max<int64_t>(256, int64_t(cus) * per_cu);
+  }();
+  const int64_t blocks = std::min<int64_t>((a.rows / a.T) * ((a.T + TR - 1) / TR), tune(23) > 0 ? tune(23) : slots);
+  if (blocks <= 0) return SEL_OK;
+  hipLaunchKernelGGL((k_conv_c1_bf16<TO, TR>), dim3(unsigned(blocks)), dim3(256), 0, s, a,
+                     static_cast<const __bf16*>(in), static_cast<const __bf16*>(wp), bias,
+                     static_cast<const TO*>(aux), static_cast<const TO*>(res), static_cast<TO*>(out));
+  SEL_LAUNCH_CHECK();
+  return SEL_OK;
+}
+
 template <typename TI, typename TO>
 int dispatch_fwd(const Args& a, const void* in, const void* wp, const float* bias, const void* aux,
                  const void* res, void* out, hipStream_t s) {
@@ -4908,23 +4933,9 @@ int dispatch_fwd(const Args& a, const void* in, const void* wp, const float* bia
   }
   if constexpr (sizeof(TI) == 2) {
     if (a.C == 1 && a.N % 8 == 0 && a.N <= C1_NMAX && a.K <= C1_KMAX && (a.K - 1) * a.dil <= C1_HALO &&
-        tune(3) == 0) {
-      // one round of resident workgroups (they prefetch their next tile)
-      static const int64_t slots = [] {
-        int dev = 0, cus = 0, per_cu = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_conv_c1_bf16<TO>, 256, 0) != hipSuccess)
-          return int64_t(4096);
-        return std::max<int64_t>(256, int64_t(cus) * per_cu);
-      }();
-      const int64_t blocks = std::min<int64_t>((a.rows / a.T) * ((a.T + C1_TR - 1) / C1_TR), tune(23) > 0 ? tune(23) : slots);
-      hipLaunchKernelGGL(k_conv_c1_bf16<TO>, dim3(unsigned(blocks)), dim3(256), 0, s, a,
-                         static_cast<const __bf16*>(in), static_cast<const __bf16*>(wp), bias,
-                         static_cast<const TO*>(aux), static_cast<const TO*>(res), static_cast<TO*>(out));
-      SEL_LAUNCH_CHECK();
-      return SEL_OK;
-    }
+        tune(3) == 0)
+      return tune(44) == 1 ? launch_c1<TO, 256>(a, in, wp, bias, aux, res, out, s)
+                           : launch_c1<TO, C1F_TR>(a, in, wp, bias, aux, res, out, s);
     const int v = tune(0);
     const bool fast = (a.C % CK) == 0 && (a.K - 1) * a.dil <= F4_HALOMAX && a.K <= 8 && (v == 0 || v > 20);
     if (fast) {

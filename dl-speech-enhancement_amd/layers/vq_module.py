@@ -72,7 +72,16 @@ class ResidualVQ(nn.Module):
         self.layers = nn.ModuleList([VectorQuantize(**kwargs) for _ in range(num_quantizers)])
 
     def _stacked(self):
-        return torch.stack([l.embed for l in self.layers])
+        # the (S, D, K) codebook stack, rebuilt only when a codebook changed
+        # (EMA update, load_state_dict, .to(): new storage or a bumped version)
+        embeds = [l.embed for l in self.layers]
+        if any(e.requires_grad for e in embeds):
+            return torch.stack(embeds)
+        key = tuple((e.data_ptr(), e._version, e.dtype, e.device) for e in embeds)
+        if getattr(self, "_stack_key", None) != key:
+            self._stack_cache = torch.stack(embeds)
+            self._stack_key = key
+        return self._stack_cache
 
     def forward(self, x):
         if any(l.training for l in self.layers):

@@ -233,3 +233,21 @@ def test_trainer_checkpoint_roundtrip_with_reference_file(tmp_path):
         else:
             assert a == b, path
     same(mine, ref)
+
+
+def test_rvq_codebook_stack_cache_follows_updates():
+    """ResidualVQ._stacked: the (S, D, K) codebook stack is reused while no
+    codebook changes and rebuilt after an in-place update (EMA / load_state_dict)."""
+    from layers.vq_module import ResidualVQ
+    torch.manual_seed(0)
+    rvq = ResidualVQ(num_quantizers=3, dim=8, codebook_size=16)
+    a = rvq._stacked()
+    assert rvq._stacked() is a
+    assert torch.equal(a, torch.stack([l.embed for l in rvq.layers]))
+    with torch.no_grad():
+        rvq.layers[1].embed.mul_(2.0)
+    b = rvq._stacked()
+    assert b is not a and torch.equal(b, torch.stack([l.embed for l in rvq.layers]))
+    sd = {k: v.clone() + 1.0 for k, v in rvq.state_dict().items()}
+    rvq.load_state_dict(sd)
+    assert torch.equal(rvq._stacked(), torch.stack([l.embed for l in rvq.layers]))

@@ -19,6 +19,8 @@ Z, R = CO.PAD_ZERO, CO.PAD_REPLICATE
 # name, rows, T, C, N, K, dil, pad, mode, in_elu, aux, res, bias
 SHAPES = [
     ("first 1->32 k7", 1536000, 24000, 1, 32, 7, 1, 6, Z, 0, 0, 0, 0),
+    ("last dgrad 1->32 k7", 1536000, 24000, 1, 32, 7, 1, 0, Z, 0, 0, 0, 0),
+    ("last 32->1 k7", 1536000, 24000, 32, 1, 7, 1, 6, Z, 0, 0, 0, 1),
     ("RU32 k7d9 fwd", 1536000, 24000, 32, 32, 7, 9, 54, Z, 1, 0, 0, 0),
     ("RU32 1x1 fwd", 1536000, 24000, 32, 32, 1, 1, 0, Z, 1, 0, 1, 0),
     ("RU32 k7d9 dgrad", 1536000, 24000, 32, 32, 7, 9, 0, Z, 0, 1, 1, 0),
