@@ -2168,6 +2168,9 @@ struct WgPlanD {
   int tiles_per_seq, tiles_per_split, ntg, nt;
 };
 
+// split-partial budget per layer (bytes; tune key 45 > 0: MB, A/B sweeps)
+inline int64_t wg_cap() { return int64_t(tune(45) > 0 ? tune(45) : 64) << 20; }
+
 WgPlanD wg_plan(const sel_dconv_desc* d, int dtype) {
   WgPlanD p{};
   const int width = d->So * d->Ng;
@@ -2209,7 +2212,7 @@ WgPlanD wg_plan(const sel_dconv_desc* d, int dtype) {
     const int64_t ntiles = p.flat_p ? p.tiles_per_seq : int64_t(d->B) * p.tiles_per_seq;
     const int64_t blocks = int64_t(width / (32 * p.w3_nt)) * (nred / (32 * p.w3_ct));
     int64_t want = std::max<int64_t>(1, (512 + blocks - 1) / blocks);
-    want = std::min<int64_t>(want, std::max<int64_t>(1, (int64_t(64) << 20) / (nw * 4)));
+    want = std::min<int64_t>(want, std::max<int64_t>(1, wg_cap() / (nw * 4)));
     want = std::min<int64_t>(want, std::max<int64_t>(1, ntiles));
     p.tiles_per_split = int((ntiles + want - 1) / want);
     p.nsplit = int((ntiles + p.tiles_per_split - 1) / p.tiles_per_split);
@@ -2220,14 +2223,14 @@ WgPlanD wg_plan(const sel_dconv_desc* d, int dtype) {
     const int64_t ntiles = int64_t(d->B) * p.tiles_per_seq;
     const int64_t blocks = int64_t(d->G) * ((width + 16 * p.nt - 1) / (16 * p.nt)) * ((nred + 31) / 32) * p.ntg;
     int64_t want = std::max<int64_t>(1, (1024 + blocks - 1) / blocks);
-    want = std::min<int64_t>(want, std::max<int64_t>(1, (int64_t(64) << 20) / (nw * 4)));
+    want = std::min<int64_t>(want, std::max<int64_t>(1, wg_cap() / (nw * 4)));
     want = std::min<int64_t>(want, std::max<int64_t>(1, ntiles));
     p.tiles_per_split = int((ntiles + want - 1) / want);
     p.nsplit = int((ntiles + p.tiles_per_split - 1) / p.tiles_per_split);
   } else {
     const int64_t want_threads = int64_t(1) << 20;
     int64_t want = std::max<int64_t>(1, want_threads / std::max<int64_t>(1, nw + int64_t(d->G) * width));
-    want = std::min<int64_t>(want, std::max<int64_t>(1, (int64_t(64) << 20) / ((nw + width * d->G) * 4)));
+    want = std::min<int64_t>(want, std::max<int64_t>(1, wg_cap() / ((nw + width * d->G) * 4)));
     want = std::min<int64_t>(want, std::max<int64_t>(1, rows));
     p.rows_per_split = int((rows + want - 1) / want);
     p.nsplit = int((rows + p.rows_per_split - 1) / p.rows_per_split);
