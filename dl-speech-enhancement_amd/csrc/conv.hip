@@ -4469,7 +4469,9 @@ bool ws8w_ok(const Args& a) {
 // 16-multiple C within the zero source, halo within the staged span, the
 // 4-slot ring within 160 KB
 bool ws_ok(const Args& a) {
-  return (a.K == 3 || a.K == 7) && a.N % WS_BN == 0 && a.C % WS_CK == 0 && a.C <= WS_CMAX &&
+  // (K = 2: the phase-view transposed convs and their adjoints, round 4;
+  // tune key 46 = 1: those on the tiled kernel again)
+  return ((a.K == 2 && tune(46) != 1) || a.K == 3 || a.K == 7) && a.N % WS_BN == 0 && a.C % WS_CK == 0 && a.C <= WS_CMAX &&
          (a.K - 1) * a.dil <= F4_HALOMAX && ws_lds_bytes(a.K) <= 160 * 1024;
 }
 
@@ -4493,7 +4495,7 @@ int fwd4_choice(const Args& a) {
   if (a.N >= 256 && a.rows >= 16384) return tune(38) == 1 && ws8w_ok(a) ? 29 : ws_ok(a) ? 27 : 24;
   if (a.N <= 64 || a.rows < 65536) return 23;
   if (ws8_gen_pick(a)) return 28;
-  if (a.N == 128 && ws_ok(a) && (a.K == 3 || (a.K == 7 && a.pad == 0 && !a.in_elu))) return 27;
+  if (a.N == 128 && ws_ok(a) && (a.K <= 3 || (a.K == 7 && a.pad == 0 && !a.in_elu))) return 27;
   if (a.N == 128 && a.K > 1 && a.pad == 0 && !a.in_elu) return 22;
   return 24;
 }
@@ -4543,7 +4545,7 @@ int fwd4_variant(int v, const Args& a, const void* in, const void* wp, const flo
   // the k7 forwards with their ELU'd 54-row halo (48.6 -> 52.9 us);
   // tools/conv_bench.py.
   if (ws8_gen_pick(a)) return launch_ws8<7, TO, 512, 128, 64>(a, in, wp, bias, aux, res, out, s);
-  if (a.N == 128 && ws_ok(a) && (a.K == 3 || (a.K == 7 && a.pad == 0 && !a.in_elu)))
+  if (a.N == 128 && ws_ok(a) && (a.K <= 3 || (a.K == 7 && a.pad == 0 && !a.in_elu)))
     return launch_ws_k<TO>(a, in, wp, bias, aux, res, out, s);
   // 128-wide k7 dgrad at 2000 samples (pad 0, no input ELU): 128x32 tiles (76.5 -> 62.6 us)
   if (a.N == 128 && a.K > 1 && a.pad == 0 && !a.in_elu)

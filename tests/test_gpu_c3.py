@@ -40,6 +40,10 @@ FWD = [
     ("down128_256_s5", 640, 256, 3, 1, 0, 0, 256, 400, 0, 0),
     ("down256_512_s5", 1280, 512, 3, 1, 0, 0, 512, 80, 0, 0),
     ("up512_256_s5", 512, 1280, 2, 1, 1, 0, 256, 80, 0, 0),
+    # the 2-tap phase-view transposed convs at 400 / 2000 rows per sample
+    # (warp-specialised kernel since round 4, forward and adjoint forms)
+    ("up256_128_s5", 256, 640, 2, 1, 1, 0, 640, 400, 0, 0),
+    ("up128_64_s2", 128, 256, 2, 1, 1, 0, 256, 2000, 0, 0),
 ]
 
 

@@ -39,6 +39,10 @@ SHAPES = [
     ("RU256 1x1 fwd", 25600, 400, 256, 256, 1, 1, 0, Z, 1, 0, 1, 0),
     ("RU256 1x1 dgrad", 25600, 400, 256, 256, 1, 1, 0, Z, 0, 1, 0, 0),
     ("down1 256->128 k3", 128000, 2000, 256, 128, 3, 1, 2, Z, 0, 0, 0, 1),
+    ("up k2 128->256 rep", 128000, 2000, 128, 256, 2, 1, 1, R, 0, 0, 0, 1),
+    ("up k2 dgrad 256->128", 128000, 2000, 256, 128, 2, 1, 0, Z, 0, 0, 0, 0),
+    ("up k2 256->640 rep", 25600, 400, 256, 640, 2, 1, 1, R, 0, 0, 0, 1),
+    ("up k2 dgrad 640->256", 25600, 400, 640, 256, 2, 1, 0, Z, 0, 0, 0, 0),
     ("RU256 k7d1 fwd", 25600, 400, 256, 256, 7, 1, 6, Z, 1, 0, 0, 0),
     ("RU256 k7 dgrad", 25600, 400, 256, 256, 7, 1, 0, Z, 0, 1, 1, 0),
     ("down2 640->256 k3", 25600, 400, 640, 256, 3, 1, 2, Z, 0, 0, 0, 1),
