@@ -128,7 +128,11 @@ C3_CONFIG = "symAD_libritts_24000_hop300"
 FORCE_DDP = os.environ.get("SEL_BENCH_FORCE_DDP", "0") == "1"
 
 
-def c3_setup(dev, B, world, local, graph=False, dtype=torch.bfloat16):
+def c3_setup(dev, B, world, local, graph=False, dtype=torch.bfloat16, batch=None):
+    """The timed C3 step.  batch: an explicit GLOBAL (clean, noise) pair of CPU
+    tensors instead of the synthetic per-rank one (each rank takes its shard):
+    tests/ddp_product_worker.py's "bench" case runs this very step under a
+    process group against one process on the same global batch."""
     from sel import configs
     from sel.convops import precision
     from models.autoencoder.AudioDec import Generator
@@ -164,7 +168,13 @@ def c3_setup(dev, B, world, local, graph=False, dtype=torch.bfloat16):
     sched = torch.optim.lr_scheduler.StepLR(opt, **cfg["generator_scheduler_params"])
     tr = Trainer(steps=0, epochs=0, data_loader={}, model=model, criterion={"mel": mel},
                  optimizer={"generator": opt}, scheduler={"generator": sched}, config=cfg, device=dev)
-    clean, noise = synthetic_batch(B, SR, seed=93 + 2 * int(os.environ.get("RANK", "0")))
+    if batch is None:
+        clean, noise = synthetic_batch(B, SR, seed=93 + 2 * int(os.environ.get("RANK", "0")))
+    else:
+        from sel.dist import shard
+        clean, noise = batch
+        if world > 1:
+            clean, noise = shard(clean), shard(noise)
     clean, noise = clean.to(dev), noise.to(dev)
     if world > 1:
         # batch-global add_noise norms over all ranks' shards (data_utils.py:15-16)
@@ -176,6 +186,7 @@ def c3_setup(dev, B, world, local, graph=False, dtype=torch.bfloat16):
     def step():
         with precision(dtype):
             tr._train_step((mixed, clean))
+    step.trainer, step.generator = tr, G
     return step
 
 

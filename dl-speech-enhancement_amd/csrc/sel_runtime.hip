@@ -76,6 +76,8 @@ int sel_tune(int key, int value) {
   return prev;
 }
 
+int sel_tune_get(int key) { return (key >= 0 && key < 64) ? sel::g_tune[key] : -1; }
+
 }  // extern "C"
 
 // ---------------------------------------------------------------------------

@@ -29,6 +29,22 @@ class VectorQuantize(nn.Module):
         self.register_buffer("embed", embed)
         self.register_buffer("cluster_size", torch.zeros(n_embed))
         self.register_buffer("embed_avg", embed.clone())
+        # bumped by every codebook write this module makes or sees (EMA update,
+        # load_state_dict, .to()/.cuda()); ResidualVQ's stack cache keys on it.
+        # A write that bypasses both (.data / raw device pointers) must call
+        # invalidate_codebook().
+        self._codebook_epoch = 0
+
+    def invalidate_codebook(self):
+        self._codebook_epoch += 1
+
+    def _apply(self, fn, *args, **kwargs):
+        self._codebook_epoch += 1
+        return super()._apply(fn, *args, **kwargs)
+
+    def _load_from_state_dict(self, *args, **kwargs):
+        self._codebook_epoch += 1
+        return super()._load_from_state_dict(*args, **kwargs)
 
     @property
     def codebook(self):
@@ -44,6 +60,7 @@ class VectorQuantize(nn.Module):
             n = self.cluster_size.sum()
             cs = (self.cluster_size + self.eps) / (n + self.n_embed * self.eps) * n
             self.embed.copy_(self.embed_avg / cs.unsqueeze(0))
+        self._codebook_epoch += 1
 
     def forward(self, input):
         flatten = input.reshape(-1, self.dim)
@@ -73,11 +90,14 @@ class ResidualVQ(nn.Module):
 
     def _stacked(self):
         # the (S, D, K) codebook stack, rebuilt only when a codebook changed
-        # (EMA update, load_state_dict, .to(): new storage or a bumped version)
+        # (EMA update, load_state_dict, .to(): a bumped epoch, new storage or
+        # a bumped version; writes through .data or raw pointers must call
+        # VectorQuantize.invalidate_codebook())
         embeds = [l.embed for l in self.layers]
         if any(e.requires_grad for e in embeds):
             return torch.stack(embeds)
-        key = tuple((e.data_ptr(), e._version, e.dtype, e.device) for e in embeds)
+        key = tuple((l._codebook_epoch, e.data_ptr(), e._version, e.dtype, e.device)
+                    for l, e in zip(self.layers, embeds))
         if getattr(self, "_stack_key", None) != key:
             self._stack_cache = torch.stack(embeds)
             self._stack_key = key

@@ -26,6 +26,7 @@ SIGNATURES = {
     "sel_last_error": (ctypes.c_char_p, []),
     "sel_version": (I32, []),
     "sel_tune": (I32, [I32, I32]),
+    "sel_tune_get": (I32, [I32]),
     "sel_probe_buffer_b64": (I32, [P, I32, I32, P, P]),
     "sel_probe_copy_f4": (I32, [P, P, I64, I32, P]),
     "sel_stft_mag_fwd": (I32, [P, I64, I64, I32, I32, I32, P, F32, P, P]),

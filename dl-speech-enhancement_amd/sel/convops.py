@@ -421,7 +421,20 @@ DDP_STATS = {"bucket_flushes": 0, "jobs": 0}
 
 
 def register_grad_buckets(reducer):
-    _REDUCERS.append(weakref.ref(reducer))
+    """A module wrapped again: the older reducer of any of its parameters is
+    detached (hooks removed, dropped from the registry), so exactly one reducer
+    owns a parameter; dead references are pruned."""
+    live = []
+    for ref in _REDUCERS:
+        r = ref()
+        if r is None:
+            continue
+        if any(s[3]() is not None and reducer.owns(s[3]()) for s in list(r.slots.values())):
+            r.detach()
+            continue
+        live.append(ref)
+    live.append(weakref.ref(reducer))
+    _REDUCERS[:] = live
 
 
 def _owner(p):
@@ -654,11 +667,9 @@ def resunit_bwd(d1, gf, h, xf, wd1, wd2, want_gh):
 
 
 def _tune_value(key):
-    """Current value of a sel_tune knob (sel_tune sets and returns the previous one)."""
-    lib = L.lib()
-    v = lib.sel_tune(key, 0)
-    lib.sel_tune(key, v)
-    return v
+    """Current value of a sel_tune knob (read-only: no window in which another
+    thread's dispatch could see it changed)."""
+    return L.lib().sel_tune_get(key)
 
 
 def _ru_bwd_meta(d1, xf, want_gh, wgrad=False):

@@ -14,10 +14,14 @@ flat fp32 buffer, cut into ~4 MB buckets in backward order:
 * when a bucket is complete, its pending reductions run as ONE launch, the
   slice is scaled by 1/W and all-reduced asynchronously (RCCL overlaps the rest
   of the backward);
+* buckets are all-reduced strictly in index order: a complete bucket waits for
+  every lower-indexed one, so all ranks issue the same collectives in the same
+  order whatever order their gradients arrive in;
 * an autograd final callback launches any bucket left incomplete (parameters
-  unused in this backward: their slots are zeroed, .grad stays None) in bucket
-  order, so every rank issues the same collectives, and waits for them all
-  before backward() returns.
+  unused on this rank contribute a zeroed slot) and waits for them all before
+  backward() returns.  One float per parameter ("used here") rides in the last
+  bucket: a parameter some other rank used gets the averaged gradient, one no
+  rank used keeps .grad None (torch DDP with find_unused_parameters).
 
 torch DDP copied every gradient into its bucket and zero-filled buckets each
 step (~0.3-0.4 ms per C3 step on one GPU, profiles/r4_ddp_ab.md); this keeps
@@ -43,29 +47,43 @@ class GradBuckets:
         if any(p.device != dev or p.dtype != torch.float32 for p in params):
             raise ValueError("GradBuckets: fp32 parameters on one device")
         total = sum(p.numel() for p in params)
-        self.flat = torch.zeros(total, dtype=torch.float32, device=dev)
+        # + one "used" flag per parameter after the last gradient: it rides in
+        # the last bucket's all-reduce, so which parameters ANY rank used is
+        # known without a collective of its own (torch DDP's local_used_map)
+        self.nparams = len(params)
+        self.flat = torch.zeros(total + self.nparams, dtype=torch.float32, device=dev)
         cap = max(1, int(bucket_cap_mb * (1 << 20) / 4))
-        self.slots = {}     # id(p) -> (offset, numel, bucket index, weakref(p))
+        self.slots = {}     # id(p) -> (offset, numel, bucket index, weakref(p), flag index)
         self.buckets = []   # [lo, hi, [param ids]]
         off = 0
-        for p in reversed(params):  # backward order ~ reverse registration order
+        for j, p in enumerate(reversed(params)):  # backward order ~ reverse registration order
             if not self.buckets or (self.buckets[-1][1] - self.buckets[-1][0] + p.numel() > cap
                                     and self.buckets[-1][2]):
                 self.buckets.append([off, off, []])
             b = self.buckets[-1]
-            self.slots[id(p)] = (off, p.numel(), len(self.buckets) - 1, weakref.ref(p))
+            self.slots[id(p)] = (off, p.numel(), len(self.buckets) - 1, weakref.ref(p), j)
             b[2].append(id(p))
             off += p.numel()
             b[1] = off
+        self.buckets[-1][1] = off + self.nparams   # the flags
+        self.flags = self.flat.narrow(0, total, self.nparams)
         self._hooks = [p.register_post_accumulate_grad_hook(self._arrived) for p in params]
-        self.stats = {"buckets": 0, "copies": 0}
+        self.stats = {"buckets": 0, "copies": 0, "order": []}
         self._reset()
 
     def _reset(self):
         self.count = [0] * len(self.buckets)
-        self.launched = [False] * len(self.buckets)
+        self.next = 0        # lowest bucket index not yet all-reduced in this backward
+        self.used = set()    # ids of the parameters that took a gradient here
         self.works = []
         self.armed = False
+
+    def detach(self):
+        """Stop reducing (the module was wrapped again): hooks off, nothing owned."""
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+        self.slots = {}
 
     def owns(self, p):
         s = self.slots.get(id(p))
@@ -74,7 +92,7 @@ class GradBuckets:
     def view(self, p):
         """A fresh view of p's slot (a new tensor object each call, so that
         AccumulateGrad can keep it as .grad)."""
-        off, n, _, _ = self.slots[id(p)]
+        off, n = self.slots[id(p)][:2]
         return self.flat.narrow(0, off, n).view(p.shape)
 
     def _arrived(self, p):
@@ -83,7 +101,7 @@ class GradBuckets:
         if not self.armed:
             self.armed = True
             torch.autograd.Variable._execution_engine.queue_callback(self._finish)
-        off, n, bi, _ = self.slots[id(p)]
+        off, n, bi = self.slots[id(p)][:3]
         g = p.grad
         if g.data_ptr() != self.flat.data_ptr() + 4 * off or g.numel() != n or g.dtype != torch.float32:
             # a gradient from outside the sel weight-gradient ops: into the slot
@@ -91,33 +109,52 @@ class GradBuckets:
             v.copy_(g)
             p.grad = v
             self.stats["copies"] += 1
-        self.count[bi] += 1
-        if self.count[bi] == len(self.buckets[bi][2]):
-            self._launch(bi)
+        if id(p) not in self.used:
+            self.used.add(id(p))
+            self.count[bi] += 1
+        # all-reduces leave in bucket-index order on every rank, whatever order
+        # the buckets complete in (RCCL matches collectives by issue order)
+        while self.next < len(self.buckets) and self.count[self.next] == len(self.buckets[self.next][2]):
+            self._launch(self.next)
 
     def _launch(self, bi):
+        assert bi == self.next
         lo, hi, ids = self.buckets[bi]
+        if bi == len(self.buckets) - 1 and self.world > 1:
+            if len(self.used) == self.nparams:
+                self.flags.fill_(1.0)
+            else:
+                f = torch.zeros(self.nparams, dtype=torch.float32)
+                for i in self.used:
+                    f[self.slots[i][4]] = 1.0
+                self.flags.copy_(f, non_blocking=False)
         ps = [self.slots[i][3]() for i in ids]
         CO.flush_params([p for p in ps if p is not None])
         sl = self.flat[lo:hi]
         if self.world > 1:
             sl.div_(self.world)
             self.works.append(dist.all_reduce(sl, group=self.pg, async_op=True))
-        self.launched[bi] = True
+        self.next += 1
         self.stats["buckets"] += 1
+        self.stats["order"].append(bi)
 
     def _finish(self):
-        for bi, (lo, hi, ids) in enumerate(self.buckets):
-            if self.launched[bi]:
-                continue
-            for i in ids:  # parameters that took no gradient in this backward
-                p = self.slots[i][3]()
-                if p is not None and p.grad is None:
-                    off, n, _, _ = self.slots[i]
-                    self.flat.narrow(0, off, n).zero_()
-            self._launch(bi)
+        unused = [i for i in self.slots if i not in self.used]
+        for i in unused:  # parameters that took no gradient here contribute zeros
+            off, n = self.slots[i][:2]
+            self.flat.narrow(0, off, n).zero_()
+        while self.next < len(self.buckets):
+            self._launch(self.next)
         for w in self.works:
             w.wait()
+        if unused and self.world > 1:
+            # a parameter another rank used gets the average (this rank's zeros
+            # included), as under torch DDP; one nobody used keeps .grad None
+            flags = self.flags.tolist()
+            for i in unused:
+                p = self.slots[i][3]()
+                if p is not None and flags[self.slots[i][4]] > 0:
+                    p.grad = self.view(p)
         self._reset()
 
 
@@ -135,7 +172,7 @@ class SelDDP(torch.nn.Module):
                     dist.broadcast(p.data, src=dist.get_global_rank(process_group, 0) if process_group else 0,
                                    group=process_group)
         self.reducer = GradBuckets(module.parameters(), bucket_cap_mb, process_group)
-        CO.register_grad_buckets(self.reducer)
+        CO.register_grad_buckets(self.reducer)   # (detaches an older reducer of these parameters)
 
     def forward(self, *args, **kwargs):
         return self.module(*args, **kwargs)

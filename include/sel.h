@@ -44,6 +44,8 @@ int sel_version(void);
 /* tuning knobs for A/B runs inside one process (key 0: conv fwd kernel variant,
  * 0 = built-in heuristic); returns the previous value. */
 int sel_tune(int key, int value);
+/* current value of a tuning knob, read-only (-1 for a key out of range). */
+int sel_tune_get(int key);
 /* diagnostics: out[2i], out[2i+1] = raw_buffer_load_b64 of x at byte offset 4i
  * (i < n-1) through the STFT kernels' buffer resource (spectral.hip fetch_frame);
  * mode 0: elements taken as scalars, mode 1: __builtin_bit_cast of the vector

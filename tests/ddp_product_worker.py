@@ -23,6 +23,9 @@ Cases:
         gradients), 4 global clips of 1 s, data parallel through sel.ddp (the
         deferred weight-gradient reductions run per gradient bucket, right
         before its all-reduce).
+  bench — bench.py's own C3 step (bench.c3_setup): full width, bf16,
+        sel.optim.Adam, SelDDP with 4 MB buckets, 8 clips per rank (16 global),
+        batch-global add_noise.
   gan — train_denoise.DenoiseStep.model_step in GAN mode (:138-165, :213-263)
         on a reduced-width without-PQC generator + HiFi-GAN discriminator, with
         lambda_snr_loss = 1 so the global SNR surrogate runs; generator and
@@ -114,6 +117,32 @@ def run_pqc(dev, full=False):
                                        if p.requires_grad}}
 
 
+BENCH_CLIPS = 16
+
+
+def run_bench(dev):
+    import bench
+    from sel import dist as D
+    from sel import optim as O
+    g = torch.Generator().manual_seed(4242)
+    clean = 0.1 * torch.randn(BENCH_CLIPS, 1, 24000, generator=g)
+    noise = 0.1 * torch.randn(BENCH_CLIPS, 1, 24000, generator=g)
+    world = D.rank_world()[1]
+    step = bench.c3_setup(dev, BENCH_CLIPS // world, world, 0, batch=(clean, noise))
+    assert isinstance(step.trainer.optimizer["generator"], O.Adam)
+    if world > 1:
+        from sel.ddp import SelDDP
+        assert isinstance(step.trainer.model["generator"], SelDDP)
+    steps = []
+    for _ in range(STEPS):
+        step()
+        tot = step.trainer.total_train_loss
+        steps.append(_floats({k: tot[k] for k in list(tot.keys()) if "loss" in k}))
+    G = step.generator
+    return {"steps": steps, "params": {k: p.detach().cpu().clone() for k, p in G.named_parameters()
+                                       if p.requires_grad}}
+
+
 def run_gan(dev):
     import warnings
     from models.autoencoder_without_PQC.AudioDec import Generator
@@ -146,7 +175,7 @@ def run_gan(dev):
 
 
 def run_case(case, dev):
-    return {"pqc": run_pqc, "c3": lambda d: run_pqc(d, full=True), "gan": run_gan}[case](dev)
+    return {"pqc": run_pqc, "c3": lambda d: run_pqc(d, full=True), "bench": run_bench, "gan": run_gan}[case](dev)
 
 
 def main():

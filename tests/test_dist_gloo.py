@@ -175,6 +175,71 @@ def test_sel_ddp_buckets_average_like_full_batch():
             torch.testing.assert_close(g, gr, rtol=1e-5, atol=1e-6)
 
 
+class _Branches(torch.nn.Module):
+    """Two independent branches (their gradients arrive in the reverse order of
+    their forward), a head used on rank 0 only and a layer no rank uses."""
+
+    def __init__(self):
+        super().__init__()
+        torch.manual_seed(5)
+        self.a = torch.nn.Conv1d(1, 4, 5, padding=2)
+        self.b = torch.nn.Conv1d(1, 6, 3, padding=1)
+        self.head = torch.nn.Linear(4, 3)
+        self.never = torch.nn.Linear(2, 2)
+
+    def loss(self, x, y, rank):
+        if rank == 0:
+            ya, yb = self.a(x), self.b(x)
+        else:  # the other forward order: the backward completes buckets differently
+            yb, ya = self.b(x), self.a(x)
+        loss = torch.nn.functional.l1_loss(ya.mean(1, keepdim=True) + yb.mean(1, keepdim=True), y)
+        if rank == 0:
+            loss = loss + 0.1 * self.head(ya.mean(-1)).square().mean()
+        return loss
+
+
+def _order_case(rank):
+    """sel.ddp: the ranks' gradients arrive in different orders, yet every rank
+    issues its all-reduces in bucket-index order (one-parameter buckets of
+    different sizes: an order mismatch would pair unequal tensors); the head,
+    used on rank 0 only, gets the average on BOTH ranks; the unused layer keeps
+    .grad None; a second wrap of the same module detaches the first reducer."""
+    from sel.ddp import SelDDP
+    from sel import dist as D
+    model = _Branches()
+    first = SelDDP(model, bucket_cap_mb=1e-6)
+    m = SelDDP(model, bucket_cap_mb=1e-6)          # wrapped again: `first` is detached
+    assert not first.reducer.slots and not first.reducer._hooks
+    arrivals = []
+    for name, p in model.named_parameters():
+        p.register_post_accumulate_grad_hook(lambda p, name=name: arrivals.append(name))
+    x, y = _batch()
+    model.zero_grad(set_to_none=True)
+    model.loss(D.shard(x), D.shard(y), rank).backward()
+    assert m.reducer.stats["order"] == list(range(len(m.reducer.buckets)))
+    assert model.never.weight.grad is None and model.never.bias.grad is None
+    assert model.head.weight.grad is not None
+    first_a = min(i for i, n in enumerate(arrivals) if n.startswith("a."))
+    first_b = min(i for i, n in enumerate(arrivals) if n.startswith("b."))
+    names = [n for n, p in model.named_parameters() if p.grad is not None]
+    return [torch.tensor([first_a < first_b])] + [p.grad.clone() for n, p in model.named_parameters()
+                                                    if p.grad is not None] + [torch.tensor(len(names))]
+
+
+def test_sel_ddp_ordered_buckets_and_unused_parameters():
+    out = _run(_order_case)
+    # the two ranks really completed the branches in different orders
+    assert bool(out[0][0]) != bool(out[1][0])
+    model = _Branches()
+    x, y = _batch()
+    ((model.loss(x[:2], y[:2], 0) + model.loss(x[2:], y[2:], 1)) / WORLD).backward()
+    ref = [p.grad for n, p in model.named_parameters() if p.grad is not None]
+    for r in range(WORLD):
+        assert int(out[r][-1]) == len(ref)
+        for g, gr in zip(out[r][1:-1], ref):
+            torch.testing.assert_close(g, gr, rtol=1e-5, atol=1e-7)
+
+
 def _shard_case(rank):
     from sel import dist as D
     t = torch.arange(8)

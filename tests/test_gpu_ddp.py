@@ -77,13 +77,13 @@ def _update_check(p0, ref, got, lr):
             (du_ref ** 2).sum().item())
 
 
-@pytest.mark.parametrize("case", ["pqc", "c3", "gan"])
+@pytest.mark.parametrize("case", ["pqc", "c3", "bench", "gan"])
 def test_ddp_product_step_matches_single_process(gpu, case, tmp_path):
     import ddp_product_worker as W
     ranks = _run_ranks(case, tmp_path)
     assert [tuple(r["rank_world"]) for r in ranks] == [(0, 2), (1, 2)]
     assert all(r["deferred_pending"] == 0 for r in ranks)
-    if case in ("pqc", "c3"):
+    if case in ("pqc", "c3", "bench"):
         # the generator's weight-gradient reductions were deferred under the
         # process group and run by the sel reducer, per bucket
         for r in ranks:
@@ -95,10 +95,16 @@ def test_ddp_product_step_matches_single_process(gpu, case, tmp_path):
     torch.manual_seed(0)
     ref = W.run_case(case, gpu)
     torch.cuda.synchronize()
+    # bench: the bf16 conv kernels are chosen by row count (sel fwd4_choice:
+    # 8 clips per rank put the 256-wide layers at 3,200 rows, under the tiles the
+    # 16-clip process uses), so the two runs round differently in bf16; 1e-3
+    # bounds that (measured 2.6e-4 on the mel loss before any update).  The other
+    # cases run the same kernels on both sides: 1e-5.
+    rtol = 1e-3 if case == "bench" else 1e-5
     for s, ref_s in enumerate(ref["steps"]):
         for name, v in ref_s.items():
             got = sum(r["steps"][s][name] for r in ranks) / len(ranks)
-            assert abs(got - v) <= 1e-5 * abs(v) + 1e-7, (case, s, name, got, v, [r["steps"][s][name] for r in ranks])
+            assert abs(got - v) <= rtol * abs(v) + 1e-7, (case, s, name, got, v, [r["steps"][s][name] for r in ranks])
     # the exchanged terms are load-bearing: without them the rank values would differ
     if case == "pqc":
         sc = [r["steps"][0]["train/spectral_convergence_loss"] for r in ranks]
@@ -114,9 +120,16 @@ def test_ddp_product_step_matches_single_process(gpu, case, tmp_path):
         g[1] += n
         g[2] += num
         g[3] += den
+    # Adam's first steps move each weight by about +-lr whatever the gradient's
+    # size, so a weight whose tiny gradient changes sign costs (4 lr)^2 of
+    # squared error against (2 lr)^2 of update: 0.25% sign changes alone give a
+    # 10% norm-wise error.  The bench case (16 clips, full width, bf16, kernels
+    # chosen by row count, 10k RVQ argmins whose near-ties flip with the
+    # rounding) runs at 0.11: bounded at 0.15, with the 2% flip bound unchanged.
+    nbound = 0.15 if case == "bench" else 0.10
     for name, (flips, tot, num, den) in groups.items():
         assert tot > 0 and flips <= 0.02 * tot, (case, name, flips, tot)
-        assert (num / den) ** 0.5 <= 0.10, (case, name, (num / den) ** 0.5)
+        assert (num / den) ** 0.5 <= nbound, (case, name, (num / den) ** 0.5)
 
 
 def _initial_params(case, dev):
@@ -125,6 +138,12 @@ def _initial_params(case, dev):
     import ddp_product_worker as W
     from sel import configs
     torch.manual_seed(0)
+    if case == "bench":
+        import bench
+        from models.autoencoder.AudioDec import Generator
+        torch.manual_seed(93)   # bench.c3_setup's seed
+        G = Generator(**configs.get(bench.C3_CONFIG)["generator_params"])
+        return {k: p.detach().clone() for k, p in G.named_parameters()}
     if case in ("pqc", "c3"):
         from models.autoencoder.AudioDec import Generator
         cfg = configs.get("symAD_libritts_24000_hop300")

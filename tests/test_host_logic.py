@@ -251,3 +251,13 @@ def test_rvq_codebook_stack_cache_follows_updates():
     sd = {k: v.clone() + 1.0 for k, v in rvq.state_dict().items()}
     rvq.load_state_dict(sd)
     assert torch.equal(rvq._stacked(), torch.stack([l.embed for l in rvq.layers]))
+    # a write through .data bumps no version: invalidate_codebook() is the contract
+    c = rvq._stacked()
+    rvq.layers[2].embed.data.add_(1.0)
+    assert rvq._stacked() is c
+    rvq.layers[2].invalidate_codebook()
+    assert torch.equal(rvq._stacked(), torch.stack([l.embed for l in rvq.layers]))
+    # load_state_dict of the same values into the same storage still rebuilds
+    d = rvq._stacked()
+    rvq.load_state_dict({k: v.clone() for k, v in rvq.state_dict().items()})
+    assert rvq._stacked() is not d
