@@ -17,13 +17,11 @@
 // LDS-staged gout/input tiles, deterministic split reduce.
 #include <algorithm>
 
-#include "sel_common.h"
+#include "conv_common.h"
 
 namespace sel {
 namespace conv {
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 constexpr int CK = 32;  // channels per reduction chunk
 
@@ -31,56 +29,7 @@ template <typename T> struct Pitch;
 template <> struct Pitch<float> { static constexpr int v = 36; };   // 144 B rows: conflict-free b128
 template <> struct Pitch<__bf16> { static constexpr int v = 40; };  // 80 B rows: conflict-free b128
 
-__device__ __forceinline__ float to_f(float v) { return v; }
-__device__ __forceinline__ float to_f(__bf16 v) { return float(v); }
-template <typename T> __device__ __forceinline__ T from_f(float v);
-template <> __device__ __forceinline__ float from_f<float>(float v) { return v; }
-template <> __device__ __forceinline__ __bf16 from_f<__bf16>(float v) { return __bf16(v); }
 
-__device__ __forceinline__ float elu(float v) { return v > 0.f ? v : expm1f(v); }
-__device__ __forceinline__ float elu_grad(float v) { return v > 0.f ? 1.f : expf(v); }
-// bf16 path: the result is rounded to bf16 (8-bit mantissa), so the hardware
-// exp (v_exp_f32, a few ulp of fp32) replaces the libm expm1/exp range reduction.
-__device__ __forceinline__ float elu_fast(float v) { return v > 0.f ? v : __expf(v) - 1.f; }
-// v > 0 ? 1 : exp(v) as one min: exp(v) >= 1 exactly when v >= 0 (monotone
-// hardware exp, exp(0) = 1), so the result is bit-identical to the select
-__device__ __forceinline__ float elu_grad_fast(float v) { return fminf(__expf(v), 1.f); }
-
-// elu_fast over 8 bf16 (round-to-nearest back to bf16), with the log2(e) scale
-// and the -1 as packed fp32 ops: per element the same arithmetic as elu_fast
-// (exp(v) = v_exp_f32(v * log2 e), as __expf lowers), so bit-identical
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ uint4 elu8(uint4 w) {
-  const unsigned in[4] = {w.x, w.y, w.z, w.w};
-  unsigned o[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const f32x2 f = {__uint_as_float(in[q] << 16), __uint_as_float(in[q] & 0xffff0000u)};
-    const f32x2 t = f * 1.44269502f;
-    f32x2 e = {__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};
-    e = e - 1.f;
-    const f32x2 r = {f.x > 0.f ? f.x : e.x, f.y > 0.f ? f.y : e.y};
-    o[q] = __builtin_bit_cast(unsigned, __builtin_convertvector(r, bf16x2));  // v_cvt_pk_bf16_f32
-  }
-  return make_uint4(o[0], o[1], o[2], o[3]);
-}
-
-struct Args {
-  int64_t rows;
-  int T, C, N, K, dil, pad, pad_mode, in_elu, bias_period;
-  // discriminator layers on the warp-specialised kernel (sel_dconv_desc; the
-  // generator's own descriptors set tin_valid = tin_pitch = tout_valid = T,
-  // ldx = C, ldo = N, epi = 0): input rows valid / allocated per sequence and
-  // row pitches, output rows computed per sequence (later rows written as
-  // zeros), epilogue 1 = (v + bias + res) * LeakyReLU'(aux), LeakyReLU if act
-  int tin_valid, tin_pitch, ldx, ldo, tout_valid, epi, act;
-  float slope;
-  // > 0: flat tiling of all sequences' rows as one row space (equal input and
-  // output pitch seq_pitch, zero gaps between sequences): input rows valid where
-  // row % seq_pitch < tin_valid, outputs where row % seq_pitch < tout_valid
-  int seq_pitch;
-};
 
 // Flat input row for (output row m, tap k) or -1 (zero).
 __device__ __forceinline__ int64_t in_row(const Args& a, int64_t m, int k) {
@@ -308,8 +257,6 @@ __global__ __launch_bounds__(256) void k_conv_fwd(Args a, const TI* __restrict__
 // fallback waits.  MFMA: v_mfma_f32_32x32x16_bf16; staged rows are 80 B apart,
 // which makes its 16-B fragment reads bank-conflict free.
 // ---------------------------------------------------------------------------
-typedef float floatx16 __attribute__((ext_vector_type(16)));
-constexpr int F4_HALOMAX = 64;
 // residual-unit kernels' occupancy targets (waves per SIMD the register
 // allocation must allow)
 #ifndef SEL_W_RU32F
@@ -329,30 +276,6 @@ constexpr int F4_HALOMAX = 64;
 #endif
 constexpr int F4_P = 40;  // staged row pitch (bf16 elements) = 80 B
 
-// XCD-aware block order for multi-column-tile launches (1-D grid of
-// row tiles x ncol): workgroups are dealt round-robin over the 8 XCDs, so the
-// ncol column tiles of one row tile are given ids 8 apart (one XCD, adjacent in
-// that XCD's dispatch order) and share the input tile through its L2 instead
-// of each XCD fetching it from HBM.  ncol == 0 means a 2-D (row, column) grid.
-__device__ __forceinline__ void xcd_tile(int ncol, int64_t& mt, int& nt) {
-  if (ncol == 0) {
-    mt = blockIdx.x;
-    nt = blockIdx.y;
-    return;
-  }
-  const int64_t L = blockIdx.x;
-  const int64_t mtiles = int64_t(gridDim.x) / ncol;
-  const int64_t full = (mtiles / 8) * 8 * ncol;
-  if (L < full) {
-    const int64_t q = L >> 3;
-    nt = int(q % ncol);
-    mt = (q / ncol) * 8 + (L & 7);
-  } else {
-    const int64_t r = L - full;
-    nt = int(r % ncol);
-    mt = (mtiles / 8) * 8 + r / ncol;
-  }
-}
 
 template <int BM, int BN, int WAVES_M, int KMAX, typename TO>
 __global__ __launch_bounds__(256) void k_conv_fwd_bf16(Args a, const __bf16* __restrict__ in,
@@ -587,14 +510,7 @@ inline size_t ws_lds_bytes(int K, int cpb = 1) {
   return std::max(size_t(WS_NBUF) * cpb * ws_buf_bytes(K), size_t(WS_BM) * WS_EP * sizeof(float));
 }
 
-// s_waitcnt vmcnt(N) alone (expcnt / lgkmcnt left at their no-wait maxima)
-template <int N>
-__device__ __forceinline__ void ws_wait_vm() {
-  static_assert(N >= 0 && N < 64, "vmcnt");
-  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
-}
 
-typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 // DMA piece of producer wave pw's u-th slot: q = 4u + pw, clamped to the last piece
 template <int TI>
@@ -4486,13 +4402,24 @@ int launch_ws_k(const Args& a, const void* in, const void* wp, const float* bias
 
 // Variant the dispatcher picks for a bf16 forward launch (see fwd4_variant);
 // -1 when the generic (non-pipelined) kernel is used.
+// the sample-tile kernel (conv_wss.hip, variant 30) for the 256-wide layers at
+// T = 400: tune key 47 = 1 on, 2 off, 0 = kWssDefault
+constexpr bool kWssDefault = true;
+bool wss_pick(const Args& a) {
+  const int k = tune(47);
+  return (k == 1 || (k == 0 && kWssDefault)) && a.N >= 256 && a.rows >= 16384 && wss_ok(a);
+}
+
 int fwd4_choice(const Args& a) {
   const int v = tune(0);
   if (!((a.C % CK) == 0 && (a.K - 1) * a.dil <= F4_HALOMAX && a.K <= 8 && (v == 0 || v > 20))) return -1;
-  if (v > 20 && (v != 27 || ws_ok(a)) && (v != 28 || ws8_gen_ok(a)) && (v != 29 || ws8w_ok(a))) return v;
+  if (v > 20 && (v != 27 || ws_ok(a)) && (v != 28 || ws8_gen_ok(a)) && (v != 29 || ws8w_ok(a)) &&
+      (v != 30 || wss_ok(a)))
+    return v;
   if (a.N <= 32 || (a.N % 64) != 0 || a.rows < 8192) return 22;
   if (a.N >= 256 && a.K == 1) return 26;
-  if (a.N >= 256 && a.rows >= 16384) return tune(38) == 1 && ws8w_ok(a) ? 29 : ws_ok(a) ? 27 : 24;
+  if (a.N >= 256 && a.rows >= 16384)
+    return wss_pick(a) ? 30 : tune(38) == 1 && ws8w_ok(a) ? 29 : ws_ok(a) ? 27 : 24;
   if (a.N <= 64 || a.rows < 65536) return 23;
   if (ws8_gen_pick(a)) return 28;
   if (a.N == 128 && ws_ok(a) && (a.K <= 3 || (a.K == 7 && a.pad == 0 && !a.in_elu))) return 27;
@@ -4520,6 +4447,9 @@ int fwd4_variant(int v, const Args& a, const void* in, const void* wp, const flo
       if (!ws8w_ok(a)) break;
       if (a.K == 7) return launch_ws8<7, TO, 256, 128, 64, 2>(a, in, wp, bias, aux, res, out, s);
       return launch_ws8<3, TO, 256, 128, 64, 2>(a, in, wp, bias, aux, res, out, s);
+    case 30:
+      if (!wss_ok(a)) break;
+      return launch_wss<TO>(a, in, wp, bias, aux, res, out, s);
     default: break;
   }
   // heuristic from tools/conv_bench.py on the C3 layer shapes (profiles/r1_conv_bench.md):
@@ -4534,6 +4464,7 @@ int fwd4_variant(int v, const Args& a, const void* in, const void* wp, const flo
   // RU256 k7 fwd+dgrad 43.5 -> 38.4 us, down2 46.6 -> 41.8), else 256x64 tiles
   // (RU256 k7 fwd 50.7 -> 36.2 us, dgrad 54.2 -> 43.0, down2 51.2 -> 43.1)
   if (a.N >= 256 && a.rows >= 16384) {
+    if (wss_pick(a)) return launch_wss<TO>(a, in, wp, bias, aux, res, out, s);
     if (tune(38) == 1 && ws8w_ok(a)) return fwd4_variant<KMAX, TO>(29, a, in, wp, bias, aux, res, out, s);
     if (ws_ok(a)) return launch_ws_k<TO>(a, in, wp, bias, aux, res, out, s);
     return launch_fwd4<256, 64, 4, KMAX, TO>(a, in, wp, bias, aux, res, out, s);
@@ -5175,6 +5106,7 @@ int sel_conv_fwd_kernel_id(const sel_conv_desc* d, int in_dtype, int out_dtype, 
   if (v == 27) return 900000000 + a.K;
   if (v == 28) return 910000000 + a.K;
   if (v == 29) return 920000000 + a.K;
+  if (v == 30) return 940000000 + a.K;
   const int kmax = a.K == 1 ? 1 : (a.K <= 3 ? 3 : 8);
   static const int bm[] = {256, 128, 128, 256, 128, 64}, bn[] = {32, 32, 64, 64, 128, 128}, wm[] = {4, 4, 2, 4, 2, 1};
   const int i = v - 21;

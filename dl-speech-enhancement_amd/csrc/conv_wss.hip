@@ -1,0 +1,423 @@
+// Sample-tile warp-specialised conv (k_conv_wss): the conv primitive of
+// conv.hip (include/sel.h sel_conv_fwd) for short sequences, T <= 400 — the
+// C3 generator's 256-wide stage: the RU256 k7 convs and their adjoints
+// (models/autoencoder/modules/residual_unit.py:43-46 over
+// layers/conv_layer.py:139-142), the stride-5 down conv in its phase-packed
+// 3-tap form and the 2-tap transposed conv (conv_layer.py:180-183).
+//
+// Why a second warp-specialised kernel.  k_conv_ws_bf16 computes 256 x 128
+// tiles: a 400-row sample takes two row tiles, the second 56% useful, so the
+// chip computes 1.28x the outputs, one tile per CU, 8 waves of 64 x 64.
+// Here one tile is a WHOLE sample x 64 output channels (B x N/64 tiles: 256 at
+// C3), so no output row is computed twice or padded beyond the 16-row MFMA
+// strip (400 = 25 strips of 16), and the 25 strips are dealt so every SIMD gets
+// the same MFMA count:
+//   - 4 consumer waves (one per SIMD) on v_mfma_f32_16x16x32_bf16; wave w owns
+//     Q = S/4 full strips (all 4 column strips: 4Q accumulators) plus R = S%4
+//     (strip, column-strip) pairs of the last S%4 strips: 4Q + R MFMAs per
+//     (tap, 32-channel chunk) on every SIMD (25 at S = 25);
+//   - per tap a wave reads 4 + 1 weight fragments and Q + R input fragments
+//     (ds_read_b128) for 4Q + R MFMAs (0.48 reads per 16-cycle MFMA at S = 25);
+//   - 4 producer waves DMA each 32-channel chunk (the input span of T + halo
+//     rows and the KT x 64 weight rows, 64-B LDS rows, global_load_lds_dwordx4
+//     1-KB pieces) into a 2-slot ring one chunk ahead and apply the input ELU
+//     in place (each lane rewrites the 16 B its own DMA landed).
+// LDS rows are 64 B: 16-B slot p of row r holds source slot p ^ wss_swz(r), so
+// the 16 lanes of each ds_read_b128 lane group hit 16 distinct 16-B bank groups
+// (the DMA destination is lane-linear: the swizzle is applied to the source).
+// Epilogue: accumulators -> fp32 [T][64 + 4] tile over the drained ring, then
+// all 8 waves write 16-B row-contiguous output vectors with the bias, ELU'(aux)
+// and residual terms of the conv.hip epilogue (same order, same roundings).
+// The MFMA shape differs from k_conv_ws_bf16's 32x32x16, so the fp32 sums are
+// ordered differently: outputs agree to bf16 rounding, not bit for bit
+// (tests/test_gpu_c3.py checks every variant against fp64 of the same operands).
+#include "conv_common.h"
+
+namespace sel {
+namespace conv {
+
+constexpr int WSS_BN = 64;                 // output channels per tile
+constexpr int WSS_CK = 32;                 // channels per chunk = one MFMA k-step
+constexpr int WSS_ROWB = WSS_CK * 2;       // bytes per LDS row
+constexpr int WSS_RPP = 1024 / WSS_ROWB;   // LDS rows per 1-KB DMA piece
+constexpr int WSS_EP = WSS_BN + 4;         // fp32 epilogue tile pitch
+constexpr int WSS_CMAX = 4096;             // input channels the zero source covers
+constexpr int WSS_NB = 2;                  // ring slots
+
+__device__ __attribute__((aligned(64))) __bf16 g_wss_zero[WSS_CMAX];
+
+template <int KT, int S>
+struct WssGeo {
+  static constexpr int Q = S / 4, R = S % 4;
+  static constexpr int XROWS = (S * 16 + F4_HALOMAX + WSS_RPP - 1) / WSS_RPP * WSS_RPP;  // staged input rows
+  static constexpr int XI = XROWS / WSS_RPP;            // input DMA pieces per chunk
+  static constexpr int WI = KT * WSS_BN / WSS_RPP;      // weight DMA pieces per chunk
+  static constexpr int TI = XI + WI;
+  static constexpr int PW = (TI + 3) / 4;               // pieces per producer wave
+  static constexpr int SLOT = (XROWS + KT * WSS_BN) * WSS_ROWB;
+  static constexpr int RING = WSS_NB * SLOT;
+  static constexpr int EPI = S * 16 * WSS_EP * 4;
+  static constexpr int LDS = RING > EPI ? RING : EPI;
+};
+
+// 16-B slot XOR of LDS row `row`: ds_read_b128 serves a wave in four 16-lane
+// groups {0-3, 12-15, 20-27}, {4-11, 16-19, 28-31} (+32); a fragment read puts
+// lanes l on rows r0 + (l & 15), slot l >> 4, so each group holds rows r0 + j
+// for every j mod 16, in slots that differ by bit 0.  With (row >> 1) & 2 the
+// 16 lanes of every group hit 16 distinct 16-B bank groups for ANY r0 (the taps
+// shift r0 by k * dil), brute-force checked; (row >> 2) & 3 left them 2-way
+// (PMC: SQ_LDS_BANK_CONFLICT 44% of SQ_LDS_IDX_ACTIVE).
+__device__ __forceinline__ int wss_swz(int row) { return (row >> 1) & 2; }
+
+template <int KT, int S, typename TO>
+__global__ __launch_bounds__(512) void k_conv_wss(Args a, const __bf16* __restrict__ in,
+                                                  const __bf16* __restrict__ wp, const float* __restrict__ bias,
+                                                  const TO* __restrict__ aux, const TO* __restrict__ res,
+                                                  TO* __restrict__ out, int ncol, int dbg) {
+  using G = WssGeo<KT, S>;
+  constexpr int Q = G::Q, R = G::R, XR = G::XROWS, XI = G::XI, TI = G::TI, PW = G::PW;
+  static_assert(2 * PW < 64, "vmcnt range");
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  int64_t b;
+  int nt;
+  xcd_tile(ncol, b, nt);
+  const int T = a.T;
+  const int64_t m0 = b * T;
+  const int n0 = nt * WSS_BN;
+  const int nchunk = a.C / WSS_CK;
+  const int span = T + (KT - 1) * a.dil;
+  // diagnostic (tune key 48 bit 4): s_memtime stamps of block phases, written
+  // over the first output bytes at the end (st[0] start, [1] first chunk ready,
+  // [2] consumer loop done, [3] tile in LDS, [4] end, [5]/[6] realtime start/end)
+  uint64_t st[5] = {0, 0, 0, 0, 0};
+  uint64_t rt0 = 0;
+  if (dbg & 16) {
+    st[0] = __builtin_amdgcn_s_memtime();
+    rt0 = __builtin_amdgcn_s_memrealtime();
+  }
+
+  // epilogue operands: thread t owns the 16-B output vectors v = t + 512 u; their
+  // ELU'(aux) and residual rows are requested early (producers after their
+  // last DMA, consumers right after their MFMAs) so the epilogue does not wait
+  // on HBM
+  struct alignas(16) V8 { TO v[8]; };
+  constexpr int NT = 512, EV = (S * 16 * (WSS_BN / 8) + NT - 1) / NT;
+  const int nvec = T * (WSS_BN / 8);
+  V8 av[EV], rv[EV];
+  auto prefetch_epi = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < EV; ++u) {
+      const int v = tid + u * NT;
+      if (v >= nvec) break;
+      const int64_t o = (m0 + (v >> 3)) * a.N + n0 + (v & 7) * 8;
+      if (aux) av[u] = *reinterpret_cast<const V8*>(aux + o);
+      if (res) rv[u] = *reinterpret_cast<const V8*>(res + o);
+    }
+  };
+
+  if (wave >= 4) {
+    // ---------------- producers ----------------
+    const int pw = wave - 4;
+    const __bf16* src[PW];
+#pragma unroll
+    for (int u = 0; u < PW; ++u) {
+      const int q = u * 4 + pw < TI ? u * 4 + pw : TI - 1;  // a wave short of PW repeats the last piece
+      const int rr = (q < XI ? q : q - XI) * WSS_RPP + (lane >> 2);
+      const int ls = (lane & 3) ^ wss_swz(rr);
+      if (q < XI) {
+        int ti = rr - a.pad;
+        const bool valid = rr < span && ((ti >= 0 && ti < T) || a.pad_mode == SEL_PAD_REPLICATE);
+        ti = ti < 0 ? 0 : (ti >= T ? T - 1 : ti);
+        src[u] = valid ? in + (m0 + ti) * a.C + 8 * ls : g_wss_zero + 8 * ls;
+      } else {
+        const int k = rr / WSS_BN, n = rr % WSS_BN;
+        src[u] = wp + (int64_t(n0 + n) * KT + k) * a.C + 8 * ls;
+      }
+    }
+    const int xi_used = (span + WSS_RPP - 1) / WSS_RPP;  // input pieces holding rows < span
+    auto issue = [&](int ch) __attribute__((always_inline)) {
+      unsigned char* const base = smem + (ch % WSS_NB) * G::SLOT;
+#pragma unroll
+      for (int u = 0; u < PW; ++u) {
+        const int q = u * 4 + pw < TI ? u * 4 + pw : TI - 1;
+        const int off = q < XI ? q * 1024 : XR * WSS_ROWB + (q - XI) * 1024;
+        if (q >= xi_used && q < XI) continue;  // rows past the span: never read
+        if (dbg & 2) continue;  // diagnostic (tune key 48 bit 1): no DMA
+        __builtin_amdgcn_global_load_lds((const void*)(src[u] + ch * WSS_CK), (lds_ptr_t)(base + off), 16, 0, 0);
+      }
+    };
+    // in-place ELU of this wave's input pieces (q = 4u + pw): the eight reads
+    // and their wait in ONE asm statement (reads past the input pieces land in
+    // the weight slices and are not written back), then ELU + write back.
+    // Inline asm: a plain LDS access here would make hipcc drain vmcnt (the next
+    // chunk's DMA) first; one statement: the compiler cannot hoist a use of a
+    // result above the wait.
+    constexpr int PX = (XI + 3) / 4;
+    static_assert(PX == 8 && XR * WSS_ROWB + G::WI * 1024 >= (4 * (PX - 1) + 3 + 1) * 1024, "ELU pass pieces");
+    auto elu_pass = [&](int ch) __attribute__((always_inline)) {
+      unsigned char* const base = smem + (ch % WSS_NB) * G::SLOT + lane * 16 + pw * 1024;
+      const unsigned addr = unsigned(reinterpret_cast<uintptr_t>(base));
+      bf16x8 v[PX];
+      asm volatile(
+          "ds_read_b128 %0, %8\n\t"
+          "ds_read_b128 %1, %8 offset:4096\n\t"
+          "ds_read_b128 %2, %8 offset:8192\n\t"
+          "ds_read_b128 %3, %8 offset:12288\n\t"
+          "ds_read_b128 %4, %8 offset:16384\n\t"
+          "ds_read_b128 %5, %8 offset:20480\n\t"
+          "ds_read_b128 %6, %8 offset:24576\n\t"
+          "ds_read_b128 %7, %8 offset:28672\n\t"
+          "s_waitcnt lgkmcnt(0)"
+          : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]), "=&v"(v[7])
+          : "v"(addr)
+          : "memory");
+#pragma unroll
+      for (int u = 0; u < PX; ++u) {
+        const int q = u * 4 + pw;
+        if (q >= XI || q >= xi_used) break;
+        const bf16x8 e = __builtin_bit_cast(bf16x8, elu8(__builtin_bit_cast(uint4, v[u])));
+        asm volatile("ds_write_b128 %0, %1 offset:%2" : : "v"(addr), "v"(e), "i"(u * 4096) : "memory");
+      }
+    };
+    // prologue: chunk 0 alone first (every CU bursts at once: one chunk lands
+    // in about half the time of two), chunk 1 behind it, over chunk 0's ELU
+    issue(0);
+    ws_wait_vm<0>();
+    if (nchunk > 1) issue(1);
+    if (a.in_elu && !(dbg & 4)) elu_pass(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    for (int ch = 0; ch < nchunk; ++ch) {
+      // the consumers compute chunk ch; chunk ch + 1 (the only DMA in flight) lands, then its ELU
+      if (ch + 1 < nchunk) {
+        ws_wait_vm<0>();
+        if (ch + 2 == nchunk) prefetch_epi();  // the last DMA has landed
+        if (a.in_elu && !(dbg & 4)) elu_pass(ch + 1);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      // slot ch % 2 is free now
+      if (ch + 2 < nchunk) issue(ch + 2);
+    }
+  } else {
+    // ---------------- consumers ----------------
+    const int w = wave;
+    const int l16 = lane & 15, kq = lane >> 4;
+    // lane's byte offset within a 16-row group of weight rows (row = 16 cs + l16
+    // of tap k's 64 rows; the swizzle depends on l16 only) and the extra pairs
+    const int lane_w = l16 * WSS_ROWB + ((kq ^ wss_swz(l16)) << 4);
+    int xstrip[R > 0 ? R : 1], xcol[R > 0 ? R : 1];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const int p = w * R + i;
+      xstrip[i] = 4 * Q + p / 4;
+      xcol[i] = p % 4;
+    }
+    floatx4 acc[Q][4], accx[R > 0 ? R : 1];
+#pragma unroll
+    for (int i = 0; i < Q; ++i)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[i][c] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < R; ++i) accx[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    bf16x8 fw[2][4], fx[2][Q], fwx[2][R > 0 ? R : 1], fxx[2][R > 0 ? R : 1];
+    // fragments of tap k of the chunk in ring slot sl into buffer q
+    static_assert(WSS_NB == 2, "two chunks per trip, one per ring slot");
+    auto fetch = [&](int sl, int k, int q) __attribute__((always_inline)) {
+      const unsigned char* const xb = smem + sl * G::SLOT;
+      const unsigned char* const xw = xb + w * Q * 1024;  // this wave's first full strip
+      const unsigned char* const wb = xb + XR * WSS_ROWB;
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        fw[q][c] = *reinterpret_cast<const bf16x8*>(wb + (k * WSS_BN + c * 16) * WSS_ROWB + lane_w);
+      const int r = l16 + k * a.dil;  // + 16 s: the swizzle of row r + 16 s is r's
+      int lx = r * WSS_ROWB + ((kq ^ wss_swz(r)) << 4);
+      // computed here, per fetch (a few VALU): hoisted out of the loop, the
+      // 2 x KT per-step addresses would take the registers the pipeline needs
+      asm volatile("" : "+v"(lx));
+#pragma unroll
+      for (int i = 0; i < Q; ++i) fx[q][i] = *reinterpret_cast<const bf16x8*>(xw + i * 1024 + lx);
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        fwx[q][i] = *reinterpret_cast<const bf16x8*>(wb + (k * WSS_BN + xcol[i] * 16) * WSS_ROWB + lane_w);
+        fxx[q][i] = *reinterpret_cast<const bf16x8*>(xb + xstrip[i] * 1024 + lx);
+      }
+    };
+    auto mfmas = [&](int q) __attribute__((always_inline)) {
+#pragma unroll
+      for (int i = 0; i < Q; ++i)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[q][c], fx[q][i], acc[i][c], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < R; ++i)
+        accx[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fwx[q][i], fxx[q][i], accx[i], 0, 0, 0);
+    };
+
+    __syncthreads();
+    if (dbg & 16) st[1] = __builtin_amdgcn_s_memtime();
+    __builtin_amdgcn_s_setprio(2);
+    if (dbg & 1) {  // diagnostic (tune key 48 bit 0): consumers skip the MFMA phase
+      for (int ch = 0; ch < nchunk; ++ch) __builtin_amdgcn_s_barrier();
+    } else {
+      // one software pipeline over the (chunk, tap) steps, two chunks per trip so
+      // the fragment buffer of every step is a compile-time index: step (ch, k)
+      // issues the reads of the next step before its own MFMAs.  At a chunk's
+      // last tap the wave's reads of that chunk are all done, so it meets the
+      // producers' barrier there (slot ch free for chunk ch + 2, chunk ch + 1
+      // ready) and the first reads of chunk ch + 1 overlap the last tap's MFMAs.
+      fetch(0, 0, 0);
+      for (int ch = 0; ch < nchunk; ch += 2) {
+#pragma unroll
+        for (int i = 0; i < 2 * KT; ++i) {
+          // chunk ch + i / KT (ch even) sits in ring slot i / KT
+          const int sl = i / KT, k = i % KT, q = i & 1;
+          if (k + 1 < KT) {
+            fetch(sl, k + 1, q ^ 1);
+          } else {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            fetch(sl ^ 1, 0, q ^ 1);  // (after the last chunk: a dead read of the other slot, no branch)
+          }
+          mfmas(q);
+          // the next step's reads go out between this step's MFMAs (one per
+          // two), not as a burst that leaves the matrix pipe idle
+          constexpr int NRD = 4 + Q + 2 * R, NMF = 4 * Q + R;
+          constexpr int REST = NMF > 2 * NRD ? NMF - 2 * NRD : 0;
+#pragma unroll
+          for (int j = 0; j < NRD; ++j) {
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // one DS read
+            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // two MFMAs
+          }
+          if (REST > 0) __builtin_amdgcn_sched_group_barrier(0x008, REST, 0);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    }
+    __builtin_amdgcn_s_setprio(0);
+    if (dbg & 16) st[2] = __builtin_amdgcn_s_memtime();
+    prefetch_epi();
+    // accumulators -> fp32 [S*16][64 + 4] tile over the drained ring: lane ->
+    // time row 16 s + l16, channels 16 c + 4 kq .. + 3
+    float* const tile = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int i = 0; i < Q; ++i)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        *reinterpret_cast<floatx4*>(tile + ((w * Q + i) * 16 + l16) * WSS_EP + c * 16 + 4 * kq) = acc[i][c];
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+      *reinterpret_cast<floatx4*>(tile + (xstrip[i] * 16 + l16) * WSS_EP + xcol[i] * 16 + 4 * kq) = accx[i];
+  }
+  // (a raw barrier: __syncthreads() would also wait for the prefetched rows)
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (dbg & 16) st[3] = __builtin_amdgcn_s_memtime();
+
+  // epilogue by all 8 waves: 8 consecutive channels per thread, row-contiguous
+  // 16-B accesses (aux / res fetched for every vector first); k_conv_ws_bf16's
+  // term order
+  const float* const tile = reinterpret_cast<const float*>(smem);
+#pragma unroll
+  for (int u = 0; u < EV; ++u) {
+    const int v = tid + u * NT;
+    if (v >= nvec) break;
+    const int row = v >> 3, c8 = (v & 7) * 8;
+    const int64_t o = (m0 + row) * a.N + n0 + c8;
+    const floatx4 lo = *reinterpret_cast<const floatx4*>(tile + row * WSS_EP + c8);
+    const floatx4 hi = *reinterpret_cast<const floatx4*>(tile + row * WSS_EP + c8 + 4);
+    float x[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    if (bias && a.bias_period) {
+      if (a.bias_period % 8 == 0) {
+        const float* const bp = bias + (n0 + c8) % a.bias_period;
+        const floatx4 b0 = *reinterpret_cast<const floatx4*>(bp), b1 = *reinterpret_cast<const floatx4*>(bp + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[e] += b0[e], x[e + 4] += b1[e];
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x[e] += bias[(n0 + c8 + e) % a.bias_period];
+      }
+    }
+    if (aux) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] *= elu_grad_fast(to_f(av[u].v[e]));
+    }
+    if (res) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] += to_f(rv[u].v[e]);
+    }
+    V8 ov;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) ov.v[e] = from_f<TO>(x[e]);
+    if (!(dbg & 8)) *reinterpret_cast<V8*>(out + o) = ov;  // bit 3: diagnostic without the stores
+  }
+  if (dbg & 16) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (lane == 0) reinterpret_cast<uint64_t*>(out)[int64_t(blockIdx.x) * 16 + 8 + wave] = st[0];  // each wave's start
+    if (tid == 0) {
+      uint64_t* const d = reinterpret_cast<uint64_t*>(out) + int64_t(blockIdx.x) * 16;
+      d[0] = st[0];
+      d[1] = st[1];
+      d[2] = st[2];
+      d[3] = st[3];
+      d[4] = __builtin_amdgcn_s_memtime();
+      d[5] = rt0;
+      d[6] = __builtin_amdgcn_s_memrealtime();
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+constexpr int WSS_S = 25;  // the compiled strip count: 384 < T <= 400
+
+bool wss_ok(const Args& a) {
+  const int S = (a.T + 15) / 16;
+  const bool kt = a.K == 7 || a.K == 3 || a.K == 2;
+  return kt && S == WSS_S && a.N % WSS_BN == 0 && a.C % (2 * WSS_CK) == 0 && a.C <= WSS_CMAX &&
+         (a.K - 1) * a.dil <= F4_HALOMAX && a.pad <= (a.K - 1) * a.dil && a.seq_pitch == 0 && a.epi == 0 &&
+         a.tin_valid == a.T && a.tin_pitch == a.T && a.tout_valid == a.T && a.ldx == a.C && a.ldo == a.N &&
+         a.rows % a.T == 0;
+}
+
+template <int KT, typename TO>
+static int launch_wss_t(const Args& a, const void* in, const void* wp, const float* bias, const void* aux,
+                        const void* res, void* out, hipStream_t s) {
+  using G = WssGeo<KT, WSS_S>;
+  static_assert(G::LDS <= 160 * 1024, "LDS");
+  const int64_t tiles = a.rows / a.T;
+  const int ncol = a.N / WSS_BN;
+  if (tiles == 0) return SEL_OK;
+  SEL_REQUIRE(tiles * ncol < (int64_t(1) << 31), SEL_ERR_UNSUPPORTED, "k_conv_wss: grid too large");
+  auto kern = k_conv_wss<KT, WSS_S, TO>;
+  SEL_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, int(G::LDS)));
+  hipLaunchKernelGGL(kern, dim3(unsigned(tiles * ncol)), dim3(512), G::LDS, s, a, static_cast<const __bf16*>(in),
+                     static_cast<const __bf16*>(wp), bias, static_cast<const TO*>(aux), static_cast<const TO*>(res),
+                     static_cast<TO*>(out), ncol, tune(48));
+  SEL_LAUNCH_CHECK();
+  return SEL_OK;
+}
+
+template <typename TO>
+int launch_wss(const Args& a, const void* in, const void* wp, const float* bias, const void* aux, const void* res,
+               void* out, hipStream_t s) {
+  SEL_REQUIRE(wss_ok(a), SEL_ERR_ARG, "k_conv_wss: unsupported shape T=%d C=%d N=%d K=%d dil=%d", a.T, a.C, a.N,
+              a.K, a.dil);
+  switch (a.K) {
+    case 7: return launch_wss_t<7, TO>(a, in, wp, bias, aux, res, out, s);
+    case 3: return launch_wss_t<3, TO>(a, in, wp, bias, aux, res, out, s);
+    default: return launch_wss_t<2, TO>(a, in, wp, bias, aux, res, out, s);
+  }
+}
+
+template int launch_wss<__bf16>(const Args&, const void*, const void*, const float*, const void*, const void*, void*,
+                                hipStream_t);
+template int launch_wss<float>(const Args&, const void*, const void*, const float*, const void*, const void*, void*,
+                               hipStream_t);
+
+}  // namespace conv
+}  // namespace sel

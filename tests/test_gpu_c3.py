@@ -3,7 +3,10 @@
 1. Every bf16 tile variant of the MFMA conv primitive (tune key 0 = 21..27,
    conv.hip fwd4_variant; 27 = the warp-specialised k_conv_ws_bf16, 28 / 29 =
    its eight-wave forms k_conv_ws8 (512 x 128 tiles of 128 x 64 wave tiles /
-   256 x 128 of 64 x 64), bit-identical to 27 where they apply)
+   256 x 128 of 64 x 64), bit-identical to 27 where they apply; 30 = the
+   sample-tile kernel k_conv_wss of conv_wss.hip, whole 400-row samples x 64
+   channels on 16x16x32 MFMAs: another fp32 summation order, so it is held to
+   the fp64 bound only)
    on the real C3 layer shapes in primitive form,
    forward and dgrad (adjoint) forms, against an fp64 reference computed from
    the SAME bf16 operands.  Both accumulate exact bf16 products (fp32 vs fp64
@@ -113,12 +116,12 @@ def test_fwd4_tile_variants_on_c3_shapes(gpu, shape, form):
     p42 = lib.sel_tune(42, 1)  # and so would the pointwise kernel on the 1x1 shapes
     try:
         default_name = CO.fwd_kernel_name(d, torch.bfloat16, torch.bfloat16)
-        assert default_name.startswith(("k_conv_fwd_bf16", "k_conv_ws_bf16", "k_conv_ws8")), default_name
+        assert default_name.startswith(("k_conv_fwd_bf16", "k_conv_ws_bf16", "k_conv_ws8", "k_conv_wss")), default_name
         default = CO.prim(d, x, wp, bias=b, aux=a_, res=r_).clone()
         _check(default, ref, (form, "default", default_name))
         matched = False
         ws = {}
-        for v in range(21, 30):
+        for v in range(21, 31):
             p0 = lib.sel_tune(0, v)
             try:
                 name = CO.fwd_kernel_name(d, torch.bfloat16, torch.bfloat16)

@@ -80,7 +80,8 @@ def run(shape, variant, iters=20):
     L.lib().sel_tune(6, 127 if variant in (32, 33, 36, 37) else 0)
     L.lib().sel_tune(12, 127 ^ 0b101 if variant in (34, 36) else 0)
     L.lib().sel_tune(11, 1 if variant in (35, 37) else 0)
-    L.lib().sel_tune(0, 0 if thin or variant == 0 else variant)
+    # 50: the sample-tile kernel k_conv_wss (tune key 0 = 30)
+    L.lib().sel_tune(0, 0 if thin or variant == 0 else (30 if variant == 50 else variant))
     try:
         for _ in range(3):
             y = CO.prim(d, x, wp, bias=b, aux=a_, res=r_)
