@@ -461,8 +461,9 @@ def stft_kernel_roofline(dev, B=2048):
     256 MB Infinity Cache, so nothing is served from it across launches), timed
     with a HIP event pair around each launch on its stream, against the 8 TB/s
     spec and against two measured copy rates of this box: a float4 stream-copy
-    kernel (sel_probe_copy_f4, 4 x 16-B loads in flight per thread, one resident
-    round of workgroups) and torch's copy_, each over 1 GiB buffers."""
+    kernel (sel_probe_copy_f4: each workgroup copies one contiguous 16-KB piece,
+    4 x 16-B nontemporal loads in flight per thread, tools/copy_probe.py) and
+    torch's copy_, each over 1 GiB buffers."""
     from sel import _lib as L
     T, (n, h, w) = SR, STFT_RES[0]
     F, K = 1 + T // h, n // 2 + 1

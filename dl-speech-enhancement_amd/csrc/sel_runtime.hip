@@ -126,6 +126,7 @@ extern "C" int sel_probe_buffer_b64(const float* x, int n, int mode, float* out,
 // HBM sustains for a plain read + write of the same bytes.
 // ---------------------------------------------------------------------------
 namespace {
+// grid-stride form (mode 1, the round-1 probe): 4 x 16-B loads in flight per thread
 __global__ __launch_bounds__(256) void k_probe_copy_f4(const float4* __restrict__ src, float4* __restrict__ dst,
                                                        int64_t n) {
   const int64_t stride = int64_t(gridDim.x) * 256 * 4;
@@ -139,12 +140,66 @@ __global__ __launch_bounds__(256) void k_probe_copy_f4(const float4* __restrict_
       if (i + u * 256 < n) dst[i + u * 256] = v[u];
   }
 }
+// one-shot form (default): every workgroup copies one contiguous 256 x U x 16-B
+// piece (no loop, U loads in flight per thread), the grid covers the buffer;
+// NT: nontemporal loads and stores (the copied bytes are not re-read)
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void k_probe_copy_once(const float4* __restrict__ src, float4* __restrict__ dst,
+                                                         int64_t n) {
+  const int64_t i = int64_t(blockIdx.x) * 256 * U + threadIdx.x;
+  float4 v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if (i + u * 256 < n) {
+      if (NT) {
+        const float4* p = src + i + u * 256;
+        v[u] = make_float4(__builtin_nontemporal_load(&p->x), __builtin_nontemporal_load(&p->y),
+                           __builtin_nontemporal_load(&p->z), __builtin_nontemporal_load(&p->w));
+      } else {
+        v[u] = src[i + u * 256];
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if (i + u * 256 < n) {
+      if (NT) {
+        float4* p = dst + i + u * 256;
+        __builtin_nontemporal_store(v[u].x, &p->x);
+        __builtin_nontemporal_store(v[u].y, &p->y);
+        __builtin_nontemporal_store(v[u].z, &p->z);
+        __builtin_nontemporal_store(v[u].w, &p->w);
+      } else {
+        dst[i + u * 256] = v[u];
+      }
+    }
+  }
+}
 }  // namespace
 
+// mode (tune key 49): 0 = one-shot, 4 loads in flight, nontemporal (5.91 TB/s
+// on 1 GiB, tools/copy_probe.py); 1 = the grid-stride form over `blocks`
+// workgroups (the round-1..4 probe, 5.07-5.17 TB/s at 4-32 blocks per CU);
+// 2 / 3 = one-shot, 8 in flight, plain / nontemporal (3.61 / 5.65); 4 =
+// one-shot, 4 in flight, plain (5.37)
 extern "C" int sel_probe_copy_f4(const void* src, void* dst, int64_t n16, int blocks, sel_stream_t stream) {
   SEL_REQUIRE(src && dst && n16 > 0 && blocks > 0, SEL_ERR_ARG, "bad copy probe arguments");
-  hipLaunchKernelGGL(k_probe_copy_f4, dim3(unsigned(blocks)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
-                     static_cast<const float4*>(src), static_cast<float4*>(dst), n16);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const float4* in = static_cast<const float4*>(src);
+  float4* out = static_cast<float4*>(dst);
+  const int mode = sel::tune(49);
+  auto once = [&](auto kern, int U) {
+    const int64_t g = (n16 + 256 * U - 1) / (256 * U);
+    hipLaunchKernelGGL(kern, dim3(unsigned(g)), dim3(256), 0, s, in, out, n16);
+  };
+  SEL_REQUIRE(n16 / 1024 < (int64_t(1) << 31), SEL_ERR_ARG, "copy probe buffer too large");
+  switch (mode) {
+    case 1: hipLaunchKernelGGL(k_probe_copy_f4, dim3(unsigned(blocks)), dim3(256), 0, s, in, out, n16); break;
+    case 2: once(k_probe_copy_once<8, false>, 8); break;
+    case 3: once(k_probe_copy_once<8, true>, 8); break;
+    case 4: once(k_probe_copy_once<4, false>, 4); break;
+    default: once(k_probe_copy_once<4, true>, 4); break;
+  }
   SEL_LAUNCH_CHECK();
   return SEL_OK;
 }
