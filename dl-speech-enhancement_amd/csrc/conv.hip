@@ -4409,6 +4409,18 @@ bool wss_pick(const Args& a) {
   const int k = tune(47);
   return (k == 1 || (k == 0 && kWssDefault)) && a.N >= 256 && a.rows >= 16384 && wss_ok(a);
 }
+// ... and its 512-row tiles (S = 32) for the 128-wide layers at T = 2000 without an
+// input ELU or replicate pad (the k7 / k3 / k2 adjoints and the s4 down conv:
+// tools/conv_bench.py RU128 k7d9 dgrad 47.3 -> 40.9 us, down1 45.3 -> 43.2; the
+// ELU'd forwards gain nothing, the replicate-pad up conv loses); tune key 50:
+// 1 = on, 2 = off, 0 = kWssTallDefault
+constexpr bool kWssTallDefault = true;
+bool wss_pick_tall(const Args& a) {
+  const int k = tune(50);
+  int S = 0, tm = 0;
+  return (k == 1 || (k == 0 && kWssTallDefault)) && a.N == 128 && a.rows >= 65536 && !a.in_elu &&
+         a.pad_mode == SEL_PAD_ZERO && wss_ok(a) && wss_geometry(a, S, tm) && S == 32;
+}
 
 int fwd4_choice(const Args& a) {
   const int v = tune(0);
@@ -4421,6 +4433,7 @@ int fwd4_choice(const Args& a) {
   if (a.N >= 256 && a.rows >= 16384)
     return wss_pick(a) ? 30 : tune(38) == 1 && ws8w_ok(a) ? 29 : ws_ok(a) ? 27 : 24;
   if (a.N <= 64 || a.rows < 65536) return 23;
+  if (wss_pick_tall(a)) return 30;
   if (ws8_gen_pick(a)) return 28;
   if (a.N == 128 && ws_ok(a) && (a.K <= 3 || (a.K == 7 && a.pad == 0 && !a.in_elu))) return 27;
   if (a.N == 128 && a.K > 1 && a.pad == 0 && !a.in_elu) return 22;
@@ -4448,7 +4461,7 @@ int fwd4_variant(int v, const Args& a, const void* in, const void* wp, const flo
       if (a.K == 7) return launch_ws8<7, TO, 256, 128, 64, 2>(a, in, wp, bias, aux, res, out, s);
       return launch_ws8<3, TO, 256, 128, 64, 2>(a, in, wp, bias, aux, res, out, s);
     case 30:
-      if (!wss_ok(a)) break;
+      if (!wss_ok_out(a, sizeof(TO) == 4)) break;
       return launch_wss<TO>(a, in, wp, bias, aux, res, out, s);
     default: break;
   }
@@ -4464,7 +4477,7 @@ int fwd4_variant(int v, const Args& a, const void* in, const void* wp, const flo
   // RU256 k7 fwd+dgrad 43.5 -> 38.4 us, down2 46.6 -> 41.8), else 256x64 tiles
   // (RU256 k7 fwd 50.7 -> 36.2 us, dgrad 54.2 -> 43.0, down2 51.2 -> 43.1)
   if (a.N >= 256 && a.rows >= 16384) {
-    if (wss_pick(a)) return launch_wss<TO>(a, in, wp, bias, aux, res, out, s);
+    if (wss_pick(a) && wss_ok_out(a, sizeof(TO) == 4)) return launch_wss<TO>(a, in, wp, bias, aux, res, out, s);
     if (tune(38) == 1 && ws8w_ok(a)) return fwd4_variant<KMAX, TO>(29, a, in, wp, bias, aux, res, out, s);
     if (ws_ok(a)) return launch_ws_k<TO>(a, in, wp, bias, aux, res, out, s);
     return launch_fwd4<256, 64, 4, KMAX, TO>(a, in, wp, bias, aux, res, out, s);
@@ -4475,6 +4488,7 @@ int fwd4_variant(int v, const Args& a, const void* in, const void* wp, const flo
   // (RU128 d9: 63.6 -> 53.2 us) and the k3 convs (down1: 49.3 -> 44.1 us), not
   // the k7 forwards with their ELU'd 54-row halo (48.6 -> 52.9 us);
   // tools/conv_bench.py.
+  if (wss_pick_tall(a) && wss_ok_out(a, sizeof(TO) == 4)) return launch_wss<TO>(a, in, wp, bias, aux, res, out, s);
   if (ws8_gen_pick(a)) return launch_ws8<7, TO, 512, 128, 64>(a, in, wp, bias, aux, res, out, s);
   if (a.N == 128 && ws_ok(a) && (a.K <= 3 || (a.K == 7 && a.pad == 0 && !a.in_elu)))
     return launch_ws_k<TO>(a, in, wp, bias, aux, res, out, s);
@@ -5106,7 +5120,11 @@ int sel_conv_fwd_kernel_id(const sel_conv_desc* d, int in_dtype, int out_dtype, 
   if (v == 27) return 900000000 + a.K;
   if (v == 28) return 910000000 + a.K;
   if (v == 29) return 920000000 + a.K;
-  if (v == 30) return 940000000 + a.K;
+  if (v == 30) {  // sample-tile kernel: 9.4e8 + 10 S + K
+    int S = 0, tm = 0;
+    wss_geometry(a, S, tm);
+    return 940000000 + 10 * S + a.K;
+  }
   const int kmax = a.K == 1 ? 1 : (a.K <= 3 ? 3 : 8);
   static const int bm[] = {256, 128, 128, 256, 128, 64}, bn[] = {32, 32, 64, 64, 128, 128}, wm[] = {4, 4, 2, 4, 2, 1};
   const int i = v - 21;

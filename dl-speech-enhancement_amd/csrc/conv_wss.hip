@@ -73,20 +73,26 @@ template <int KT, int S, typename TO>
 __global__ __launch_bounds__(512) void k_conv_wss(Args a, const __bf16* __restrict__ in,
                                                   const __bf16* __restrict__ wp, const float* __restrict__ bias,
                                                   const TO* __restrict__ aux, const TO* __restrict__ res,
-                                                  TO* __restrict__ out, int ncol, int dbg) {
+                                                  TO* __restrict__ out, int ncol, int tm, int dbg) {
   using G = WssGeo<KT, S>;
   constexpr int Q = G::Q, R = G::R, XR = G::XROWS, XI = G::XI, TI = G::TI, PW = G::PW;
   static_assert(2 * PW < 64, "vmcnt range");
   extern __shared__ __align__(16) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  int64_t b;
+  // tile = tm rows of one sample (tm <= 16 S; T = 400: the whole sample) x 64
+  // output channels
+  int64_t mt;
   int nt;
-  xcd_tile(ncol, b, nt);
+  xcd_tile(ncol, mt, nt);
   const int T = a.T;
-  const int64_t m0 = b * T;
+  const int tps = (T + tm - 1) / tm;
+  const int64_t b = mt / tps;
+  const int t0 = int(mt - b * tps) * tm;
+  const int mrows = T - t0 < tm ? T - t0 : tm;
+  const int64_t m0 = b * T + t0;
   const int n0 = nt * WSS_BN;
   const int nchunk = a.C / WSS_CK;
-  const int span = T + (KT - 1) * a.dil;
+  const int span = tm + (KT - 1) * a.dil;
   // diagnostic (tune key 48 bit 4): s_memtime stamps of block phases, written
   // over the first output bytes at the end (st[0] start, [1] first chunk ready,
   // [2] consumer loop done, [3] tile in LDS, [4] end, [5]/[6] realtime start/end)
@@ -103,7 +109,7 @@ __global__ __launch_bounds__(512) void k_conv_wss(Args a, const __bf16* __restri
   // on HBM
   struct alignas(16) V8 { TO v[8]; };
   constexpr int NT = 512, EV = (S * 16 * (WSS_BN / 8) + NT - 1) / NT;
-  const int nvec = T * (WSS_BN / 8);
+  const int nvec = mrows * (WSS_BN / 8);
   V8 av[EV], rv[EV];
   auto prefetch_epi = [&]() __attribute__((always_inline)) {
 #pragma unroll
@@ -126,10 +132,10 @@ __global__ __launch_bounds__(512) void k_conv_wss(Args a, const __bf16* __restri
       const int rr = (q < XI ? q : q - XI) * WSS_RPP + (lane >> 2);
       const int ls = (lane & 3) ^ wss_swz(rr);
       if (q < XI) {
-        int ti = rr - a.pad;
+        int ti = t0 + rr - a.pad;
         const bool valid = rr < span && ((ti >= 0 && ti < T) || a.pad_mode == SEL_PAD_REPLICATE);
         ti = ti < 0 ? 0 : (ti >= T ? T - 1 : ti);
-        src[u] = valid ? in + (m0 + ti) * a.C + 8 * ls : g_wss_zero + 8 * ls;
+        src[u] = valid ? in + (b * T + ti) * a.C + 8 * ls : g_wss_zero + 8 * ls;
       } else {
         const int k = rr / WSS_BN, n = rr % WSS_BN;
         src[u] = wp + (int64_t(n0 + n) * KT + k) * a.C + 8 * ls;
@@ -153,31 +159,35 @@ __global__ __launch_bounds__(512) void k_conv_wss(Args a, const __bf16* __restri
     // Inline asm: a plain LDS access here would make hipcc drain vmcnt (the next
     // chunk's DMA) first; one statement: the compiler cannot hoist a use of a
     // result above the wait.
-    constexpr int PX = (XI + 3) / 4;
-    static_assert(PX == 8 && XR * WSS_ROWB + G::WI * 1024 >= (4 * (PX - 1) + 3 + 1) * 1024, "ELU pass pieces");
+    constexpr int PX = (XI + 3) / 4, NGRP = (PX + 7) / 8;
+    // (the reads past the input pieces stay inside the allocation; never written)
+    static_assert((WSS_NB - 1) * G::SLOT + (4 * (8 * NGRP - 1) + 3 + 1) * 1024 <= G::LDS, "ELU pass reads");
     auto elu_pass = [&](int ch) __attribute__((always_inline)) {
-      unsigned char* const base = smem + (ch % WSS_NB) * G::SLOT + lane * 16 + pw * 1024;
-      const unsigned addr = unsigned(reinterpret_cast<uintptr_t>(base));
-      bf16x8 v[PX];
-      asm volatile(
-          "ds_read_b128 %0, %8\n\t"
-          "ds_read_b128 %1, %8 offset:4096\n\t"
-          "ds_read_b128 %2, %8 offset:8192\n\t"
-          "ds_read_b128 %3, %8 offset:12288\n\t"
-          "ds_read_b128 %4, %8 offset:16384\n\t"
-          "ds_read_b128 %5, %8 offset:20480\n\t"
-          "ds_read_b128 %6, %8 offset:24576\n\t"
-          "ds_read_b128 %7, %8 offset:28672\n\t"
-          "s_waitcnt lgkmcnt(0)"
-          : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]), "=&v"(v[7])
-          : "v"(addr)
-          : "memory");
 #pragma unroll
-      for (int u = 0; u < PX; ++u) {
-        const int q = u * 4 + pw;
-        if (q >= XI || q >= xi_used) break;
-        const bf16x8 e = __builtin_bit_cast(bf16x8, elu8(__builtin_bit_cast(uint4, v[u])));
-        asm volatile("ds_write_b128 %0, %1 offset:%2" : : "v"(addr), "v"(e), "i"(u * 4096) : "memory");
+      for (int gq = 0; gq < NGRP; ++gq) {
+        unsigned char* const base = smem + (ch % WSS_NB) * G::SLOT + lane * 16 + (pw + 32 * gq) * 1024;
+        const unsigned addr = unsigned(reinterpret_cast<uintptr_t>(base));
+        bf16x8 v[8];
+        asm volatile(
+            "ds_read_b128 %0, %8\n\t"
+            "ds_read_b128 %1, %8 offset:4096\n\t"
+            "ds_read_b128 %2, %8 offset:8192\n\t"
+            "ds_read_b128 %3, %8 offset:12288\n\t"
+            "ds_read_b128 %4, %8 offset:16384\n\t"
+            "ds_read_b128 %5, %8 offset:20480\n\t"
+            "ds_read_b128 %6, %8 offset:24576\n\t"
+            "ds_read_b128 %7, %8 offset:28672\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]), "=&v"(v[7])
+            : "v"(addr)
+            : "memory");
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int q = (8 * gq + u) * 4 + pw;
+          if (q >= XI || q >= xi_used) break;
+          const bf16x8 e = __builtin_bit_cast(bf16x8, elu8(__builtin_bit_cast(uint4, v[u])));
+          asm volatile("ds_write_b128 %0, %1 offset:%2" : : "v"(addr), "v"(e), "i"(u * 4096) : "memory");
+        }
       }
     };
     // prologue: chunk 0 alone first (every CU bursts at once: one chunk lands
@@ -373,31 +383,44 @@ __global__ __launch_bounds__(512) void k_conv_wss(Args a, const __bf16* __restri
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
-constexpr int WSS_S = 25;  // the compiled strip count: 384 < T <= 400
+// Compiled tile heights: S = 25 strips (the whole sample at 384 < T <= 400) and
+// S = 32 (tm in (496, 512]: T = 2000 in four 500-row tiles, 512 tiles at C3)
+bool wss_geometry(const Args& a, int& S, int& tm) {
+  const int S1 = (a.T + 15) / 16;
+  if (S1 == 25) {
+    S = 25;
+    tm = a.T;
+    return true;
+  }
+  const int ntps = (a.T + 511) / 512;
+  tm = (a.T + ntps - 1) / ntps;
+  S = (tm + 15) / 16;
+  return S == 32;
+}
 
 bool wss_ok(const Args& a) {
-  const int S = (a.T + 15) / 16;
+  int S, tm;
   const bool kt = a.K == 7 || a.K == 3 || a.K == 2;
-  return kt && S == WSS_S && a.N % WSS_BN == 0 && a.C % (2 * WSS_CK) == 0 && a.C <= WSS_CMAX &&
+  return kt && wss_geometry(a, S, tm) && a.N % WSS_BN == 0 && a.C % (2 * WSS_CK) == 0 && a.C <= WSS_CMAX &&
          (a.K - 1) * a.dil <= F4_HALOMAX && a.pad <= (a.K - 1) * a.dil && a.seq_pitch == 0 && a.epi == 0 &&
          a.tin_valid == a.T && a.tin_pitch == a.T && a.tout_valid == a.T && a.ldx == a.C && a.ldo == a.N &&
          a.rows % a.T == 0;
 }
 
-template <int KT, typename TO>
-static int launch_wss_t(const Args& a, const void* in, const void* wp, const float* bias, const void* aux,
+template <int KT, int S, typename TO>
+static int launch_wss_t(const Args& a, int tm, const void* in, const void* wp, const float* bias, const void* aux,
                         const void* res, void* out, hipStream_t s) {
-  using G = WssGeo<KT, WSS_S>;
+  using G = WssGeo<KT, S>;
   static_assert(G::LDS <= 160 * 1024, "LDS");
-  const int64_t tiles = a.rows / a.T;
+  const int64_t tiles = (a.rows / a.T) * ((a.T + tm - 1) / tm);
   const int ncol = a.N / WSS_BN;
   if (tiles == 0) return SEL_OK;
   SEL_REQUIRE(tiles * ncol < (int64_t(1) << 31), SEL_ERR_UNSUPPORTED, "k_conv_wss: grid too large");
-  auto kern = k_conv_wss<KT, WSS_S, TO>;
+  auto kern = k_conv_wss<KT, S, TO>;
   SEL_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, int(G::LDS)));
   hipLaunchKernelGGL(kern, dim3(unsigned(tiles * ncol)), dim3(512), G::LDS, s, a, static_cast<const __bf16*>(in),
                      static_cast<const __bf16*>(wp), bias, static_cast<const TO*>(aux), static_cast<const TO*>(res),
-                     static_cast<TO*>(out), ncol, tune(48));
+                     static_cast<TO*>(out), ncol, tm, tune(48));
   SEL_LAUNCH_CHECK();
   return SEL_OK;
 }
@@ -407,11 +430,29 @@ int launch_wss(const Args& a, const void* in, const void* wp, const float* bias,
                void* out, hipStream_t s) {
   SEL_REQUIRE(wss_ok(a), SEL_ERR_ARG, "k_conv_wss: unsupported shape T=%d C=%d N=%d K=%d dil=%d", a.T, a.C, a.N,
               a.K, a.dil);
-  switch (a.K) {
-    case 7: return launch_wss_t<7, TO>(a, in, wp, bias, aux, res, out, s);
-    case 3: return launch_wss_t<3, TO>(a, in, wp, bias, aux, res, out, s);
-    default: return launch_wss_t<2, TO>(a, in, wp, bias, aux, res, out, s);
+  int S, tm;
+  wss_geometry(a, S, tm);
+  if (S == 25) {
+    switch (a.K) {
+      case 7: return launch_wss_t<7, 25, TO>(a, tm, in, wp, bias, aux, res, out, s);
+      case 3: return launch_wss_t<3, 25, TO>(a, tm, in, wp, bias, aux, res, out, s);
+      default: return launch_wss_t<2, 25, TO>(a, tm, in, wp, bias, aux, res, out, s);
+    }
   }
+  if constexpr (sizeof(TO) == 2) {  // (fp32 outputs: the epilogue rows do not fit the S = 32 registers)
+    switch (a.K) {
+      case 7: return launch_wss_t<7, 32, TO>(a, tm, in, wp, bias, aux, res, out, s);
+      case 3: return launch_wss_t<3, 32, TO>(a, tm, in, wp, bias, aux, res, out, s);
+      default: return launch_wss_t<2, 32, TO>(a, tm, in, wp, bias, aux, res, out, s);
+    }
+  }
+  set_error("k_conv_wss: fp32 output needs T <= 400");
+  return SEL_ERR_UNSUPPORTED;
+}
+
+bool wss_ok_out(const Args& a, bool out_f32) {
+  int S, tm;
+  return wss_ok(a) && (!out_f32 || (wss_geometry(a, S, tm) && S == 25));
 }
 
 template int launch_wss<__bf16>(const Args&, const void*, const void*, const float*, const void*, const void*, void*,
