@@ -4421,6 +4421,15 @@ bool wss_pick_tall(const Args& a) {
   return (k == 1 || (k == 0 && kWssTallDefault)) && a.N == 128 && a.rows >= 65536 && !a.in_elu &&
          a.pad_mode == SEL_PAD_ZERO && wss_ok(a) && wss_geometry(a, S, tm) && S == 32;
 }
+// the (16, 128) tiles for the ELU'd 128-wide forwards at T = 2000 (tune key 52:
+// 1 = on, 2 = off, 0 = kWssEluDefault)
+constexpr bool kWssEluDefault = false;
+bool wss_pick_elu(const Args& a) {
+  const int k = tune(52);
+  int S = 0, tm = 0;
+  return (k == 1 || (k == 0 && kWssEluDefault)) && a.N == 128 && a.rows >= 65536 && a.in_elu &&
+         a.pad_mode == SEL_PAD_ZERO && wss_ok(a) && wss_geometry(a, S, tm) && S == 16;
+}
 
 int fwd4_choice(const Args& a) {
   const int v = tune(0);
@@ -4433,7 +4442,7 @@ int fwd4_choice(const Args& a) {
   if (a.N >= 256 && a.rows >= 16384)
     return wss_pick(a) ? 30 : tune(38) == 1 && ws8w_ok(a) ? 29 : ws_ok(a) ? 27 : 24;
   if (a.N <= 64 || a.rows < 65536) return 23;
-  if (wss_pick_tall(a)) return 30;
+  if (wss_pick_tall(a) || wss_pick_elu(a)) return 30;
   if (ws8_gen_pick(a)) return 28;
   if (a.N == 128 && ws_ok(a) && (a.K <= 3 || (a.K == 7 && a.pad == 0 && !a.in_elu))) return 27;
   if (a.N == 128 && a.K > 1 && a.pad == 0 && !a.in_elu) return 22;
@@ -4488,7 +4497,8 @@ int fwd4_variant(int v, const Args& a, const void* in, const void* wp, const flo
   // (RU128 d9: 63.6 -> 53.2 us) and the k3 convs (down1: 49.3 -> 44.1 us), not
   // the k7 forwards with their ELU'd 54-row halo (48.6 -> 52.9 us);
   // tools/conv_bench.py.
-  if (wss_pick_tall(a) && wss_ok_out(a, sizeof(TO) == 4)) return launch_wss<TO>(a, in, wp, bias, aux, res, out, s);
+  if ((wss_pick_tall(a) || wss_pick_elu(a)) && wss_ok_out(a, sizeof(TO) == 4))
+    return launch_wss<TO>(a, in, wp, bias, aux, res, out, s);
   if (ws8_gen_pick(a)) return launch_ws8<7, TO, 512, 128, 64>(a, in, wp, bias, aux, res, out, s);
   if (a.N == 128 && ws_ok(a) && (a.K <= 3 || (a.K == 7 && a.pad == 0 && !a.in_elu)))
     return launch_ws_k<TO>(a, in, wp, bias, aux, res, out, s);
@@ -5120,10 +5130,10 @@ int sel_conv_fwd_kernel_id(const sel_conv_desc* d, int in_dtype, int out_dtype, 
   if (v == 27) return 900000000 + a.K;
   if (v == 28) return 910000000 + a.K;
   if (v == 29) return 920000000 + a.K;
-  if (v == 30) {  // sample-tile kernel: 9.4e8 + 10 S + K
-    int S = 0, tm = 0;
-    wss_geometry(a, S, tm);
-    return 940000000 + 10 * S + a.K;
+  if (v == 30) {  // sample-tile kernel: 9.4e8 + 1e4 BN + 10 S + K
+    int S = 0, tm = 0, BN = 0;
+    wss_geometry(a, S, tm, BN);
+    return 940000000 + 10000 * BN + 10 * S + a.K;
   }
   const int kmax = a.K == 1 ? 1 : (a.K <= 3 ? 3 : 8);
   static const int bm[] = {256, 128, 128, 256, 128, 64}, bn[] = {32, 32, 64, 64, 128, 128}, wm[] = {4, 4, 2, 4, 2, 1};

@@ -105,7 +105,8 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 namespace sel {
 namespace conv {
 // conv_wss.hip: sample-tile warp-specialised kernel (T <= 400)
-bool wss_geometry(const Args& a, int& S, int& tm);  // strips per tile and tile rows
+bool wss_geometry(const Args& a, int& S, int& tm, int& BN);  // strips per tile, tile rows, channels
+bool wss_geometry(const Args& a, int& S, int& tm);
 bool wss_ok(const Args& a);
 bool wss_ok_out(const Args& a, bool out_f32);  // wss_ok and an instance for that output type
 template <typename TO>

@@ -36,27 +36,31 @@
 namespace sel {
 namespace conv {
 
-constexpr int WSS_BN = 64;                 // output channels per tile
 constexpr int WSS_CK = 32;                 // channels per chunk = one MFMA k-step
 constexpr int WSS_ROWB = WSS_CK * 2;       // bytes per LDS row
 constexpr int WSS_RPP = 1024 / WSS_ROWB;   // LDS rows per 1-KB DMA piece
-constexpr int WSS_EP = WSS_BN + 4;         // fp32 epilogue tile pitch
 constexpr int WSS_CMAX = 4096;             // input channels the zero source covers
 constexpr int WSS_NB = 2;                  // ring slots
 
 __device__ __attribute__((aligned(64))) __bf16 g_wss_zero[WSS_CMAX];
 
-template <int KT, int S>
+// KT taps, S 16-row strips per tile, BN output channels per tile (64 or 128:
+// NCS = BN / 16 column strips).  Wave w owns Q = S / 4 full strips (all NCS
+// column strips) plus E of the R * NCS (strip, column strip) pairs of the last
+// R = S % 4 strips.
+template <int KT, int S, int BN>
 struct WssGeo {
-  static constexpr int Q = S / 4, R = S % 4;
+  static constexpr int Q = S / 4, R = S % 4, NCS = BN / 16, E = R * NCS / 4;
+  static_assert((R * NCS) % 4 == 0, "extra pairs split evenly over the four consumers");
+  static constexpr int EP = BN + 4;  // fp32 epilogue tile pitch
   static constexpr int XROWS = (S * 16 + F4_HALOMAX + WSS_RPP - 1) / WSS_RPP * WSS_RPP;  // staged input rows
   static constexpr int XI = XROWS / WSS_RPP;            // input DMA pieces per chunk
-  static constexpr int WI = KT * WSS_BN / WSS_RPP;      // weight DMA pieces per chunk
+  static constexpr int WI = KT * BN / WSS_RPP;          // weight DMA pieces per chunk
   static constexpr int TI = XI + WI;
   static constexpr int PW = (TI + 3) / 4;               // pieces per producer wave
-  static constexpr int SLOT = (XROWS + KT * WSS_BN) * WSS_ROWB;
+  static constexpr int SLOT = (XROWS + KT * BN) * WSS_ROWB;
   static constexpr int RING = WSS_NB * SLOT;
-  static constexpr int EPI = S * 16 * WSS_EP * 4;
+  static constexpr int EPI = S * 16 * EP * 4;
   static constexpr int LDS = RING > EPI ? RING : EPI;
 };
 
@@ -69,13 +73,14 @@ struct WssGeo {
 // (PMC: SQ_LDS_BANK_CONFLICT 44% of SQ_LDS_IDX_ACTIVE).
 __device__ __forceinline__ int wss_swz(int row) { return (row >> 1) & 2; }
 
-template <int KT, int S, typename TO>
+template <int KT, int S, int BN, typename TO>
 __global__ __launch_bounds__(512) void k_conv_wss(Args a, const __bf16* __restrict__ in,
                                                   const __bf16* __restrict__ wp, const float* __restrict__ bias,
                                                   const TO* __restrict__ aux, const TO* __restrict__ res,
                                                   TO* __restrict__ out, int ncol, int tm, int dbg) {
-  using G = WssGeo<KT, S>;
-  constexpr int Q = G::Q, R = G::R, XR = G::XROWS, XI = G::XI, TI = G::TI, PW = G::PW;
+  using G = WssGeo<KT, S, BN>;
+  constexpr int Q = G::Q, NCS = G::NCS, E = G::E, XR = G::XROWS, XI = G::XI, TI = G::TI, PW = G::PW;
+  constexpr int EP = G::EP;
   static_assert(2 * PW < 64, "vmcnt range");
   extern __shared__ __align__(16) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -90,7 +95,7 @@ __global__ __launch_bounds__(512) void k_conv_wss(Args a, const __bf16* __restri
   const int t0 = int(mt - b * tps) * tm;
   const int mrows = T - t0 < tm ? T - t0 : tm;
   const int64_t m0 = b * T + t0;
-  const int n0 = nt * WSS_BN;
+  const int n0 = nt * BN;
   const int nchunk = a.C / WSS_CK;
   const int span = tm + (KT - 1) * a.dil;
   // diagnostic (tune key 48 bit 4): s_memtime stamps of block phases, written
@@ -108,15 +113,15 @@ __global__ __launch_bounds__(512) void k_conv_wss(Args a, const __bf16* __restri
   // last DMA, consumers right after their MFMAs) so the epilogue does not wait
   // on HBM
   struct alignas(16) V8 { TO v[8]; };
-  constexpr int NT = 512, EV = (S * 16 * (WSS_BN / 8) + NT - 1) / NT;
-  const int nvec = mrows * (WSS_BN / 8);
+  constexpr int NT = 512, VPR = BN / 8, EV = (S * 16 * VPR + NT - 1) / NT;  // VPR: 16-B vectors per row
+  const int nvec = mrows * VPR;
   V8 av[EV], rv[EV];
   auto prefetch_epi = [&]() __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < EV; ++u) {
       const int v = tid + u * NT;
       if (v >= nvec) break;
-      const int64_t o = (m0 + (v >> 3)) * a.N + n0 + (v & 7) * 8;
+      const int64_t o = (m0 + v / VPR) * a.N + n0 + (v % VPR) * 8;
       if (aux) av[u] = *reinterpret_cast<const V8*>(aux + o);
       if (res) rv[u] = *reinterpret_cast<const V8*>(res + o);
     }
@@ -137,7 +142,7 @@ __global__ __launch_bounds__(512) void k_conv_wss(Args a, const __bf16* __restri
         ti = ti < 0 ? 0 : (ti >= T ? T - 1 : ti);
         src[u] = valid ? in + (b * T + ti) * a.C + 8 * ls : g_wss_zero + 8 * ls;
       } else {
-        const int k = rr / WSS_BN, n = rr % WSS_BN;
+        const int k = rr / BN, n = rr % BN;
         src[u] = wp + (int64_t(n0 + n) * KT + k) * a.C + 8 * ls;
       }
     }
@@ -215,24 +220,25 @@ __global__ __launch_bounds__(512) void k_conv_wss(Args a, const __bf16* __restri
     const int w = wave;
     const int l16 = lane & 15, kq = lane >> 4;
     // lane's byte offset within a 16-row group of weight rows (row = 16 cs + l16
-    // of tap k's 64 rows; the swizzle depends on l16 only) and the extra pairs
+    // of tap k's BN rows; the swizzle depends on l16 only) and the extra pairs
     const int lane_w = l16 * WSS_ROWB + ((kq ^ wss_swz(l16)) << 4);
-    int xstrip[R > 0 ? R : 1], xcol[R > 0 ? R : 1];
+    constexpr int E1 = E > 0 ? E : 1;
+    int xstrip[E1], xcol[E1];
 #pragma unroll
-    for (int i = 0; i < R; ++i) {
-      const int p = w * R + i;
-      xstrip[i] = 4 * Q + p / 4;
-      xcol[i] = p % 4;
+    for (int i = 0; i < E; ++i) {
+      const int p = w * E + i;
+      xstrip[i] = 4 * Q + p / NCS;
+      xcol[i] = p % NCS;
     }
-    floatx4 acc[Q][4], accx[R > 0 ? R : 1];
+    floatx4 acc[Q][NCS], accx[E1];
 #pragma unroll
     for (int i = 0; i < Q; ++i)
 #pragma unroll
-      for (int c = 0; c < 4; ++c) acc[i][c] = floatx4{0.f, 0.f, 0.f, 0.f};
+      for (int c = 0; c < NCS; ++c) acc[i][c] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int i = 0; i < R; ++i) accx[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < E; ++i) accx[i] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-    bf16x8 fw[2][4], fx[2][Q], fwx[2][R > 0 ? R : 1], fxx[2][R > 0 ? R : 1];
+    bf16x8 fw[2][NCS], fx[2][Q], fwx[2][E1], fxx[2][E1];
     // fragments of tap k of the chunk in ring slot sl into buffer q
     static_assert(WSS_NB == 2, "two chunks per trip, one per ring slot");
     auto fetch = [&](int sl, int k, int q) __attribute__((always_inline)) {
@@ -240,8 +246,8 @@ __global__ __launch_bounds__(512) void k_conv_wss(Args a, const __bf16* __restri
       const unsigned char* const xw = xb + w * Q * 1024;  // this wave's first full strip
       const unsigned char* const wb = xb + XR * WSS_ROWB;
 #pragma unroll
-      for (int c = 0; c < 4; ++c)
-        fw[q][c] = *reinterpret_cast<const bf16x8*>(wb + (k * WSS_BN + c * 16) * WSS_ROWB + lane_w);
+      for (int c = 0; c < NCS; ++c)
+        fw[q][c] = *reinterpret_cast<const bf16x8*>(wb + (k * BN + c * 16) * WSS_ROWB + lane_w);
       const int r = l16 + k * a.dil;  // + 16 s: the swizzle of row r + 16 s is r's
       int lx = r * WSS_ROWB + ((kq ^ wss_swz(r)) << 4);
       // computed here, per fetch (a few VALU): hoisted out of the loop, the
@@ -250,8 +256,8 @@ __global__ __launch_bounds__(512) void k_conv_wss(Args a, const __bf16* __restri
 #pragma unroll
       for (int i = 0; i < Q; ++i) fx[q][i] = *reinterpret_cast<const bf16x8*>(xw + i * 1024 + lx);
 #pragma unroll
-      for (int i = 0; i < R; ++i) {
-        fwx[q][i] = *reinterpret_cast<const bf16x8*>(wb + (k * WSS_BN + xcol[i] * 16) * WSS_ROWB + lane_w);
+      for (int i = 0; i < E; ++i) {
+        fwx[q][i] = *reinterpret_cast<const bf16x8*>(wb + (k * BN + xcol[i] * 16) * WSS_ROWB + lane_w);
         fxx[q][i] = *reinterpret_cast<const bf16x8*>(xb + xstrip[i] * 1024 + lx);
       }
     };
@@ -259,10 +265,10 @@ __global__ __launch_bounds__(512) void k_conv_wss(Args a, const __bf16* __restri
 #pragma unroll
       for (int i = 0; i < Q; ++i)
 #pragma unroll
-        for (int c = 0; c < 4; ++c)
+        for (int c = 0; c < NCS; ++c)
           acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[q][c], fx[q][i], acc[i][c], 0, 0, 0);
 #pragma unroll
-      for (int i = 0; i < R; ++i)
+      for (int i = 0; i < E; ++i)
         accx[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fwx[q][i], fxx[q][i], accx[i], 0, 0, 0);
     };
 
@@ -294,7 +300,7 @@ __global__ __launch_bounds__(512) void k_conv_wss(Args a, const __bf16* __restri
           mfmas(q);
           // the next step's reads go out between this step's MFMAs (one per
           // two), not as a burst that leaves the matrix pipe idle
-          constexpr int NRD = 4 + Q + 2 * R, NMF = 4 * Q + R;
+          constexpr int NRD = NCS + Q + 2 * E, NMF = NCS * Q + E;
           constexpr int REST = NMF > 2 * NRD ? NMF - 2 * NRD : 0;
 #pragma unroll
           for (int j = 0; j < NRD; ++j) {
@@ -309,17 +315,17 @@ __global__ __launch_bounds__(512) void k_conv_wss(Args a, const __bf16* __restri
     __builtin_amdgcn_s_setprio(0);
     if (dbg & 16) st[2] = __builtin_amdgcn_s_memtime();
     prefetch_epi();
-    // accumulators -> fp32 [S*16][64 + 4] tile over the drained ring: lane ->
+    // accumulators -> fp32 [S*16][BN + 4] tile over the drained ring: lane ->
     // time row 16 s + l16, channels 16 c + 4 kq .. + 3
     float* const tile = reinterpret_cast<float*>(smem);
 #pragma unroll
     for (int i = 0; i < Q; ++i)
 #pragma unroll
-      for (int c = 0; c < 4; ++c)
-        *reinterpret_cast<floatx4*>(tile + ((w * Q + i) * 16 + l16) * WSS_EP + c * 16 + 4 * kq) = acc[i][c];
+      for (int c = 0; c < NCS; ++c)
+        *reinterpret_cast<floatx4*>(tile + ((w * Q + i) * 16 + l16) * EP + c * 16 + 4 * kq) = acc[i][c];
 #pragma unroll
-    for (int i = 0; i < R; ++i)
-      *reinterpret_cast<floatx4*>(tile + (xstrip[i] * 16 + l16) * WSS_EP + xcol[i] * 16 + 4 * kq) = accx[i];
+    for (int i = 0; i < E; ++i)
+      *reinterpret_cast<floatx4*>(tile + (xstrip[i] * 16 + l16) * EP + xcol[i] * 16 + 4 * kq) = accx[i];
   }
   // (a raw barrier: __syncthreads() would also wait for the prefetched rows)
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -334,10 +340,10 @@ __global__ __launch_bounds__(512) void k_conv_wss(Args a, const __bf16* __restri
   for (int u = 0; u < EV; ++u) {
     const int v = tid + u * NT;
     if (v >= nvec) break;
-    const int row = v >> 3, c8 = (v & 7) * 8;
+    const int row = v / VPR, c8 = (v % VPR) * 8;
     const int64_t o = (m0 + row) * a.N + n0 + c8;
-    const floatx4 lo = *reinterpret_cast<const floatx4*>(tile + row * WSS_EP + c8);
-    const floatx4 hi = *reinterpret_cast<const floatx4*>(tile + row * WSS_EP + c8 + 4);
+    const floatx4 lo = *reinterpret_cast<const floatx4*>(tile + row * EP + c8);
+    const floatx4 hi = *reinterpret_cast<const floatx4*>(tile + row * EP + c8 + 4);
     float x[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
     if (bias && a.bias_period) {
       if (a.bias_period % 8 == 0) {
@@ -383,14 +389,31 @@ __global__ __launch_bounds__(512) void k_conv_wss(Args a, const __bf16* __restri
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
-// Compiled tile heights: S = 25 strips (the whole sample at 384 < T <= 400) and
-// S = 32 (tm in (496, 512]: T = 2000 in four 500-row tiles, 512 tiles at C3)
-bool wss_geometry(const Args& a, int& S, int& tm) {
+// Compiled tile shapes (S strips x BN channels):
+//   (25, 64):  the whole sample at 384 < T <= 400 (C3's 256-wide stage: 256 tiles);
+//   (32, 64):  500-row tiles at T = 2000 (tm in (496, 512]; 512 tiles at C3);
+//   (16, 128): 250-row tiles x 128 channels at T = 2000 (tm in (240, 256]): the
+//              input ELU once per 128 output channels instead of twice, for the
+//              ELU'd forwards (the RU128 k7 convs; 512 tiles at C3).
+// tune key 51: 1 = (16, 128) wherever it applies, 2 = never, 0 = for in_elu only
+bool wss_geometry(const Args& a, int& S, int& tm, int& BN) {
+  BN = 64;
   const int S1 = (a.T + 15) / 16;
   if (S1 == 25) {
     S = 25;
     tm = a.T;
     return true;
+  }
+  const int k51 = tune(51);
+  if (a.N % 128 == 0 && (k51 == 1 || (k51 == 0 && a.in_elu))) {
+    const int n = (a.T + 255) / 256;
+    const int t = (a.T + n - 1) / n;
+    if ((t + 15) / 16 == 16) {
+      S = 16;
+      tm = t;
+      BN = 128;
+      return true;
+    }
   }
   const int ntps = (a.T + 511) / 512;
   tm = (a.T + ntps - 1) / ntps;
@@ -398,25 +421,30 @@ bool wss_geometry(const Args& a, int& S, int& tm) {
   return S == 32;
 }
 
+bool wss_geometry(const Args& a, int& S, int& tm) {
+  int BN;
+  return wss_geometry(a, S, tm, BN);
+}
+
 bool wss_ok(const Args& a) {
-  int S, tm;
+  int S, tm, BN;
   const bool kt = a.K == 7 || a.K == 3 || a.K == 2;
-  return kt && wss_geometry(a, S, tm) && a.N % WSS_BN == 0 && a.C % (2 * WSS_CK) == 0 && a.C <= WSS_CMAX &&
+  return kt && wss_geometry(a, S, tm, BN) && a.N % BN == 0 && a.C % (2 * WSS_CK) == 0 && a.C <= WSS_CMAX &&
          (a.K - 1) * a.dil <= F4_HALOMAX && a.pad <= (a.K - 1) * a.dil && a.seq_pitch == 0 && a.epi == 0 &&
          a.tin_valid == a.T && a.tin_pitch == a.T && a.tout_valid == a.T && a.ldx == a.C && a.ldo == a.N &&
          a.rows % a.T == 0;
 }
 
-template <int KT, int S, typename TO>
+template <int KT, int S, int BN, typename TO>
 static int launch_wss_t(const Args& a, int tm, const void* in, const void* wp, const float* bias, const void* aux,
                         const void* res, void* out, hipStream_t s) {
-  using G = WssGeo<KT, S>;
+  using G = WssGeo<KT, S, BN>;
   static_assert(G::LDS <= 160 * 1024, "LDS");
   const int64_t tiles = (a.rows / a.T) * ((a.T + tm - 1) / tm);
-  const int ncol = a.N / WSS_BN;
+  const int ncol = a.N / BN;
   if (tiles == 0) return SEL_OK;
   SEL_REQUIRE(tiles * ncol < (int64_t(1) << 31), SEL_ERR_UNSUPPORTED, "k_conv_wss: grid too large");
-  auto kern = k_conv_wss<KT, S, TO>;
+  auto kern = k_conv_wss<KT, S, BN, TO>;
   SEL_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, int(G::LDS)));
   hipLaunchKernelGGL(kern, dim3(unsigned(tiles * ncol)), dim3(512), G::LDS, s, a, static_cast<const __bf16*>(in),
                      static_cast<const __bf16*>(wp), bias, static_cast<const TO*>(aux), static_cast<const TO*>(res),
@@ -425,26 +453,27 @@ static int launch_wss_t(const Args& a, int tm, const void* in, const void* wp, c
   return SEL_OK;
 }
 
+template <int S, int BN, typename TO>
+static int launch_wss_k(const Args& a, int tm, const void* in, const void* wp, const float* bias, const void* aux,
+                        const void* res, void* out, hipStream_t s) {
+  switch (a.K) {
+    case 7: return launch_wss_t<7, S, BN, TO>(a, tm, in, wp, bias, aux, res, out, s);
+    case 3: return launch_wss_t<3, S, BN, TO>(a, tm, in, wp, bias, aux, res, out, s);
+    default: return launch_wss_t<2, S, BN, TO>(a, tm, in, wp, bias, aux, res, out, s);
+  }
+}
+
 template <typename TO>
 int launch_wss(const Args& a, const void* in, const void* wp, const float* bias, const void* aux, const void* res,
                void* out, hipStream_t s) {
   SEL_REQUIRE(wss_ok(a), SEL_ERR_ARG, "k_conv_wss: unsupported shape T=%d C=%d N=%d K=%d dil=%d", a.T, a.C, a.N,
               a.K, a.dil);
-  int S, tm;
-  wss_geometry(a, S, tm);
-  if (S == 25) {
-    switch (a.K) {
-      case 7: return launch_wss_t<7, 25, TO>(a, tm, in, wp, bias, aux, res, out, s);
-      case 3: return launch_wss_t<3, 25, TO>(a, tm, in, wp, bias, aux, res, out, s);
-      default: return launch_wss_t<2, 25, TO>(a, tm, in, wp, bias, aux, res, out, s);
-    }
-  }
-  if constexpr (sizeof(TO) == 2) {  // (fp32 outputs: the epilogue rows do not fit the S = 32 registers)
-    switch (a.K) {
-      case 7: return launch_wss_t<7, 32, TO>(a, tm, in, wp, bias, aux, res, out, s);
-      case 3: return launch_wss_t<3, 32, TO>(a, tm, in, wp, bias, aux, res, out, s);
-      default: return launch_wss_t<2, 32, TO>(a, tm, in, wp, bias, aux, res, out, s);
-    }
+  int S, tm, BN;
+  wss_geometry(a, S, tm, BN);
+  if (S == 25) return launch_wss_k<25, 64, TO>(a, tm, in, wp, bias, aux, res, out, s);
+  if constexpr (sizeof(TO) == 2) {  // (fp32 outputs: the epilogue rows do not fit the taller tiles' registers)
+    if (S == 16) return launch_wss_k<16, 128, TO>(a, tm, in, wp, bias, aux, res, out, s);
+    return launch_wss_k<32, 64, TO>(a, tm, in, wp, bias, aux, res, out, s);
   }
   set_error("k_conv_wss: fp32 output needs T <= 400");
   return SEL_ERR_UNSUPPORTED;
