@@ -4407,7 +4407,11 @@ int launch_ws_k(const Args& a, const void* in, const void* wp, const float* bias
 constexpr bool kWssDefault = true;
 bool wss_pick(const Args& a) {
   const int k = tune(47);
-  return (k == 1 || (k == 0 && kWssDefault)) && a.N >= 256 && a.rows >= 16384 && wss_ok(a);
+  int S = 0, tm = 0;
+  // (at T = 2000 not the replicate-pad transposed conv 128 -> 256 phases:
+  // tools/conv_bench.py 49.6 us on k_conv_ws_bf16 against 53.0)
+  return (k == 1 || (k == 0 && kWssDefault)) && a.N >= 256 && a.rows >= 16384 && wss_ok(a) &&
+         wss_geometry(a, S, tm) && (S == 25 || a.pad_mode == SEL_PAD_ZERO);
 }
 // ... and its 512-row tiles (S = 32) for the 128-wide layers at T = 2000 without an
 // input ELU or replicate pad (the k7 / k3 / k2 adjoints and the s4 down conv:
