@@ -71,6 +71,7 @@ SIGNATURES = {
     "sel_add_noise": (I32, [P, P, I64, F32, P, P, SZ, P]),
     "sel_power_mel_fwd": (I32, [P, I64, I64, I32, I32, I32, P, P, P, I32, F32, P, P]),
     "sel_pack_many": (I32, [P, I32, I64, I32, P]),
+    "sel_pack_many_host": (I32, [P, I32, I64, I32, P]),
     "sel_conv_wgrad_unpacked": (I32, [P, I32, P, P, I32, I32, I32, I32, I32, P, P, P, SZ, P]),
     "sel_sumsq2": (I32, [P, P, I64, P, P, SZ, P]),
     "sel_mix_noise": (I32, [P, P, I64, P, F32, P, P]),

@@ -260,6 +260,10 @@ typedef struct sel_pack_job {
   int32_t kind, cout, cin, k, stride, reserved;
 } sel_pack_job;
 int sel_pack_many(const sel_pack_job* jobs, int njobs, int64_t total, int dtype, sel_stream_t stream);
+/* The same with `jobs` in HOST memory (copied into the kernel arguments, 48
+ * jobs per launch; offsets increasing): no device job table to stage.  The
+ * product path (sel.convops.PackCache) uses this one. */
+int sel_pack_many_host(const sel_pack_job* jobs, int njobs, int64_t total, int dtype, sel_stream_t stream);
 /* gwpack (packed fp32) -> torch layout gw (kind as in sel_pack_weight). */
 int sel_unpack_wgrad(int kind, const float* gwpack, int cout, int cin, int k, int stride,
                      float* gw, sel_stream_t stream);
