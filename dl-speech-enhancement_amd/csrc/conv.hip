@@ -2840,6 +2840,113 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(Args a, const TI* __restrict
     bpart[int64_t(split) * a.N + n0 + threadIdx.x] = bsum;
 }
 
+// fp32 weight gradient on sample-aligned 64-row tiles (the reference-precision
+// path; the generic k_conv_wgrad above remains for other shapes).  One
+// workgroup owns 64 output channels (16 per wave) x 32 input channels x all K
+// taps and a contiguous range of 64-row tiles that never cross a sample, so
+// the causal halo is zero- or replicate-filled while staging and the MFMA loop
+// has no per-row address arithmetic or masks.  The next tile's g and x rows
+// are fetched (16-B loads) into registers while the current tile's MFMAs run.
+// MFMA v_mfma_f32_16x16x4_f32: A = g^T (lane: n = l & 15, row 4q + l >> 4),
+// B = ELU(x) rows shifted by the tap (col c = l & 15); the 4 rows of one
+// k-step are 80 / 48 floats apart in LDS (distinct 16-bank groups).
+constexpr int WF_BM = 64, WF_GP = 80, WF_XP = 48, WF_XR = 128;
+template <int KM>
+__global__ __launch_bounds__(256) void k_wgrad_f32(Args a, const float* __restrict__ gout,
+                                                   const float* __restrict__ in, int tps, int64_t n_tiles,
+                                                   int tiles_per_split, float* __restrict__ part,
+                                                   float* __restrict__ bpart) {
+  __shared__ __align__(16) float gs[WF_BM * WF_GP];
+  __shared__ __align__(16) float xs[WF_XR * WF_XP];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n0 = blockIdx.x * 64, c0 = blockIdx.y * 32;
+  const int split = blockIdx.z;
+  const int64_t tb = int64_t(split) * tiles_per_split;
+  const int64_t te = tb + tiles_per_split < n_tiles ? tb + tiles_per_split : n_tiles;
+  const int span = WF_BM + (a.K - 1) * a.dil;
+  const bool want_bias = bpart != nullptr && c0 == 0;
+
+  floatx4 acc[KM][2];
+#pragma unroll
+  for (int k = 0; k < KM; ++k) acc[k][0] = acc[k][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+  float bsum = 0.f;
+
+  float4 gr[4], xr[4];
+  auto fetch = [&](int64_t tile) {
+    const int64_t b = tile / tps;
+    const int t0 = int(tile - b * tps) * WF_BM;
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = i * 16 + (tid >> 4), n = n0 + (tid & 15) * 4;
+      const int t = t0 + r;
+      gr[i] = t < a.T && n < a.N ? *reinterpret_cast<const float4*>(gout + (b * a.T + t) * a.N + n) : z;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = i * 32 + (tid >> 3), c = c0 + (tid & 7) * 4;
+      int ti = t0 - a.pad + r;
+      bool ok = r < span && c < a.C;
+      if (ti < 0 || ti >= a.T) {
+        if (a.pad_mode == SEL_PAD_ZERO) ok = false;
+        ti = ti < 0 ? 0 : a.T - 1;
+      }
+      xr[i] = ok ? *reinterpret_cast<const float4*>(in + (b * a.T + ti) * a.C + c) : z;
+    }
+  };
+  auto put = [&]() {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      *reinterpret_cast<float4*>(gs + (i * 16 + (tid >> 4)) * WF_GP + (tid & 15) * 4) = gr[i];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float4 v = xr[i];
+      if (a.in_elu) v = make_float4(elu(v.x), elu(v.y), elu(v.z), elu(v.w));
+      *reinterpret_cast<float4*>(xs + (i * 32 + (tid >> 3)) * WF_XP + (tid & 7) * 4) = v;
+    }
+  };
+
+  if (tb < te) fetch(tb);
+  const float* gcol = gs + wave * 16 + (lane & 15);
+  const float* xcol = xs + (lane & 15);
+  for (int64_t tile = tb; tile < te; ++tile) {
+    __syncthreads();  // the previous tile's MFMAs are done with gs / xs
+    put();
+    __syncthreads();
+    if (tile + 1 < te) fetch(tile + 1);
+    if (want_bias && tid < 64)
+      for (int r = 0; r < WF_BM; ++r) bsum += gs[r * WF_GP + tid];
+#pragma unroll 2
+    for (int q = 0; q < WF_BM / 4; ++q) {
+      const int r = 4 * q + (lane >> 4);
+      const float av = gcol[r * WF_GP];
+#pragma unroll
+      for (int k = 0; k < KM; ++k) {
+        if (k >= a.K) break;
+        const float* xrow = xcol + (r + k * a.dil) * WF_XP;
+        acc[k][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, xrow[0], acc[k][0], 0, 0, 0);
+        acc[k][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, xrow[16], acc[k][1], 0, 0, 0);
+      }
+    }
+  }
+  // partials: part[split][n][k][c] (C/D: col = c (lane & 15), row = n (4 (lane >> 4) + e))
+  float* pdst = part + int64_t(split) * a.N * a.K * a.C;
+#pragma unroll
+  for (int k = 0; k < KM; ++k) {
+    if (k >= a.K) break;
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) {
+      const int c = c0 + ct * 16 + (lane & 15);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int n = n0 + wave * 16 + 4 * (lane >> 4) + e;
+        if (n < a.N && c < a.C) pdst[(int64_t(n) * a.K + k) * a.C + c] = acc[k][ct][e];
+      }
+    }
+  }
+  if (want_bias && tid < 64 && n0 + tid < a.N) bpart[int64_t(split) * a.N + n0 + tid] = bsum;
+}
+
 // bf16 weight gradient.  One workgroup owns (n-tile BN, c-tile 32, all K taps) and
 // a contiguous range of 64-row m-tiles that never cross a sample boundary (so
 // the causal halo can be zero/replicate-filled while staging and no per-element
@@ -5385,6 +5492,15 @@ int wgrad_impl(const sel_conv_desc* d, int dtype, const void* gout, const void* 
     else if (p.bn == 32) SEL_WG_LAUNCH(32)
     else SEL_WG_LAUNCH(64)
 #undef SEL_WG_LAUNCH
+    SEL_LAUNCH_CHECK();
+  } else if (d->rows > 0 && dtype == SEL_F32 && d->C % 4 == 0 && d->N % 4 == 0 && d->K <= 8 &&
+             (d->K - 1) * d->dil <= WF_XR - WF_BM && d->pad <= (d->K - 1) * d->dil && tune(54) != 1) {
+    // fp32 on sample-aligned tiles (tune key 54 = 1: the generic kernel below);
+    // every split of the plan owns at least one tile
+    dim3 grid(unsigned((d->N + 63) / 64), unsigned((d->C + 31) / 32), unsigned(p.nsplit));
+    auto kern = d->K == 1 ? k_wgrad_f32<1> : d->K <= 3 ? k_wgrad_f32<3> : k_wgrad_f32<8>;
+    hipLaunchKernelGGL(kern, grid, dim3(256), 0, s, a, static_cast<const float*>(gout), static_cast<const float*>(in),
+                       int(p.tiles_per_sample), p.n_tiles, p.tiles_per_split, part, bpart);
     SEL_LAUNCH_CHECK();
   } else if (d->rows > 0 && dtype == SEL_F32) {
     // fp32 parity path: flat row ranges, same number of splits as the plan

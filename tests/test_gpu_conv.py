@@ -212,6 +212,51 @@ def test_wgrad_kernels_agree(gpu, shape):
             assert eb < 1e-5, (variant, eb)
 
 
+@pytest.mark.parametrize("shape", WGRAD_SHAPES)
+def test_wgrad_fp32_kernels_agree(gpu, shape):
+    """fp32 weight gradients: the sample-tiled k_wgrad_f32 (default where it
+    applies) and the generic k_conv_wgrad (tune key 54 = 1) against fp64 of the
+    same fp32 operands, 1e-5 norm-wise (fp32 products and sums, other orders);
+    includes ragged tiles (T % 64 != 0), replicate padding and the C = 1 layers."""
+    from sel import _lib as L
+    from sel import convops as CO
+    C, N, K, dil, mode, elu, bias, T = shape
+    B = 3
+    T = T + 13  # ragged last tile of every sample
+    pad = (K - 1) * dil if mode == 0 else 1
+    d = CO.ConvDesc(B * T, T, C, N, K, dil, pad, mode, elu, bias)
+    torch.manual_seed(C + N + K + 1)
+    x = 0.5 * torch.randn(B * T, C, device=gpu)
+    g = 0.5 * torch.randn(B * T, N, device=gpu)
+    xa = x.double().view(B, T, C)
+    if elu:
+        xa = torch.where(xa > 0, xa, torch.expm1(xa))
+    ga = g.double().view(B, T, N)
+    ref = torch.zeros(N, K, C, dtype=torch.float64, device=gpu)
+    for k in range(K):
+        idx = torch.arange(T, device=gpu) + k * dil - pad
+        if mode == 0:
+            ok = (idx >= 0) & (idx < T)
+            xs = torch.zeros(B, T, C, dtype=torch.float64, device=gpu)
+            xs[:, ok] = xa[:, idx[ok]]
+        else:
+            xs = xa[:, idx.clamp(0, T - 1)]
+        ref[:, k, :] = torch.einsum("btn,btc->nc", ga, xs)
+    bref = ga.sum((0, 1)).view(-1, bias).sum(0) if bias else None
+    lib = L.lib()
+    for variant in (0, 1):
+        prev = lib.sel_tune(54, variant)
+        try:
+            gw, gb = CO.wgrad(d, g, x, bool(bias))
+        finally:
+            lib.sel_tune(54, prev)
+        e = ((gw.double() - ref).norm() / ref.norm()).item()
+        assert e < 1e-5, (variant, e)
+        if bias:
+            eb = ((gb.double() - bref).norm() / bref.norm()).item()
+            assert eb < 1e-5, (variant, eb)
+
+
 @pytest.mark.parametrize("C,N,K,dil,elu,aux,res", [(1, 32, 7, 1, 0, 0, 0), (1, 32, 7, 1, 1, 1, 1), (1, 64, 3, 2, 0, 1, 0)])
 def test_single_channel_kernel_matches_generic(gpu, C, N, K, dil, elu, aux, res):
     """The streaming C=1 kernel (tune key 3 = 0) against the generic implicit-GEMM
