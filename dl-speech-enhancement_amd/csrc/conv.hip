@@ -247,6 +247,161 @@ __global__ __launch_bounds__(256) void k_conv_fwd(Args a, const TI* __restrict__
 }
 
 // ---------------------------------------------------------------------------
+// fp32 forward primitive on sample-aligned tiles (the reference-precision path;
+// also every fp32 dgrad, as the forward of the adjoint descriptor).  BM x BN
+// output tile, 4 waves of (BM / WM) x 32, v_mfma_f32_16x16x4_f32.  Per
+// 16-channel chunk the input span (tile + halo, ELU applied once, zero- or
+// replicate-filled per sample: no masks in the MFMA loop) and the weights of
+// all K taps are staged in LDS (80-B rows: conflict-free 16-B fragment reads;
+// 16 instead of 32 channels keeps the K = 7 stage at 46 KB, 3 workgroups per
+// CU, where the generic kernel's 82 KB allowed one), and the next chunk's
+// rows and weights are fetched into registers (16-B loads) during this
+// chunk's MFMAs.  Epilogue as k_conv_fwd (bias, ELU'(aux), residual, in that
+// order) through an fp32 LDS tile.
+constexpr int FF_CK = 16, FF_P = 20, FF_HALO = 64;
+// v or zeros, component-wise (a ternary on the float4 struct makes hipcc select
+// between two ADDRESSES: both operands go to scratch memory)
+__device__ __forceinline__ float4 keep4(bool ok, const float4& v) {
+  return make_float4(ok ? v.x : 0.f, ok ? v.y : 0.f, ok ? v.z : 0.f, ok ? v.w : 0.f);
+}
+template <int BM, int BN>
+constexpr int ff_xv() { return ((BM + FF_HALO) * (FF_CK / 4) + 255) / 256; }
+template <int KM, int BM, int BN>
+__global__ __launch_bounds__(256) void k_conv_fwd_f32(Args a, const float* __restrict__ in,
+                                                      const float* __restrict__ wp, const float* __restrict__ bias,
+                                                      const float* __restrict__ aux, const float* __restrict__ res,
+                                                      float* __restrict__ out) {
+  constexpr int WN = BN / 32, WM = 4 / WN, TM = BM / WM / 16, TN = 2;
+  constexpr int XV = ff_xv<BM, BN>();
+  constexpr int WV = (KM * BN * (FF_CK / 4) + 255) / 256;
+  extern __shared__ __align__(16) unsigned char smem[];
+  float* const xs = reinterpret_cast<float*>(smem);      // [BM + halo][FF_P]
+  float* const ws = xs + (BM + FF_HALO) * FF_P;          // [K][BN][FF_P]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int tps = (a.T + BM - 1) / BM;
+  const int64_t b = blockIdx.x / tps;
+  const int t0 = int(blockIdx.x - b * tps) * BM;
+  const int n0 = blockIdx.y * BN;
+  const int span = BM + (a.K - 1) * a.dil;
+  const float* __restrict__ xb = in + b * a.T * int64_t(a.C);
+
+  // raw loads and their predicates: the zero select happens in put(), after
+  // the next chunk's MFMAs (a select right behind a load waits for it)
+  floatx4 xr[XV], wr[WV];
+  bool xok[XV];
+  auto fetch = [&](int c0) {
+#pragma unroll
+    for (int u = 0; u < XV; ++u) {
+      const int v = tid + u * 256;
+      const int r = v >> 2, c = c0 + (v & 3) * 4;
+      int ti = t0 - a.pad + r;
+      bool ok = r < span;
+      if (ti < 0 || ti >= a.T) {
+        if (a.pad_mode == SEL_PAD_ZERO) ok = false;
+        ti = ti < 0 ? 0 : a.T - 1;
+      }
+      // unconditional load of a clamped (valid) row: a load under a
+      // per-element condition becomes a branch with its own vmcnt(0) wait
+      xr[u] = *reinterpret_cast<const floatx4*>(xb + int64_t(ti) * a.C + c);
+      xok[u] = ok;
+    }
+#pragma unroll
+    for (int u = 0; u < WV; ++u) {
+      const int v = tid + u * 256;
+      const int q = v & 3, row = v >> 2;  // row = k * BN + n
+      const int k = row / BN, n = row % BN;
+      const int kc = k < a.K ? k : a.K - 1;  // taps past K: never stored
+      wr[u] = *reinterpret_cast<const floatx4*>(wp + (int64_t(n0 + n) * a.K + kc) * a.C + c0 + 4 * q);
+    }
+  };
+  auto put = [&]() {
+#pragma unroll
+    for (int u = 0; u < XV; ++u) {
+      const int v = tid + u * 256;
+      const int r = v >> 2;
+      const bool ok = xok[u];
+      floatx4 x = floatx4{ok ? xr[u][0] : 0.f, ok ? xr[u][1] : 0.f, ok ? xr[u][2] : 0.f, ok ? xr[u][3] : 0.f};
+      if (a.in_elu) x = floatx4{elu(x[0]), elu(x[1]), elu(x[2]), elu(x[3])};
+      if (r < BM + FF_HALO) *reinterpret_cast<floatx4*>(xs + r * FF_P + (v & 3) * 4) = x;
+    }
+#pragma unroll
+    for (int u = 0; u < WV; ++u) {
+      const int v = tid + u * 256;
+      // (the stage holds K, not KM, taps)
+      if ((v >> 2) < a.K * BN) *reinterpret_cast<floatx4*>(ws + (v >> 2) * FF_P + (v & 3) * 4) = wr[u];
+    }
+  };
+
+  floatx4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int arow = wm * (BM / WM) + (lane & 15);
+  const int g4 = 4 * (lane >> 4);
+  fetch(0);
+  for (int c0 = 0; c0 < a.C; c0 += FF_CK) {
+    __syncthreads();  // every wave is done with the previous chunk
+    put();
+    __syncthreads();
+    if (c0 + FF_CK < a.C) fetch(c0 + FF_CK);
+    for (int k = 0; k < a.K; ++k) {
+      float4 av[TM], bv[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) av[i] = *reinterpret_cast<const float4*>(xs + (arow + 16 * i + k * a.dil) * FF_P + g4);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        bv[j] = *reinterpret_cast<const float4*>(ws + (k * BN + wn * 32 + 16 * j + (lane & 15)) * FF_P + g4);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i].x, bv[j].x, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i].y, bv[j].y, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i].z, bv[j].z, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i].w, bv[j].w, acc[i][j], 0, 0, 0);
+        }
+    }
+  }
+  // epilogue: accumulators -> LDS (fp32) -> 16-B vectors with bias / ELU' / residual
+  constexpr int OP = BN + 4;
+  __syncthreads();
+  float* ot = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = wn * 32 + j * 16 + (lane & 15);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) ot[(wm * (BM / WM) + i * 16 + g4 + e) * OP + col] = acc[i][j][e];
+    }
+  __syncthreads();
+  const int mrows = a.T - t0 < BM ? a.T - t0 : BM;
+  for (int idx = tid; idx < BM * (BN / 4); idx += 256) {
+    const int r = idx / (BN / 4), cv = (idx % (BN / 4)) * 4;
+    if (r >= mrows) continue;
+    const int64_t o = (b * a.T + t0 + r) * a.N + n0 + cv;
+    float v[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int ne = n0 + cv + e;
+      const float bv = (bias && a.bias_period) ? bias[ne % a.bias_period] : 0.f;
+      v[e] = ot[r * OP + cv + e] + bv;
+    }
+    if (aux) {
+      const float4 av = *reinterpret_cast<const float4*>(aux + o);
+      v[0] *= elu_grad(av.x), v[1] *= elu_grad(av.y), v[2] *= elu_grad(av.z), v[3] *= elu_grad(av.w);
+    }
+    if (res) {
+      const float4 rv = *reinterpret_cast<const float4*>(res + o);
+      v[0] += rv.x, v[1] += rv.y, v[2] += rv.z, v[3] += rv.w;
+    }
+    *reinterpret_cast<float4*>(out + o) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // bf16 forward primitive (the hot one).  Per 32-channel chunk the input rows
 // [m0 - pad, m0 + BM + (K-1)*dil - pad) are staged ONCE (ELU applied once per
 // element) together with the packed weights of all K taps; the K taps then
@@ -2871,16 +3026,21 @@ __global__ __launch_bounds__(256) void k_wgrad_f32(Args a, const float* __restri
   for (int k = 0; k < KM; ++k) acc[k][0] = acc[k][1] = floatx4{0.f, 0.f, 0.f, 0.f};
   float bsum = 0.f;
 
+  // raw loads of clamped (valid) addresses and their predicates; the zero
+  // select happens in put() (a load under a per-element condition is a branch
+  // with a vmcnt(0) wait, and a select right behind a load waits for it)
   float4 gr[4], xr[4];
+  bool gok[4], xok[4];
   auto fetch = [&](int64_t tile) {
     const int64_t b = tile / tps;
     const int t0 = int(tile - b * tps) * WF_BM;
-    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int r = i * 16 + (tid >> 4), n = n0 + (tid & 15) * 4;
       const int t = t0 + r;
-      gr[i] = t < a.T && n < a.N ? *reinterpret_cast<const float4*>(gout + (b * a.T + t) * a.N + n) : z;
+      const int tc = t < a.T ? t : a.T - 1, nc = n < a.N ? n : a.N - 4;
+      gr[i] = *reinterpret_cast<const float4*>(gout + (b * a.T + tc) * a.N + nc);
+      gok[i] = t < a.T && n < a.N;
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -2891,16 +3051,17 @@ __global__ __launch_bounds__(256) void k_wgrad_f32(Args a, const float* __restri
         if (a.pad_mode == SEL_PAD_ZERO) ok = false;
         ti = ti < 0 ? 0 : a.T - 1;
       }
-      xr[i] = ok ? *reinterpret_cast<const float4*>(in + (b * a.T + ti) * a.C + c) : z;
+      xr[i] = *reinterpret_cast<const float4*>(in + (b * a.T + ti) * a.C + (c < a.C ? c : a.C - 4));
+      xok[i] = ok;
     }
   };
   auto put = [&]() {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      *reinterpret_cast<float4*>(gs + (i * 16 + (tid >> 4)) * WF_GP + (tid & 15) * 4) = gr[i];
+      *reinterpret_cast<float4*>(gs + (i * 16 + (tid >> 4)) * WF_GP + (tid & 15) * 4) = keep4(gok[i], gr[i]);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      float4 v = xr[i];
+      float4 v = keep4(xok[i], xr[i]);
       if (a.in_elu) v = make_float4(elu(v.x), elu(v.y), elu(v.z), elu(v.w));
       *reinterpret_cast<float4*>(xs + (i * 32 + (tid >> 3)) * WF_XP + (tid & 7) * 4) = v;
     }
@@ -4467,6 +4628,33 @@ int launch_fwd(const Args& a, const void* in, const void* wp, const float* bias,
   return SEL_OK;
 }
 
+template <int BM, int BN>
+int launch_fwd_f32(const Args& a, const void* in, const void* wp, const float* bias, const void* aux,
+                   const void* res, void* out, hipStream_t s) {
+  const size_t stage = (size_t(BM + FF_HALO) + size_t(a.K) * BN) * FF_P * sizeof(float);
+  const size_t epi = size_t(BM) * (BN + 4) * sizeof(float);
+  const size_t lds = stage > epi ? stage : epi;
+  const int64_t tiles = (a.rows / a.T) * ((a.T + BM - 1) / BM);  // sample-aligned tiles
+  if (tiles == 0) return SEL_OK;
+  dim3 grid(unsigned(tiles), unsigned(a.N / BN));
+  const void* kern = a.K == 1 ? (const void*)k_conv_fwd_f32<1, BM, BN>
+                     : a.K <= 3 ? (const void*)k_conv_fwd_f32<3, BM, BN> : (const void*)k_conv_fwd_f32<8, BM, BN>;
+  if (lds > 64 * 1024) SEL_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
+  const float* x = static_cast<const float*>(in);
+  const float* w = static_cast<const float*>(wp);
+  const float* ax = static_cast<const float*>(aux);
+  const float* rs = static_cast<const float*>(res);
+  float* o = static_cast<float*>(out);
+  if (a.K == 1)
+    hipLaunchKernelGGL((k_conv_fwd_f32<1, BM, BN>), grid, dim3(256), lds, s, a, x, w, bias, ax, rs, o);
+  else if (a.K <= 3)
+    hipLaunchKernelGGL((k_conv_fwd_f32<3, BM, BN>), grid, dim3(256), lds, s, a, x, w, bias, ax, rs, o);
+  else
+    hipLaunchKernelGGL((k_conv_fwd_f32<8, BM, BN>), grid, dim3(256), lds, s, a, x, w, bias, ax, rs, o);
+  SEL_LAUNCH_CHECK();
+  return SEL_OK;
+}
+
 template <int BM, int BN, int WAVES_M, int KMAX, typename TO>
 int launch_fwd4(const Args& a, const void* in, const void* wp, const float* bias, const void* aux,
                 const void* res, void* out, hipStream_t s) {
@@ -5082,6 +5270,13 @@ int dispatch_fwd(const Args& a, const void* in, const void* wp, const float* bia
     }
   }
   if (sizeof(TI) == 4) {
+    if constexpr (sizeof(TO) == 4) {
+      // sample-aligned fp32 tiles (tune key 55 = 1: the generic kernel)
+      if (a.C % FF_CK == 0 && a.N % 32 == 0 && a.K <= 8 && (a.K - 1) * a.dil <= FF_HALO && tune(55) != 1) {
+        if (a.N % 64 == 0) return launch_fwd_f32<64, 64>(a, in, wp, bias, aux, res, out, s);
+        return launch_fwd_f32<128, 32>(a, in, wp, bias, aux, res, out, s);
+      }
+    }
     if (a.N <= 32) return launch_fwd<TI, TO, 128, 32>(a, in, wp, bias, aux, res, out, s);
     return launch_fwd<TI, TO, 64, 64>(a, in, wp, bias, aux, res, out, s);
   }
