@@ -2698,11 +2698,23 @@ __device__ __forceinline__ void c1_stage(const Args& a, const __bf16* __restrict
 // Thread = (8-wide output group g, row lane rl): its 8 x K weights live in
 // registers; per row it reads K staged samples and writes one 16-B vector, the
 // NG lanes of a row together writing the row's contiguous N outputs.
-template <typename TO, int TR>
-__global__ __launch_bounds__(256) void k_conv_c1_bf16(Args a, const __bf16* __restrict__ in,
-                                                      const __bf16* __restrict__ wp, const float* __restrict__ bias,
-                                                      const TO* __restrict__ aux, const TO* __restrict__ res,
-                                                      TO* __restrict__ out) {
+// TI = float (the reference-precision path): exact expm1 / exp in the ELU and
+// ELU' (the bf16 build rounds its result to bf16 and uses the hardware exp)
+template <typename TI>
+__device__ __forceinline__ float c1_act(float v) {
+  if constexpr (sizeof(TI) == 4) return elu(v);
+  else return elu_fast(v);
+}
+template <typename TI>
+__device__ __forceinline__ float c1_act_grad(float v) {
+  if constexpr (sizeof(TI) == 4) return elu_grad(v);
+  else return elu_grad_fast(v);
+}
+template <typename TI, typename TO, int TR>
+__global__ __launch_bounds__(256) void k_conv_c1(Args a, const TI* __restrict__ in,
+                                                 const TI* __restrict__ wp, const float* __restrict__ bias,
+                                                 const TO* __restrict__ aux, const TO* __restrict__ res,
+                                                 TO* __restrict__ out) {
   __shared__ float xs[TR + C1_HALO];
   constexpr int PV = (TR + C1_HALO + 255) / 256;  // staged samples per thread
   constexpr int V = Vec16<TO>::n;  // outputs per vector store (8 bf16 / 4 fp32)
@@ -2714,7 +2726,7 @@ __global__ __launch_bounds__(256) void k_conv_c1_bf16(Args a, const __bf16* __re
     const int n = grp * V + e;
     bs[e] = (bias && a.bias_period) ? bias[n % a.bias_period] : 0.f;
 #pragma unroll
-    for (int k = 0; k < C1_KMAX; ++k) w[e][k] = k < a.K ? float(wp[n * a.K + k]) : 0.f;
+    for (int k = 0; k < C1_KMAX; ++k) w[e][k] = k < a.K ? to_f(wp[n * a.K + k]) : 0.f;
   }
   const int tps = (a.T + TR - 1) / TR;
   const int64_t ntiles = (a.rows / a.T) * tps;
@@ -2731,8 +2743,8 @@ __global__ __launch_bounds__(256) void k_conv_c1_bf16(Args a, const __bf16* __re
       int ti = t0 - a.pad + r;
       const bool ok = r < span && ((ti >= 0 && ti < a.T) || a.pad_mode == SEL_PAD_REPLICATE);
       ti = ti < 0 ? 0 : (ti >= a.T ? a.T - 1 : ti);
-      const float v = ok ? float(in[b * a.T + ti]) : 0.f;
-      pre[u] = ok && a.in_elu ? elu_fast(v) : v;
+      const float v = ok ? to_f(in[b * a.T + ti]) : 0.f;
+      pre[u] = ok && a.in_elu ? c1_act<TI>(v) : v;
     }
   };
   if (int64_t(blockIdx.x) < ntiles) fetch(blockIdx.x);
@@ -2762,7 +2774,7 @@ __global__ __launch_bounds__(256) void k_conv_c1_bf16(Args a, const __bf16* __re
         TO av[V];
         *reinterpret_cast<uint4*>(av) = *reinterpret_cast<const uint4*>(aux + o);
 #pragma unroll
-        for (int e = 0; e < V; ++e) v[e] *= elu_grad_fast(to_f(av[e]));
+        for (int e = 0; e < V; ++e) v[e] *= c1_act_grad<TI>(to_f(av[e]));
       }
       if (res) {
         TO rv[V];
@@ -2783,10 +2795,35 @@ __global__ __launch_bounds__(256) void k_conv_c1_bf16(Args a, const __bf16* __re
 // each block walks its contiguous range of sample-aligned 256-row tiles with the
 // samples staged in LDS, then reduces its lanes (shuffles, LDS over waves) into
 // one partial per block.
-template <int NG>  // 1, 2, 4 or 8 n-groups (N / 8)
-__global__ __launch_bounds__(256) void k_wgrad_c1_bf16(Args a, const __bf16* __restrict__ gout,
-                                                       const __bf16* __restrict__ in, int64_t tiles_per_split,
-                                                       float* __restrict__ part, float* __restrict__ bpart) {
+// 8 consecutive gout values of one row: one 16-B load (bf16) or two (fp32)
+struct F8 {
+  float4 lo, hi;
+};
+template <typename TI> struct G8;
+template <> struct G8<__bf16> {
+  using type = uint4;
+  static __device__ __forceinline__ type load(const __bf16* p) { return *reinterpret_cast<const uint4*>(p); }
+  static __device__ __forceinline__ void get(const type& v, float (&f)[8]) {
+    const __bf16* h = reinterpret_cast<const __bf16*>(&v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] = float(h[e]);
+  }
+};
+template <> struct G8<float> {
+  using type = F8;
+  static __device__ __forceinline__ type load(const float* p) {
+    return F8{*reinterpret_cast<const float4*>(p), *reinterpret_cast<const float4*>(p + 4)};
+  }
+  static __device__ __forceinline__ void get(const type& v, float (&f)[8]) {
+    f[0] = v.lo.x, f[1] = v.lo.y, f[2] = v.lo.z, f[3] = v.lo.w;
+    f[4] = v.hi.x, f[5] = v.hi.y, f[6] = v.hi.z, f[7] = v.hi.w;
+  }
+};
+
+template <typename TI, int NG>  // 1, 2, 4 or 8 n-groups (N / 8)
+__global__ __launch_bounds__(256) void k_wgrad_c1(Args a, const TI* __restrict__ gout,
+                                                  const TI* __restrict__ in, int64_t tiles_per_split,
+                                                  float* __restrict__ part, float* __restrict__ bpart) {
   __shared__ float xs[C1_TR + C1_HALO];
   __shared__ float red[4][C1_NMAX * (C1_KMAX + 1)];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -2815,13 +2852,14 @@ __global__ __launch_bounds__(256) void k_wgrad_c1_bf16(Args a, const __bf16* __r
       int ti = t0 - a.pad + r;
       const bool ok = r < span && ((ti >= 0 && ti < a.T) || a.pad_mode == SEL_PAD_REPLICATE);
       ti = ti < 0 ? 0 : (ti >= a.T ? a.T - 1 : ti);
-      const float v = ok ? float(in[b * a.T + ti]) : 0.f;
-      pre[u] = ok && a.in_elu ? elu_fast(v) : v;
+      const float v = ok ? to_f(in[b * a.T + ti]) : 0.f;
+      pre[u] = ok && a.in_elu ? c1_act<TI>(v) : v;
     }
   };
   constexpr int MAXR = C1_TR * NG / 256;  // rows per thread and tile
   // this tile's gout rows (next tile's: requested before this tile's FMAs)
-  uint4 gq[MAXR];
+  using GV = typename G8<TI>::type;
+  GV gq[MAXR];
   auto fetch_g = [&](int64_t tile) {
     const int64_t b = tile / tps;
     const int t0 = int(tile % tps) * C1_TR;
@@ -2830,7 +2868,7 @@ __global__ __launch_bounds__(256) void k_wgrad_c1_bf16(Args a, const __bf16* __r
     for (int j = 0; j < MAXR; ++j) {
       const int r = rl + j * nrl;
       if (j * nrl < C1_TR && r < rows)
-        gq[j] = *reinterpret_cast<const uint4*>(gout + (b * a.T + t0 + r) * a.N + grp * 8);
+        gq[j] = G8<TI>::load(gout + (b * a.T + t0 + r) * a.N + grp * 8);
     }
   };
   if (tb < te) {
@@ -2846,24 +2884,22 @@ __global__ __launch_bounds__(256) void k_wgrad_c1_bf16(Args a, const __bf16* __r
     __syncthreads();
     if (tile + 1 < te) fetch(tile + 1);
     const int rows = a.T - t0 < C1_TR ? a.T - t0 : C1_TR;
-    uint4 gc[MAXR];
+    GV gc[MAXR];
 #pragma unroll
     for (int j = 0; j < MAXR; ++j) gc[j] = gq[j];
     if (tile + 1 < te) fetch_g(tile + 1);
-    __bf16 gvs[MAXR][8];
-#pragma unroll
-    for (int j = 0; j < MAXR; ++j) *reinterpret_cast<uint4*>(gvs[j]) = gc[j];
 #pragma unroll
     for (int j = 0; j < MAXR; ++j) {
       const int r = rl + j * nrl;
       if (j * nrl >= C1_TR || r >= rows) break;
-      const __bf16* gv = gvs[j];
+      float gv[8];
+      G8<TI>::get(gc[j], gv);
       float xv[C1_KMAX];
 #pragma unroll
       for (int k = 0; k < C1_KMAX; ++k) xv[k] = k < a.K ? xs[r + k * a.dil] : 0.f;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const float g = float(gv[e]);
+        const float g = gv[e];
         bsum[e] += g;
 #pragma unroll
         for (int k = 0; k < C1_KMAX; ++k) acc[e][k] = fmaf(g, xv[k], acc[e][k]);
@@ -5217,21 +5253,21 @@ bool ru_fused_ok(const Args& a) {
 // single-input-channel forward (k_conv_c1_bf16): one resident round of
 // workgroups walking TR-row tiles (they prefetch their next tile); tune key
 // 44 = 1: the round-3 256-row tiles
-template <typename TO, int TR>
+template <typename TI, typename TO, int TR>
 int launch_c1(const Args& a, const void* in, const void* wp, const float* bias, const void* aux, const void* res,
               void* out, hipStream_t s) {
   static const int64_t slots = [] {
     int dev = 0, cus = 0, per_cu = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_conv_c1_bf16<TO, TR>, 256, 0) != hipSuccess)
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_conv_c1<TI, TO, TR>, 256, 0) != hipSuccess)
       return int64_t(4096);
     return std::max<int64_t>(256, int64_t(cus) * per_cu);
   }();
   const int64_t blocks = std::min<int64_t>((a.rows / a.T) * ((a.T + TR - 1) / TR), tune(23) > 0 ? tune(23) : slots);
   if (blocks <= 0) return SEL_OK;
-  hipLaunchKernelGGL((k_conv_c1_bf16<TO, TR>), dim3(unsigned(blocks)), dim3(256), 0, s, a,
-                     static_cast<const __bf16*>(in), static_cast<const __bf16*>(wp), bias,
+  hipLaunchKernelGGL((k_conv_c1<TI, TO, TR>), dim3(unsigned(blocks)), dim3(256), 0, s, a,
+                     static_cast<const TI*>(in), static_cast<const TI*>(wp), bias,
                      static_cast<const TO*>(aux), static_cast<const TO*>(res), static_cast<TO*>(out));
   SEL_LAUNCH_CHECK();
   return SEL_OK;
@@ -5250,8 +5286,8 @@ int dispatch_fwd(const Args& a, const void* in, const void* wp, const float* bia
   if constexpr (sizeof(TI) == 2) {
     if (a.C == 1 && a.N % 8 == 0 && a.N <= C1_NMAX && a.K <= C1_KMAX && (a.K - 1) * a.dil <= C1_HALO &&
         tune(3) == 0)
-      return tune(44) == 1 ? launch_c1<TO, 256>(a, in, wp, bias, aux, res, out, s)
-                           : launch_c1<TO, C1F_TR>(a, in, wp, bias, aux, res, out, s);
+      return tune(44) == 1 ? launch_c1<TI, TO, 256>(a, in, wp, bias, aux, res, out, s)
+                           : launch_c1<TI, TO, C1F_TR>(a, in, wp, bias, aux, res, out, s);
     const int v = tune(0);
     const bool fast = (a.C % CK) == 0 && (a.K - 1) * a.dil <= F4_HALOMAX && a.K <= 8 && (v == 0 || v > 20);
     if (fast) {
@@ -5271,6 +5307,10 @@ int dispatch_fwd(const Args& a, const void* in, const void* wp, const float* bia
   }
   if (sizeof(TI) == 4) {
     if constexpr (sizeof(TO) == 4) {
+      // single input channel: the streaming kernel with exact fp32 ELU (tune key 55 = 1: generic)
+      if (a.C == 1 && a.N % 4 == 0 && a.N <= C1_NMAX && a.K <= C1_KMAX && (a.K - 1) * a.dil <= C1_HALO &&
+          tune(55) != 1)
+        return launch_c1<TI, TO, C1F_TR>(a, in, wp, bias, aux, res, out, s);
       // sample-aligned fp32 tiles (tune key 55 = 1: the generic kernel)
       if (a.C % FF_CK == 0 && a.N % 32 == 0 && a.K <= 8 && (a.K - 1) * a.dil <= FF_HALO && tune(55) != 1) {
         if (a.N % 64 == 0) return launch_fwd_f32<64, 64>(a, in, wp, bias, aux, res, out, s);
@@ -5311,7 +5351,8 @@ bool wgrad_c1_ok(const sel_conv_desc* d) {
 }
 
 int wgrad_mode(const sel_conv_desc* d, int dtype) {
-  if (dtype != SEL_BF16) return 0;
+  // fp32: the single-channel kernel where it applies (tune key 54 = 1: generic)
+  if (dtype != SEL_BF16) return wgrad_c1_ok(d) && tune(54) != 1 ? 4 : 0;
   const int t = tune(1);
   if (wgrad_c1_ok(d) && t != 1) return 4;
   if (t == 1 || !wgrad_tr_ok(d)) return 0;
@@ -5642,11 +5683,17 @@ int wgrad_impl(const sel_conv_desc* d, int dtype, const void* gout, const void* 
   float* part = static_cast<float*>(ws);
   float* bpart = gbias ? part + size_t(p.nsplit) * d->N * d->K * d->C : nullptr;
   if (d->rows > 0 && p.mode == 4) {
-    auto kc1 = d->N == 8 ? k_wgrad_c1_bf16<1> : d->N == 16 ? k_wgrad_c1_bf16<2>
-               : d->N == 32 ? k_wgrad_c1_bf16<4> : k_wgrad_c1_bf16<8>;
-    hipLaunchKernelGGL(kc1, dim3(unsigned(p.nsplit)), dim3(256), 0, s, a,
-                       static_cast<const __bf16*>(gout), static_cast<const __bf16*>(in), int64_t(p.tiles_per_split),
-                       part, bpart);
+    if (dtype == SEL_F32) {
+      auto kc1 = d->N == 8 ? k_wgrad_c1<float, 1> : d->N == 16 ? k_wgrad_c1<float, 2>
+                 : d->N == 32 ? k_wgrad_c1<float, 4> : k_wgrad_c1<float, 8>;
+      hipLaunchKernelGGL(kc1, dim3(unsigned(p.nsplit)), dim3(256), 0, s, a, static_cast<const float*>(gout),
+                         static_cast<const float*>(in), int64_t(p.tiles_per_split), part, bpart);
+    } else {
+      auto kc1 = d->N == 8 ? k_wgrad_c1<__bf16, 1> : d->N == 16 ? k_wgrad_c1<__bf16, 2>
+                 : d->N == 32 ? k_wgrad_c1<__bf16, 4> : k_wgrad_c1<__bf16, 8>;
+      hipLaunchKernelGGL(kc1, dim3(unsigned(p.nsplit)), dim3(256), 0, s, a, static_cast<const __bf16*>(gout),
+                         static_cast<const __bf16*>(in), int64_t(p.tiles_per_split), part, bpart);
+    }
     SEL_LAUNCH_CHECK();
   } else if (d->rows > 0 && p.mode == 3) {
     const __bf16* g16 = static_cast<const __bf16*>(gout);

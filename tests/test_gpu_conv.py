@@ -257,6 +257,55 @@ def test_wgrad_fp32_kernels_agree(gpu, shape):
             assert eb < 1e-5, (variant, eb)
 
 
+@pytest.mark.parametrize("shape", WGRAD_SHAPES)
+def test_fwd_fp32_kernels_agree(gpu, shape):
+    """fp32 forward primitive: the sample-tiled k_conv_fwd_f32 (default where it
+    applies) and the generic k_conv_fwd (tune key 55 = 1) against fp64 of the
+    same operands with bias, ELU'(aux) and residual epilogues: 1e-5 norm-wise;
+    ragged tiles (T % 64 != 0), replicate padding and the C = 1 layers."""
+    from sel import _lib as L
+    from sel import convops as CO
+    C, N, K, dil, mode, elu, bias, T = shape
+    B = 3
+    T = T + 13
+    pad = (K - 1) * dil if mode == 0 else 1
+    d = CO.ConvDesc(B * T, T, C, N, K, dil, pad, mode, elu, N if bias else 0)
+    torch.manual_seed(C + N + K + 2)
+    x = 0.5 * torch.randn(B * T, C, device=gpu)
+    wp = 0.2 * torch.randn(N, K, C, device=gpu)
+    b = torch.randn(N, device=gpu) if bias else None
+    aux = torch.randn(B * T, N, device=gpu)
+    res = torch.randn(B * T, N, device=gpu)
+    xa = x.double().view(B, T, C)
+    if elu:
+        xa = torch.where(xa > 0, xa, torch.expm1(xa))
+    ref = torch.zeros(B, T, N, dtype=torch.float64, device=gpu)
+    for k in range(K):
+        idx = torch.arange(T, device=gpu) + k * dil - pad
+        if mode == 0:
+            ok = (idx >= 0) & (idx < T)
+            xs = torch.zeros(B, T, C, dtype=torch.float64, device=gpu)
+            xs[:, ok] = xa[:, idx[ok]]
+        else:
+            xs = xa[:, idx.clamp(0, T - 1)]
+        ref += torch.einsum("btc,nc->btn", xs, wp[:, k, :].double())
+    if bias:
+        ref += b.double()
+    ref = ref.view(B * T, N)
+    refe = ref * torch.where(aux.double() > 0, 1.0, torch.exp(aux.double())) + res.double()
+    lib = L.lib()
+    for variant in (0, 1):
+        prev = lib.sel_tune(55, variant)
+        try:
+            y = CO.prim(d, x, wp, bias=b)
+            ye = CO.prim(d, x, wp, bias=b, aux=aux, res=res)
+        finally:
+            lib.sel_tune(55, prev)
+        for got, want in ((y, ref), (ye, refe)):
+            e = ((got.double() - want).norm() / want.norm()).item()
+            assert e < 1e-5, (variant, e)
+
+
 @pytest.mark.parametrize("C,N,K,dil,elu,aux,res", [(1, 32, 7, 1, 0, 0, 0), (1, 32, 7, 1, 1, 1, 1), (1, 64, 3, 2, 0, 1, 0)])
 def test_single_channel_kernel_matches_generic(gpu, C, N, K, dil, elu, aux, res):
     """The streaming C=1 kernel (tune key 3 = 0) against the generic implicit-GEMM
