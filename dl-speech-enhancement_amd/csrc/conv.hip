@@ -3041,46 +3041,59 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(Args a, const TI* __restrict
 // MFMA v_mfma_f32_16x16x4_f32: A = g^T (lane: n = l & 15, row 4q + l >> 4),
 // B = ELU(x) rows shifted by the tap (col c = l & 15); the 4 rows of one
 // k-step are 80 / 48 floats apart in LDS (distinct 16-bank groups).
-constexpr int WF_BM = 64, WF_GP = 80, WF_XP = 48, WF_XR = 128;
-template <int KM>
+constexpr int WF_BM = 64, WF_XR = 128;
+// NB output x CB input channels per workgroup: (64, 32), or (32, 64) / (32, 32)
+// for the 32-wide layers (a 64-wide block would leave two of its waves on
+// absent output channels); waves = (NB / 16) along n x the rest along c, each
+// 16 n x CT 16-wide c tiles x all taps.  Row pitches NB + 16 / CB + 16 floats
+// put the 4 rows of one k-step in distinct 16-bank groups.
+template <int KM, int NB, int CB>
 __global__ __launch_bounds__(256) void k_wgrad_f32(Args a, const float* __restrict__ gout,
                                                    const float* __restrict__ in, int tps, int64_t n_tiles,
                                                    int tiles_per_split, float* __restrict__ part,
                                                    float* __restrict__ bpart) {
-  __shared__ __align__(16) float gs[WF_BM * WF_GP];
-  __shared__ __align__(16) float xs[WF_XR * WF_XP];
+  constexpr int GP = NB + 16, XP = CB + 16;
+  constexpr int WN = NB / 16, WC = 4 / WN, CT = CB / (16 * WC);
+  constexpr int G4 = NB / 4, GRP = 256 / G4, GI = WF_BM / GRP;   // gout float4 per row, rows per pass, passes
+  constexpr int X4 = CB / 4, XRP = 256 / X4, XI = WF_XR / XRP;   // input float4 per row, rows per pass, passes
+  static_assert(WN * WC == 4 && CT >= 1, "wave layout");
+  __shared__ __align__(16) float gs[WF_BM * GP];
+  __shared__ __align__(16) float xs[WF_XR * XP];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int n0 = blockIdx.x * 64, c0 = blockIdx.y * 32;
+  const int wn = wave % WN, wc = wave / WN;
+  const int n0 = blockIdx.x * NB, c0 = blockIdx.y * CB;
   const int split = blockIdx.z;
   const int64_t tb = int64_t(split) * tiles_per_split;
   const int64_t te = tb + tiles_per_split < n_tiles ? tb + tiles_per_split : n_tiles;
   const int span = WF_BM + (a.K - 1) * a.dil;
   const bool want_bias = bpart != nullptr && c0 == 0;
 
-  floatx4 acc[KM][2];
+  floatx4 acc[KM][CT];
 #pragma unroll
-  for (int k = 0; k < KM; ++k) acc[k][0] = acc[k][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int k = 0; k < KM; ++k)
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) acc[k][ct] = floatx4{0.f, 0.f, 0.f, 0.f};
   float bsum = 0.f;
 
   // raw loads of clamped (valid) addresses and their predicates; the zero
   // select happens in put() (a load under a per-element condition is a branch
   // with a vmcnt(0) wait, and a select right behind a load waits for it)
-  float4 gr[4], xr[4];
-  bool gok[4], xok[4];
+  float4 gr[GI], xr[XI];
+  bool gok[GI], xok[XI];
   auto fetch = [&](int64_t tile) {
     const int64_t b = tile / tps;
     const int t0 = int(tile - b * tps) * WF_BM;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = i * 16 + (tid >> 4), n = n0 + (tid & 15) * 4;
+    for (int i = 0; i < GI; ++i) {
+      const int r = i * GRP + tid / G4, n = n0 + (tid % G4) * 4;
       const int t = t0 + r;
       const int tc = t < a.T ? t : a.T - 1, nc = n < a.N ? n : a.N - 4;
       gr[i] = *reinterpret_cast<const float4*>(gout + (b * a.T + tc) * a.N + nc);
       gok[i] = t < a.T && n < a.N;
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = i * 32 + (tid >> 3), c = c0 + (tid & 7) * 4;
+    for (int i = 0; i < XI; ++i) {
+      const int r = i * XRP + tid / X4, c = c0 + (tid % X4) * 4;
       int ti = t0 - a.pad + r;
       bool ok = r < span && c < a.C;
       if (ti < 0 || ti >= a.T) {
@@ -3093,36 +3106,37 @@ __global__ __launch_bounds__(256) void k_wgrad_f32(Args a, const float* __restri
   };
   auto put = [&]() {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      *reinterpret_cast<float4*>(gs + (i * 16 + (tid >> 4)) * WF_GP + (tid & 15) * 4) = keep4(gok[i], gr[i]);
+    for (int i = 0; i < GI; ++i)
+      *reinterpret_cast<float4*>(gs + (i * GRP + tid / G4) * GP + (tid % G4) * 4) = keep4(gok[i], gr[i]);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < XI; ++i) {
       float4 v = keep4(xok[i], xr[i]);
       if (a.in_elu) v = make_float4(elu(v.x), elu(v.y), elu(v.z), elu(v.w));
-      *reinterpret_cast<float4*>(xs + (i * 32 + (tid >> 3)) * WF_XP + (tid & 7) * 4) = v;
+      *reinterpret_cast<float4*>(xs + (i * XRP + tid / X4) * XP + (tid % X4) * 4) = v;
     }
   };
 
   if (tb < te) fetch(tb);
-  const float* gcol = gs + wave * 16 + (lane & 15);
-  const float* xcol = xs + (lane & 15);
+  const float* gcol = gs + wn * 16 + (lane & 15);
+  const float* xcol = xs + wc * CT * 16 + (lane & 15);
   for (int64_t tile = tb; tile < te; ++tile) {
     __syncthreads();  // the previous tile's MFMAs are done with gs / xs
     put();
     __syncthreads();
     if (tile + 1 < te) fetch(tile + 1);
-    if (want_bias && tid < 64)
-      for (int r = 0; r < WF_BM; ++r) bsum += gs[r * WF_GP + tid];
+    if (want_bias && tid < NB)
+      for (int r = 0; r < WF_BM; ++r) bsum += gs[r * GP + tid];
 #pragma unroll 2
     for (int q = 0; q < WF_BM / 4; ++q) {
       const int r = 4 * q + (lane >> 4);
-      const float av = gcol[r * WF_GP];
+      const float av = gcol[r * GP];
 #pragma unroll
       for (int k = 0; k < KM; ++k) {
         if (k >= a.K) break;
-        const float* xrow = xcol + (r + k * a.dil) * WF_XP;
-        acc[k][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, xrow[0], acc[k][0], 0, 0, 0);
-        acc[k][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, xrow[16], acc[k][1], 0, 0, 0);
+        const float* xrow = xcol + (r + k * a.dil) * XP;
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct)
+          acc[k][ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, xrow[16 * ct], acc[k][ct], 0, 0, 0);
       }
     }
   }
@@ -3132,16 +3146,16 @@ __global__ __launch_bounds__(256) void k_wgrad_f32(Args a, const float* __restri
   for (int k = 0; k < KM; ++k) {
     if (k >= a.K) break;
 #pragma unroll
-    for (int ct = 0; ct < 2; ++ct) {
-      const int c = c0 + ct * 16 + (lane & 15);
+    for (int ct = 0; ct < CT; ++ct) {
+      const int c = c0 + (wc * CT + ct) * 16 + (lane & 15);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int n = n0 + wave * 16 + 4 * (lane >> 4) + e;
+        const int n = n0 + wn * 16 + 4 * (lane >> 4) + e;
         if (n < a.N && c < a.C) pdst[(int64_t(n) * a.K + k) * a.C + c] = acc[k][ct][e];
       }
     }
   }
-  if (want_bias && tid < 64 && n0 + tid < a.N) bpart[int64_t(split) * a.N + n0 + tid] = bsum;
+  if (want_bias && tid < NB && n0 + tid < a.N) bpart[int64_t(split) * a.N + n0 + tid] = bsum;
 }
 
 // bf16 weight gradient.  One workgroup owns (n-tile BN, c-tile 32, all K taps) and
@@ -5739,10 +5753,20 @@ int wgrad_impl(const sel_conv_desc* d, int dtype, const void* gout, const void* 
              (d->K - 1) * d->dil <= WF_XR - WF_BM && d->pad <= (d->K - 1) * d->dil && tune(54) != 1) {
     // fp32 on sample-aligned tiles (tune key 54 = 1: the generic kernel below);
     // every split of the plan owns at least one tile
-    dim3 grid(unsigned((d->N + 63) / 64), unsigned((d->C + 31) / 32), unsigned(p.nsplit));
-    auto kern = d->K == 1 ? k_wgrad_f32<1> : d->K <= 3 ? k_wgrad_f32<3> : k_wgrad_f32<8>;
-    hipLaunchKernelGGL(kern, grid, dim3(256), 0, s, a, static_cast<const float*>(gout), static_cast<const float*>(in),
-                       int(p.tiles_per_sample), p.n_tiles, p.tiles_per_split, part, bpart);
+    // block shape: 64 x 32 channels, or 32 x 64 / 32 x 32 for the 32-wide layers
+    const int nb = d->N <= 32 ? 32 : 64, cb = nb == 64 ? 32 : (d->C % 64 == 0 ? 64 : 32);
+    dim3 grid(unsigned((d->N + nb - 1) / nb), unsigned((d->C + cb - 1) / cb), unsigned(p.nsplit));
+#define SEL_WGF(NB, CB)                                                                                       \
+  {                                                                                                           \
+    auto kern = d->K == 1 ? k_wgrad_f32<1, NB, CB> : d->K <= 3 ? k_wgrad_f32<3, NB, CB> : k_wgrad_f32<8, NB, CB>; \
+    hipLaunchKernelGGL(kern, grid, dim3(256), 0, s, a, static_cast<const float*>(gout),                       \
+                       static_cast<const float*>(in), int(p.tiles_per_sample), p.n_tiles, p.tiles_per_split, \
+                       part, bpart);                                                                          \
+  }
+    if (nb == 64) SEL_WGF(64, 32)
+    else if (cb == 64) SEL_WGF(32, 64)
+    else SEL_WGF(32, 32)
+#undef SEL_WGF
     SEL_LAUNCH_CHECK();
   } else if (d->rows > 0 && dtype == SEL_F32) {
     // fp32 parity path: flat row ranges, same number of splits as the plan
