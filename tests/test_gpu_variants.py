@@ -1,7 +1,8 @@
 """Every kernel-variant knob that still selects compiled code (include/sel.h
 sel_tune; DESIGN.md §6 lists them) against the default path, at the configs'
-own layer shapes.  Knobs covered elsewhere: 0 (tile variants, test_gpu_c3),
-1/3/4/5/11 (test_gpu_conv), 2 (RVQ kernels, test_gpu_model), 9/18/19/21/22/26/
+own layer shapes.  Knobs covered elsewhere: 0 and 47/50/51/52 (tile variants
+and the sample-tile kernel, test_gpu_c3), 1/3/4/5/11/54/55 (test_gpu_conv; 54 /
+55: the fp32 kernels), 2 and 39 (RVQ kernels, test_gpu_model), 9/18/19/21/22/26/
 30 (discriminator variants, test_gpu_dconv_variants / test_gpu_c5), 24
 (test_gpu_conv).  The rest are here:
 
