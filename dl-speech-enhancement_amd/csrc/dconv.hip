@@ -1004,10 +1004,14 @@ __global__ __launch_bounds__(256) void k_dwgrad_mfma(D d, const __bf16* __restri
 // through transposing reads, 32x32x16 MFMA.
 constexpr int W3_BM = 128, W3_HALO = 64;
 
+// bpart != nullptr: the bias partials of the same split too (per output column,
+// summed from the staged gout tiles by the first reduction-channel block of
+// each column block: gap rows are staged as zeros), replacing a separate pass
+// over gout (k_dbias_part_v) per layer.
 template <int NT, int CT, int MAXT>
 __global__ __launch_bounds__(256) void k_dwgrad_w3(D d, const __bf16* __restrict__ gout, const __bf16* __restrict__ x,
                                                    int tiles_per_seq, int64_t n_tiles, int tiles_per_split,
-                                                   float* __restrict__ part, int flat_p) {
+                                                   float* __restrict__ part, int flat_p, float* __restrict__ bpart) {
   constexpr int NB = 32 * NT, CB = 32 * CT;
   constexpr int XROWS = W3_BM + W3_HALO;
   constexpr int GV = W3_BM * NB / 8 / 256;
@@ -1099,12 +1103,19 @@ __global__ __launch_bounds__(256) void k_dwgrad_w3(D d, const __bf16* __restrict
   const int q = (lane & 15) >> 2;
   const int lrow = (4 * h + q) * 32 + col;
 
+  const bool bias_on = bpart != nullptr && blockIdx.z == 0;  // block-uniform
+  const int bn = tid % NB;
+  float bsum = 0.f;
   if (tb < te) load(tb, true);
   int buf = 0;
   for (int64_t tile = tb; tile < te; ++tile, buf ^= 1) {
     store(buf);
     __syncthreads();
     load(tile + 1 < te ? tile + 1 : tile, tile + 1 < te);  // unconditional: exact counts
+    if (bias_on) {
+      const __bf16* gb = base + buf * (GS + XS) + (bn >> 5) * (W3_BM * 32) + (bn & 31);
+      for (int r = tid / NB; r < W3_BM; r += 256 / NB) bsum += float(gb[r * 32]);
+    }
     const __bf16* g = base + buf * (GS + XS) + nt * (W3_BM * 32);
     const __bf16* xx = base + buf * (GS + XS) + GS;
     for (int kh = 0; kh < RROWS / 16; ++kh) {
@@ -1153,6 +1164,17 @@ __global__ __launch_bounds__(256) void k_dwgrad_w3(D d, const __bf16* __restrict
       const int ct = pi / d.K, k = pi % d.K;
       const int n = n0 + ni * 32 + (e >> 5), c = c0 + ct * 32 + (e & 31);
       pdst[(int64_t(n) * d.K + k) * nred + c] = v;
+    }
+  }
+  if (bias_on) {  // the 256 / NB row lanes of each column, added in lane order
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);
+    red[tid] = bsum;
+    __syncthreads();
+    if (tid < NB) {
+      float v = 0.f;
+      for (int q = 0; q < 256 / NB; ++q) v += red[q * NB + tid];
+      bpart[split * d.Ng + n0 + tid] = v;
     }
   }
 }
@@ -2239,6 +2261,7 @@ WgPlanD wg_plan(const sel_dconv_desc* d, int dtype) {
   p.brows_per_split = int((rows + bwant - 1) / bwant);
   p.bsplit = int((rows + p.brows_per_split - 1) / std::max(1, p.brows_per_split));
   if (p.bsplit < 1) p.bsplit = 1;
+  if (p.w3) p.bsplit = p.nsplit;  // k_dwgrad_w3 writes the bias partials of its own splits
   return p;
 }
 
@@ -2301,15 +2324,14 @@ hipError_t wgrad_fill(const sel_dconv_desc* d, int dtype, const WgPlanD& p, cons
     const size_t lds = 2 * (size_t(p.w3_nt) * W3_BM * 32 + size_t(p.w3_ct) * (W3_BM + W3_HALO) * 32) * sizeof(__bf16);
     const int64_t ntiles = p.flat_p ? p.tiles_per_seq : int64_t(d->B) * p.tiles_per_seq;
     dim3 grid(unsigned(p.nsplit), unsigned(width / NB), unsigned(nred / CB));
-#define SEL_W3(NT_, CT_, MT_)                                                                                    if (p.w3_nt == NT_ && p.w3_ct == CT_ && p.w3_maxt == MT_) {                                                      auto kern = k_dwgrad_w3<NT_, CT_, MT_>;                                                                        if (lds > 64 * 1024) {                                                                                           const hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,                                                int(lds));                                                            if (e != hipSuccess) return e;                                                                               }                                                                                                              hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, *d, static_cast<const __bf16*>(gout),                                            static_cast<const __bf16*>(x), p.tiles_per_seq, ntiles, p.tiles_per_split, part, p.flat_p);         } else
+#define SEL_W3(NT_, CT_, MT_)                                                                                    if (p.w3_nt == NT_ && p.w3_ct == CT_ && p.w3_maxt == MT_) {                                                      auto kern = k_dwgrad_w3<NT_, CT_, MT_>;                                                                        if (lds > 64 * 1024) {                                                                                           const hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,                                                int(lds));                                                            if (e != hipSuccess) return e;                                                                               }                                                                                                              hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, *d, static_cast<const __bf16*>(gout),                                            static_cast<const __bf16*>(x), p.tiles_per_seq, ntiles, p.tiles_per_split, part, p.flat_p, bpart);  } else
     SEL_W3(1, 1, 1) SEL_W3(1, 1, 2) SEL_W3(1, 1, 3) SEL_W3(1, 1, 4) SEL_W3(1, 1, 5)
     SEL_W3(1, 2, 1) SEL_W3(1, 2, 2) SEL_W3(1, 2, 3) SEL_W3(1, 2, 4) SEL_W3(1, 2, 5)
     SEL_W3(2, 1, 1) SEL_W3(2, 1, 2) SEL_W3(2, 1, 3) SEL_W3(2, 1, 4) SEL_W3(2, 1, 5) SEL_W3(2, 1, 8)
     SEL_W3(2, 2, 1) SEL_W3(2, 2, 2) SEL_W3(2, 2, 3) SEL_W3(2, 2, 4) SEL_W3(2, 2, 5) SEL_W3(2, 2, 8)
     { return hipErrorInvalidValue; }
 #undef SEL_W3
-    if (bpart) launch_dbias_part(d, static_cast<const __bf16*>(gout), p.brows_per_split, p.bsplit, bpart, s);
-    return hipGetLastError();
+    return hipGetLastError();  // (bias partials: in the kernel, p.bsplit == p.nsplit)
   }
   if (p.mfma) {
     const int bn = 16 * p.nt;
