@@ -4050,7 +4050,7 @@ __host__ __device__ constexpr int wgrad3_xrows(int K, int dil) { return W2_BM + 
 // registers during the MFMAs.  Grid x = row split (fastest), so the blocks
 // sharing a row range are 8-aligned apart... i.e. on the same XCD when the
 // split count is a multiple of 8.
-template <int NT, int CT, int MAXT>
+template <int NT, int CT, int MAXT, bool PIPE>
 __global__ __launch_bounds__(256) void k_wgrad3_bf16(Args a, const __bf16* __restrict__ gout,
                                                      const __bf16* __restrict__ in, int tiles_per_sample,
                                                      int64_t n_tiles, int tiles_per_split,
@@ -4171,20 +4171,55 @@ __global__ __launch_bounds__(256) void k_wgrad3_bf16(Args a, const __bf16* __res
     const __bf16* g = base + buf * (GS + XS) + nt * (W2_BM * 32);
     const __bf16* x = base + buf * (GS + XS) + GS;
     if (do_bias) {
-      const __bf16* gb = base + buf * (GS + XS) + (bcol >> 5) * (W2_BM * 32) + (bcol & 31);
-      for (int r = brow; r < W2_BM; r += 256 / NB) bsum += float(gb[r * 32]);
+      // the column's rows in four independent chains (a single running sum
+      // made every 2-byte LDS read wait for the previous one: the bias blocks
+      // then trailed the others by ~3 k cycles per tile)
+      constexpr int BSTEP = 256 / NB, BN_ = W2_BM / BSTEP;
+      const __bf16* gb = base + buf * (GS + XS) + (bcol >> 5) * (W2_BM * 32) + (bcol & 31) + brow * 32;
+      float b4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < BN_; ++i) b4[i & 3] += float(gb[i * BSTEP * 32]);
+      bsum += (b4[0] + b4[1]) + (b4[2] + b4[3]);
     }
-    for (int kh = 0; kh < RROWS / 16; ++kh) {
+    // fragments of row step kh + 1 are read while step kh's MFMAs run (two
+    // register sets, two steps per trip: RROWS / 16 is even)
+    struct Frags {
+      bf16x8 A, B[MAXT];
+    };
+    auto fetch = [&](int kh, Frags& f) {
       const int R = (rg * RROWS + kh * 16) * 32 + lrow;
       const v4i16 a0 = tr_read(g + R);
       const v4i16 a1 = tr_read(g + R + 8 * 32);
-      const bf16x8 A = __builtin_bit_cast(bf16x8, __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7));
+      f.A = __builtin_bit_cast(bf16x8, __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7));
 #pragma unroll
       for (int j = 0; j < MAXT; ++j) {
         const v4i16 b0 = tr_read(x + xoff[j] + R);
         const v4i16 b1 = tr_read(x + xoff[j] + R + 8 * 32);
-        const bf16x8 Bf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7));
-        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, Bf, acc[j], 0, 0, 0);
+        f.B[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+    };
+    auto mma = [&](const Frags& f) {
+#pragma unroll
+      for (int j = 0; j < MAXT; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.A, f.B[j], acc[j], 0, 0, 0);
+    };
+    const int nk = RROWS / 16;
+    if constexpr (PIPE) {
+      Frags f0, f1;
+      fetch(0, f0);
+      for (int kh = 0; kh < nk; kh += 2) {
+        fetch(kh + 1, f1);
+        mma(f0);
+        if (kh + 2 < nk) fetch(kh + 2, f0);
+        mma(f1);
+      }
+    } else {
+      // four pairs per wave (the k7 layers) and the short layers (T <= 400):
+      // measured 2-6% slower pipelined (the second register set costs
+      // occupancy), so one set, one step at a time
+      for (int kh = 0; kh < nk; ++kh) {
+        Frags f;
+        fetch(kh, f);
+        mma(f);
       }
     }
   }
@@ -5434,9 +5469,12 @@ hipError_t launch_wgrad3(const WgPlan& p, const Args& a, const __bf16* gout, con
   constexpr size_t lds_max = size_t(2) * (NT * W2_BM * 32 + CT * (W2_BM + W2_HALO) * 32) * sizeof(__bf16);
   const size_t lds = size_t(2) * (NT * W2_BM * 32 + CT * wgrad3_xrows(a.K, a.dil) * 32) * sizeof(__bf16);
   dim3 grid(unsigned(p.nsplit), unsigned(a.N / (32 * NT)), unsigned(a.C / (32 * CT)));
+  // the two-set fragment pipeline where it measured faster (tools/ab_wgrad.sh:
+  // k2 / k3 layers with >= 64 k rows, e.g. the 256 -> 128 down conv 69 -> 58 us)
+  const bool pipe = p.maxt <= 3 && a.rows >= 65536;
 #define SEL_WG3(MT)                                                                                            \
   {                                                                                                            \
-    auto kern = k_wgrad3_bf16<NT, CT, MT>;                                                                     \
+    auto kern = pipe ? k_wgrad3_bf16<NT, CT, MT, (MT <= 3)> : k_wgrad3_bf16<NT, CT, MT, false>;                \
     if (lds_max > 64 * 1024) {                                                                                 \
       hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds_max)); \
       if (e != hipSuccess) return e;                                                                           \
