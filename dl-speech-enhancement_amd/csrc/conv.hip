@@ -4866,8 +4866,10 @@ bool wss_pick_tall(const Args& a) {
          a.pad_mode == SEL_PAD_ZERO && wss_ok(a) && wss_geometry(a, S, tm) && S == 32;
 }
 // the (16, 128) tiles for the ELU'd 128-wide forwards at T = 2000 (tune key 52:
-// 1 = on, 2 = off, 0 = kWssEluDefault)
-constexpr bool kWssEluDefault = false;
+// 1 = on, 2 = off, 0 = kWssEluDefault): tools/conv_bench.py RU128 k7d9 fwd
+// 49.4 (k_conv_fwd_bf16<256, 64>) -> 43.9 us; neutral in the step (the
+// launches overlap the side-stream weight gradients)
+constexpr bool kWssEluDefault = true;
 bool wss_pick_elu(const Args& a) {
   const int k = tune(52);
   int S = 0, tm = 0;
