@@ -1744,8 +1744,13 @@ __device__ __forceinline__ void ru_store(__bf16* p, bf16x8 v) {
 // next tile's prefetch exactly (a conditional store made the staging wait at
 // the top of the next tile fall back to vmcnt(0), i.e. wait for these stores'
 // completion too).
+// AUX: the store's cache policy (2 = nt, streaming).  nt measured only where a
+// lane group writes whole 64-B rows that nothing re-reads soon: k_ru32_bwd's
+// gx (without gh: 85.8 -> 79 us per unit); on the forward's h / out rows
+// (two waves' 32-B halves per row line) nt doubled the time (68 -> 105 us)
+template <int AUX = 0>
 __device__ __forceinline__ void ru_bstore(__amdgpu_buffer_rsrc_t rs, int byte_off, bf16x8 v) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, byte_off, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, byte_off, 0, AUX);
 }
 
 // N dropped stores (a zero-byte region; distinct offsets so that the compiler
@@ -2661,8 +2666,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 128 ? 
       bf16x8 of[2];
       ru_acc_to_frags(v, of);
       const int off = ((t0 + lr) * RU_C + 8 * hl) * 2;
-      ru_bstore(rgx, valid ? off : RU_OOB, of[0]);
-      ru_bstore(rgx, valid ? off + 32 : RU_OOB, of[1]);
+      ru_bstore<2>(rgx, valid ? off : RU_OOB, of[0]);
+      ru_bstore<2>(rgx, valid ? off + 32 : RU_OOB, of[1]);
     }
   }
 }
