@@ -1748,6 +1748,15 @@ __device__ __forceinline__ void ru_store(__bf16* p, bf16x8 v) {
 // lane group writes whole 64-B rows that nothing re-reads soon: k_ru32_bwd's
 // gx (without gh: 85.8 -> 79 us per unit); on the forward's h / out rows
 // (two waves' 32-B halves per row line) nt doubled the time (68 -> 105 us)
+// k_ru32_fwd's h rows (read again only by the backward, much later) leave as
+// nt stores: 68-69 -> 66-67 us; nt on both h and out measured 1.5-2x slower,
+// nt on out alone neutral (A/B builds: SEL_RU_FWD_*NT)
+#ifndef SEL_RU_FWD_HNT
+#define SEL_RU_FWD_HNT 2
+#endif
+#ifndef SEL_RU_FWD_ONT
+#define SEL_RU_FWD_ONT 0
+#endif
 template <int AUX = 0>
 __device__ __forceinline__ void ru_bstore(__amdgpu_buffer_rsrc_t rs, int byte_off, bf16x8 v) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, byte_off, 0, AUX);
@@ -2112,8 +2121,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU32F
       bf16x8 hf[2];
       ru_acc_to_frags(v, hf);
       const bool hst = valid && !(dbg & 1);  // tune key 15 bit 0: diagnostic without the h store
-      ru_bstore(rh, hst ? off : RU_OOB, hf[0]);
-      ru_bstore(rh, hst ? off + 32 : RU_OOB, hf[1]);
+      ru_bstore<SEL_RU_FWD_HNT>(rh, hst ? off : RU_OOB, hf[0]);
+      ru_bstore<SEL_RU_FWD_HNT>(rh, hst ? off + 32 : RU_OOB, hf[1]);
       floatx16 acc2;
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc2[e] = 0.f;
@@ -2134,8 +2143,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU32F
       bf16x8 of[2];
       ru_acc_to_frags(v, of);
       const bool ost = valid && !(dbg & 2);  // bit 1: diagnostic without the out store
-      ru_bstore(ro, ost ? off : RU_OOB, of[0]);
-      ru_bstore(ro, ost ? off + 32 : RU_OOB, of[1]);
+      ru_bstore<SEL_RU_FWD_ONT>(ro, ost ? off : RU_OOB, of[0]);
+      ru_bstore<SEL_RU_FWD_ONT>(ro, ost ? off + 32 : RU_OOB, of[1]);
     }
   }
 }
@@ -2284,6 +2293,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU64F
       bf16x8 hf[2];
       ru_acc_to_frags(v, hf);
       const int off = ((t0 + lr) * C + ns * 32 + 8 * hl) * 2;
+      // (plain stores: nt on these h rows, whose 128-B lines the two
+      // channel-slice waves write in halves, measured 60 -> 79 us)
       ru_bstore(rh, lr < mrows ? off : RU_OOB, hf[0]);
       ru_bstore(rh, lr < mrows ? off + 32 : RU_OOB, hf[1]);
 #pragma unroll
