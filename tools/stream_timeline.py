@@ -1,6 +1,7 @@
 """Per-stream busy time, GPU-busy union and idle gaps of one step window in a
-rocprofv3 kernel trace.  usage: stream_timeline.py <prof_dir> [first_kernel_substr]
-The window: the last N 'k_adam_many' launches delimit steps (one per step)."""
+rocprofv3 kernel trace.  usage: stream_timeline.py <prof_dir> [optimizer launches per step]
+The window ends at the last 'k_adam_many' launch and starts after the one
+that many launches earlier (C3: 1 per step, C5: 2)."""
 import collections
 import csv
 import glob
@@ -13,7 +14,8 @@ rows = list(csv.DictReader(open(f)))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 adam = [i for i, r in enumerate(rows) if "adam_many" in r["Kernel_Name"]]
 # step window = between the last two optimizer launches
-i0, i1 = adam[-2] + 1, adam[-1] + 1
+per = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+i0, i1 = adam[-1 - per] + 1, adam[-1] + 1
 win = rows[i0:i1]
 t0 = int(win[0]["Start_Timestamp"])
 t1 = max(int(r["End_Timestamp"]) for r in win)
