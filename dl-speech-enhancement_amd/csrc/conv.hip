@@ -417,6 +417,9 @@ __global__ __launch_bounds__(256) void k_conv_fwd_f32(Args a, const float* __res
 #ifndef SEL_W_RU32F
 #define SEL_W_RU32F 3
 #endif
+#ifndef SEL_W_RU32F128
+#define SEL_W_RU32F128 4
+#endif
 #ifndef SEL_W_RU32B
 #define SEL_W_RU32B 3
 #endif
@@ -1744,18 +1747,26 @@ __device__ __forceinline__ void ru_store(__bf16* p, bf16x8 v) {
 // next tile's prefetch exactly (a conditional store made the staging wait at
 // the top of the next tile fall back to vmcnt(0), i.e. wait for these stores'
 // completion too).
-// AUX: the store's cache policy (2 = nt, streaming).  nt measured only where a
-// lane group writes whole 64-B rows that nothing re-reads soon: k_ru32_bwd's
-// gx (without gh: 85.8 -> 79 us per unit); on the forward's h / out rows
-// (two waves' 32-B halves per row line) nt doubled the time (68 -> 105 us)
+// AUX: the store's cache policy (2 = nt, streaming).  Judged inside the
+// profiled step (tools/ru_bench.py re-reads its own inputs, which favours
+// anything that keeps them cached): nt pays on k_ru32_fwd's h rows (read
+// again only by the backward), and loses on outputs the next kernel reads
+// (k_ru32_bwd's gx) or on rows two waves write in halves (k_ru64_fwd's h)
 // k_ru32_fwd's h rows (read again only by the backward, much later) leave as
-// nt stores: 68-69 -> 66-67 us; nt on both h and out measured 1.5-2x slower,
-// nt on out alone neutral (A/B builds: SEL_RU_FWD_*NT)
+// nt stores: 71.7-72.5 -> 69.1-69.5 us per unit inside the profiled C3 step;
+// nt on both h and out measured 1.5-2x slower, nt on out alone neutral
+// (A/B builds: SEL_RU_FWD_*NT)
 #ifndef SEL_RU_FWD_HNT
 #define SEL_RU_FWD_HNT 2
 #endif
 #ifndef SEL_RU_FWD_ONT
 #define SEL_RU_FWD_ONT 0
+#endif
+// k_ru32_bwd's gx rows: plain stores.  nt measured 86 -> 79 us per unit in
+// tools/ru_bench.py but 87.4-88.0 -> 90.8-91.0 us inside the profiled C3 step
+// (the next layer's backward reads gx right away); A/B builds: SEL_RU32B_GXNT=2
+#ifndef SEL_RU32B_GXNT
+#define SEL_RU32B_GXNT 0
 #endif
 template <int AUX = 0>
 __device__ __forceinline__ void ru_bstore(__amdgpu_buffer_rsrc_t rs, int byte_off, bf16x8 v) {
@@ -2046,7 +2057,7 @@ __device__ __forceinline__ void ru_wfrags(const __bf16* __restrict__ wp, bf16x8 
 }
 
 template <int R>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEL_W_RU32F))) void k_ru32_fwd(Args a, const __bf16* __restrict__ x,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 128 ? SEL_W_RU32F128 : SEL_W_RU32F))) void k_ru32_fwd(Args a, const __bf16* __restrict__ x,
                                                   const __bf16* __restrict__ w1p, const float* __restrict__ b1,
                                                   const __bf16* __restrict__ w2p, const float* __restrict__ b2,
                                                   __bf16* __restrict__ hout, __bf16* __restrict__ out,
@@ -2677,8 +2688,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 128 ? 
       bf16x8 of[2];
       ru_acc_to_frags(v, of);
       const int off = ((t0 + lr) * RU_C + 8 * hl) * 2;
-      ru_bstore<2>(rgx, valid ? off : RU_OOB, of[0]);
-      ru_bstore<2>(rgx, valid ? off + 32 : RU_OOB, of[1]);
+      ru_bstore<SEL_RU32B_GXNT>(rgx, valid ? off : RU_OOB, of[0]);
+      ru_bstore<SEL_RU32B_GXNT>(rgx, valid ? off + 32 : RU_OOB, of[1]);
     }
   }
 }
@@ -5644,7 +5655,12 @@ int sel_resunit_fwd(const sel_conv_desc* d1, int dtype, const void* x, const voi
   SEL_REQUIRE(dtype == SEL_BF16 && ru_fused_ok(a), SEL_ERR_UNSUPPORTED,
               "sel_resunit_fwd: fused path needs bf16, C = N in {32, 64}, K = 7, causal zero pad, ELU prologue");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (a.C == 32) return launch_ru32_fwd<256>(a, x, w1pack, b1, w2pack, b2, h, out, s);
+  // tune key 56 = 1: 128-row tiles (4 resident workgroups per CU instead of 3):
+  // 66-67 -> 58.6-59 us per unit in tools/ru_bench.py, which re-reads the same
+  // input, but 69.5 -> 72.6 us inside the profiled C3 step, so off
+  if (a.C == 32)
+    return tune(56) == 1 ? launch_ru32_fwd<128>(a, x, w1pack, b1, w2pack, b2, h, out, s)
+                         : launch_ru32_fwd<256>(a, x, w1pack, b1, w2pack, b2, h, out, s);
   // tune key 24 < 0: the LDS-staged k_ru_thin_bf16 (round 2) instead of k_ru64_fwd
   if (tune(24) < 0) return launch_ru_thin<64, 7, 64>(a, x, w1pack, b1, w2pack, b2, h, out, s);
   return launch_ru64_fwd<128>(a, x, w1pack, b1, w2pack, b2, h, out, s);

@@ -762,7 +762,9 @@ def _ru_meta(d1, xf, wp1, wp2):
     es = xf.element_size()
     nbytes = 3 * d1.rows * d1.C * es + (wp1.numel() + wp2.numel()) * es
     flops = 2.0 * d1.rows * d1.N * d1.C * (d1.K + 1)
-    return ("k_ru32_fwd<256>" if d1.C == 32 else "k_ru64_fwd<128>"), nbytes, flops
+    # (the 32-channel unit's tile rows: 256, or 128 under tune key 56 = 1)
+    tag = f"k_ru32_fwd<{128 if _tune_value(56) == 1 else 256}>" if d1.C == 32 else "k_ru64_fwd<128>"
+    return tag, nbytes, flops
 
 
 class ResidualUnitFn(torch.autograd.Function):
