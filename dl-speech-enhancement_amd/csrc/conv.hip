@@ -5498,9 +5498,11 @@ hipError_t launch_wgrad3(const WgPlan& p, const Args& a, const __bf16* gout, con
   constexpr size_t lds_max = size_t(2) * (NT * W2_BM * 32 + CT * (W2_BM + W2_HALO) * 32) * sizeof(__bf16);
   const size_t lds = size_t(2) * (NT * W2_BM * 32 + CT * wgrad3_xrows(a.K, a.dil) * 32) * sizeof(__bf16);
   dim3 grid(unsigned(p.nsplit), unsigned(a.N / (32 * NT)), unsigned(a.C / (32 * CT)));
-  // the two-set fragment pipeline where it measured faster (tools/ab_wgrad.sh:
-  // k2 / k3 layers with >= 64 k rows, e.g. the 256 -> 128 down conv 69 -> 58 us)
-  const bool pipe = p.maxt <= 3 && a.rows >= 65536;
+  // the two-set fragment pipeline (tune key 57 = 1) for the k2 / k3 layers
+  // with >= 64 k rows: faster in tools/ab_wgrad.sh (256 -> 128 down conv
+  // 69 -> 58 us, inputs re-read from the cache), not inside the profiled C3
+  // step (<2, 1, 2> 55.8 -> 59 us, <2, 2, 3> 53.5 -> 52.3 us), so off
+  const bool pipe = p.maxt <= 3 && a.rows >= 65536 && tune(57) == 1;
 #define SEL_WG3(MT)                                                                                            \
   {                                                                                                            \
     auto kern = pipe ? k_wgrad3_bf16<NT, CT, MT, (MT <= 3)> : k_wgrad3_bf16<NT, CT, MT, false>;                \
