@@ -461,8 +461,8 @@ def stft_kernel_roofline(dev, B=2048):
     256 MB Infinity Cache, so nothing is served from it across launches), timed
     with a HIP event pair around each launch on its stream, against the 8 TB/s
     spec and against two measured copy rates of this box: a float4 stream-copy
-    kernel (sel_probe_copy_f4: each workgroup copies one contiguous 16-KB piece,
-    4 x 16-B nontemporal loads in flight per thread, tools/copy_probe.py) and
+    kernel (sel_probe_copy_f4: one 16-B nontemporal load and store per thread,
+    one-shot grid, 6.4 TB/s; tools/copy_probe.py sweeps its other forms) and
     torch's copy_, each over 1 GiB buffers."""
     from sel import _lib as L
     T, (n, h, w) = SR, STFT_RES[0]

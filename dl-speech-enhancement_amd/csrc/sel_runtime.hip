@@ -148,6 +148,34 @@ __global__ __launch_bounds__(256) void k_probe_copy_once(const float4* __restric
                                                          int64_t n) {
   const int64_t i = int64_t(blockIdx.x) * 256 * U + threadIdx.x;
   float4 v[U];
+  // every workgroup but the last: loads with no per-element guard (a guarded
+  // load compiles to a branch with its own vmcnt(0): the loads then go out one
+  // at a time)
+  if (int64_t(blockIdx.x + 1) * 256 * U <= n) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (NT) {
+        const float4* p = src + i + u * 256;
+        v[u] = make_float4(__builtin_nontemporal_load(&p->x), __builtin_nontemporal_load(&p->y),
+                           __builtin_nontemporal_load(&p->z), __builtin_nontemporal_load(&p->w));
+      } else {
+        v[u] = src[i + u * 256];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (NT) {
+        float4* p = dst + i + u * 256;
+        __builtin_nontemporal_store(v[u].x, &p->x);
+        __builtin_nontemporal_store(v[u].y, &p->y);
+        __builtin_nontemporal_store(v[u].z, &p->z);
+        __builtin_nontemporal_store(v[u].w, &p->w);
+      } else {
+        dst[i + u * 256] = v[u];
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     if (i + u * 256 < n) {
@@ -177,11 +205,14 @@ __global__ __launch_bounds__(256) void k_probe_copy_once(const float4* __restric
 }
 }  // namespace
 
-// mode (tune key 49): 0 = one-shot, 4 loads in flight, nontemporal (5.91 TB/s
-// on 1 GiB, tools/copy_probe.py); 1 = the grid-stride form over `blocks`
-// workgroups (the round-1..4 probe, 5.07-5.17 TB/s at 4-32 blocks per CU);
-// 2 / 3 = one-shot, 8 in flight, plain / nontemporal (3.61 / 5.65); 4 =
-// one-shot, 4 in flight, plain (5.37)
+// mode (tune key 49), 1 GiB each way, tools/copy_probe.py (two runs):
+//   0 (default) = one-shot, one 16-B piece per thread, nontemporal: 6.40 TB/s
+//   1 = the grid-stride form over `blocks` workgroups (the round-1..4 probe,
+//       4.7-5.1 TB/s at 4-32 blocks per CU)
+//   2 / 3 = one-shot, 8 pieces per thread, plain / nontemporal (5.44-5.49 / 5.83)
+//   4 = one-shot, 4 per thread, plain (5.72-5.77)
+//   5 / 6 / 7 = one-shot, 2 / 4 / 16 per thread, nontemporal (6.00-6.03 /
+//       5.97-6.03 / 5.08-5.15)
 extern "C" int sel_probe_copy_f4(const void* src, void* dst, int64_t n16, int blocks, sel_stream_t stream) {
   SEL_REQUIRE(src && dst && n16 > 0 && blocks > 0, SEL_ERR_ARG, "bad copy probe arguments");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -198,7 +229,10 @@ extern "C" int sel_probe_copy_f4(const void* src, void* dst, int64_t n16, int bl
     case 2: once(k_probe_copy_once<8, false>, 8); break;
     case 3: once(k_probe_copy_once<8, true>, 8); break;
     case 4: once(k_probe_copy_once<4, false>, 4); break;
-    default: once(k_probe_copy_once<4, true>, 4); break;
+    case 5: once(k_probe_copy_once<2, true>, 2); break;
+    case 6: once(k_probe_copy_once<4, true>, 4); break;
+    case 7: once(k_probe_copy_once<16, true>, 16); break;
+    default: once(k_probe_copy_once<1, true>, 1); break;
   }
   SEL_LAUNCH_CHECK();
   return SEL_OK;

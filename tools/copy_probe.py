@@ -31,7 +31,7 @@ def main():
 
     lib = L.lib()
     print(f"torch copy_: {nbytes / timed(lambda: dst.copy_(src)) / 1e9:.0f} GB/s")
-    for mode in (0, 4, 2, 3):
+    for mode in (0, 4, 2, 3, 5, 6, 7):
         lib.sel_tune(49, mode)
         t = timed(lambda: L.call("sel_probe_copy_f4", L.ptr(src), L.ptr(dst), src.numel() // 4, 8 * cus, L.stream()))
         ok = torch.equal(dst, src)
