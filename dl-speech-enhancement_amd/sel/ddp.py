@@ -25,7 +25,10 @@ flat fp32 buffer, cut into ~4 MB buckets in backward order:
 
 torch DDP copied every gradient into its bucket and zero-filled buckets each
 step (~0.3-0.4 ms per C3 step on one GPU, profiles/r4_ddp_ab.md); this keeps
-the one-GPU schedule.  Parameters are broadcast from rank 0 at construction,
+the one-GPU schedule.  As with torch DDP outside no_sync(), gradients are
+not accumulated over several backward calls (each backward averages its
+buckets in place): the reference's trainers zero_grad before every backward.
+Parameters are broadcast from rank 0 at construction,
 as DDP does; buffers are not (broadcast_buffers=False in every call site).
 """
 import weakref
@@ -100,6 +103,7 @@ class GradBuckets:
             return
         if not self.armed:
             self.armed = True
+            self.stats["order"] = []   # this backward's launch order only (bounded)
             torch.autograd.Variable._execution_engine.queue_callback(self._finish)
         off, n, bi = self.slots[id(p)][:3]
         g = p.grad
@@ -132,15 +136,22 @@ class GradBuckets:
         CO.flush_params([p for p in ps if p is not None])
         sl = self.flat[lo:hi]
         if self.world > 1:
-            sl.div_(self.world)
+            self._scale(sl)
             self.works.append(dist.all_reduce(sl, group=self.pg, async_op=True))
         self.next += 1
         self.stats["buckets"] += 1
         self.stats["order"].append(bi)
 
+    def _scale(self, sl):
+        """Pre-divide a bucket by W so the all-reduce SUM is the average."""
+        sl.div_(self.world)
+
     def _finish(self):
         unused = [i for i in self.slots if i not in self.used]
         for i in unused:  # parameters that took no gradient here contribute zeros
+            p = self.slots[i][3]()
+            if p is not None and p.grad is not None:
+                continue   # a gradient kept from an earlier backward stays (see the class note)
             off, n = self.slots[i][:2]
             self.flat.narrow(0, off, n).zero_()
         while self.next < len(self.buckets):

@@ -83,7 +83,47 @@ def _floats(d):
     return {k: float(v) for k, v in d.items()}
 
 
-def run_pqc(dev, full=False):
+class GradTap:
+    """Snapshots every trainable parameter's gradient the FIRST time the
+    training step hands it to clip_grad_norm_ or an optimizer's step(): i.e.
+    the step-0 gradient after backward (and, under a process group, after the
+    sel reducer's all-reduce), before clipping and before the update.  The
+    step-0 weights are the same seeded ones on every side, so these gradients
+    compare directly."""
+
+    def __init__(self, named, optimizers):
+        self.names = {id(p): k for k, p in named}
+        self.grads = {}
+        self._clip = torch.nn.utils.clip_grad_norm_
+        tap = self
+
+        def clip(params, *a, **k):
+            params = list(params) if not torch.is_tensor(params) else [params]
+            tap.take(params)
+            return tap._clip(params, *a, **k)
+        torch.nn.utils.clip_grad_norm_ = clip
+        for opt in optimizers:
+            self._wrap(opt)
+
+    def _wrap(self, opt):
+        orig = opt.step
+
+        def step(*a, **k):
+            self.take([p for g in opt.param_groups for p in g["params"]])
+            return orig(*a, **k)
+        opt.step = step
+
+    def take(self, params):
+        for p in params:
+            k = self.names.get(id(p))
+            if k is not None and k not in self.grads and p.grad is not None:
+                self.grads[k] = p.grad.detach().cpu().clone()
+
+    def close(self):
+        torch.nn.utils.clip_grad_norm_ = self._clip
+
+
+def run_pqc(dev, full=False, sim=0):
     from dataloader.data_utils import add_noise  # noqa: F401
     from losses import MultiMelSpectrogramLoss, MultiResolutionSTFTLoss
     from models.autoencoder.AudioDec import Generator
@@ -106,41 +146,118 @@ def run_pqc(dev, full=False):
     sched = torch.optim.lr_scheduler.StepLR(opt, **cfg["generator_scheduler_params"])
     tr = Trainer(steps=0, epochs=0, data_loader={}, model=model, criterion=crit, optimizer={"generator": opt},
                  scheduler={"generator": sched}, config=cfg, device=dev)
+    dtype = torch.bfloat16 if full else torch.float32
+    if sim:
+        return _simulate(tr, G, _global_batch(24000), sim, dev, dtype)
     clean, mixed = _mix(*_global_batch(24000 if full else 4800), dev)
+    tap = GradTap(G.named_parameters(), [opt])
     steps = []
     for _ in range(STEPS):
-        with precision(torch.bfloat16 if full else torch.float32):
+        with precision(dtype):
             tr._train_step((mixed, clean))
         tot = tr.total_train_loss
         steps.append(_floats({k: tot[k] for k in list(tot.keys()) if "loss" in k}))
-    return {"steps": steps, "params": {k: p.detach().cpu().clone() for k, p in G.named_parameters()
-                                       if p.requires_grad}}
+    tap.close()
+    return {"steps": steps, "grads": tap.grads,
+            "params": {k: p.detach().cpu().clone() for k, p in G.named_parameters() if p.requires_grad}}
 
 
 BENCH_CLIPS = 16
 
 
-def run_bench(dev):
-    import bench
-    from sel import dist as D
-    from sel import optim as O
+def _bench_batch():
     g = torch.Generator().manual_seed(4242)
     clean = 0.1 * torch.randn(BENCH_CLIPS, 1, 24000, generator=g)
     noise = 0.1 * torch.randn(BENCH_CLIPS, 1, 24000, generator=g)
+    return clean, noise
+
+
+def run_bench(dev, sim=0):
+    import bench
+    from sel import dist as D
+    from sel import optim as O
+    clean, noise = _bench_batch()
     world = D.rank_world()[1]
-    step = bench.c3_setup(dev, BENCH_CLIPS // world, world, 0, batch=(clean, noise))
+    step = bench.c3_setup(dev, BENCH_CLIPS // max(world, sim or 1), world, 0, batch=(clean, noise))
     assert isinstance(step.trainer.optimizer["generator"], O.Adam)
     if world > 1:
         from sel.ddp import SelDDP
         assert isinstance(step.trainer.model["generator"], SelDDP)
+    G = step.generator
+    if sim:
+        return _simulate(step.trainer, G, (clean, noise), sim, dev, torch.bfloat16)
+    tap = GradTap(G.named_parameters(), [step.trainer.optimizer["generator"]])
     steps = []
     for _ in range(STEPS):
         step()
         tot = step.trainer.total_train_loss
         steps.append(_floats({k: tot[k] for k in list(tot.keys()) if "loss" in k}))
-    G = step.generator
-    return {"steps": steps, "params": {k: p.detach().cpu().clone() for k, p in G.named_parameters()
-                                       if p.requires_grad}}
+    tap.close()
+    return {"steps": steps, "grads": tap.grads,
+            "params": {k: p.detach().cpu().clone() for k, p in G.named_parameters() if p.requires_grad}}
+
+
+def _simulate(tr, G, batch, world, dev, dtype):
+    """Data parallelism over `world` ranks SIMULATED in this one process, with
+    no process group: every step runs the trainer's own forward and loss
+    (trainer/denoise.py _train_step) on each rank's shard in turn, with the
+    shard's mixture built from the batch-global norms exactly as
+    sel.dist.add_noise_global does (per-shard fp64 sums of squares, summed in
+    rank order: for two ranks that is bit-for-bit the all-reduce), then sets
+    every gradient to the sum of the per-shard gradients each pre-divided by
+    `world` (sel/ddp.py GradBuckets._scale + all-reduce SUM) and runs the
+    trainer's clip / Adam / scheduler.  Each shard runs exactly the kernels a
+    rank runs (same row counts), so the data-parallel step's gradients should
+    equal these bit-for-bit: this is the reference that pins the all-reduce
+    and its 1/W (tests/test_gpu_ddp.py), where the single-process full batch
+    can only pin the losses (bf16 kernels are chosen by row count)."""
+    from sel import dist as D
+    from sel.convops import precision
+    clean, noise = batch
+    shards = [(D.shard(clean, r, world).to(dev).contiguous(), D.shard(noise, r, world).to(dev).contiguous())
+              for r in range(world)]
+    sums = None
+    for c, n in shards:
+        s_ = D._local_sumsq(c, n)
+        sums = s_ if sums is None else sums + s_
+    mixed = [D._mix(c, n, sums, 15.0) for c, n in shards]
+    params = [(k, p) for k, p in G.named_parameters() if p.requires_grad]
+    opt, sched, cfg = tr.optimizer["generator"], tr.scheduler["generator"], tr.config
+    # one running loss record per simulated rank (the trainer's records sum
+    # over the steps since the last log, as each rank's do)
+    totals = [type(tr.total_train_loss)() for _ in range(world)]
+    steps, grads0 = [], None
+    for _ in range(STEPS):
+        acc = [torch.zeros_like(p) for _, p in params]
+        vals = {}
+        for r, ((c, _), m) in enumerate(zip(shards, mixed)):
+            tr.total_train_loss = totals[r]
+            opt.zero_grad()
+            with precision(dtype):
+                tr._gen().quantizer.codebook.eval()
+                y_nc, zq, z, vqloss, perplexity = tr.model["generator"](m)
+                loss = tr._vq_loss(vqloss, mode="train")
+                loss = loss + tr._metric_loss(y_nc, c, mode="train")
+                tr._record_loss("generator_loss", loss, mode="train")
+                loss.backward()
+            for a, (_, p) in zip(acc, params):
+                if p.grad is not None:
+                    a.add_(p.grad / world)
+            tot = tr.total_train_loss
+            for k in list(tot.keys()):
+                if "loss" in k:
+                    vals.setdefault(k, []).append(float(tot[k]))
+        for a, (_, p) in zip(acc, params):
+            p.grad = a
+        if grads0 is None:
+            grads0 = {k: p.grad.detach().cpu().clone() for k, p in params}
+        if cfg["generator_grad_norm"] > 0:
+            torch.nn.utils.clip_grad_norm_([p for _, p in params], cfg["generator_grad_norm"])
+        opt.step()
+        sched.step()
+        steps.append({k: v for k, v in vals.items()})   # per-rank values, in rank order
+    return {"steps": steps, "grads": grads0,
+            "params": {k: p.detach().cpu().clone() for k, p in params}}
 
 
 def run_gan(dev):
@@ -165,21 +282,32 @@ def run_gan(dev):
     st.model["discriminator"] = D.wrap_ddp(Dm, dev)
     st.discriminator_enabled = True
     clean, mixed = _mix(*_global_batch(9600), dev)
+    named = [(f"G.{k}", p) for k, p in G.named_parameters()] + [(f"D.{k}", p) for k, p in Dm.named_parameters()]
+    tap = GradTap(named, [st.optimizer["generator"], st.optimizer["discriminator"]])
     steps = []
     for _ in range(STEPS):
         gen, dis, frags = st.model_step(clean, mixed)
         steps.append(_floats(dict([("gen", gen), ("dis", dis)] + list(frags))))
+    tap.close()
     params = {f"G.{k}": p.detach().cpu().clone() for k, p in G.named_parameters() if p.requires_grad}
     params.update({f"D.{k}": p.detach().cpu().clone() for k, p in Dm.named_parameters()})
-    return {"steps": steps, "params": params}
+    return {"steps": steps, "grads": tap.grads, "params": params}
 
 
-def run_case(case, dev):
+def run_case(case, dev, sim=0):
+    """sim > 0: the simulated `sim`-rank reference in this process (c3, bench)."""
+    if sim:
+        return {"c3": lambda d: run_pqc(d, full=True, sim=sim), "bench": lambda d: run_bench(d, sim=sim)}[case](dev)
     return {"pqc": run_pqc, "c3": lambda d: run_pqc(d, full=True), "bench": run_bench, "gan": run_gan}[case](dev)
 
 
 def main():
     case, out = sys.argv[1], sys.argv[2]
+    if os.environ.get("SEL_TEST_DDP_NO_SCALE") == "1":
+        # negative control (tests/test_gpu_ddp.py): the reducer's 1/W dropped,
+        # so the all-reduce returns the SUM of the rank gradients
+        from sel import ddp
+        ddp.GradBuckets._scale = lambda self, sl: None
     import torch.distributed as dist
     from sel import dist as D
     D.init_from_env(backend="gloo")
