@@ -87,12 +87,6 @@ def c2_setup(dev, B):
     return step
 
 
-def c2_bytes_per_launch(name, B):
-    """Algorithmic HBM bytes of one launch of the fused STFT-loss forward at the
-    n_fft=512 resolution: read x and y once (B*T fp32 each); partials negligible."""
-    return 2 * 4 * B * SR
-
-
 def c2_cpu_baseline(B_sample=4, steps=20):
     from oracle import ref_ops as R
     from oracle.melfilters import mel as melbank
@@ -373,6 +367,7 @@ def c5_cpu_baseline(B_sample=1, steps=5):
 # ---------------------------------------------------------------------------
 
 MFMA_BF16_PEAK_TFS = 2500.0  # MI355X dense bf16 (MI355X_MICROARCH.md)
+FP32_PEAK_TFS = 157.3        # MI355X fp32 vector (= fp32 MFMA) peak (MI355X_MICROARCH.md)
 
 
 def pmc_file(cfg):
@@ -426,32 +421,50 @@ def pmc_traffic(tag, B, cfg="c3"):
 def roofline(cfg, timer, dom, B, steps):
     """Dominant timed kernel instance -> achieved vs peak (HIP events, same stream)."""
     summ = timer.summary()
-    if cfg == "c2":
-        # one fused STFT-loss forward per resolution per step; n_fft=512 is the last one
-        durs = timer.durations_ms(dom)
-        per_step = len(durs) // steps
-        sel_d = durs[per_step - 1::per_step]
-        avg_ms = float(np.mean(sel_d))
-        achieved = c2_bytes_per_launch(dom, B) / (avg_ms * 1e-3) / 1e9
-        return {"bound": "hbm", "kernel": dom + " (n_fft=512)", "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "avg_launch_us": round(avg_ms * 1e3, 2), "traffic": None}
-    tag, (n, ms, nbytes, flops) = max(summ.items(), key=lambda kv: kv[1][1])
+    total_ms = sum(v[1] for v in summ.values())
+    ranked = sorted(summ.items(), key=lambda kv: kv[1][1], reverse=True)
+    # c2 computes in fp32 (the FFTs on the vector ALUs): its compute roof is
+    # the fp32 vector peak; c3 / c5 convs run bf16 MFMA
+    peak = FP32_PEAK_TFS if cfg == "c2" else MFMA_BF16_PEAK_TFS
+    top = [_roof_entry(tag, v, total_ms, B, cfg, peak) for tag, v in ranked[:3]]
+    r = dict(top[0])
+    r["top3"] = top
+    r["timed_entry_points"] = sorted(timer.names)
+    return r
+
+
+# the fused residual-unit forwards also write h = conv1(ELU(x)) for the
+# backward: a design choice (the backward could recompute it from x), whose
+# bytes are counted in the kernel's algorithmic bytes (one of its three
+# activation tensors)
+H_STASH = {"k_ru32_fwd", "k_ru64_fwd"}
+
+
+def _roof_entry(tag, v, total_ms, B, cfg, peak_tfs=None):
+    """One timed kernel instance -> achieved vs its roofline (mfma when its
+    arithmetic intensity is past the bf16 ridge, else hbm)."""
+    n, ms, nbytes, flops = v
+    peak_tfs = peak_tfs or MFMA_BF16_PEAK_TFS
     intensity = flops / max(nbytes, 1)
-    ridge = MFMA_BF16_PEAK_TFS * 1e12 / (HBM_PEAK_GBS * 1e9)
-    if intensity > ridge:
+    ridge = peak_tfs * 1e12 / (HBM_PEAK_GBS * 1e9)
+    if nbytes == 0 and flops == 0:
+        r = {"bound": None, "achieved": None, "peak": None, "unit": None, "frac": None}
+    elif intensity > ridge:
         ach = flops / (ms * 1e-3) / 1e12
-        r = {"bound": "mfma", "achieved": round(ach, 1), "peak": MFMA_BF16_PEAK_TFS, "unit": "TFLOP/s",
-             "frac": round(ach / MFMA_BF16_PEAK_TFS, 4)}
+        r = {"bound": "mfma" if peak_tfs == MFMA_BF16_PEAK_TFS else "valu-fp32", "achieved": round(ach, 1),
+             "peak": peak_tfs, "unit": "TFLOP/s", "frac": round(ach / peak_tfs, 4)}
     else:
         ach = nbytes / (ms * 1e-3) / 1e9
         r = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
              "frac": round(ach / HBM_PEAK_GBS, 4)}
     r.update({"kernel": tag, "launches": n, "event_timed_steps": 1, "avg_launch_us": round(1e3 * ms / n, 2),
               "bytes_per_launch": int(nbytes / n), "flops_per_launch": int(flops / n),
-              "share_of_timed_conv_ms": round(ms / sum(v[1] for v in summ.values()), 3),
+              "share_of_timed_ms": round(ms / total_ms, 3),
               "traffic": pmc_traffic(tag, B, cfg), "traffic_unit": "bytes/launch (rocprofv3 PMC, profiles/)",
               "traffic_file": os.path.basename(pmc_file(cfg)) or None})
+    if tag.split("<")[0] in H_STASH:
+        r["note"] = ("bytes include the h stash (1 of 3 activation tensors; a design choice: "
+                     "the backward could recompute h from x)")
     return r
 
 
@@ -602,7 +615,7 @@ def main():
     sr = SR48 if cfg == "c5" else SR
     if cfg == "c2":
         step = c2_setup(dev, B)
-        dom = "sel_stft_loss_fwd"
+        dom = "sel_stft_loss_fwd"   # + the backward and the fused mel launch (timer below)
         workload = "configs[1]: MR-STFT(3 res) + mel(2048/300/80) loss fwd+bwd, fp32, 1 s @ 24 kHz"
         dtype = "fp32"
     elif cfg == "c3":
@@ -621,8 +634,11 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    timer = (_lib.KernelTimer([dom] + (["sel_resunit_fwd", "sel_resunit_bwd", "sel_resunit_bwd_wgrad"]
-                                       if cfg == "c3" else []))
+    # every entry point that launches a conv-stack kernel of the step (the
+    # dominant kernel is the largest total time over all of them)
+    timer = (_lib.KernelTimer([dom] + (["sel_resunit_fwd", "sel_resunit_bwd", "sel_resunit_bwd_wgrad",
+                                        "sel_conv_wgrad_partials", "sel_wgrad_finish_many"]
+                                       if cfg == "c3" else ["sel_stft_loss_bwd", "sel_mel_l1_fwd_grad"]))
              if cfg != "c5" else None)  # C5: a serialised extra step below
     elapsed, per_step = _timed_steps(step, args.steps, world, dev, timer)
 
@@ -638,7 +654,8 @@ def main():
         # the timed region; each launch's events then bracket that launch alone
         prev = os.environ.get("SEL_D_STREAMS")
         os.environ["SEL_D_STREAMS"] = "0"
-        timer = _lib.KernelTimer([dom, "sel_dconv_fwd"])
+        timer = _lib.KernelTimer([dom, "sel_dconv_fwd", "sel_dconv_wgrad_partials", "sel_resunit_fwd",
+                                  "sel_resunit_bwd", "sel_conv_wgrad_partials", "sel_wgrad_finish_many"])
         torch.cuda.synchronize()
         _lib.TIMER = timer
         step()

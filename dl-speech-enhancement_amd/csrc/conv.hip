@@ -4904,18 +4904,20 @@ bool wss_pick_elu(const Args& a) {
          a.pad_mode == SEL_PAD_ZERO && wss_ok(a) && wss_geometry(a, S, tm) && S == 16;
 }
 
-int fwd4_choice(const Args& a) {
+// out_f32: an fp32-output launch (the sample-tile kernel takes those at T <= 400
+// only, wss_ok_out; fwd4_variant's dispatch applies the same condition)
+int fwd4_choice(const Args& a, bool out_f32) {
   const int v = tune(0);
   if (!((a.C % CK) == 0 && (a.K - 1) * a.dil <= F4_HALOMAX && a.K <= 8 && (v == 0 || v > 20))) return -1;
   if (v > 20 && (v != 27 || ws_ok(a)) && (v != 28 || ws8_gen_ok(a)) && (v != 29 || ws8w_ok(a)) &&
-      (v != 30 || wss_ok(a)))
+      (v != 30 || wss_ok_out(a, out_f32)))
     return v;
   if (a.N <= 32 || (a.N % 64) != 0 || a.rows < 8192) return 22;
   if (a.N >= 256 && a.K == 1) return 26;
   if (a.N >= 256 && a.rows >= 16384)
-    return wss_pick(a) ? 30 : tune(38) == 1 && ws8w_ok(a) ? 29 : ws_ok(a) ? 27 : 24;
+    return wss_pick(a) && wss_ok_out(a, out_f32) ? 30 : tune(38) == 1 && ws8w_ok(a) ? 29 : ws_ok(a) ? 27 : 24;
   if (a.N <= 64 || a.rows < 65536) return 23;
-  if (wss_pick_tall(a) || wss_pick_elu(a)) return 30;
+  if ((wss_pick_tall(a) || wss_pick_elu(a)) && wss_ok_out(a, out_f32)) return 30;
   if (ws8_gen_pick(a)) return 28;
   if (a.N == 128 && ws_ok(a) && (a.K <= 3 || (a.K == 7 && a.pad == 0 && !a.in_elu))) return 27;
   if (a.N == 128 && a.K > 1 && a.pad == 0 && !a.in_elu) return 22;
@@ -5614,7 +5616,7 @@ int sel_conv_fwd_kernel_id(const sel_conv_desc* d, int in_dtype, int out_dtype, 
     const bool e = thin_variant(a, has_epilogue != 0, r);
     return 1000000000 + (e ? 500000000 : 0) + ((r / 32 * 1000 + a.C) * 1000 + a.N) * 10 + a.K;
   }
-  const int v = fwd4_choice(a);
+  const int v = fwd4_choice(a, out_dtype == SEL_F32);
   if (v < 0) return -1;
   // warp-specialised kernels: 9e8 + K (12 waves), 9.1e8 + K (eight waves, 512 x 128)
   if (v == 27) return 900000000 + a.K;

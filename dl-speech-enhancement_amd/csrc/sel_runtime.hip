@@ -219,11 +219,13 @@ extern "C" int sel_probe_copy_f4(const void* src, void* dst, int64_t n16, int bl
   const float4* in = static_cast<const float4*>(src);
   float4* out = static_cast<float4*>(dst);
   const int mode = sel::tune(49);
+  // the one-shot forms' grid of (n16 / (256 U)) workgroups must fit the
+  // unsigned grid dimension for the U actually launched (U >= 1: checked at U = 1)
+  SEL_REQUIRE((n16 + 255) / 256 < (int64_t(1) << 31), SEL_ERR_ARG, "copy probe buffer too large");
   auto once = [&](auto kern, int U) {
     const int64_t g = (n16 + 256 * U - 1) / (256 * U);
     hipLaunchKernelGGL(kern, dim3(unsigned(g)), dim3(256), 0, s, in, out, n16);
   };
-  SEL_REQUIRE(n16 / 1024 < (int64_t(1) << 31), SEL_ERR_ARG, "copy probe buffer too large");
   switch (mode) {
     case 1: hipLaunchKernelGGL(k_probe_copy_f4, dim3(unsigned(blocks)), dim3(256), 0, s, in, out, n16); break;
     case 2: once(k_probe_copy_once<8, false>, 8); break;

@@ -463,13 +463,31 @@ def _grad_out(p, shape, device):
     return r.view(p) if r is not None else torch.empty(shape, dtype=torch.float32, device=device)
 
 
+def _wgrad_meta(desc, x, nsplit):
+    """(tag, algorithmic bytes, flops) of one split-row weight-gradient partial
+    launch: read gout and x once, write nsplit fp32 partials of the N x K x C
+    weight (the partials are the split design's own traffic, counted)."""
+    es = x.element_size()
+    nw = desc.N * desc.K * desc.C
+    nbytes = desc.rows * (desc.N + desc.C) * es + 4 * nsplit * nw
+    return (f"wgrad_partials[N={desc.N},K={desc.K},C={desc.C},T={desc.T}]", nbytes,
+            2.0 * desc.rows * desc.N * desc.K * desc.C)
+
+
+def _finish_meta(group):
+    """k_wgrad_finish_many: read every job's fp32 split partials, write its gradient."""
+    nbytes = sum(4 * j.nw * (j.nsplit + 1) for j in group)
+    return "k_wgrad_finish_many", nbytes, 0.0
+
+
 def _run_jobs(entries):
     """sel_wgrad_finish_many over deferred entries, one launch per stream."""
     cur = torch.cuda.current_stream()
     for st in dict.fromkeys(e[3] for e in entries):
         group = [e[0] for e in entries if e[3] == st]
         jobs = (_WgradJob * len(group))(*group)
-        L.call("sel_wgrad_finish_many", ctypes.cast(jobs, ctypes.c_void_p), len(group), ctypes.c_void_p(st))
+        L.call("sel_wgrad_finish_many", ctypes.cast(jobs, ctypes.c_void_p), len(group), ctypes.c_void_p(st),
+               meta=lambda: _finish_meta(group))
         if (st or 0) != cur.cuda_stream:  # (a null-stream handle reads as None)
             # the gradients are read on the current stream from here on (the
             # optimizer / the all-reduce): order it after this finish on ANY
@@ -538,7 +556,8 @@ def wgrad_torch(desc, gout, x, kind, w_shape, stride, want_bias, params=None):
                 t.record_stream(side)
             st = ctypes.c_void_p(side.cuda_stream)
         L.call("sel_conv_wgrad_partials", ctypes.byref(desc), _code(x.dtype), L.ptr(gout), L.ptr(x),
-               int(want_bias), L.ptr(ws), ws.numel(), ctypes.byref(ns), st)
+               int(want_bias), L.ptr(ws), ws.numel(), ctypes.byref(ns), st,
+               meta=lambda: _wgrad_meta(desc, x, ns.value))
         job = _WgradJob(ws.data_ptr(), gw.data_ptr(), gb.data_ptr() if gb is not None else None,
                         desc.N * desc.K * desc.C, ns.value, desc.N, desc.bias_period, kind, cout, cin, k,
                         stride)

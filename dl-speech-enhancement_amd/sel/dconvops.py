@@ -286,9 +286,19 @@ def wgrad(sp, desc, gout, x, w_or_v, wg, want_w, want_b, pending=None):
         L.call("sel_dconv_wgrad", *args, L.stream())
     else:
         job = _DwgradJob()
-        L.call("sel_dconv_wgrad_partials", *args, ctypes.byref(job), L.stream())
+        L.call("sel_dconv_wgrad_partials", *args, ctypes.byref(job), L.stream(),
+               meta=lambda: _wgrad_meta(desc, x, gout))
         pending.append((job, ws, v, g))  # the finish reads ws, v and g
     return (gw if want_w else None), gg, gb
+
+
+def _wgrad_meta(d, x, gout):
+    """(tag, algorithmic bytes, flops) of one weight-gradient partial launch:
+    the forward's contraction over the same operands (read x and gout once)."""
+    width = d.So * d.Ng
+    flops = 2.0 * d.B * d.Tvalid * d.G * width * d.K * d.S * d.Cg
+    nbytes = x.numel() * x.element_size() + gout.numel() * gout.element_size()
+    return f"dconv_wgrad_partials[G={d.G},Cg={d.Cg},K={d.K},S={d.S},T={d.Tvalid}]", nbytes, flops
 
 
 def finish_pending(pending):

@@ -32,6 +32,22 @@ def _frames(T, hop):
     return 1 + T // hop
 
 
+def _fft_flops(n):
+    """Radix-2 count of one real-input length-n FFT (2.5 n log2 n)."""
+    import math
+    return 2.5 * n * math.log2(n)
+
+
+def _spec_meta(tag, B, T, hop, n_fft, n_io, n_fft_per_frame, extra_per_frame=0.0):
+    """(tag, algorithmic bytes, flops) of a fused spectral launch for bench.py's
+    timer: n_io fp32 (B, T) waveforms read or written once (frames are formed
+    in-kernel; their overlap is served on chip), n_fft_per_frame transforms
+    per frame."""
+    F = _frames(T, hop)
+    return (f"{tag}[n_fft={n_fft}]", 4 * n_io * B * T,
+            B * F * (n_fft_per_frame * _fft_flops(n_fft) + extra_per_frame))
+
+
 class StftMag(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, n_fft, hop, win_length, window, eps):
@@ -115,7 +131,8 @@ class StftLoss(torch.autograd.Function):
         sums = torch.empty(3, dtype=torch.float64, device=x.device)
         ws = L.workspace(lib.sel_stft_loss_workspace(B, T, n_fft, hop, win_length), x.device)
         L.call("sel_stft_loss_fwd", L.ptr(x), L.ptr(y), B, T, n_fft, hop, win_length, L.ptr(window),
-                                      L.ptr(sums), L.ptr(ws), ws.numel(), L.stream())
+               L.ptr(sums), L.ptr(ws), ws.numel(), L.stream(),
+               meta=lambda: _spec_meta("k_stft_loss_fwd", B, T, hop, n_fft, 2, 2))
         n = B * _frames(T, hop) * (n_fft // 2 + 1)
         sums, n, ctx.scale = D.global_loss_sums(sums, n)  # data parallel: global-batch SC
         out = torch.empty(2, dtype=torch.float32, device=x.device)
@@ -137,7 +154,8 @@ class StftLoss(torch.autograd.Function):
         gx = torch.empty_like(x)
         ws = L.workspace(lib.sel_stft_loss_workspace(B, T, n_fft, hop, win), x.device)
         L.call("sel_stft_loss_bwd", L.ptr(x), L.ptr(y), B, T, n_fft, hop, win, L.ptr(window),
-                                      L.ptr(coef), L.ptr(gx), L.ptr(ws), ws.numel(), L.stream())
+               L.ptr(coef), L.ptr(gx), L.ptr(ws), ws.numel(), L.stream(),
+               meta=lambda: _spec_meta("k_stft_loss_bwd", B, T, hop, n_fft, 3, 3))
         return gx, None, None, None, None, None
 
 
@@ -224,7 +242,8 @@ class MelL1(torch.autograd.Function):
             ws = L.workspace(lib.sel_mel_l1_workspace(B, T, n_fft, hop, win_length), x.device)
             L.call("sel_mel_l1_fwd_grad", L.ptr(x), L.ptr(y), B, T, n_fft, hop, win_length, L.ptr(window),
                    L.ptr(melmat), L.ptr(krange), L.ptr(mrange), M, float(eps), log_kind, L.ptr(loss), L.ptr(gx1),
-                   L.ptr(ws), ws.numel(), s)
+                   L.ptr(ws), ws.numel(), s,
+                   meta=lambda: _spec_meta("k_mel_l1", B, T, hop, n_fft, 3, 3, 3 * 2.0 * (n_fft // 2 + 1) * M))
             ctx.save_for_backward(gx1)
             return loss
         if MEL_PAIR_ONE_LAUNCH:

@@ -12,7 +12,9 @@ and the sample-tile kernel, test_gpu_c3), 1/3/4/5/11/54/55 (test_gpu_conv; 54 /
   prefetch flipped on every thin instance), 20 (two-pass split reduction),
   40 (k_ru64_bwdw workgroup target: another split of the weight-gradient
   rows), 41 (the 64-channel backward without gh on the eight-wave kernel
-  instead of k_ru64_bwd: bit-identical);
+  instead of k_ru64_bwd: bit-identical), 56 (128-row tiles for k_ru32_fwd),
+  57 (the two-set fragment pipeline of k_wgrad3_bf16 for the k2 / k3 layers
+  with >= 64 k rows: B = 12 clips put the down convs' weight gradients there);
 * discriminator (C5 widths, B = 2 x 1 s @ 48 kHz, bf16, fwd + bwd incl.
   weight-norm grads): 16 (no prefetching kernels: k_dconv_mfma tiles and the
   generic weight gradient), 25 (scalar bias partials), 28 (128-row tiles for
@@ -29,7 +31,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 GEN_KNOBS = [(6, 0xFFFF, False), (7, 0xFFFF, False), (8, 1, True), (12, 0xFFFF, False), (20, 1, True),
-             (40, 64, False), (41, 1, True)]
+             (40, 64, False), (41, 1, True), (56, 1, False), (57, 1, False, 12)]
 DISC_KNOBS = [(16, 1, False), (25, 1, False), (28, 1, False), (31, 1, False)]
 
 
@@ -51,15 +53,16 @@ def test_generator_variant_knobs(gpu, knob):
     from sel import _lib as Lb
     from sel import configs
     from sel.convops import precision
-    key, val, exact = knob
+    key, val, exact = knob[:3]
+    B = knob[3] if len(knob) > 3 else 2
     lib = Lb.lib()
     cfg = configs.get("symAD_libritts_24000_hop300")
     torch.manual_seed(3)
     G = Generator(**cfg["generator_params"]).to(gpu)
     G.quantizer.codebook.eval()
     g = torch.Generator(device=gpu).manual_seed(4)
-    x = 0.1 * torch.randn(2, 1, 24000, device=gpu, generator=g)
-    gy = torch.randn(2, 1, 24000, device=gpu, generator=g)
+    x = 0.1 * torch.randn(B, 1, 24000, device=gpu, generator=g)
+    gy = torch.randn(B, 1, 24000, device=gpu, generator=g)
     params = [p for p in G.parameters() if p.requires_grad]
 
     def run():
@@ -87,7 +90,8 @@ def test_discriminator_variant_knobs(gpu, knob):
     from sel import _lib as Lb
     from sel import configs
     from sel.convops import precision
-    key, val, exact = knob
+    key, val, exact = knob[:3]
+    B = knob[3] if len(knob) > 3 else 2
     lib = Lb.lib()
     dp = configs.get("symAD_vctk_48000_hop300")["discriminator_params"]
     torch.manual_seed(8)
