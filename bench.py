@@ -150,13 +150,13 @@ def c3_setup(dev, B, world, local, graph=False, dtype=torch.bfloat16, batch=None
     mel = MultiMelSpectrogramLoss(**cfg["mel_loss_params"]).to(dev)
     opt_kw = dict(cfg["generator_optimizer_params"])
     if graph:
-        opt_kw["capturable"] = True  # step count on device: the update replays inside a HIP graph
+        opt_kw["capturable"] = True  # step count and lr on device: the update replays inside a HIP graph
     if os.environ.get("SEL_ADAM_FOREACH", "0") != "1":
         # one fused multi-tensor Adam launch instead of torch's 7 foreach passes
         # (128 us/step at C3, profiles/r1_c3_v22_kernel_stats.md); same update rule
         opt_kw.setdefault("fused", True)
-    # sel.optim.Adam (one sel_adam_step_many launch) unless SEL_ADAM=torch or a
-    # HIP-graph replay needs torch's capturable form
+    # sel.optim.Adam (one sel_adam_step_many launch; capturable: the device-count
+    # form sel_adam_step_many_dev) unless SEL_ADAM=torch
     from sel import optim as sel_optim
     opt = sel_optim.adam(G.parameters(), **opt_kw)
     sched = torch.optim.lr_scheduler.StepLR(opt, **cfg["generator_scheduler_params"])
@@ -180,6 +180,14 @@ def c3_setup(dev, B, world, local, graph=False, dtype=torch.bfloat16, batch=None
     def step():
         with precision(dtype):
             tr._train_step((mixed, clean))
+    if graph:
+        # the whole trainer step as one HIP-graph replay (trainer/graph.py)
+        from trainer.graph import GraphedTrainStep
+        with precision(dtype):
+            gs = GraphedTrainStep(tr, (mixed, clean))
+        gs.eager = step
+        gs.trainer, gs.generator = tr, G
+        return gs
     step.trainer, step.generator = tr, G
     return step
 
@@ -581,6 +589,8 @@ def main():
     ap.add_argument("--batch", type=int, default=0, help="per-GPU batch (default: config's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fp32-companion", action="store_true")
+    ap.add_argument("--eager", action="store_true",
+                    help="c3: issue every launch from Python instead of replaying the step's HIP graph")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -619,7 +629,10 @@ def main():
         workload = "configs[1]: MR-STFT(3 res) + mel(2048/300/80) loss fwd+bwd, fp32, 1 s @ 24 kHz"
         dtype = "fp32"
     elif cfg == "c3":
-        step = c3_setup(dev, B, world, local)
+        # one process: the trainer step replays as a HIP graph (trainer/graph.py);
+        # under a process group the bucketed all-reduce stays eager
+        use_graph = world == 1 and not FORCE_DDP and not args.eager and os.environ.get("SEL_BENCH_GRAPH", "1") != "0"
+        step = c3_setup(dev, B, world, local, graph=use_graph)
         dom = "sel_conv_fwd"
         workload = (f"configs[2]/[3]: denoise-trainer step (trainer/denoise.py) on the PQC AudioDec generator, "
                     f"{C3_CONFIG} (derived), bf16 convs / fp32 losses, {B} x 1 s @ 24 kHz per GPU")
@@ -640,7 +653,17 @@ def main():
                                         "sel_conv_wgrad_partials", "sel_wgrad_finish_many"]
                                        if cfg == "c3" else ["sel_stft_loss_bwd", "sel_mel_l1_fwd_grad"]))
              if cfg != "c5" else None)  # C5: a serialised extra step below
-    elapsed, per_step = _timed_steps(step, args.steps, world, dev, timer)
+    graphed = cfg == "c3" and hasattr(step, "graph")
+    elapsed, per_step = _timed_steps(step, args.steps, world, dev, None if graphed else timer)
+    if graphed:
+        # per-launch HIP events cannot sit inside a replay: the roofline comes
+        # from one eager step of the same trainer after the timed region (the
+        # same kernels on the same shapes)
+        torch.cuda.synchronize()
+        _lib.TIMER = timer
+        step.eager()
+        torch.cuda.synchronize()
+        _lib.TIMER = None
 
     ms_per_step = 1e3 * elapsed / args.steps
     frames_per_step = world * B * sr / HOP
@@ -666,6 +689,8 @@ def main():
         else:
             os.environ["SEL_D_STREAMS"] = prev
     roof = roofline(cfg, timer, dom, B, 1)  # the timer covered one step (C3: the last timed one)
+    if graphed:
+        roof["timing"] = "one eager step after the timed graph replays (same kernels)"
     if cfg == "c5":
         roof["timing"] = "one extra step with the sub-discriminator chains serialised (SEL_D_STREAMS=0)"
 
@@ -703,7 +728,8 @@ def main():
             "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": dtype, "data": "synthetic",
             "config": {"workload": workload, "global_batch": world * B, "seq_len": sr,
-                       "parallelism": f"dp{world}"},
+                       "parallelism": f"dp{world}",
+                       "issue": "hip-graph replay" if (cfg == "c3" and hasattr(step, "graph")) else "eager"},
             "roofline": roof, "cpu_baseline": cpu, "fp32_companion": fp32, "stft_kernel": stft_roof,
         }
         print(json.dumps(out), flush=True)

@@ -147,7 +147,25 @@ __device__ __forceinline__ void adam_one(float& p, float g, float& m, float& v, 
   p = p - step_size * m / denom;
 }
 
-__global__ __launch_bounds__(256) void k_adam_many(AdamJobs aj, AdamConst c) {
+// Capturable form (sel_adam_step_many_dev): the step count and the learning
+// rate live on the device, so a captured update stays correct on every replay.
+// One thread advances the count and writes (step_size, bc2_sqrt), rounded to
+// float from double exactly as the host form's caller does; the update kernel
+// then reads them (stream order: no reader sees a half-advanced count).
+__global__ void k_adam_consts(const float* __restrict__ lr, float* __restrict__ step, double b1, double b2,
+                              float* __restrict__ out) {
+  const float t = step[0] + 1.f;
+  step[0] = t;
+  out[0] = float(double(lr[0]) / (1.0 - pow(b1, double(t))));
+  out[1] = float(sqrt(1.0 - pow(b2, double(t))));
+}
+
+template <bool DEV>
+__global__ __launch_bounds__(256) void k_adam_many(AdamJobs aj, AdamConst c, const float* __restrict__ dc) {
+  if constexpr (DEV) {
+    c.step_size = dc[0];
+    c.bc2_sqrt = dc[1];
+  }
   int j = 0;
   while (j + 1 < aj.nt && int(blockIdx.x) >= aj.bstart[j + 1]) ++j;  // block-uniform
   const int64_t n = aj.n[j];
@@ -244,20 +262,15 @@ int sel_snr_bwd(const float* pred, const float* target, int64_t B, int64_t T, co
   return SEL_OK;
 }
 
-int sel_adam_step_many(const sel_adam_tensor* ts, int nt, double beta1, double beta2, double eps, double weight_decay,
-                       double step_size, double bc2_sqrt, sel_stream_t stream) {
+}  // extern "C"
+
+namespace {
+int adam_launch(const sel_adam_tensor* ts, int nt, const sel::glue::AdamConst& c, const float* dc, hipStream_t s) {
   using namespace sel::glue;
-  SEL_REQUIRE(nt >= 0 && (nt == 0 || ts), SEL_ERR_ARG, "bad Adam tensor list");
-  SEL_REQUIRE(bc2_sqrt > 0.0 && eps >= 0.0, SEL_ERR_ARG, "bad Adam constants");
-  // (1 - beta) rounded once from the double, as torch's kernels receive it:
-  // 1 - float(0.999) is 1.3e-5 away from 0.001
-  const AdamConst c{float(beta1), float(1.0 - beta1), float(beta2),     float(1.0 - beta2),
-                    float(eps),   float(weight_decay), float(step_size), float(bc2_sqrt)};
   for (int j = 0; j < nt; ++j)
     SEL_REQUIRE(ts[j].n >= 0 && (ts[j].n == 0 || (ts[j].p && ts[j].g && ts[j].m && ts[j].v)) &&
                     (ts[j].n + ADAM_EPB - 1) / ADAM_EPB < (int64_t(1) << 30),
                 SEL_ERR_ARG, "bad Adam tensor %d", j);
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   int j = 0;
   while (j < nt) {
     AdamJobs aj{};
@@ -279,11 +292,45 @@ int sel_adam_step_many(const sel_adam_tensor* ts, int nt, double beta1, double b
     aj.bstart[k] = int(blocks);
     aj.nt = k;
     if (blocks > 0) {
-      hipLaunchKernelGGL(k_adam_many, dim3(unsigned(blocks)), dim3(256), 0, s, aj, c);
+      if (dc)
+        hipLaunchKernelGGL(k_adam_many<true>, dim3(unsigned(blocks)), dim3(256), 0, s, aj, c, dc);
+      else
+        hipLaunchKernelGGL(k_adam_many<false>, dim3(unsigned(blocks)), dim3(256), 0, s, aj, c, dc);
       SEL_LAUNCH_CHECK();
     }
   }
   return SEL_OK;
+}
+
+// (1 - beta) rounded once from the double, as torch's kernels receive it:
+// 1 - float(0.999) is 1.3e-5 away from 0.001
+sel::glue::AdamConst adam_const(double beta1, double beta2, double eps, double weight_decay, double step_size,
+                                double bc2_sqrt) {
+  return sel::glue::AdamConst{float(beta1), float(1.0 - beta1), float(beta2),        float(1.0 - beta2),
+                              float(eps),   float(weight_decay), float(step_size), float(bc2_sqrt)};
+}
+}  // namespace
+
+extern "C" {
+
+int sel_adam_step_many(const sel_adam_tensor* ts, int nt, double beta1, double beta2, double eps, double weight_decay,
+                       double step_size, double bc2_sqrt, sel_stream_t stream) {
+  SEL_REQUIRE(nt >= 0 && (nt == 0 || ts), SEL_ERR_ARG, "bad Adam tensor list");
+  SEL_REQUIRE(bc2_sqrt > 0.0 && eps >= 0.0, SEL_ERR_ARG, "bad Adam constants");
+  return adam_launch(ts, nt, adam_const(beta1, beta2, eps, weight_decay, step_size, bc2_sqrt), nullptr,
+                     reinterpret_cast<hipStream_t>(stream));
+}
+
+int sel_adam_step_many_dev(const sel_adam_tensor* ts, int nt, double beta1, double beta2, double eps,
+                           double weight_decay, const float* lr, float* step, float* consts, sel_stream_t stream) {
+  using namespace sel::glue;
+  SEL_REQUIRE(nt >= 0 && (nt == 0 || ts), SEL_ERR_ARG, "bad Adam tensor list");
+  SEL_REQUIRE(lr && step && consts, SEL_ERR_ARG, "null lr / step / consts");
+  SEL_REQUIRE(beta2 < 1.0 && eps >= 0.0, SEL_ERR_ARG, "bad Adam constants");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(k_adam_consts, dim3(1), dim3(1), 0, s, lr, step, beta1, beta2, consts);
+  SEL_LAUNCH_CHECK();
+  return adam_launch(ts, nt, adam_const(beta1, beta2, eps, weight_decay, 0.0, 1.0), consts, s);
 }
 
 }  // extern "C"

@@ -94,6 +94,7 @@ SIGNATURES = {
     "sel_dconv_wgrad_partials": (I32, [P, I32, P, P, I32, I32, I32, I32, I32, P, P, P, P, P, P, SZ, P, P]),
     "sel_dconv_wgrad_finish_many": (I32, [P, I32, P]),
     "sel_adam_step_many": (I32, [P, I32, F64, F64, F64, F64, F64, F64, P]),
+    "sel_adam_step_many_dev": (I32, [P, I32, F64, F64, F64, F64, P, P, P, P]),
     "sel_avgpool1d_fwd": (I32, [P, I32, I32, I32, I32, I32, I32, I32, I32, P, P]),
     "sel_avgpool1d_bwd": (I32, [P, I32, I32, I32, I32, I32, I32, I32, I32, P, P]),
     "sel_mpd_fold": (I32, [P, I32, I32, I32, I32, I32, P, P]),

@@ -322,6 +322,15 @@ typedef struct {
 } sel_adam_tensor;
 int sel_adam_step_many(const sel_adam_tensor* ts, int nt, double beta1, double beta2, double eps,
                        double weight_decay, double step_size, double bc2_sqrt, sel_stream_t stream);
+/* The same update with the step count and learning rate on the device (the
+ * capturable form: a HIP-graph replay of a training step stays correct, the
+ * role of torch.optim.Adam(capturable=True)): *step += 1, then step_size =
+ * lr[0] / (1 - b1^t), bc2_sqrt = sqrt(1 - b2^t) computed in double on the
+ * device into consts[0..1] (caller-owned, 2 floats), then the update.  One
+ * step count for all nt tensors (one parameter group). */
+int sel_adam_step_many_dev(const sel_adam_tensor* ts, int nt, double beta1, double beta2, double eps,
+                           double weight_decay, const float* lr, float* step, float* consts,
+                           sel_stream_t stream);
 
 /* ---- SNR term of train_denoise.py:140 (torchmetrics 1.2.0 SignalNoiseRatio,
  * zero_mean=False): snr_b = 10 log10((sum t^2 + eps) / (sum (t-p)^2 + eps)) over the
