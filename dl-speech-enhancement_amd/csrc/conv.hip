@@ -4526,6 +4526,82 @@ __global__ void k_pack_many_arg(PackJobs pj, int64_t lo, int64_t hi, int64_t tot
   (void)total;
 }
 
+// Tiled form of k_pack_many_arg (the product's per-step repack): a workgroup
+// owns a 32 (n) x 32 (cp) x KP tile of one job's packed geometry, gathers it
+// from the torch-layout weight with (cp, kp)-contiguous reads into an fp32 LDS
+// tile, then writes the tile's forward form Wp[n][kp][cp] (32 consecutive cp per
+// run) and its dgrad form Wd[cp][KP-1-kp][n] (32 consecutive n per run): both
+// forms leave as coalesced runs.  The per-element form gathered the dgrad
+// form's source across whole weight rows (one cache line per lane): 72 us per
+// C3 step for 31 MB of traffic (rocprof, profiles/r6f_kernel_stats.md).  Same
+// values (a copy with the same rounding).
+constexpr int PT_T = 32, PT_KMAX = 8, PT_P = PT_T + 1;
+struct PackTiles {
+  sel_pack_job j[PM_MAXJ];
+  int tstart[PM_MAXJ + 1];  // first tile of each job; tstart[n] = tile count
+  int n;
+};
+__device__ __forceinline__ void pack_geom(const sel_pack_job& J, unsigned& N, unsigned& KP, unsigned& CP) {
+  const unsigned s = unsigned(J.stride), cin = unsigned(J.cin), cout = unsigned(J.cout), K = unsigned(J.k);
+  if (J.kind == SEL_PACK_FWD) N = cout, KP = K, CP = cin;
+  else if (J.kind == SEL_PACK_FWD_STRIDED) N = cout, KP = 3, CP = s * cin;
+  else N = s * cout, KP = 2, CP = cin;
+}
+template <typename TO>
+__global__ __launch_bounds__(256) void k_pack_tiles(PackTiles pt) {
+  __shared__ float tile[PT_T * PT_KMAX * PT_P];
+  int a = 0, b = pt.n - 1;
+  const int t = int(blockIdx.x);
+  while (a < b) {  // block-uniform
+    const int mid = (a + b + 1) >> 1;
+    if (pt.tstart[mid] <= t) a = mid;
+    else b = mid - 1;
+  }
+  const sel_pack_job& J = pt.j[a];
+  unsigned N, KP, CP;
+  pack_geom(J, N, KP, CP);
+  const unsigned s = unsigned(J.stride), cin = unsigned(J.cin), cout = unsigned(J.cout), K = unsigned(J.k);
+  const unsigned ntc = (CP + PT_T - 1) / PT_T;
+  const unsigned lt = unsigned(t - pt.tstart[a]);
+  const unsigned n0 = (lt / ntc) * PT_T, c0 = (lt % ntc) * PT_T;
+  const unsigned tot = PT_T * PT_T * KP;
+  // gather: e = (nl * 32 + cl) * KP + kp (kp fastest: contiguous in the FWD source)
+  for (unsigned e = threadIdx.x; e < tot; e += 256) {
+    const unsigned kp = e % KP, r = e / KP, cl = r % PT_T, nl = r / PT_T;
+    const unsigned n = n0 + nl, cp = c0 + cl;
+    float v = 0.f;
+    if (n < N && cp < CP) {
+      if (J.kind == SEL_PACK_FWD) {
+        v = J.w[(n * cin + cp) * K + kp];
+      } else if (J.kind == SEL_PACK_FWD_STRIDED) {
+        const unsigned ph = cp / cin, ci = cp - ph * cin;
+        const int k = strided_k(int(kp), int(ph), int(s));
+        v = k >= 0 ? J.w[(n * cin + ci) * (2 * s) + unsigned(k)] : 0.f;
+      } else {
+        const unsigned ph = n / cout, co = n - ph * cout;
+        const unsigned k = kp == 0 ? ph + s : ph;
+        v = J.w[(cp * cout + co) * (2 * s) + k];
+      }
+    }
+    tile[(nl * KP + kp) * PT_P + cl] = v;
+  }
+  __syncthreads();
+  TO* const wp = static_cast<TO*>(J.wpack);
+  for (unsigned e = threadIdx.x; e < tot; e += 256) {  // Wp[n][kp][cp]: cp fastest
+    const unsigned cl = e % PT_T, r = e / PT_T, kp = r % KP, nl = r / KP;
+    const unsigned n = n0 + nl, cp = c0 + cl;
+    if (n < N && cp < CP) wp[(n * KP + kp) * CP + cp] = from_f<TO>(tile[(nl * KP + kp) * PT_P + cl]);
+  }
+  if (J.wdgrad) {
+    TO* const wd = static_cast<TO*>(J.wdgrad);
+    for (unsigned e = threadIdx.x; e < tot; e += 256) {  // Wd[cp][j][n]: n fastest
+      const unsigned nl = e % PT_T, r = e / PT_T, j = r % KP, cl = r / KP;
+      const unsigned n = n0 + nl, cp = c0 + cl;
+      if (n < N && cp < CP) wd[(cp * KP + j) * N + n] = from_f<TO>(tile[(nl * KP + (KP - 1 - j)) * PT_P + cl]);
+    }
+  }
+}
+
 // Packed index of torch-layout weight element i (the gather map of k_unpack).
 __device__ __forceinline__ int64_t unpack_src(int kind, int64_t i, int cout, int cin, int K, int s) {
   if (kind == SEL_PACK_FWD) {
@@ -4912,6 +4988,8 @@ int fwd4_choice(const Args& a, bool out_f32) {
   if (v > 20 && (v != 27 || ws_ok(a)) && (v != 28 || ws8_gen_ok(a)) && (v != 29 || ws8w_ok(a)) &&
       (v != 30 || wss_ok_out(a, out_f32)))
     return v;
+  // (the T = 80 layers: 128 x 64 / 128 x 128 / 64 x 128 tiles measured 13-50 us
+  // slower per graph-replayed C3 step, round 6)
   if (a.N <= 32 || (a.N % 64) != 0 || a.rows < 8192) return 22;
   if (a.N >= 256 && a.K == 1) return 26;
   if (a.N >= 256 && a.rows >= 16384)
@@ -6096,6 +6174,31 @@ int sel_pack_many_host(const sel_pack_job* jobs, int njobs, int64_t total, int d
       pj.j[j] = jobs[j0 + j];
       SEL_REQUIRE(pj.j[j].offset >= 0 && pj.j[j].offset < total && (j == 0 || pj.j[j].offset > pj.j[j - 1].offset),
                   SEL_ERR_ARG, "pack jobs must have increasing offsets within total");
+    }
+    // tiled kernel (k_pack_tiles) unless a job's taps exceed its tile (K > 8)
+    // or tune key 60 = 1 asks for the per-element form
+    PackTiles pt{};
+    bool tiled = tune(60) != 1;
+    int64_t tiles = 0;
+    pt.n = pj.n;
+    for (int j = 0; j < pj.n && tiled; ++j) {
+      const sel_pack_job& J = pj.j[j];
+      const int64_t N = J.kind == SEL_PACK_CONVT ? int64_t(J.stride) * J.cout : J.cout;
+      const int64_t KP = J.kind == SEL_PACK_FWD ? J.k : J.kind == SEL_PACK_FWD_STRIDED ? 3 : 2;
+      const int64_t CP = J.kind == SEL_PACK_FWD_STRIDED ? int64_t(J.stride) * J.cin : J.cin;
+      if (KP > PT_KMAX) tiled = false;
+      pt.j[j] = J;
+      pt.tstart[j] = int(tiles);
+      tiles += ((N + PT_T - 1) / PT_T) * ((CP + PT_T - 1) / PT_T);
+    }
+    pt.tstart[pt.n] = int(tiles);
+    if (tiled && tiles > 0 && tiles < (int64_t(1) << 31)) {
+      if (dtype == SEL_F32)
+        hipLaunchKernelGGL(k_pack_tiles<float>, dim3(unsigned(tiles)), dim3(256), 0, s, pt);
+      else
+        hipLaunchKernelGGL(k_pack_tiles<__bf16>, dim3(unsigned(tiles)), dim3(256), 0, s, pt);
+      SEL_LAUNCH_CHECK();
+      continue;
     }
     const int64_t lo = pj.j[0].offset;
     const int64_t hi = j0 + pj.n < njobs ? jobs[j0 + pj.n].offset : total;

@@ -792,16 +792,28 @@ def test_deferred_wgrad_reduction_bit_identical(gpu, monkeypatch):
         assert torch.equal(a_, b_ + 1.0)
 
 
-def test_pack_many_matches_per_layer_pack(gpu):
-    """PackCache's one-launch refresh (sel_pack_many: Wp and the dgrad form Wd
-    written as two coalesced ranges) writes the same bytes as sel_pack_weight
-    + sel_pack_dgrad per layer, for the three packed kinds (causal conv,
-    phase-view strided conv, transposed conv) in both dtypes."""
+@pytest.mark.parametrize("per_element", [0, 1])
+def test_pack_many_matches_per_layer_pack(gpu, per_element):
+    """PackCache's one-launch refresh (sel_pack_many_host: the tiled
+    k_pack_tiles, or the per-element k_pack_many_arg under tune key 60 = 1)
+    writes the same bytes as sel_pack_weight + sel_pack_dgrad per layer, for
+    the three packed kinds (causal conv, phase-view strided conv, transposed
+    conv; ragged 32-tiles included) in both dtypes."""
+    from sel import _lib as Lb
     from sel import convops as CO
+    prev = Lb.lib().sel_tune(60, per_element)
+    try:
+        _pack_many_check(gpu, CO)
+    finally:
+        Lb.lib().sel_tune(60, prev)
+
+
+def _pack_many_check(gpu, CO):
     torch.manual_seed(11)
     layers = [(CO.PACK_FWD, (64, 32, 7), 1), (CO.PACK_FWD, (256, 256, 1), 1), (CO.PACK_FWD_STRIDED, (128, 64, 4), 2),
               (CO.PACK_FWD_STRIDED, (512, 256, 10), 5), (CO.PACK_CONVT, (256, 128, 6), 3),
-              (CO.PACK_CONVT, (64, 96, 2), 1), (CO.PACK_FWD, (1, 32, 7), 1)]
+              (CO.PACK_CONVT, (64, 96, 2), 1), (CO.PACK_FWD, (1, 32, 7), 1), (CO.PACK_FWD, (32, 1, 7), 1),
+              (CO.PACK_FWD, (48, 40, 3), 1), (CO.PACK_FWD_STRIDED, (64, 32, 6), 3), (CO.PACK_CONVT, (64, 32, 6), 3)]
     for dt in (torch.bfloat16, torch.float32):
         cache = CO.PackCache()
         ws = [torch.randn(*shp, device=gpu) for _, shp, _ in layers]
