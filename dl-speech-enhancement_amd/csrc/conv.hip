@@ -5563,7 +5563,9 @@ WgPlan wgrad_plan(const sel_conv_desc* d, int mode) {
   int64_t want = std::max<int64_t>(1, (target + blocks - 1) / blocks);
   if (mode == 3) want = (want + 7) / 8 * 8;  // splits on x: blocks of one row range share an XCD
   const int64_t per_split = (int64_t(d->N) * d->K * d->C + d->N) * 4;
-  want = std::min<int64_t>(want, std::max<int64_t>(1, (int64_t(mode == 3 ? 32 : 64) << 20) / per_split));
+  // split partials per layer capped at 32 MB (mode 3; tune key 62 > 0: another cap in MB)
+  const int64_t cap_mb = mode == 3 ? (tune(62) > 0 ? tune(62) : 32) : 64;
+  want = std::min<int64_t>(want, std::max<int64_t>(1, (cap_mb << 20) / per_split));
   want = std::min<int64_t>(want, std::max<int64_t>(1, p.n_tiles));
   p.tiles_per_split = int((p.n_tiles + want - 1) / want);
   if (p.tiles_per_split < 1) p.tiles_per_split = 1;

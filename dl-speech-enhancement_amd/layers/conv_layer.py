@@ -12,13 +12,17 @@ import torch.nn as nn
 from sel import convops as CO
 
 
-def _run_layer(x, weight, bias, kind, stride, dilation):
-    """(B, C, T) in -> (B, C', T') out through ConvLayerFn, in the active precision."""
+def _run_layer(x, weight, bias, kind, stride, dilation, out_float=False):
+    """(B, C, T) in -> (B, C', T') out through ConvLayerFn, in the active precision
+    (out_float: fp32 output whatever the compute dtype)."""
     xc = CO.to_cl(x)
     dt = CO.compute_dtype()
     if xc.dtype != dt:
         xc = CO.cast(xc, dt)
-    y = CO.ConvLayerFn.apply(xc, weight, bias, kind, stride, dilation)
+    if out_float and dt != torch.float32:
+        y = CO.ConvLayerFn.apply(xc, weight, bias, kind, stride, dilation, True)
+    else:
+        y = CO.ConvLayerFn.apply(xc, weight, bias, kind, stride, dilation)
     return y.transpose(1, 2)
 
 
@@ -122,9 +126,13 @@ class CausalConv1d(NonCausalConv1d):
         if pad_buffer is None:
             pad_buffer = torch.zeros(1, in_channels, self.pad_length)
         self.register_buffer("pad_buffer", pad_buffer)
+        # fp32 output under bf16 compute (set on a model's last layer, whose
+        # output feeds the fp32 losses: no separate cast launch)
+        self.out_float = False
 
     def forward(self, x):
-        return _run_layer(x, self.conv.weight, self.conv.bias, CO.PACK_FWD, self.stride, self.dilation)
+        return _run_layer(x, self.conv.weight, self.conv.bias, CO.PACK_FWD, self.stride, self.dilation,
+                          self.out_float)
 
     @torch.no_grad()
     def inference(self, x):

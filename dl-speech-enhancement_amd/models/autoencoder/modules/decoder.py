@@ -65,6 +65,9 @@ class Decoder(torch.nn.Module):
             self.conv_blocks.append(DecoderBlock(cin, cout, stride, bias=bias, mode=mode))
         self.num_blocks = len(self.conv_blocks)
         self.conv2 = Conv(cout, output_channels, kernel_size, 1, bias=False)
+        # the waveform leaves in fp32 (the losses' dtype) straight from the
+        # conv epilogue, where AudioDec.py's y.float() would cast it
+        self.conv2.out_float = True
 
     def forward(self, z):
         x = z if self.skip_conv1 else self.conv1(z)

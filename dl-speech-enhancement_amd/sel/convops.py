@@ -616,9 +616,12 @@ class ConvLayerFn(torch.autograd.Function):
     """One reference conv layer (causal / strided / transposed), channels-last."""
 
     @staticmethod
-    def forward(ctx, x, w, b, kind, stride, dil):
-        # x: (B, T, Cin) contiguous in compute dtype
+    def forward(ctx, x, w, b, kind, stride, dil, *out_float):
+        # x: (B, T, Cin) contiguous in compute dtype; out_float (optional, True):
+        # an fp32 output from a bf16 layer (the epilogue rounds to fp32 instead
+        # of bf16; the backward takes the fp32 gradient to bf16 as a cast would)
         L.need_device(x, w)
+        ctx.nextra = len(out_float)
         B, T_in, cin = x.shape
         if kind == PACK_CONVT:
             cout, k = w.shape[1], w.shape[2]
@@ -631,7 +634,7 @@ class ConvLayerFn(torch.autograd.Function):
         desc, T_out, c_out = _layer_desc(kind, B, T_in, cin, cout, k, stride, dil, b is not None)
         wp, wd = PACKS.get(kind, w, stride, x.dtype)
         bias = b.detach().contiguous().float() if b is not None else None
-        y = prim(desc, x, wp, bias=bias)
+        y = prim(desc, x, wp, bias=bias, out_dtype=torch.float32 if out_float and out_float[0] else None)
         ctx.save_for_backward(x, wp, wd)
         ctx.meta = (desc, kind, stride, tuple(w.shape), b is not None)
         ctx.prefs = (weakref.ref(w), weakref.ref(b) if b is not None else None)
@@ -657,7 +660,7 @@ class ConvLayerFn(torch.autograd.Function):
             gw, gb = wgrad_torch(desc, gy, x, kind, w_shape, stride, want_b, params)
             if not ctx.needs_input_grad[1]:
                 gw = None
-        return gx, gw, gb, None, None, None
+        return (gx, gw, gb, None, None, None) + (None,) * ctx.nextra
 
 
 # fused residual unit (sel_resunit_fwd / sel_resunit_bwd): ON by default at 32

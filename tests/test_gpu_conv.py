@@ -333,6 +333,39 @@ def test_single_channel_kernel_matches_generic(gpu, C, N, K, dil, elu, aux, res)
     assert e < 4e-3, e
 
 
+@pytest.mark.parametrize("C,K,dil,pad_mode,elu,bias,out32,T", [
+    (32, 7, 1, 0, 0, 0, 1, 24000), (32, 7, 1, 0, 0, 0, 0, 1000), (64, 7, 3, 0, 1, 1, 1, 777),
+    (64, 3, 1, 1, 0, 1, 0, 500), (32, 2, 1, 1, 1, 0, 1, 61), (32, 7, 9, 0, 0, 1, 0, 40)])
+def test_one_output_channel_conv(gpu, C, K, dil, pad_mode, elu, bias, out32, T):
+    """N = 1 convs (the decoder's last layer, whose fp32 output feeds the
+    losses: decoder.conv2.out_float) in bf16 and fp32 output against fp64 of
+    the same bf16 operands: ragged T and T < halo, zero and replicate padding.
+    (A dedicated one-output-channel kernel was measured slower than the tiled
+    kernel in round 6 -- 87-92 against 37 us -- and dropped.)"""
+    from sel import convops as CO
+    B = 3
+    pad = (K - 1) * dil if pad_mode == 0 else 1
+    d = CO.ConvDesc(B * T, T, C, 1, K, dil, pad, CO.PAD_ZERO if pad_mode == 0 else CO.PAD_REPLICATE, elu,
+                    1 if bias else 0)
+    torch.manual_seed(C + K + T)
+    x = torch.randn(B * T, C, device=gpu).to(torch.bfloat16)
+    wp = (0.3 * torch.randn(1, K, C, device=gpu)).to(torch.bfloat16)
+    b = torch.randn(1, device=gpu) if bias else None
+    od = torch.float32 if out32 else torch.bfloat16
+    o = CO.prim(d, x, wp, bias=b, out_dtype=od).double()
+    # fp64 truth of the same operands (the ELU'd input rounded to bf16 as the kernels stage it)
+    xt = x.double().view(B, T, C)
+    if elu:
+        xt = torch.nn.functional.elu(xt).to(torch.bfloat16).double()
+    xp = torch.nn.functional.pad(xt.transpose(1, 2), (pad, (K - 1) * dil - pad),
+                                 mode="constant" if pad_mode == 0 else "replicate")
+    ref = torch.nn.functional.conv1d(xp, wp.double().permute(0, 2, 1), dilation=dil).transpose(1, 2).reshape(-1, 1)
+    if bias:
+        ref = ref + b.double()
+    e = ((o - ref).norm() / ref.norm()).item()
+    assert e < (1e-5 if out32 else 4e-3), e
+
+
 # (C, N, K, dil, pad_mode, in_elu, aux, res, bias, B, T): every thin-kernel instance in
 # its forward and adjoint forms, plus ragged T (tails shorter than one tile) and T < halo
 THIN_SHAPES = [(32, 32, 7, 9, 0, 1, 0, 0, 0, 3, 1000), (32, 32, 7, 9, 0, 0, 1, 1, 0, 2, 777),
