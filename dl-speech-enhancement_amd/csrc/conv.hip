@@ -2704,7 +2704,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 128 ? 
 constexpr int C1_NMAX = 64;
 constexpr int C1_KMAX = 8;
 constexpr int C1_TR = 256;    // rows per sample-aligned tile (weight gradient)
-constexpr int C1F_TR = 1024;  // rows per tile of the forward kernel
+// rows per tile of the forward kernel: 768 (round 6; was 1024).  One resident
+// round is 1024 workgroups at C3: 64 x 24000 rows in 1024-row tiles are 1536
+// tiles, so half the workgroups ran two and the launch took two tile times;
+// 768-row tiles are 2048 tiles, two per workgroup, 1.5 (1024-row) tile times
+constexpr int C1F_TR = 768;
 constexpr int C1_HALO = 64;   // max (K-1)*dil
 
 // Stage act(x) for input times [t0 - pad, t0 - pad + C1_TR + halo) of sample b as
@@ -5444,8 +5448,9 @@ int dispatch_fwd(const Args& a, const void* in, const void* wp, const float* bia
   if constexpr (sizeof(TI) == 2) {
     if (a.C == 1 && a.N % 8 == 0 && a.N <= C1_NMAX && a.K <= C1_KMAX && (a.K - 1) * a.dil <= C1_HALO &&
         tune(3) == 0)
-      return tune(44) == 1 ? launch_c1<TI, TO, 256>(a, in, wp, bias, aux, res, out, s)
-                           : launch_c1<TI, TO, C1F_TR>(a, in, wp, bias, aux, res, out, s);
+      return tune(44) == 1   ? launch_c1<TI, TO, 256>(a, in, wp, bias, aux, res, out, s)
+             : tune(44) == 2 ? launch_c1<TI, TO, 1024>(a, in, wp, bias, aux, res, out, s)
+                             : launch_c1<TI, TO, C1F_TR>(a, in, wp, bias, aux, res, out, s);
     const int v = tune(0);
     const bool fast = (a.C % CK) == 0 && (a.K - 1) * a.dil <= F4_HALOMAX && a.K <= 8 && (v == 0 || v > 20);
     if (fast) {

@@ -323,14 +323,19 @@ def test_single_channel_kernel_matches_generic(gpu, C, N, K, dil, elu, aux, res)
     r_ = torch.randn(B * T, N, device=gpu).to(torch.bfloat16) if res else None
     lib = L.lib()
     outs = []
-    for v in (0, 1):
-        prev = lib.sel_tune(3, v)
+    # (key 3, key 44): the streaming kernel on its 768-row tiles (default), on
+    # 256-row (44 = 1) and 1024-row (44 = 2) tiles, then the generic kernel
+    for v, t44 in ((0, 0), (0, 1), (0, 2), (1, 0)):
+        prev, prev44 = lib.sel_tune(3, v), lib.sel_tune(44, t44)
         try:
             outs.append(CO.prim(d, x, wp, bias=b, aux=a_, res=r_).float())
         finally:
             lib.sel_tune(3, prev)
-    e = ((outs[0] - outs[1]).norm() / outs[1].norm()).item()
-    assert e < 4e-3, e
+            lib.sel_tune(44, prev44)
+    for o in outs[:3]:
+        e = ((o - outs[-1]).norm() / outs[-1].norm()).item()
+        assert e < 4e-3, e
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])  # tiling only: same bits
 
 
 @pytest.mark.parametrize("C,K,dil,pad_mode,elu,bias,out32,T", [
