@@ -4986,6 +4986,17 @@ bool wss_pick_elu(const Args& a) {
 
 // out_f32: an fp32-output launch (the sample-tile kernel takes those at T <= 400
 // only, wss_ok_out; fwd4_variant's dispatch applies the same condition)
+// the sample-tile kernel on five-sample tiles for the wide T = 80 layers (the
+// C3 down / up convs at the 512-wide stage and their adjoints: 128 x 32 tiles ran
+// them at 80 of 128 rows per tile): 55.7 -> 52.7, 50.6 -> 45.4, 46.2 -> 44.8 us
+// (rocprof, round 6).  Not for N < 512: 13 tiles per 64-wide column are too few
+// workgroups (projector 14.9 -> 23.3, decoder.conv1's adjoint 22.2 -> 39.2 us).
+// Tune key 67: 1 = on wherever it applies, 2 = off, 0 = default (N >= 512)
+bool wss_pick_short(const Args& a) {
+  const int k = tune(67);
+  return k != 2 && (k == 1 || a.N >= 512) && wss_spt(a) > 1 && a.N % 64 == 0 && wss_ok(a);
+}
+
 int fwd4_choice(const Args& a, bool out_f32) {
   const int v = tune(0);
   if (!((a.C % CK) == 0 && (a.K - 1) * a.dil <= F4_HALOMAX && a.K <= 8 && (v == 0 || v > 20))) return -1;
@@ -4994,6 +5005,7 @@ int fwd4_choice(const Args& a, bool out_f32) {
     return v;
   // (the T = 80 layers: 128 x 64 / 128 x 128 / 64 x 128 tiles measured 13-50 us
   // slower per graph-replayed C3 step, round 6)
+  if (wss_pick_short(a) && wss_ok_out(a, out_f32)) return 30;
   if (a.N <= 32 || (a.N % 64) != 0 || a.rows < 8192) return 22;
   if (a.N >= 256 && a.K == 1) return 26;
   if (a.N >= 256 && a.rows >= 16384)
@@ -5034,6 +5046,7 @@ int fwd4_variant(int v, const Args& a, const void* in, const void* wp, const flo
   // heuristic from tools/conv_bench.py on the C3 layer shapes (profiles/r1_conv_bench.md):
   // narrow / non-64-multiple outputs and short row counts favour 128x32 tiles
   // (more workgroups in flight); wide layers 128x64 or 256x64.
+  if (wss_pick_short(a) && wss_ok_out(a, sizeof(TO) == 4)) return launch_wss<TO>(a, in, wp, bias, aux, res, out, s);
   if (a.N <= 32 || (a.N % 64) != 0 || a.rows < 8192)
     return launch_fwd4<128, 32, 4, KMAX, TO>(a, in, wp, bias, aux, res, out, s);
   // 256-wide 1x1 (RU256 1x1 fwd 27.5 -> 20.9 us, dgrad 22.5 -> 19.2): 64x128 tiles
@@ -5707,10 +5720,10 @@ int sel_conv_fwd_kernel_id(const sel_conv_desc* d, int in_dtype, int out_dtype, 
   if (v == 27) return 900000000 + a.K;
   if (v == 28) return 910000000 + a.K;
   if (v == 29) return 920000000 + a.K;
-  if (v == 30) {  // sample-tile kernel: 9.4e8 + 1e4 BN + 10 S + K
+  if (v == 30) {  // sample-tile kernel: 9.4e8 + 1e6 (SPT - 1) + 1e4 BN + 10 S + K
     int S = 0, tm = 0, BN = 0;
     wss_geometry(a, S, tm, BN);
-    return 940000000 + 10000 * BN + 10 * S + a.K;
+    return 940000000 + 1000000 * (wss_spt(a) - 1) + 10000 * BN + 10 * S + a.K;
   }
   const int kmax = a.K == 1 ? 1 : (a.K <= 3 ? 3 : 8);
   static const int bm[] = {256, 128, 128, 256, 128, 64}, bn[] = {32, 32, 64, 64, 128, 128}, wm[] = {4, 4, 2, 4, 2, 1};

@@ -108,6 +108,7 @@ namespace conv {
 bool wss_geometry(const Args& a, int& S, int& tm, int& BN);  // strips per tile, tile rows, channels
 bool wss_geometry(const Args& a, int& S, int& tm);
 bool wss_ok(const Args& a);
+int wss_spt(const Args& a);  // samples per sample-tile (1, or 400 / T for short T)
 bool wss_ok_out(const Args& a, bool out_f32);  // wss_ok and an instance for that output type
 template <typename TO>
 int launch_wss(const Args& a, const void* in, const void* wp, const float* bias, const void* aux, const void* res,

@@ -47,13 +47,17 @@ __device__ __attribute__((aligned(64))) __bf16 g_wss_zero[WSS_CMAX];
 // KT taps, S 16-row strips per tile, BN output channels per tile (64 or 128:
 // NCS = BN / 16 column strips).  Wave w owns Q = S / 4 full strips (all NCS
 // column strips) plus E of the R * NCS (strip, column strip) pairs of the last
-// R = S % 4 strips.
-template <int KT, int S, int BN>
+// R = S % 4 strips.  SPT > 1 (round 6): a tile is SPT whole short samples (T =
+// 16 S / SPT rows each: the C3 T = 80 convs, five samples per 400-row tile),
+// each staged as its own segment of T + halo rows (rounded to 16) so a strip
+// never reads another sample's rows.
+template <int KT, int S, int BN, int SPT = 1>
 struct WssGeo {
   static constexpr int Q = S / 4, R = S % 4, NCS = BN / 16, E = R * NCS / 4;
   static_assert((R * NCS) % 4 == 0, "extra pairs split evenly over the four consumers");
   static constexpr int EP = BN + 4;  // fp32 epilogue tile pitch
-  static constexpr int XROWS = (S * 16 + F4_HALOMAX + WSS_RPP - 1) / WSS_RPP * WSS_RPP;  // staged input rows
+  static constexpr int XROWS = SPT == 1 ? (S * 16 + F4_HALOMAX + WSS_RPP - 1) / WSS_RPP * WSS_RPP  // staged input rows
+                                        : S * 16 + SPT * F4_HALOMAX;
   static constexpr int XI = XROWS / WSS_RPP;            // input DMA pieces per chunk
   static constexpr int WI = KT * BN / WSS_RPP;          // weight DMA pieces per chunk
   static constexpr int TI = XI + WI;
@@ -61,7 +65,11 @@ struct WssGeo {
   static constexpr int SLOT = (XROWS + KT * BN) * WSS_ROWB;
   static constexpr int RING = WSS_NB * SLOT;
   static constexpr int EPI = S * 16 * EP * 4;
-  static constexpr int LDS = RING > EPI ? RING : EPI;
+  // the ELU pass reads eight pieces 4 KB apart per group (k_conv_wss)
+  static constexpr int PX = (XI + 3) / 4, NGRP = (PX + 7) / 8;
+  static constexpr int ELUR = (WSS_NB - 1) * SLOT + (4 * (8 * NGRP - 1) + 3 + 1) * 1024;
+  static constexpr int LDS0 = RING > EPI ? RING : EPI;
+  static constexpr int LDS = LDS0 > ELUR ? LDS0 : ELUR;
 };
 
 // 16-B slot XOR of LDS row `row`: ds_read_b128 serves a wave in four 16-lane
@@ -73,12 +81,12 @@ struct WssGeo {
 // (PMC: SQ_LDS_BANK_CONFLICT 44% of SQ_LDS_IDX_ACTIVE).
 __device__ __forceinline__ int wss_swz(int row) { return (row >> 1) & 2; }
 
-template <int KT, int S, int BN, typename TO>
+template <int KT, int S, int BN, typename TO, int SPT = 1>
 __global__ __launch_bounds__(512) void k_conv_wss(Args a, const __bf16* __restrict__ in,
                                                   const __bf16* __restrict__ wp, const float* __restrict__ bias,
                                                   const TO* __restrict__ aux, const TO* __restrict__ res,
                                                   TO* __restrict__ out, int ncol, int tm, int dbg) {
-  using G = WssGeo<KT, S, BN>;
+  using G = WssGeo<KT, S, BN, SPT>;
   constexpr int Q = G::Q, NCS = G::NCS, E = G::E, XR = G::XROWS, XI = G::XI, TI = G::TI, PW = G::PW;
   constexpr int EP = G::EP;
   static_assert(2 * PW < 64, "vmcnt range");
@@ -90,14 +98,20 @@ __global__ __launch_bounds__(512) void k_conv_wss(Args a, const __bf16* __restri
   int nt;
   xcd_tile(ncol, mt, nt);
   const int T = a.T;
-  const int tps = (T + tm - 1) / tm;
-  const int64_t b = mt / tps;
-  const int t0 = int(mt - b * tps) * tm;
-  const int mrows = T - t0 < tm ? T - t0 : tm;
+  const int64_t nsamp = a.rows / T;
+  // SPT == 1: tile = tm rows of sample b from row t0; SPT > 1: samples
+  // b .. b + SPT - 1 whole (the last tile may hold fewer), their rows contiguous
+  const int tps = SPT == 1 ? (T + tm - 1) / tm : 1;
+  const int64_t b = SPT == 1 ? mt / tps : mt * SPT;
+  const int t0 = SPT == 1 ? int(mt - b * tps) * tm : 0;
+  const int nsp = SPT == 1 ? 1 : int(nsamp - b < SPT ? nsamp - b : SPT);  // samples in this tile
+  const int mrows = SPT == 1 ? (T - t0 < tm ? T - t0 : tm) : nsp * T;
   const int64_t m0 = b * T + t0;
   const int n0 = nt * BN;
   const int nchunk = a.C / WSS_CK;
-  const int span = tm + (KT - 1) * a.dil;
+  const int span = SPT == 1 ? tm + (KT - 1) * a.dil : 0;
+  // SPT > 1: each sample's segment is seg rows (T + halo, 16-row multiple)
+  const int seg = SPT == 1 ? 0 : (T + (KT - 1) * a.dil + 15) / 16 * 16;
   // diagnostic (tune key 48 bit 4): s_memtime stamps of block phases, written
   // over the first output bytes at the end (st[0] start, [1] first chunk ready,
   // [2] consumer loop done, [3] tile in LDS, [4] end, [5]/[6] realtime start/end)
@@ -137,16 +151,26 @@ __global__ __launch_bounds__(512) void k_conv_wss(Args a, const __bf16* __restri
       const int rr = (q < XI ? q : q - XI) * WSS_RPP + (lane >> 2);
       const int ls = (lane & 3) ^ wss_swz(rr);
       if (q < XI) {
-        int ti = t0 + rr - a.pad;
-        const bool valid = rr < span && ((ti >= 0 && ti < T) || a.pad_mode == SEL_PAD_REPLICATE);
+        int64_t bs = b;
+        int rl = rr;
+        bool inseg = rr < span;
+        if constexpr (SPT > 1) {  // segment j = sample b + j: rows - pad .. of it
+          const int j = rr / seg;
+          rl = rr - j * seg;
+          bs = b + j;
+          inseg = j < nsp && rl < T + (KT - 1) * a.dil;
+        }
+        int ti = t0 + rl - a.pad;
+        const bool valid = inseg && ((ti >= 0 && ti < T) || a.pad_mode == SEL_PAD_REPLICATE);
         ti = ti < 0 ? 0 : (ti >= T ? T - 1 : ti);
-        src[u] = valid ? in + (b * T + ti) * a.C + 8 * ls : g_wss_zero + 8 * ls;
+        src[u] = valid ? in + (bs * T + ti) * a.C + 8 * ls : g_wss_zero + 8 * ls;
       } else {
         const int k = rr / BN, n = rr % BN;
         src[u] = wp + (int64_t(n0 + n) * KT + k) * a.C + 8 * ls;
       }
     }
-    const int xi_used = (span + WSS_RPP - 1) / WSS_RPP;  // input pieces holding rows < span
+    const int xi_used = SPT == 1 ? (span + WSS_RPP - 1) / WSS_RPP   // input pieces holding rows < span
+                                 : (nsp * seg + WSS_RPP - 1) / WSS_RPP;
     auto issue = [&](int ch) __attribute__((always_inline)) {
       unsigned char* const base = smem + (ch % WSS_NB) * G::SLOT;
 #pragma unroll
@@ -164,9 +188,9 @@ __global__ __launch_bounds__(512) void k_conv_wss(Args a, const __bf16* __restri
     // Inline asm: a plain LDS access here would make hipcc drain vmcnt (the next
     // chunk's DMA) first; one statement: the compiler cannot hoist a use of a
     // result above the wait.
-    constexpr int PX = (XI + 3) / 4, NGRP = (PX + 7) / 8;
+    constexpr int PX = G::PX, NGRP = G::NGRP;
     // (the reads past the input pieces stay inside the allocation; never written)
-    static_assert((WSS_NB - 1) * G::SLOT + (4 * (8 * NGRP - 1) + 3 + 1) * 1024 <= G::LDS, "ELU pass reads");
+    static_assert(G::ELUR <= G::LDS, "ELU pass reads");
     auto elu_pass = [&](int ch) __attribute__((always_inline)) {
 #pragma unroll
       for (int gq = 0; gq < NGRP; ++gq) {
@@ -230,6 +254,15 @@ __global__ __launch_bounds__(512) void k_conv_wss(Args a, const __bf16* __restri
       xstrip[i] = 4 * Q + p / NCS;
       xcol[i] = p % NCS;
     }
+    // byte offset of strip st's first staged row (SPT > 1: its sample's segment;
+    // a 16-row multiple, so the row swizzle of the tap reads is unchanged)
+    const int sps = SPT == 1 ? S : T / 16;  // strips per sample
+    auto sbase = [&](int st) { return SPT == 1 ? st * 1024 : ((st / sps) * seg + (st % sps) * 16) * WSS_ROWB; };
+    int soff[Q > 0 ? Q : 1], xoff[E1];
+#pragma unroll
+    for (int i = 0; i < Q; ++i) soff[i] = sbase(w * Q + i);
+#pragma unroll
+    for (int i = 0; i < E; ++i) xoff[i] = sbase(xstrip[i]);
     floatx4 acc[Q][NCS], accx[E1];
 #pragma unroll
     for (int i = 0; i < Q; ++i)
@@ -243,7 +276,6 @@ __global__ __launch_bounds__(512) void k_conv_wss(Args a, const __bf16* __restri
     static_assert(WSS_NB == 2, "two chunks per trip, one per ring slot");
     auto fetch = [&](int sl, int k, int q) __attribute__((always_inline)) {
       const unsigned char* const xb = smem + sl * G::SLOT;
-      const unsigned char* const xw = xb + w * Q * 1024;  // this wave's first full strip
       const unsigned char* const wb = xb + XR * WSS_ROWB;
 #pragma unroll
       for (int c = 0; c < NCS; ++c)
@@ -254,11 +286,11 @@ __global__ __launch_bounds__(512) void k_conv_wss(Args a, const __bf16* __restri
       // 2 x KT per-step addresses would take the registers the pipeline needs
       asm volatile("" : "+v"(lx));
 #pragma unroll
-      for (int i = 0; i < Q; ++i) fx[q][i] = *reinterpret_cast<const bf16x8*>(xw + i * 1024 + lx);
+      for (int i = 0; i < Q; ++i) fx[q][i] = *reinterpret_cast<const bf16x8*>(xb + soff[i] + lx);
 #pragma unroll
       for (int i = 0; i < E; ++i) {
         fwx[q][i] = *reinterpret_cast<const bf16x8*>(wb + (k * BN + xcol[i] * 16) * WSS_ROWB + lane_w);
-        fxx[q][i] = *reinterpret_cast<const bf16x8*>(xb + xstrip[i] * 1024 + lx);
+        fxx[q][i] = *reinterpret_cast<const bf16x8*>(xb + xoff[i] + lx);
       }
     };
     auto mfmas = [&](int q) __attribute__((always_inline)) {
@@ -396,12 +428,18 @@ __global__ __launch_bounds__(512) void k_conv_wss(Args a, const __bf16* __restri
 //              input ELU once per 128 output channels instead of twice, for the
 //              ELU'd forwards (the RU128 k7 convs; 512 tiles at C3).
 // tune key 51: 1 = (16, 128) wherever it applies, 2 = never, 0 = for in_elu only
+// samples per tile: 400 / T for the short sequences whole 16-row strips tile
+// exactly (T = 80 at C3: five samples per 25-strip tile); tune key 67 = 2: off
+int wss_spt(const Args& a) {
+  return (a.T % 16 == 0 && a.T >= 80 && a.T < 400 && 400 % a.T == 0 && tune(67) != 2) ? 400 / a.T : 1;
+}
+
 bool wss_geometry(const Args& a, int& S, int& tm, int& BN) {
   BN = 64;
   const int S1 = (a.T + 15) / 16;
-  if (S1 == 25) {
+  if (S1 == 25 || wss_spt(a) > 1) {
     S = 25;
-    tm = a.T;
+    tm = S1 == 25 ? a.T : 400;
     return true;
   }
   const int k51 = tune(51);
@@ -435,16 +473,16 @@ bool wss_ok(const Args& a) {
          a.rows % a.T == 0;
 }
 
-template <int KT, int S, int BN, typename TO>
+template <int KT, int S, int BN, typename TO, int SPT = 1>
 static int launch_wss_t(const Args& a, int tm, const void* in, const void* wp, const float* bias, const void* aux,
                         const void* res, void* out, hipStream_t s) {
-  using G = WssGeo<KT, S, BN>;
+  using G = WssGeo<KT, S, BN, SPT>;
   static_assert(G::LDS <= 160 * 1024, "LDS");
-  const int64_t tiles = (a.rows / a.T) * ((a.T + tm - 1) / tm);
+  const int64_t tiles = SPT == 1 ? (a.rows / a.T) * ((a.T + tm - 1) / tm) : (a.rows / a.T + SPT - 1) / SPT;
   const int ncol = a.N / BN;
   if (tiles == 0) return SEL_OK;
   SEL_REQUIRE(tiles * ncol < (int64_t(1) << 31), SEL_ERR_UNSUPPORTED, "k_conv_wss: grid too large");
-  auto kern = k_conv_wss<KT, S, BN, TO>;
+  auto kern = k_conv_wss<KT, S, BN, TO, SPT>;
   SEL_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, int(G::LDS)));
   hipLaunchKernelGGL(kern, dim3(unsigned(tiles * ncol)), dim3(512), G::LDS, s, a, static_cast<const __bf16*>(in),
                      static_cast<const __bf16*>(wp), bias, static_cast<const TO*>(aux), static_cast<const TO*>(res),
@@ -453,13 +491,13 @@ static int launch_wss_t(const Args& a, int tm, const void* in, const void* wp, c
   return SEL_OK;
 }
 
-template <int S, int BN, typename TO>
+template <int S, int BN, typename TO, int SPT = 1>
 static int launch_wss_k(const Args& a, int tm, const void* in, const void* wp, const float* bias, const void* aux,
                         const void* res, void* out, hipStream_t s) {
   switch (a.K) {
-    case 7: return launch_wss_t<7, S, BN, TO>(a, tm, in, wp, bias, aux, res, out, s);
-    case 3: return launch_wss_t<3, S, BN, TO>(a, tm, in, wp, bias, aux, res, out, s);
-    default: return launch_wss_t<2, S, BN, TO>(a, tm, in, wp, bias, aux, res, out, s);
+    case 7: return launch_wss_t<7, S, BN, TO, SPT>(a, tm, in, wp, bias, aux, res, out, s);
+    case 3: return launch_wss_t<3, S, BN, TO, SPT>(a, tm, in, wp, bias, aux, res, out, s);
+    default: return launch_wss_t<2, S, BN, TO, SPT>(a, tm, in, wp, bias, aux, res, out, s);
   }
 }
 
@@ -470,7 +508,9 @@ int launch_wss(const Args& a, const void* in, const void* wp, const float* bias,
               a.K, a.dil);
   int S, tm, BN;
   wss_geometry(a, S, tm, BN);
-  if (S == 25) return launch_wss_k<25, 64, TO>(a, tm, in, wp, bias, aux, res, out, s);
+  if (S == 25 && wss_spt(a) == 5) return launch_wss_k<25, 64, TO, 5>(a, tm, in, wp, bias, aux, res, out, s);
+  if (S == 25 && wss_spt(a) == 1) return launch_wss_k<25, 64, TO>(a, tm, in, wp, bias, aux, res, out, s);
+  SEL_REQUIRE(S != 25, SEL_ERR_UNSUPPORTED, "k_conv_wss: %d samples per tile not compiled", wss_spt(a));
   if constexpr (sizeof(TO) == 2) {  // (fp32 outputs: the epilogue rows do not fit the taller tiles' registers)
     if (S == 16) return launch_wss_k<16, 128, TO>(a, tm, in, wp, bias, aux, res, out, s);
     return launch_wss_k<32, 64, TO>(a, tm, in, wp, bias, aux, res, out, s);

@@ -22,8 +22,9 @@ void set_error(const char* fmt, ...) {
 
 bool initialized() { return g_init_status == SEL_OK; }
 
-static int g_tune[64] = {0};
-int tune(int key) { return (key >= 0 && key < 64) ? g_tune[key] : 0; }
+constexpr int kTuneKeys = 128;
+static int g_tune[kTuneKeys] = {0};
+int tune(int key) { return (key >= 0 && key < kTuneKeys) ? g_tune[key] : 0; }
 
 static int do_init() {
   // FFT twiddles, computed in double on the host and rounded once to fp32.
@@ -70,13 +71,13 @@ const char* sel_last_error(void) { return sel::g_err; }
 int sel_version(void) { return 1; }
 
 int sel_tune(int key, int value) {
-  if (key < 0 || key >= 64) return -1;
+  if (key < 0 || key >= sel::kTuneKeys) return -1;
   const int prev = sel::g_tune[key];
   sel::g_tune[key] = value;
   return prev;
 }
 
-int sel_tune_get(int key) { return (key >= 0 && key < 64) ? sel::g_tune[key] : -1; }
+int sel_tune_get(int key) { return (key >= 0 && key < sel::kTuneKeys) ? sel::g_tune[key] : -1; }
 
 }  // extern "C"
 

@@ -288,9 +288,10 @@ def fwd_kernel_name(desc, in_dtype, out_dtype, has_epilogue=False):
         k, n, c, r = kid % 10, (kid // 10) % 1000, (kid // 10000) % 1000, 32 * (kid // 10000000)
         return f"k_conv_thin_bf16<{c}, {n}, {k}, {r}, {'true' if e else 'false'}>"
     to = "bf16" if out_dtype == torch.bfloat16 else "float"
-    if kid >= 94 * 10 ** 7:  # sample-tile warp-specialised kernel (conv_wss.hip): 9.4e8 + 1e4 BN + 10 S + K
+    if kid >= 94 * 10 ** 7:  # sample-tile warp-specialised kernel (conv_wss.hip): 9.4e8 + 1e6 (SPT-1) + 1e4 BN + 10 S + K
         r = kid - 94 * 10 ** 7
-        return f"k_conv_wss<{r % 10}, {(r // 10) % 1000}, {r // 10000}, {to}>"
+        spt, r = r // 10 ** 6 + 1, r % 10 ** 6
+        return f"k_conv_wss<{r % 10}, {(r // 10) % 1000}, {r // 10000}, {to}" + (f", {spt}>" if spt > 1 else ">")
     if kid >= 93 * 10 ** 7:  # pointwise (1x1) weight-stationary kernel: 9.3e8 + N
         n = kid - 93 * 10 ** 7
         return f"k_pw_bf16<{n}, {n}"

@@ -41,8 +41,9 @@ enum { SEL_LOG_E = 0, SEL_LOG_2 = 1, SEL_LOG_10 = 2 };
 int sel_init(void);                 /* uploads FFT twiddle tables; idempotent */
 const char* sel_last_error(void);   /* thread-local, never NULL */
 int sel_version(void);
-/* tuning knobs for A/B runs inside one process (key 0: conv fwd kernel variant,
- * 0 = built-in heuristic); returns the previous value. */
+/* tuning knobs for A/B runs inside one process (keys 0..127; key 0: conv fwd
+ * kernel variant, 0 = built-in heuristic); returns the previous value, -1 for a
+ * key out of range (the call then changes nothing). */
 int sel_tune(int key, int value);
 /* current value of a tuning knob, read-only (-1 for a key out of range). */
 int sel_tune_get(int key);

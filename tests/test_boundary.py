@@ -41,6 +41,20 @@ def test_library_reports_errors_without_gpu():
     assert lib.sel_version() >= 1
 
 
+def test_tune_keys_cover_every_knob():
+    """Every knob the kernels read (keys up to 67 in round 6) is settable and
+    reads back; a key out of range is refused and changes nothing (keys >= 64
+    were silently ignored before round 6, so A/B runs on them compared a
+    setting with itself)."""
+    from sel import _lib
+    lib = _lib.load()
+    for key in (0, 63, 64, 67, 127):
+        prev = lib.sel_tune(key, 7)
+        assert prev >= 0 and lib.sel_tune_get(key) == 7, key
+        assert lib.sel_tune(key, prev) == 7
+    assert lib.sel_tune(128, 1) == -1 and lib.sel_tune_get(128) == -1
+
+
 def test_product_refuses_cpu_tensors():
     from losses import MultiMelSpectrogramLoss, MultiResolutionSTFTLoss
     x = torch.randn(2, 1, 4800)

@@ -47,7 +47,41 @@ FWD = [
     # (warp-specialised kernel since round 4, forward and adjoint forms)
     ("up256_128_s5", 256, 640, 2, 1, 1, 0, 640, 400, 0, 0),
     ("up128_64_s2", 128, 256, 2, 1, 1, 0, 256, 2000, 0, 0),
+    # the other T = 80 layers (round 6: five-sample k_conv_wss tiles)
+    ("proj512_64", 512, 64, 3, 1, 0, 0, 0, 80, 0, 0),
+    ("dec_conv1_64_512", 64, 512, 7, 1, 0, 0, 0, 80, 0, 0),
 ]
+
+
+@pytest.mark.parametrize("Bs", [7, 3, 1])
+@pytest.mark.parametrize("out32", [0, 1])
+def test_sample_tiles_ragged_batches(gpu, Bs, out32):
+    """k_conv_wss on five-sample tiles (T = 80) with a batch that leaves the
+    last tile short (7 = 5 + 2, 3, 1 samples), a halo of 54 rows (k7, dil 9:
+    each sample's segment must stay its own) and replicate padding, bf16 and
+    fp32 outputs, against fp64 of the same operands."""
+    from sel import _lib as L
+    from sel import convops as CO
+    prev = L.lib().sel_tune(67, 1)  # the five-sample tiles for every width (default: N >= 512)
+    try:
+        _ragged(gpu, CO, Bs, out32)
+    finally:
+        L.lib().sel_tune(67, prev)
+
+
+def _ragged(gpu, CO, Bs, out32):
+    for (C, N, K, dil, mode) in ((64, 128, 7, 9, 0), (128, 320, 2, 1, 1), (256, 64, 3, 1, 0), (128, 512, 3, 1, 0)):
+        T = 80
+        pad = (K - 1) * dil if mode == 0 else 1
+        d = CO.ConvDesc(Bs * T, T, C, N, K, dil, pad, mode, 0, N)
+        od = torch.float32 if out32 else torch.bfloat16
+        assert CO.fwd_kernel_name(d, torch.bfloat16, od).startswith("k_conv_wss<"), CO.fwd_kernel_name(
+            d, torch.bfloat16, od)
+        gen = torch.Generator(device=gpu).manual_seed(Bs * 1000 + K)
+        x, wp, b, _, _ = _operands(d, gen, gpu, 0, 0)
+        ref = _ref(x, wp, d, Bs, b)
+        got = CO.prim(d, x, wp, bias=b, out_dtype=od)
+        _check(got, ref, (Bs, C, N, K, dil, mode, out32))
 
 
 def _ref(x, wp, d, B_, bias=None, aux=None, res=None):
