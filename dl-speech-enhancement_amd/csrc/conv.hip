@@ -4986,15 +4986,17 @@ bool wss_pick_elu(const Args& a) {
 
 // out_f32: an fp32-output launch (the sample-tile kernel takes those at T <= 400
 // only, wss_ok_out; fwd4_variant's dispatch applies the same condition)
-// the sample-tile kernel on five-sample tiles for the wide T = 80 layers (the
-// C3 down / up convs at the 512-wide stage and their adjoints: 128 x 32 tiles ran
-// them at 80 of 128 rows per tile): 55.7 -> 52.7, 50.6 -> 45.4, 46.2 -> 44.8 us
-// (rocprof, round 6).  Not for N < 512: 13 tiles per 64-wide column are too few
-// workgroups (projector 14.9 -> 23.3, decoder.conv1's adjoint 22.2 -> 39.2 us).
-// Tune key 67: 1 = on wherever it applies, 2 = off, 0 = default (N >= 512)
+// the sample-tile kernel on five-sample tiles for the T = 80 layers (the C3
+// down / up convs at the 512-wide stage and their adjoints run on 128 x 32 tiles
+// at 80 of 128 rows per tile).  Measured in round 6: 55.7 -> 52.7, 50.6 -> 45.4,
+// 46.2 -> 44.8 us for the wide layers, but 14.9 -> 23.3 and 22.2 -> 39.2 us at
+// N = 64 (13 tiles per 64-wide column are too few workgroups), and the step
+// unchanged or slower in same-call A/Bs either way (5.42-5.46 off, 5.47-5.48
+// for N >= 512, 5.50-5.51 everywhere).  So off by default; tune key 67: 1 = on
+// wherever it applies, 3 = for N >= 512 only
 bool wss_pick_short(const Args& a) {
   const int k = tune(67);
-  return k != 2 && (k == 1 || a.N >= 512) && wss_spt(a) > 1 && a.N % 64 == 0 && wss_ok(a);
+  return (k == 1 || (k == 3 && a.N >= 512)) && wss_spt(a) > 1 && a.N % 64 == 0 && wss_ok(a);
 }
 
 int fwd4_choice(const Args& a, bool out_f32) {

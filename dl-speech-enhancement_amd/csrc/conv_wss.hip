@@ -429,7 +429,8 @@ __global__ __launch_bounds__(512) void k_conv_wss(Args a, const __bf16* __restri
 //              ELU'd forwards (the RU128 k7 convs; 512 tiles at C3).
 // tune key 51: 1 = (16, 128) wherever it applies, 2 = never, 0 = for in_elu only
 // samples per tile: 400 / T for the short sequences whole 16-row strips tile
-// exactly (T = 80 at C3: five samples per 25-strip tile); tune key 67 = 2: off
+// exactly (T = 80 at C3: five samples per 25-strip tile); tune key 67 = 2: never
+// (the dispatch takes them only under key 67 = 1 / 3, conv.hip wss_pick_short)
 int wss_spt(const Args& a) {
   return (a.T % 16 == 0 && a.T >= 80 && a.T < 400 && 400 % a.T == 0 && tune(67) != 2) ? 400 / a.T : 1;
 }
