@@ -4307,29 +4307,41 @@ __global__ __launch_bounds__(256) void k_wgrad3_bf16(Args a, const __bf16* __res
 constexpr int SPLIT_GROUP = 32;
 
 // sum of the partials p[0], p[n], ... p[(cnt - 1) n] of one split group (cnt <= 32)
-__device__ __forceinline__ float split_group_sum(const float* __restrict__ p, int cnt, int64_t n) {
-  float acc = 0.f;
-  if (cnt == SPLIT_GROUP) {
-    // a full group: all 32 loads in flight at once (a serial chain of dependent
-    // adds made the compiler issue them a few at a time: latency-bound), then a
-    // fixed pairwise tree (deterministic)
-    float v[SPLIT_GROUP];
+template <int W>
+__device__ __forceinline__ float split_tree(const float* __restrict__ p, int cnt, int64_t n) {
+  // W loads in flight at once (slots past cnt hold exact zeros), then a fixed
+  // pairwise tree: deterministic for a given cnt
+  float v[W];
 #pragma unroll
-    for (int u = 0; u < SPLIT_GROUP; ++u) v[u] = p[int64_t(u) * n];
+  for (int u = 0; u < W; ++u) v[u] = u < cnt ? p[int64_t(u) * n] : 0.f;
 #pragma unroll
-    for (int w = 1; w < SPLIT_GROUP; w *= 2)
+  for (int w = 1; w < W; w *= 2)
 #pragma unroll
-      for (int u = 0; u < SPLIT_GROUP; u += 2 * w) v[u] += v[u + w];
-    acc = v[0];
-  } else {
-    int u = 0;
-    for (; u + 4 <= cnt; u += 4) {
-      const float a0 = p[int64_t(u) * n], a1 = p[int64_t(u + 1) * n], a2 = p[int64_t(u + 2) * n],
-                  a3 = p[int64_t(u + 3) * n];
-      acc += (a0 + a1) + (a2 + a3);
-    }
-    for (; u < cnt; ++u) acc += p[int64_t(u) * n];
+    for (int u = 0; u < W; u += 2 * w) v[u] += v[u + w];
+  return v[0];
+}
+__device__ __forceinline__ float split_group_sum(const float* __restrict__ p, int cnt, int64_t n,
+                                                 bool four_at_a_time = false) {
+  // a full group: all 32 loads in flight at once (a serial chain of dependent
+  // adds made the compiler issue them a few at a time: latency-bound)
+  if (cnt == SPLIT_GROUP) return split_tree<SPLIT_GROUP>(p, cnt, n);
+  // partial groups (round 6: the RU256 k7 layers' 16 splits, 29 MB each, went
+  // four loads per round trip): the smallest power-of-two tree holding cnt;
+  // tune key 68 = 1: the four-at-a-time loop
+  if (!four_at_a_time) {
+    if (cnt > 16) return split_tree<32>(p, cnt, n);
+    if (cnt > 8) return split_tree<16>(p, cnt, n);
+    if (cnt > 4) return split_tree<8>(p, cnt, n);
+    return split_tree<4>(p, cnt, n);
   }
+  float acc = 0.f;
+  int u = 0;
+  for (; u + 4 <= cnt; u += 4) {
+    const float a0 = p[int64_t(u) * n], a1 = p[int64_t(u + 1) * n], a2 = p[int64_t(u + 2) * n],
+                a3 = p[int64_t(u + 3) * n];
+    acc += (a0 + a1) + (a2 + a3);
+  }
+  for (; u < cnt; ++u) acc += p[int64_t(u) * n];
   return acc;
 }
 
@@ -6033,6 +6045,7 @@ struct FinishJobs {
   int wblocks[FM_MAXJ];  // weight blocks of job j; its bias blocks follow
   int bstart[FM_MAXJ + 1];
   int njobs;
+  int four;  // tune key 68 = 1: partial split groups four loads at a time (A/B)
 };
 
 // packed weight index -> torch-layout index (-1: a structural zero of the strided form)
@@ -6068,7 +6081,7 @@ __global__ __launch_bounds__(256) void k_wgrad_finish_many(FinishJobs fj) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   auto group = [&](const float* p, int g, int64_t n) {
     const int s0 = g * SPLIT_GROUP, cnt = J.nsplit - s0 < SPLIT_GROUP ? J.nsplit - s0 : SPLIT_GROUP;
-    return split_group_sum(p + int64_t(s0) * n, cnt, n);
+    return split_group_sum(p + int64_t(s0) * n, cnt, n, fj.four != 0);
   };
   if (lb < fj.wblocks[jb]) {
     // one packed element per thread, its group sums in order (the reduction
@@ -6127,6 +6140,7 @@ int sel_wgrad_finish_many(const sel_wgrad_job* jobs, int njobs, sel_stream_t str
   for (int j0 = 0; j0 < njobs; j0 += FM_MAXJ) {
     FinishJobs fj{};
     fj.njobs = std::min(FM_MAXJ, njobs - j0);
+    fj.four = tune(68) == 1;
     int64_t blocks = 0;
     for (int j = 0; j < fj.njobs; ++j) {
       const sel_wgrad_job& J = jobs[j0 + j];

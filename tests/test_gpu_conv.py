@@ -828,6 +828,16 @@ def test_deferred_wgrad_reduction_bit_identical(gpu, monkeypatch):
     acc = run(True, accumulate=True)
     for a_, b_ in zip(acc, ref):
         assert torch.equal(a_, b_ + 1.0)
+    # tune key 68 = 1: the batched finish sums partial split groups four loads
+    # at a time (the pre-round-6 order): the same sums to fp32 rounding
+    from sel import _lib as L
+    prev = L.lib().sel_tune(68, 1)
+    try:
+        four = run(True)
+    finally:
+        L.lib().sel_tune(68, prev)
+    for i, (a_, b_) in enumerate(zip(four, ref)):
+        assert torch.allclose(a_, b_, rtol=1e-5, atol=1e-6 * b_.abs().max().item()), i
 
 
 @pytest.mark.parametrize("per_element", [0, 1])
