@@ -5761,16 +5761,23 @@ int sel_conv_fwd(const sel_conv_desc* d, int in_dtype, int out_dtype, const void
 }
 
 /* Fused residual unit forward (residual_unit.py:43-46): h = conv1(ELU(x)) and
- * out = x + conv1x1(ELU(h)) in one pass (bf16, C = N in {32, 64}, K = 7, causal
+ * out = x + conv1x1(ELU(h)) in one pass (bf16, C = N in {32, 64}, or 128 where
+ * the (16, 128) k_conv_wss tile applies, K = 7, causal
  * zero pad, ELU prologue; d1 describes conv1, its bias_period 0 or N).  Returns
  * SEL_ERR_UNSUPPORTED for other shapes (callers then use two sel_conv_fwd calls). */
 int sel_resunit_fwd(const sel_conv_desc* d1, int dtype, const void* x, const void* w1pack, const float* b1,
                     const void* w2pack, const float* b2, void* h, void* out, sel_stream_t stream) {
   if (int rc = check_desc(d1)) return rc;
   const Args a = to_args(d1);
-  SEL_REQUIRE(dtype == SEL_BF16 && ru_fused_ok(a), SEL_ERR_UNSUPPORTED,
-              "sel_resunit_fwd: fused path needs bf16, C = N in {32, 64}, K = 7, causal zero pad, ELU prologue");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  // 128 channels (round 6): the (16, 128) k_conv_wss tile with the 1x1 in its
+  // epilogue, where conv1 alone runs on that tile (T = 2000, >= 65536 rows:
+  // the C3 RU128 units); tune key 69 = 1: off
+  if (dtype == SEL_BF16 && a.C == 128 && fwd4_choice(a, false) == 30 && wss_pw_ok(a))
+    return launch_wss_pw(a, x, w1pack, b1, w2pack, b2, h, out, s);
+  SEL_REQUIRE(dtype == SEL_BF16 && ru_fused_ok(a), SEL_ERR_UNSUPPORTED,
+              "sel_resunit_fwd: fused path needs bf16, C = N in {32, 64} (128 on the (16, 128) k_conv_wss tile), "
+              "K = 7, causal zero pad, ELU prologue");
   // tune key 56 = 1: 128-row tiles (4 resident workgroups per CU instead of 3):
   // 66-67 -> 58.6-59 us per unit in tools/ru_bench.py, which re-reads the same
   // input, but 69.5 -> 72.6 us inside the profiled C3 step, so off

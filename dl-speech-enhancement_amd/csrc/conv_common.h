@@ -109,6 +109,9 @@ bool wss_geometry(const Args& a, int& S, int& tm, int& BN);  // strips per tile,
 bool wss_geometry(const Args& a, int& S, int& tm);
 bool wss_ok(const Args& a);
 int wss_spt(const Args& a);  // samples per sample-tile (1, or 400 / T for short T)
+bool wss_pw_ok(const Args& a);  // the fused RU128 forward on k_conv_wss (PW epilogue)
+int launch_wss_pw(const Args& a, const void* x, const void* w1, const float* b1, const void* w2, const float* b2,
+                  void* h, void* out, hipStream_t s);
 bool wss_ok_out(const Args& a, bool out_f32);  // wss_ok and an instance for that output type
 template <typename TO>
 int launch_wss(const Args& a, const void* in, const void* wp, const float* bias, const void* aux, const void* res,

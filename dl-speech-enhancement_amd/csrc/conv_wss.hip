@@ -81,12 +81,34 @@ struct WssGeo {
 // (PMC: SQ_LDS_BANK_CONFLICT 44% of SQ_LDS_IDX_ACTIVE).
 __device__ __forceinline__ int wss_swz(int row) { return (row >> 1) & 2; }
 
-template <int KT, int S, int BN, typename TO, int SPT = 1>
+// RU (round 6, the 128-channel residual unit's forward, residual_unit.py:43-46,
+// on the (16, 128) tile): `out` receives h = conv_k7(ELU(x)) + b1, `out2` the
+// unit's output x + W2 ELU(h) + b2 (`res` = x).  LDS after the main loop:
+//   - W2 (128 x 128 bf16, 16-B slot p of row n at p ^ (n & 15)) and b1, DMA'd /
+//     written by the producers once the ring's slot 0 is free (after the
+//     second-to-last chunk), so they are in place when the consumers finish;
+//   - the consumers add b1 to their accumulators and write h as bf16 rows
+//     [256][136] (no fp32 tile); all waves store h row-contiguous and ELU it in
+//     place (each 16-B vector by its own thread);
+//   - wave w: rows 32w .. + 31 x 128 channels, 32x32x16 MFMAs in k_pw_bf16's
+//     operand and channel order; fp32 tile; + b2, + x (k_pw_bf16's epilogue).
+// Bit-identical to k_conv_wss + k_pw_bf16 (tests/test_gpu_conv.py).
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+constexpr int WSS_PWP = 128 + 8;           // bf16 pitch of the h rows (conflict-free b128 reads)
+constexpr int WSS_B1_OFF = 128 * 128 * 2;  // byte offsets: W2 at 0, b1, the h rows
+constexpr int WSS_HS_OFF = WSS_B1_OFF + 128 * 4;
+
+template <int KT, int S, int BN, typename TO, int SPT = 1, bool RU = false>
 __global__ __launch_bounds__(512) void k_conv_wss(Args a, const __bf16* __restrict__ in,
                                                   const __bf16* __restrict__ wp, const float* __restrict__ bias,
                                                   const TO* __restrict__ aux, const TO* __restrict__ res,
-                                                  TO* __restrict__ out, int ncol, int tm, int dbg) {
+                                                  TO* __restrict__ out, int ncol, int tm, int dbg,
+                                                  const __bf16* __restrict__ w2, const float* __restrict__ b2,
+                                                  TO* __restrict__ out2) {
   using G = WssGeo<KT, S, BN, SPT>;
+  static_assert(!RU || (BN == 128 && S == 16 && SPT == 1 && sizeof(TO) == 2), "RU: the (16, 128) bf16 tile");
+  static_assert(!RU || (WSS_HS_OFF + S * 16 * WSS_PWP * 2 <= G::SLOT + G::SLOT && G::SLOT >= WSS_B1_OFF + 512 &&
+                        G::EPI <= G::LDS), "RU LDS layout: W2 and b1 inside ring slot 0");
   constexpr int Q = G::Q, NCS = G::NCS, E = G::E, XR = G::XROWS, XI = G::XI, TI = G::TI, PW = G::PW;
   constexpr int EP = G::EP;
   static_assert(2 * PW < 64, "vmcnt range");
@@ -144,6 +166,8 @@ __global__ __launch_bounds__(512) void k_conv_wss(Args a, const __bf16* __restri
   if (wave >= 4) {
     // ---------------- producers ----------------
     const int pw = wave - 4;
+    // RU: b1 value of channel 64 pw + lane (pw < 2), staged with W2
+    const float b1v = RU && pw < 2 && bias && a.bias_period ? bias[pw * 64 + lane] : 0.f;
     const __bf16* src[PW];
 #pragma unroll
     for (int u = 0; u < PW; ++u) {
@@ -238,7 +262,19 @@ __global__ __launch_bounds__(512) void k_conv_wss(Args a, const __bf16* __restri
       __builtin_amdgcn_s_barrier();
       // slot ch % 2 is free now
       if (ch + 2 < nchunk) issue(ch + 2);
+      if constexpr (RU) {
+        if (ch + 2 == nchunk) {  // slot 0 (nchunk even): W2 and b1 for the epilogue
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const int j = u * 4 + pw, n = 4 * j + (lane >> 4), sl = (lane & 15) ^ (n & 15);
+            __builtin_amdgcn_global_load_lds((const void*)(w2 + n * 128 + sl * 8), (lds_ptr_t)(smem + j * 1024), 16,
+                                             0, 0);
+          }
+          if (pw < 2) reinterpret_cast<float*>(smem + WSS_B1_OFF)[pw * 64 + lane] = b1v;
+        }
+      }
     }
+    if constexpr (RU) ws_wait_vm<0>();  // W2 has landed before the epilogue's first barrier
   } else {
     // ---------------- consumers ----------------
     const int w = wave;
@@ -347,17 +383,36 @@ __global__ __launch_bounds__(512) void k_conv_wss(Args a, const __bf16* __restri
     __builtin_amdgcn_s_setprio(0);
     if (dbg & 16) st[2] = __builtin_amdgcn_s_memtime();
     prefetch_epi();
-    // accumulators -> fp32 [S*16][BN + 4] tile over the drained ring: lane ->
-    // time row 16 s + l16, channels 16 c + 4 kq .. + 3
-    float* const tile = reinterpret_cast<float*>(smem);
+    if constexpr (RU) {
+      // h = acc + b1 (the fp32 epilogue's add) -> bf16 rows: lane -> time row
+      // 16 s + l16, channels 16 c + 4 kq .. + 3 (E = 0 at S = 16)
+      __bf16* const hs = reinterpret_cast<__bf16*>(smem + WSS_HS_OFF);
+      const float* const b1s = reinterpret_cast<const float*>(smem + WSS_B1_OFF);
+      const bool hb = bias && a.bias_period;
 #pragma unroll
-    for (int i = 0; i < Q; ++i)
+      for (int c = 0; c < NCS; ++c) {
+        const floatx4 bb = *reinterpret_cast<const floatx4*>(b1s + c * 16 + 4 * kq);
 #pragma unroll
-      for (int c = 0; c < NCS; ++c)
-        *reinterpret_cast<floatx4*>(tile + ((w * Q + i) * 16 + l16) * EP + c * 16 + 4 * kq) = acc[i][c];
+        for (int i = 0; i < Q; ++i) {
+          bf16x4 hv;
 #pragma unroll
-    for (int i = 0; i < E; ++i)
-      *reinterpret_cast<floatx4*>(tile + (xstrip[i] * 16 + l16) * EP + xcol[i] * 16 + 4 * kq) = accx[i];
+          for (int e = 0; e < 4; ++e) hv[e] = __bf16(hb ? acc[i][c][e] + bb[e] : acc[i][c][e]);
+          *reinterpret_cast<bf16x4*>(hs + ((w * Q + i) * 16 + l16) * WSS_PWP + c * 16 + 4 * kq) = hv;
+        }
+      }
+    } else {
+      // accumulators -> fp32 [S*16][BN + 4] tile over the drained ring: lane ->
+      // time row 16 s + l16, channels 16 c + 4 kq .. + 3
+      float* const tile = reinterpret_cast<float*>(smem);
+#pragma unroll
+      for (int i = 0; i < Q; ++i)
+#pragma unroll
+        for (int c = 0; c < NCS; ++c)
+          *reinterpret_cast<floatx4*>(tile + ((w * Q + i) * 16 + l16) * EP + c * 16 + 4 * kq) = acc[i][c];
+#pragma unroll
+      for (int i = 0; i < E; ++i)
+        *reinterpret_cast<floatx4*>(tile + (xstrip[i] * 16 + l16) * EP + xcol[i] * 16 + 4 * kq) = accx[i];
+    }
   }
   // (a raw barrier: __syncthreads() would also wait for the prefetched rows)
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -368,6 +423,72 @@ __global__ __launch_bounds__(512) void k_conv_wss(Args a, const __bf16* __restri
   // 16-B accesses (aux / res fetched for every vector first); k_conv_ws_bf16's
   // term order
   const float* const tile = reinterpret_cast<const float*>(smem);
+  if constexpr (RU) {
+    __bf16* const hs = reinterpret_cast<__bf16*>(smem + WSS_HS_OFF);
+    const __bf16* const ws = reinterpret_cast<const __bf16*>(smem);
+    // h rows -> `out` (16-B row-contiguous), then ELU(h) in place for the 1x1
+#pragma unroll
+    for (int u = 0; u < EV; ++u) {
+      const int v = tid + u * NT;
+      if (v >= nvec) break;
+      uint4* const p = reinterpret_cast<uint4*>(hs + (v / VPR) * WSS_PWP + (v % VPR) * 8);
+      const uint4 hv = *p;
+      *reinterpret_cast<uint4*>(out + (m0 + v / VPR) * a.N + (v % VPR) * 8) = hv;
+      *p = elu8(hv);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    // wave w: rows 32w .. 32w + 31 x all 128 output channels (4 32x32 blocks);
+    // k_pw_bf16's fragments: weights first, channel groups g = 0 .. 7 in order
+    const __bf16* const xb = hs + (wave * 32 + (lane & 31)) * WSS_PWP + 8 * (lane >> 5);
+    bf16x8 xf[8];
+#pragma unroll
+    for (int g = 0; g < 8; ++g) xf[g] = *reinterpret_cast<const bf16x8*>(xb + 16 * g);
+    floatx16 acc2[4];
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+      const int n = cb * 32 + (lane & 31);
+      bf16x8 wf[8];
+#pragma unroll
+      for (int g = 0; g < 8; ++g)
+        wf[g] = *reinterpret_cast<const bf16x8*>(ws + n * 128 + (((2 * g + (lane >> 5)) ^ (n & 15)) * 8));
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc2[cb][e] = 0.f;
+#pragma unroll
+      for (int g = 0; g < 8; ++g) acc2[cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[g], xf[g], acc2[cb], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave's LDS reads are done: the fp32 tile goes over them
+    float* const ot = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        *reinterpret_cast<floatx4*>(ot + (wave * 32 + (lane & 31)) * EP + cb * 32 + 8 * q + 4 * (lane >> 5)) =
+            floatx4{acc2[cb][4 * q], acc2[cb][4 * q + 1], acc2[cb][4 * q + 2], acc2[cb][4 * q + 3]};
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    // k_pw_bf16's epilogue: + b2, then + x (__fadd_rn), bf16
+#pragma unroll
+    for (int u = 0; u < EV; ++u) {
+      const int v = tid + u * NT;
+      if (v >= nvec) break;
+      const int row = v / VPR, c8 = (v % VPR) * 8;
+      const floatx4 lo = *reinterpret_cast<const floatx4*>(ot + row * EP + c8);
+      const floatx4 hi = *reinterpret_cast<const floatx4*>(ot + row * EP + c8 + 4);
+      float x[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      if (b2) {
+        const floatx4 c0 = *reinterpret_cast<const floatx4*>(b2 + c8), c1 = *reinterpret_cast<const floatx4*>(b2 + c8 + 4);
+        x[0] += c0[0], x[1] += c0[1], x[2] += c0[2], x[3] += c0[3];
+        x[4] += c1[0], x[5] += c1[1], x[6] += c1[2], x[7] += c1[3];
+      }
+      V8 ov;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ov.v[e] = from_f<TO>(__fadd_rn(x[e], to_f(rv[u].v[e])));
+      *reinterpret_cast<V8*>(out2 + (m0 + row) * a.N + c8) = ov;
+    }
+    return;
+  }
 #pragma unroll
   for (int u = 0; u < EV; ++u) {
     const int v = tid + u * NT;
@@ -487,7 +608,7 @@ static int launch_wss_t(const Args& a, int tm, const void* in, const void* wp, c
   SEL_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, int(G::LDS)));
   hipLaunchKernelGGL(kern, dim3(unsigned(tiles * ncol)), dim3(512), G::LDS, s, a, static_cast<const __bf16*>(in),
                      static_cast<const __bf16*>(wp), bias, static_cast<const TO*>(aux), static_cast<const TO*>(res),
-                     static_cast<TO*>(out), ncol, tm, tune(48));
+                     static_cast<TO*>(out), ncol, tm, tune(48), nullptr, nullptr, nullptr);
   SEL_LAUNCH_CHECK();
   return SEL_OK;
 }
@@ -518,6 +639,35 @@ int launch_wss(const Args& a, const void* in, const void* wp, const float* bias,
   }
   set_error("k_conv_wss: fp32 output needs T <= 400");
   return SEL_ERR_UNSUPPORTED;
+}
+
+// the fused 128-channel residual-unit forward (RU epilogue): conv1 = `a` (C = N
+// = 128, K = 7, causal zero pad, ELU prologue) on the (16, 128) tile
+bool wss_pw_ok(const Args& a) {
+  int S, tm, BN;
+  return a.C == 128 && a.N == 128 && a.K == 7 && a.in_elu == 1 && a.pad == 6 * a.dil &&
+         a.pad_mode == SEL_PAD_ZERO && (a.bias_period == 0 || a.bias_period == a.N) && tune(69) != 1 &&
+         wss_ok(a) && wss_geometry(a, S, tm, BN) && S == 16 && BN == 128;
+}
+
+int launch_wss_pw(const Args& a, const void* x, const void* w1, const float* b1, const void* w2, const float* b2,
+                  void* h, void* out, hipStream_t s) {
+  SEL_REQUIRE(wss_pw_ok(a), SEL_ERR_UNSUPPORTED, "k_conv_wss RU: unsupported shape T=%d C=%d dil=%d", a.T, a.C,
+              a.dil);
+  int S, tm, BN;
+  wss_geometry(a, S, tm, BN);
+  using G = WssGeo<7, 16, 128>;
+  const int64_t tiles = (a.rows / a.T) * ((a.T + tm - 1) / tm);
+  if (tiles == 0) return SEL_OK;
+  SEL_REQUIRE(tiles < (int64_t(1) << 31), SEL_ERR_UNSUPPORTED, "k_conv_wss: grid too large");
+  auto kern = k_conv_wss<7, 16, 128, __bf16, 1, true>;
+  SEL_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, int(G::LDS)));
+  hipLaunchKernelGGL(kern, dim3(unsigned(tiles)), dim3(512), G::LDS, s, a, static_cast<const __bf16*>(x),
+                     static_cast<const __bf16*>(w1), b1, static_cast<const __bf16*>(nullptr),
+                     static_cast<const __bf16*>(x), static_cast<__bf16*>(h), 1, tm, tune(48) & ~16,
+                     static_cast<const __bf16*>(w2), b2, static_cast<__bf16*>(out));
+  SEL_LAUNCH_CHECK();
+  return SEL_OK;
 }
 
 bool wss_ok_out(const Args& a, bool out_f32) {

@@ -684,6 +684,21 @@ def ru_fused_ok(d1, dtype):
     return RU_FUSED != "0" and _ru_shape_ok(d1, dtype) and (RU_FUSED != "32" or d1.C == 32)
 
 
+WSS_PW_KID = 94 * 10 ** 7 + 128 * 10 ** 4 + 16 * 10 + 7   # k_conv_wss<7, 16, 128> (fwd_kernel_name)
+
+
+def ru128_fused_ok(d1, dtype):
+    """The 128-channel unit's forward as one k_conv_wss launch with the 1x1 in
+    its epilogue (conv_wss.hip PW, conv.hip sel_resunit_fwd): where conv1 itself
+    runs on the (16, 128) tile; tune key 69 = 1 turns it off."""
+    if not (RU_FUSED != "0" and dtype == torch.bfloat16 and d1.C == d1.N == 128 and d1.K == 7
+            and d1.pad == 6 * d1.dil and d1.pad_mode == PAD_ZERO and d1.in_elu == 1
+            and d1.bias_period in (0, d1.N) and _tune_value(69) != 1):
+        return False
+    kid = L.lib().sel_conv_fwd_kernel_id(ctypes.byref(d1), _code(dtype), _code(dtype), 0)
+    return kid == WSS_PW_KID
+
+
 def ru_bwd_fused_ok(d1, dtype):
     """Fused residual-unit backward (k_ru32_bwd / k_ru64_bwd)?"""
     # SEL_RU_FUSED=32: the 32-channel unit only (A/B of the 64-channel kernels)
@@ -786,6 +801,8 @@ def _ru_meta(d1, xf, wp1, wp2):
     nbytes = 3 * d1.rows * d1.C * es + (wp1.numel() + wp2.numel()) * es
     flops = 2.0 * d1.rows * d1.N * d1.C * (d1.K + 1)
     # (the 32-channel unit's tile rows: 256, or 128 under tune key 56 = 1)
+    if d1.C == 128:   # k_conv_wss PW: x is read twice (the DMA ring and the residual)
+        return "k_conv_wss<7, 16, 128, bf16, PW>", nbytes + d1.rows * d1.C * es, flops
     tag = f"k_ru32_fwd<{128 if _tune_value(56) == 1 else 256}>" if d1.C == 32 else "k_ru64_fwd<128>"
     return tag, nbytes, flops
 
@@ -809,7 +826,7 @@ class ResidualUnitFn(torch.autograd.Function):
         bb1 = b1.detach().float().contiguous() if b1 is not None else None
         bb2 = b2.detach().float().contiguous() if b2 is not None else None
         xf = x.view(B * T, C)
-        if ru_fused_ok(d1, x.dtype):
+        if ru_fused_ok(d1, x.dtype) or ru128_fused_ok(d1, x.dtype):
             h, out = resunit_fwd(d1, xf, wp1, bb1, wp2, bb2)
         else:
             h = prim(d1, xf, wp1, bias=bb1)

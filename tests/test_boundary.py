@@ -42,7 +42,7 @@ def test_library_reports_errors_without_gpu():
 
 
 def test_tune_keys_cover_every_knob():
-    """Every knob the kernels read (keys up to 67 in round 6) is settable and
+    """Every knob the kernels read (keys up to 69 in round 6) is settable and
     reads back; a key out of range is refused and changes nothing (keys >= 64
     were silently ignored before round 6, so A/B runs on them compared a
     setting with itself)."""

@@ -539,7 +539,12 @@ def test_thin_kernel_multi_tile_loops(gpu, shape, epi):
 # AudioDec dilations, ragged tails (T not a multiple of the tile rows) and T < halo
 RU_SHAPES = [(32, 1, 0, 2, 1000), (32, 3, 0, 3, 777), (32, 9, 1, 2, 1000), (32, 9, 0, 2, 40),
              (64, 1, 0, 2, 500), (64, 3, 1, 3, 333), (64, 9, 0, 2, 260), (64, 9, 1, 2, 40),
-             (64, 9, 1, 8, 8000)]
+             (64, 9, 1, 8, 8000),
+             # 128 channels: k_conv_wss<7, 16, 128> with the 1x1 in its epilogue (round 6,
+             # where conv1 runs on that tile: >= 65536 rows): 250-row tiles, a ragged
+             # last tile (T = 1990: 249 + 247), one-tile samples, and the C3 size
+             (128, 1, 1, 33, 2000), (128, 3, 0, 34, 1990), (128, 9, 1, 132, 500), (128, 9, 0, 256, 256),
+             (128, 3, 1, 64, 2000)]
 
 
 @pytest.mark.parametrize("shape", RU_SHAPES, ids=lambda s: "C{}d{}b{}B{}T{}".format(*s))
@@ -560,11 +565,20 @@ def test_fused_residual_unit_matches_two_calls(gpu, shape, monkeypatch):
     d2 = CO.ConvDesc(B * T, T, C, C, 1, 1, 0, CO.PAD_ZERO, 1, C if bias else 0)
     wp1 = CO.pack(CO.PACK_FWD, w1, 1, torch.bfloat16)
     wp2 = CO.pack(CO.PACK_FWD, w2, 1, torch.bfloat16)
-    assert CO.ru_fused_ok(d1, torch.bfloat16)
+    if C == 128:
+        assert CO.ru128_fused_ok(d1, torch.bfloat16)
+        from sel import _lib as Lb
+        p69 = Lb.lib().sel_tune(69, 1)   # off: the two-launch path
+        try:
+            assert not CO.ru128_fused_ok(d1, torch.bfloat16)
+        finally:
+            Lb.lib().sel_tune(69, p69)
+    else:
+        assert CO.ru_fused_ok(d1, torch.bfloat16)
     h, out = CO.resunit_fwd(d1, x, wp1, b1, wp2, b2)
     h_ref = CO.prim(d1, x, wp1, bias=b1)
     out_ref = CO.prim(d2, h_ref, wp2, bias=b2, res=x)
-    # k_ru32_fwd / k_ru64_fwd: same MFMA order and rounding points as the two calls
+    # k_ru32_fwd / k_ru64_fwd / k_conv_wss RU: same MFMA order and rounding points as the two calls
     assert torch.equal(h, h_ref), (h.float() - h_ref.float()).abs().max().item()
     assert torch.equal(out, out_ref), (out.float() - out_ref.float()).abs().max().item()
     if C == 64:
@@ -756,13 +770,14 @@ def _ulp_close(a, b, frac=1e-3):
     assert float((d > 0).float().mean()) <= frac, float((d > 0).float().mean())
 
 
-@pytest.mark.parametrize("C", [32, 64])
+@pytest.mark.parametrize("C", [32, 64, 128])
 def test_resunit32_autograd_fused_vs_unfused(gpu, monkeypatch, C):
-    """ResidualUnitFn at 32 / 64 channels: forward and all five gradients with
-    the fused launches (default) equal the unfused primitive path (SEL_RU_FUSED=0)."""
+    """ResidualUnitFn at 32 / 64 / 128 channels: forward and all five gradients
+    with the fused launches (default; at 128 the forward only, k_conv_wss RU)
+    equal the unfused primitive path (SEL_RU_FUSED=0)."""
     from sel import convops as CO
     torch.manual_seed(5)
-    B, T, dil = 2, 3000, 3
+    B, T, dil = (2, 3000, 3) if C < 128 else (24, 3000, 3)   # 128: >= 65536 rows (the fused tile's range)
     x0 = (0.5 * torch.randn(B, T, C, device=gpu)).to(torch.bfloat16)
     w1 = (0.1 * torch.randn(C, C, 7, device=gpu)).requires_grad_(True)
     b1 = torch.randn(C, device=gpu).requires_grad_(True)
