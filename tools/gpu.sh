@@ -28,7 +28,7 @@ case $CMD in
     cd /tmp && export TMPDIR=/tmp
     timeout -k 10 ${GPU_TIMEOUT:-400} rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/${TAG}_prof -o run -- \
       python $R/bench.py --no-cpu-baseline --no-fp32-companion "$@" > $OUT/${TAG}_prof.log 2>&1 || { echo "prof failed"; tail -5 $OUT/${TAG}_prof.log; exit 1; }
-    python $R/tools/prof_summary.py $OUT/${TAG}_prof ${STEPS_PROF:-7} > $OUT/${TAG}_kernel_stats.md
+    python $R/tools/prof_summary.py $OUT/${TAG}_prof ${STEPS_PROF:-auto} > $OUT/${TAG}_kernel_stats.md
     tail -1 $OUT/${TAG}_prof.log | cut -c1-600
     head -25 $OUT/${TAG}_kernel_stats.md | cut -c1-220 ;;
   pmc)
