@@ -40,7 +40,7 @@ case $CMD in
     done
     F=$(find $OUT/${TAG}_FETCH_SIZE -name "*counter_collection.csv" | head -1)
     W=$(find $OUT/${TAG}_WRITE_SIZE -name "*counter_collection.csv" | head -1)
-    python $R/tools/pmc_traffic.py "$F" "$W" $OUT/${TAG}_traffic.json ${STEPS_PMC:-4} > $OUT/${TAG}_traffic.md
+    python $R/tools/pmc_traffic.py "$F" "$W" $OUT/${TAG}_traffic.json ${STEPS_PMC:-auto} > $OUT/${TAG}_traffic.md
     rm -f "$F" "$W"
     head -16 $OUT/${TAG}_traffic.md ;;
   smoke)

@@ -6,7 +6,7 @@ bytes of 16-B-per-lane streaming reads on gfx950 -> x2; WRITE_SIZE (KB) is exact
 for 16-B stores.  Both count Infinity-Cache hits, so sizes must exceed 256 MB
 of live data to read them as HBM bytes (C3 per-layer tensors are 100-300 MB).
 
-usage: python tools/pmc_traffic.py <fetch_counter_collection.csv> <write_counter_collection.csv> <out.json> [steps]
+usage: python tools/pmc_traffic.py <fetch_counter_collection.csv> <write_counter_collection.csv> <out.json> [steps | auto]
 (steps: training steps in the profiled run -> a per-step total over the sel kernels,
  leaving out the bench's B = 512 STFT roofline probe)
 """
@@ -44,7 +44,9 @@ def main():
     with open(sys.argv[3], "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
     if len(sys.argv) > 4:
-        steps = int(sys.argv[4])
+        # auto: one sel Adam update per step (k_adam_many launches)
+        steps = (sum(v["launches"] for k, v in out.items() if "k_adam_many" in k) or 1) if sys.argv[4] == "auto" \
+            else int(sys.argv[4])
         tot = sum(v["traffic_bytes_per_launch"] * v["launches"] for k, v in out.items()
                   if ("sel::" in k or "_ZN3sel" in k) and "k_stft_mag_fwd" not in k)
         print(f"sel kernels, all launches except the STFT probe: {tot / 1e9:.2f} GB over {steps} steps = "
