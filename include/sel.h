@@ -194,7 +194,9 @@ int sel_conv_fwd(const sel_conv_desc* d, int in_dtype, int out_dtype, const void
 /* Fused residual unit forward (replaces the two sel_conv_fwd calls of
  * models/autoencoder/modules/residual_unit.py:43-46, conv_layer.py:19-23 + :139-142):
  * h = conv1(ELU(x)) [saved for the backward] and out = x + conv1x1(ELU(h)), bf16,
- * C = N in {32, 64}, K = 7, causal zero pad; d1 describes conv1 (in_elu = 1).
+ * C = N in {32, 64} -- or 128 where conv1 alone runs on the (16, 128)
+ * k_conv_wss tile (T = 2000-like sequences, >= 65536 rows; sel_tune key 69 = 1
+ * turns that off) -- K = 7, causal zero pad; d1 describes conv1 (in_elu = 1).
  * Returns SEL_ERR_UNSUPPORTED for any other shape. */
 int sel_resunit_fwd(const sel_conv_desc* d1, int dtype, const void* x, const void* w1pack, const float* b1,
                     const void* w2pack, const float* b2, void* h, void* out, sel_stream_t stream);
