@@ -376,9 +376,11 @@ struct MfmaGeo {
 
 // one thread per (stage, tile, j4, lane): four B operands, zero-padded past D and K
 __global__ __launch_bounds__(256) void k_rvq_prep(const float* __restrict__ embeds, int S, int D, int K,
-                                                  float* __restrict__ ep, float* __restrict__ en) {
+                                                  float* __restrict__ ep, float* __restrict__ en,
+                                                  int32_t* __restrict__ counts) {
   const MfmaGeo g(D, K);
   const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < int64_t(S) * K) counts[i] = 0;  // the code histogram (k_rvq_hist adds into it; no memset launch)
   const int64_t total = int64_t(S) * g.stage_floats() / 4;
   if (i < total) {
     const int lane = int(i & 63);
@@ -621,10 +623,22 @@ __global__ __launch_bounds__(TM) __attribute__((amdgpu_waves_per_eu(RG == 1 ? 4 
 // code histogram of one stage's indices: LDS bins, then one global add per bin
 constexpr int kHistRows = 4096;
 constexpr int kHistMaxK = 8192;
+// (round 6) the first block of each stage also sums the stage's per-block SSE
+// partials into sqerr[s] -- k_rvq_sqerr's loop over the first 256 threads and
+// the same block_sum (the other waves add exact zeros): one launch less
 __global__ __launch_bounds__(512) void k_rvq_hist(const int64_t* __restrict__ idx, int64_t N, int K,
-                                                  int32_t* __restrict__ counts) {
+                                                  int32_t* __restrict__ counts, const double* __restrict__ partials,
+                                                  int nb, double* __restrict__ sqerr) {
   __shared__ int32_t bins[kHistMaxK];
+  __shared__ double red[16];
   const int s = blockIdx.y;
+  if (blockIdx.x == 0) {  // block-uniform
+    double v = 0.0;
+    if (threadIdx.x < 256)
+      for (int i = threadIdx.x; i < nb; i += 256) v += partials[int64_t(s) * nb + i];
+    v = block_sum<double>(v, red);
+    if (threadIdx.x == 0) sqerr[s] = v;
+  }
   for (int k = threadIdx.x; k < K; k += blockDim.x) bins[k] = 0;
   __syncthreads();
   const int64_t a = int64_t(blockIdx.x) * kHistRows, b = std::min<int64_t>(N, a + kHistRows);
@@ -711,10 +725,11 @@ int sel_rvq_fwd(const float* x, int64_t N, int D, const float* embeds, int S, in
               "bad rvq shape N=%lld D=%d S=%d K=%d", (long long)N, D, S, K);
   SEL_REQUIRE(ws_bytes >= sel_rvq_workspace(N, S, K), SEL_ERR_WORKSPACE, "workspace too small");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  SEL_HIP(hipMemsetAsync(counts, 0, size_t(S) * K * sizeof(int32_t), s));
   // tune key 2: 0 = matrix-core kernel where it applies, 1 = direct, 2 = staged
   const int variant = tune(2);
   const bool mfma = D % 4 == 0 && D <= DM && K <= kHistMaxK && S <= SM && variant == 0;
+  // (the matrix-core path zeroes the histogram in k_rvq_prep)
+  if (!mfma || N == 0) SEL_HIP(hipMemsetAsync(counts, 0, size_t(S) * K * sizeof(int32_t), s));
   const bool staged = !mfma && D % DC == 0 && K % 4 == 0 && variant != 1;
   // matrix-core rows per block: one 16-row group (tune key 39 = 2: two groups
   // sharing each codebook tile, measured slower at C3: 169 -> 193 us per RVQ
@@ -727,7 +742,8 @@ int sel_rvq_fwd(const float* x, int64_t N, int D, const float* embeds, int S, in
     float* en = reinterpret_cast<float*>(static_cast<char*>(ws) + en_offset(N, S));
     float* ep = reinterpret_cast<float*>(static_cast<char*>(ws) + ep_offset(N, S, K));
     const int64_t nprep = std::max<int64_t>(int64_t(S) * MfmaGeo(D, K).stage_floats() / 4, int64_t(S) * K);
-    hipLaunchKernelGGL(k_rvq_prep, dim3(unsigned((nprep + 255) / 256)), dim3(256), 0, s, embeds, S, D, K, ep, en);
+    hipLaunchKernelGGL(k_rvq_prep, dim3(unsigned((nprep + 255) / 256)), dim3(256), 0, s, embeds, S, D, K, ep, en,
+                       counts);
     SEL_LAUNCH_CHECK();
     const size_t lds = size_t(K) * sizeof(float);  // |e|^2 of one stage
     if (rows == 2 * RM) {
@@ -739,8 +755,9 @@ int sel_rvq_fwd(const float* x, int64_t N, int D, const float* embeds, int S, in
     }
     SEL_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_rvq_hist, dim3(unsigned((N + kHistRows - 1) / kHistRows), unsigned(S)), dim3(512), 0, s,
-                       idx, N, K, counts);
+                       idx, N, K, counts, part, nb, sqerr);
     SEL_LAUNCH_CHECK();
+    return SEL_OK;  // (sqerr summed by k_rvq_hist)
   } else if (nb > 0 && staged) {
     const size_t lds = (size_t(2) * MAXD * R2 + size_t(2) * DC * KP) * sizeof(float);
     SEL_HIP(hipFuncSetAttribute((const void*)k_rvq_fwd2, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));

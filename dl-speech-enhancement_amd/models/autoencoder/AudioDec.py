@@ -31,6 +31,10 @@ class Generator(torch.nn.Module):
                                    stride=1, bias=False, mode=mode, model=projector)
         self.quantizer = Quantizer(code_dim=code_dim, codebook_num=codebook_num, codebook_size=codebook_size,
                                    model=quantier)
+        # the quantizer works in fp32 (ResidualVQFn): the projector's conv writes
+        # z as fp32 from its epilogue instead of bf16 + a cast launch each way
+        if hasattr(self.projector.project, "out_float"):
+            self.projector.project.out_float = True
 
     def _flatten_channels(self, x):
         B, C, T = x.size()

@@ -34,12 +34,15 @@ from trainer.trainerGAN import LossTotals
 
 class _CapturedTotals(LossTotals):
     """LossTotals stand-in while capturing: every recorded vector is added
-    into consecutive slots of a pre-allocated device accumulator."""
+    into consecutive slots of a pre-allocated device accumulator -- all of a
+    step's records in one multi-tensor add at the end of the step (one graph
+    node instead of one per record)."""
 
     def __init__(self, acc):
         super().__init__()
         self.acc = acc
         self.names = []
+        self.pending = []
 
     def add(self, name, value):
         if not torch.is_tensor(value):
@@ -50,8 +53,13 @@ class _CapturedTotals(LossTotals):
         n = len(names)
         if len(self.names) + n > self.acc.numel():
             raise RuntimeError("graph capture: more loss records than accumulator slots")
-        self.acc.narrow(0, len(self.names), n).add_(value.detach().reshape(-1).float())
+        self.pending.append((self.acc.narrow(0, len(self.names), n), value.detach().reshape(-1).float()))
         self.names.extend(names)
+
+    def flush(self):
+        if self.pending:
+            torch._foreach_add_([d for d, _ in self.pending], [v for _, v in self.pending])
+            self.pending = []
 
 
 class GraphedTrainStep:
@@ -89,6 +97,7 @@ class GraphedTrainStep:
                 s.step = lambda *a, **k: None   # host state: stepped after each replay
             with torch.cuda.graph(self.graph):
                 tr._train_step(batch)
+                rec.flush()
         finally:
             for s in scheds:
                 del s.step

@@ -238,22 +238,28 @@ class TrainerGAN(abc.ABC):
 
     def _metric_loss(self, predict_y, natural_y, mode="train"):
         """trainerGAN.py:214-241 — mel / multi-resolution STFT / shape losses per use_* flags."""
+        # (the running sum starts at the first term: `0.0 + loss` would be one
+        # more device kernel per step for an exact no-op)
         metric_loss = 0.0
+
+        def acc(total, term):
+            return term if isinstance(total, float) and total == 0.0 else total + term
+
         if self.config.get("use_mel_loss", False):
             mel_loss = self.criterion["mel"](predict_y, natural_y) * self.config["lambda_mel_loss"]
             self._record_loss("mel_loss", mel_loss, mode=mode)
-            metric_loss = metric_loss + mel_loss
+            metric_loss = acc(metric_loss, mel_loss)
         if self.config.get("use_stft_loss", False):
             sc_loss, mag_loss = self.criterion["stft"](predict_y, natural_y)
             sc_loss = sc_loss * self.config["lambda_stft_loss"]
             mag_loss = mag_loss * self.config["lambda_stft_loss"]
             self._record_loss("spectral_convergence_loss", sc_loss, mode=mode)
             self._record_loss("log_stft_magnitude_loss", mag_loss, mode=mode)
-            metric_loss = metric_loss + (sc_loss + mag_loss)
+            metric_loss = acc(metric_loss, sc_loss + mag_loss)
         if self.config.get("use_shape_loss", False):
             shape_loss = self.criterion["shape"](predict_y, natural_y) * self.config["lambda_shape_loss"]
             self._record_loss("shape_loss", shape_loss, mode=mode)
-            metric_loss = metric_loss + shape_loss
+            metric_loss = acc(metric_loss, shape_loss)
         return metric_loss
 
     def _adv_loss(self, predict_p, natural_p=None, mode="train"):
