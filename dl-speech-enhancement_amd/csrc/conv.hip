@@ -4563,8 +4563,14 @@ __device__ __forceinline__ void pack_geom(const sel_pack_job& J, unsigned& N, un
   else if (J.kind == SEL_PACK_FWD_STRIDED) N = cout, KP = 3, CP = s * cin;
   else N = s * cout, KP = 2, CP = cin;
 }
-template <typename TO>
-__global__ __launch_bounds__(256) void k_pack_tiles(PackTiles pt) {
+// PT_THREADS 1024 for launches of fewer than 512 tiles (the small jobs: 32-64
+// tiles, one workgroup each; at 256 threads one wave per SIMD ran the loads
+// and their index arithmetic back to back, 17-18 us per launch), 256 for the
+// large ones.  Thread work is a (n, cp) pair of the tile with all its KP taps,
+// so no index needs a division by the job's tap count; the KP loads of a pair
+// are all issued before its LDS stores.
+template <typename TO, unsigned PT_THREADS>
+__global__ __launch_bounds__(PT_THREADS) void k_pack_tiles(PackTiles pt) {
   __shared__ float tile[PT_T * PT_KMAX * PT_P];
   int a = 0, b = pt.n - 1;
   const int t = int(blockIdx.x);
@@ -4580,40 +4586,55 @@ __global__ __launch_bounds__(256) void k_pack_tiles(PackTiles pt) {
   const unsigned ntc = (CP + PT_T - 1) / PT_T;
   const unsigned lt = unsigned(t - pt.tstart[a]);
   const unsigned n0 = (lt / ntc) * PT_T, c0 = (lt % ntc) * PT_T;
-  const unsigned tot = PT_T * PT_T * KP;
-  // gather: e = (nl * 32 + cl) * KP + kp (kp fastest: contiguous in the FWD source)
-  for (unsigned e = threadIdx.x; e < tot; e += 256) {
-    const unsigned kp = e % KP, r = e / KP, cl = r % PT_T, nl = r / PT_T;
+  // gather: pair (nl, cl), cl fastest; its KP taps are contiguous in the FWD
+  // source; out-of-range taps load w[0] and are replaced by zeros
+  for (unsigned r = threadIdx.x; r < PT_T * PT_T; r += PT_THREADS) {
+    const unsigned cl = r % PT_T, nl = r / PT_T;
     const unsigned n = n0 + nl, cp = c0 + cl;
-    float v = 0.f;
-    if (n < N && cp < CP) {
-      if (J.kind == SEL_PACK_FWD) {
-        v = J.w[(n * cin + cp) * K + kp];
-      } else if (J.kind == SEL_PACK_FWD_STRIDED) {
-        const unsigned ph = cp / cin, ci = cp - ph * cin;
-        const int k = strided_k(int(kp), int(ph), int(s));
-        v = k >= 0 ? J.w[(n * cin + ci) * (2 * s) + unsigned(k)] : 0.f;
-      } else {
-        const unsigned ph = n / cout, co = n - ph * cout;
-        const unsigned k = kp == 0 ? ph + s : ph;
-        v = J.w[(cp * cout + co) * (2 * s) + k];
-      }
+    const bool in = n < N && cp < CP;
+    unsigned base = 0, ph = 0;
+    if (J.kind == SEL_PACK_FWD) {
+      base = (n * cin + cp) * K;
+    } else if (J.kind == SEL_PACK_FWD_STRIDED) {
+      ph = cp / cin;
+      base = (n * cin + (cp - ph * cin)) * (2 * s);
+    } else {
+      ph = n / cout;
+      base = (cp * cout + (n - ph * cout)) * (2 * s);
     }
-    tile[(nl * KP + kp) * PT_P + cl] = v;
+    float v[PT_KMAX];
+    bool ok[PT_KMAX];
+#pragma unroll
+    for (unsigned kp = 0; kp < PT_KMAX; ++kp) {
+      if (kp >= KP) break;  // block-uniform
+      int k = int(kp);
+      if (J.kind == SEL_PACK_FWD_STRIDED) k = strided_k(int(kp), int(ph), int(s));
+      else if (J.kind == SEL_PACK_CONVT) k = int(kp == 0 ? ph + s : ph);
+      ok[kp] = in && k >= 0;
+      v[kp] = J.w[ok[kp] ? base + unsigned(k) : 0];
+    }
+#pragma unroll
+    for (unsigned kp = 0; kp < PT_KMAX; ++kp) {
+      if (kp >= KP) break;
+      tile[(nl * KP + kp) * PT_P + cl] = ok[kp] ? v[kp] : 0.f;
+    }
   }
   __syncthreads();
   TO* const wp = static_cast<TO*>(J.wpack);
-  for (unsigned e = threadIdx.x; e < tot; e += 256) {  // Wp[n][kp][cp]: cp fastest
-    const unsigned cl = e % PT_T, r = e / PT_T, kp = r % KP, nl = r / KP;
+  for (unsigned r = threadIdx.x; r < PT_T * PT_T; r += PT_THREADS) {  // Wp[n][kp][cp]: cp fastest
+    const unsigned cl = r % PT_T, nl = r / PT_T;
     const unsigned n = n0 + nl, cp = c0 + cl;
-    if (n < N && cp < CP) wp[(n * KP + kp) * CP + cp] = from_f<TO>(tile[(nl * KP + kp) * PT_P + cl]);
+    if (n < N && cp < CP)
+      for (unsigned kp = 0; kp < KP; ++kp) wp[(n * KP + kp) * CP + cp] = from_f<TO>(tile[(nl * KP + kp) * PT_P + cl]);
   }
   if (J.wdgrad) {
     TO* const wd = static_cast<TO*>(J.wdgrad);
-    for (unsigned e = threadIdx.x; e < tot; e += 256) {  // Wd[cp][j][n]: n fastest
-      const unsigned nl = e % PT_T, r = e / PT_T, j = r % KP, cl = r / KP;
+    for (unsigned r = threadIdx.x; r < PT_T * PT_T; r += PT_THREADS) {  // Wd[cp][j][n]: n fastest
+      const unsigned nl = r % PT_T, cl = r / PT_T;
       const unsigned n = n0 + nl, cp = c0 + cl;
-      if (n < N && cp < CP) wd[(cp * KP + j) * N + n] = from_f<TO>(tile[(nl * KP + (KP - 1 - j)) * PT_P + cl]);
+      if (n < N && cp < CP)
+        for (unsigned j = 0; j < KP; ++j)
+          wd[(cp * KP + j) * N + n] = from_f<TO>(tile[(nl * KP + (KP - 1 - j)) * PT_P + cl]);
     }
   }
 }
@@ -6237,9 +6258,11 @@ int sel_pack_many_host(const sel_pack_job* jobs, int njobs, int64_t total, int d
     pt.tstart[pt.n] = int(tiles);
     if (tiled && tiles > 0 && tiles < (int64_t(1) << 31)) {
       if (dtype == SEL_F32)
-        hipLaunchKernelGGL(k_pack_tiles<float>, dim3(unsigned(tiles)), dim3(256), 0, s, pt);
+        hipLaunchKernelGGL((k_pack_tiles<float, 256>), dim3(unsigned(tiles)), dim3(256), 0, s, pt);
+      else if (tiles < 512)
+        hipLaunchKernelGGL((k_pack_tiles<__bf16, 1024>), dim3(unsigned(tiles)), dim3(1024), 0, s, pt);
       else
-        hipLaunchKernelGGL(k_pack_tiles<__bf16>, dim3(unsigned(tiles)), dim3(256), 0, s, pt);
+        hipLaunchKernelGGL((k_pack_tiles<__bf16, 256>), dim3(unsigned(tiles)), dim3(256), 0, s, pt);
       SEL_LAUNCH_CHECK();
       continue;
     }

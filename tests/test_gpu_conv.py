@@ -866,17 +866,20 @@ def test_pack_many_matches_per_layer_pack(gpu, per_element):
     from sel import convops as CO
     prev = Lb.lib().sel_tune(60, per_element)
     try:
-        _pack_many_check(gpu, CO)
+        layers = [(CO.PACK_FWD, (64, 32, 7), 1), (CO.PACK_FWD, (256, 256, 1), 1),
+                  (CO.PACK_FWD_STRIDED, (128, 64, 4), 2), (CO.PACK_FWD_STRIDED, (512, 256, 10), 5),
+                  (CO.PACK_CONVT, (256, 128, 6), 3), (CO.PACK_CONVT, (64, 96, 2), 1), (CO.PACK_FWD, (1, 32, 7), 1),
+                  (CO.PACK_FWD, (32, 1, 7), 1), (CO.PACK_FWD, (48, 40, 3), 1),
+                  (CO.PACK_FWD_STRIDED, (64, 32, 6), 3), (CO.PACK_CONVT, (64, 32, 6), 3)]
+        _pack_many_check(gpu, CO, layers)   # >= 512 tiles in the launch: 256-thread workgroups
+        # < 512 tiles (the small launches of a C3 step): 1024-thread workgroups
+        _pack_many_check(gpu, CO, [l for l in layers if l[1] != (512, 256, 10)])
     finally:
         Lb.lib().sel_tune(60, prev)
 
 
-def _pack_many_check(gpu, CO):
+def _pack_many_check(gpu, CO, layers):
     torch.manual_seed(11)
-    layers = [(CO.PACK_FWD, (64, 32, 7), 1), (CO.PACK_FWD, (256, 256, 1), 1), (CO.PACK_FWD_STRIDED, (128, 64, 4), 2),
-              (CO.PACK_FWD_STRIDED, (512, 256, 10), 5), (CO.PACK_CONVT, (256, 128, 6), 3),
-              (CO.PACK_CONVT, (64, 96, 2), 1), (CO.PACK_FWD, (1, 32, 7), 1), (CO.PACK_FWD, (32, 1, 7), 1),
-              (CO.PACK_FWD, (48, 40, 3), 1), (CO.PACK_FWD_STRIDED, (64, 32, 6), 3), (CO.PACK_CONVT, (64, 32, 6), 3)]
     for dt in (torch.bfloat16, torch.float32):
         cache = CO.PackCache()
         ws = [torch.randn(*shp, device=gpu) for _, shp, _ in layers]
