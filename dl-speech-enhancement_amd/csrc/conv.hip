@@ -4563,12 +4563,12 @@ __device__ __forceinline__ void pack_geom(const sel_pack_job& J, unsigned& N, un
   else if (J.kind == SEL_PACK_FWD_STRIDED) N = cout, KP = 3, CP = s * cin;
   else N = s * cout, KP = 2, CP = cin;
 }
-// PT_THREADS 1024 for launches of fewer than 512 tiles (the small jobs: 32-64
-// tiles, one workgroup each; at 256 threads one wave per SIMD ran the loads
-// and their index arithmetic back to back, 17-18 us per launch), 256 for the
-// large ones.  Thread work is a (n, cp) pair of the tile with all its KP taps,
-// so no index needs a division by the job's tap count; the KP loads of a pair
-// are all issued before its LDS stores.
+// 1024 threads: one (n, cp) pair of the 32 x 32 tile per thread, with all its
+// KP taps, so no index needs a division by the job's tap count, and the KP
+// loads of a pair are all issued before its LDS stores.  (At 256 threads, four
+// elements a thread one after another, the small launches of a C3 step -- 32-64
+// tiles, one workgroup each -- took 17-18 us; now 6-7 us, and the 640-tile
+// launch 11.4 -> 9.8 us.)
 template <typename TO, unsigned PT_THREADS>
 __global__ __launch_bounds__(PT_THREADS) void k_pack_tiles(PackTiles pt) {
   __shared__ float tile[PT_T * PT_KMAX * PT_P];
@@ -6258,11 +6258,9 @@ int sel_pack_many_host(const sel_pack_job* jobs, int njobs, int64_t total, int d
     pt.tstart[pt.n] = int(tiles);
     if (tiled && tiles > 0 && tiles < (int64_t(1) << 31)) {
       if (dtype == SEL_F32)
-        hipLaunchKernelGGL((k_pack_tiles<float, 256>), dim3(unsigned(tiles)), dim3(256), 0, s, pt);
-      else if (tiles < 512)
-        hipLaunchKernelGGL((k_pack_tiles<__bf16, 1024>), dim3(unsigned(tiles)), dim3(1024), 0, s, pt);
+        hipLaunchKernelGGL((k_pack_tiles<float, 1024>), dim3(unsigned(tiles)), dim3(1024), 0, s, pt);
       else
-        hipLaunchKernelGGL((k_pack_tiles<__bf16, 256>), dim3(unsigned(tiles)), dim3(256), 0, s, pt);
+        hipLaunchKernelGGL((k_pack_tiles<__bf16, 1024>), dim3(unsigned(tiles)), dim3(1024), 0, s, pt);
       SEL_LAUNCH_CHECK();
       continue;
     }

@@ -871,8 +871,8 @@ def test_pack_many_matches_per_layer_pack(gpu, per_element):
                   (CO.PACK_CONVT, (256, 128, 6), 3), (CO.PACK_CONVT, (64, 96, 2), 1), (CO.PACK_FWD, (1, 32, 7), 1),
                   (CO.PACK_FWD, (32, 1, 7), 1), (CO.PACK_FWD, (48, 40, 3), 1),
                   (CO.PACK_FWD_STRIDED, (64, 32, 6), 3), (CO.PACK_CONVT, (64, 32, 6), 3)]
-        _pack_many_check(gpu, CO, layers)   # >= 512 tiles in the launch: 256-thread workgroups
-        # < 512 tiles (the small launches of a C3 step): 1024-thread workgroups
+        _pack_many_check(gpu, CO, layers)   # 640 + tiles in one launch
+        # < 512 tiles (as the small launches of a C3 step)
         _pack_many_check(gpu, CO, [l for l in layers if l[1] != (512, 256, 10)])
     finally:
         Lb.lib().sel_tune(60, prev)
