@@ -142,9 +142,12 @@ class CausalConv1d(NonCausalConv1d):
         forward(cat(0^j, buffer, x))[..., m:] equals the valid conv of
         cat(buffer, x), where j = 0 and m = pad_length / stride for stride 1, and
         j = 1, m = 2 for the kernel-2s stride-s downsampling convs."""
-        if self.pad_length == 0:
-            raise NotImplementedError("sel: streaming a kernel-1 CausalConv1d (reference keeps the whole input)")
         xb = torch.cat((self.pad_buffer.to(x.dtype).expand(x.shape[0], -1, -1), x), -1)
+        if self.pad_length == 0:
+            # kernel 1: the reference keeps x[:, :, -0:], i.e. the whole
+            # concatenated input, and returns the conv over all of it
+            self.pad_buffer = xb.contiguous()
+            return self.forward(xb)
         self.pad_buffer = xb[:, :, -self.pad_length:].contiguous()
         s = self.stride
         if s == 1:

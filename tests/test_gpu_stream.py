@@ -115,3 +115,24 @@ def test_stream_without_pqc_chunks_vs_oracle(gpu):
         S_enc = R.stream_encode(P, S, xc, geo, project=False)
         nclose(h, S_enc, 1e-5, f"h.{c}")
         nclose(G.decode(h), R.stream_decode(P, S, S_enc.transpose(2, 1), geo, pqc=False), 1e-5, f"y.{c}")
+
+
+def test_kernel1_causal_conv_inference_keeps_whole_input(gpu):
+    """A kernel-1 CausalConv1d streams as the reference's inference does
+    (conv_layer.py:144-147 with pad_length 0): the buffer becomes the whole
+    concatenated input (x[:, :, -0:]), so the second call returns the conv over
+    both chunks."""
+    from layers.conv_layer import CausalConv1d
+    torch.manual_seed(3)
+    conv = CausalConv1d(16, 24, kernel_size=1).to(gpu).eval()
+    x1 = torch.randn(1, 16, 40, device=gpu)
+    x2 = torch.randn(1, 16, 24, device=gpu)
+    with torch.no_grad():
+        y1 = conv.inference(x1)
+        y2 = conv.inference(x2)
+        w, b = conv.conv.weight.cpu(), conv.conv.bias.cpu()   # reference on the host
+        ref1 = torch.nn.functional.conv1d(x1.cpu(), w, b)
+        ref2 = torch.nn.functional.conv1d(torch.cat((x1, x2), -1).cpu(), w, b)
+    assert conv.pad_buffer.shape == (1, 16, 64)
+    nclose(y1, ref1, 1e-5, "y1")
+    nclose(y2, ref2, 1e-5, "y2")
