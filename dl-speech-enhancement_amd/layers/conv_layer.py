@@ -10,6 +10,7 @@ import torch
 import torch.nn as nn
 
 from sel import convops as CO
+from sel import genconv as GC
 
 
 def _run_layer(x, weight, bias, kind, stride, dilation, out_float=False):
@@ -37,10 +38,9 @@ class Conv1d1x1(nn.Conv1d):
 
 
 class NonCausalConv1d(nn.Module):
-    """1D noncausal convolution w/ 2-sides padding (conv_layer.py:26-65).
-
-    Only the stride-1, groups-1, symmetric-padding form is lowered to the HIP
-    primitive (the shipped configs are all mode 'causal')."""
+    """1D noncausal convolution w/ 2-sides padding (conv_layer.py:26-65): any
+    stride, padding, dilation and groups (sel.genconv lowers them onto the
+    stride-1 HIP primitive; the stride-1 'same' form is a single launch)."""
 
     def __init__(self, in_channels, out_channels, kernel_size, stride=1, padding=-1, dilation=1,
                  groups=1, bias=True):
@@ -53,49 +53,28 @@ class NonCausalConv1d(nn.Module):
         self.dilation = dilation
         self.conv = nn.Conv1d(in_channels=in_channels, out_channels=out_channels, kernel_size=kernel_size,
                               stride=stride, padding=padding, dilation=dilation, groups=groups, bias=bias)
+        self.out_float = False   # fp32 output under bf16 compute (see CausalConv1d)
 
     def forward(self, x):
         c = self.conv
-        if c.stride[0] != 1 or c.groups != 1 or 2 * c.padding[0] != (c.kernel_size[0] - 1) * c.dilation[0]:
-            raise NotImplementedError("sel: NonCausalConv1d is lowered for stride 1 / 'same' padding only")
-        xc = CO.to_cl(x)
-        dt = CO.compute_dtype()
-        if xc.dtype != dt:
-            xc = CO.cast(xc, dt)
-        y = _NonCausalFn.apply(xc, c.weight, c.bias, c.dilation[0], c.padding[0])
-        return y.transpose(1, 2)
+        y = _general(x, lambda xc: GC.conv1d(xc, c.weight, c.bias, c.stride[0], c.padding[0], c.dilation[0],
+                                              c.groups))
+        return CO.cast(y, torch.float32) if self.out_float else y
 
 
-class _NonCausalFn(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, x, w, b, dil, pad):
-        B, T, C = x.shape
-        N, _, K = w.shape
-        d = CO.ConvDesc(B * T, T, C, N, K, dil, pad, CO.PAD_ZERO, 0, N if b is not None else 0)
-        wp = CO.pack(CO.PACK_FWD, w, 1, x.dtype)
-        y = CO.prim(d, x, wp, bias=b.detach().float().contiguous() if b is not None else None)
-        ctx.save_for_backward(x, wp)
-        ctx.meta = (d, tuple(w.shape), b is not None)
-        return y.view(B, T, N)
-
-    @staticmethod
-    def backward(ctx, gy):
-        x, wp = ctx.saved_tensors
-        d, ws, hb = ctx.meta
-        gy = gy.contiguous()
-        if gy.dtype != x.dtype:
-            gy = CO.cast(gy, x.dtype)
-        gx = CO.prim(d.adjoint(), gy, CO.pack_dgrad(wp)).view(x.shape) if ctx.needs_input_grad[0] else None
-        gw = gb = None
-        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
-            gwp, gb = CO.wgrad(d, gy, x, hb and ctx.needs_input_grad[2])
-            gw = CO.unpack(CO.PACK_FWD, gwp, ws, 1)
-        return gx, gw, gb, None, None
+def _general(x, fn):
+    """(B, C, T) -> fn(channels-last x in the compute dtype) -> (B, C', T')."""
+    xc = CO.to_cl(x)
+    dt = CO.compute_dtype()
+    if xc.dtype != dt:
+        xc = CO.cast(xc, dt)
+    return fn(xc).transpose(1, 2)
 
 
 class NonCausalConvTranspose1d(nn.Module):
-    """1D noncausal transpose convolution (conv_layer.py:68-106); parameters only —
-    the shipped configs use the causal variant."""
+    """1D noncausal transpose convolution (conv_layer.py:68-106): any stride,
+    padding, output_padding and groups (sel.genconv: one primitive launch
+    producing the stride's output phases per input row)."""
 
     def __init__(self, in_channels, out_channels, kernel_size, stride, padding=-1, output_padding=-1,
                  groups=1, bias=True):
@@ -109,7 +88,9 @@ class NonCausalConvTranspose1d(nn.Module):
                                          output_padding=output_padding, groups=groups, bias=bias)
 
     def forward(self, x):
-        raise NotImplementedError("sel: NonCausalConvTranspose1d is not on the causal hot path")
+        d = self.deconv
+        return _general(x, lambda xc: GC.conv_transpose1d(xc, d.weight, d.bias, d.stride[0], d.padding[0],
+                                                           d.output_padding[0], d.groups))
 
 
 class CausalConv1d(NonCausalConv1d):
@@ -119,8 +100,6 @@ class CausalConv1d(NonCausalConv1d):
                  pad_buffer=None):
         super().__init__(in_channels=in_channels, out_channels=out_channels, kernel_size=kernel_size,
                          stride=stride, padding=0, dilation=dilation, groups=groups, bias=bias)
-        if groups != 1:
-            raise NotImplementedError("sel: grouped CausalConv1d is not on the AudioDec hot path")
         self.stride = stride
         self.pad_length = (kernel_size - 1) * dilation
         if pad_buffer is None:
@@ -130,9 +109,21 @@ class CausalConv1d(NonCausalConv1d):
         # output feeds the fp32 losses: no separate cast launch)
         self.out_float = False
 
+    def _packed_form(self, T):
+        """The dedicated ConvLayerFn packing applies (ungrouped; stride 1, or
+        the k = 2s downsampling conv on a stride-aligned input)?"""
+        s = self.stride
+        return self.conv.groups == 1 and (s == 1 or (self.kernel_size == 2 * s and T % s == 0))
+
     def forward(self, x):
-        return _run_layer(x, self.conv.weight, self.conv.bias, CO.PACK_FWD, self.stride, self.dilation,
-                          self.out_float)
+        if self._packed_form(x.shape[-1]):
+            return _run_layer(x, self.conv.weight, self.conv.bias, CO.PACK_FWD, self.stride, self.dilation,
+                              self.out_float)
+        # grouped / other strides (sel.genconv): left pad (k-1)*d, T_out = ceil(T / s)
+        c = self.conv
+        y = _general(x, lambda xc: GC.conv1d(xc, c.weight, c.bias, self.stride, self.pad_length, self.dilation,
+                                              c.groups, (x.shape[-1] - 1) // self.stride + 1))
+        return CO.cast(y, torch.float32) if self.out_float else y
 
     @torch.no_grad()
     def inference(self, x):
@@ -150,10 +141,12 @@ class CausalConv1d(NonCausalConv1d):
             return self.forward(xb)
         self.pad_buffer = xb[:, :, -self.pad_length:].contiguous()
         s = self.stride
+        c = self.conv
+        if c.groups != 1 or (s > 1 and self.kernel_size != 2 * s):
+            # the valid conv of cat(buffer, x) (sel.genconv, no padding)
+            return _general(xb, lambda xc: GC.conv1d(xc, c.weight, c.bias, s, 0, self.dilation, c.groups))
         if s == 1:
             return self.forward(xb)[:, :, self.pad_length:]
-        if self.pad_length != 2 * s - 1:
-            raise NotImplementedError("sel: streaming strided CausalConv1d is lowered for kernel_size == 2*stride")
         xz = torch.cat((xb.new_zeros(xb.shape[0], xb.shape[1], 1), xb), -1)
         return self.forward(xz)[:, :, 2:]
 
@@ -163,22 +156,30 @@ class CausalConv1d(NonCausalConv1d):
 
 class CausalConvTranspose1d(NonCausalConvTranspose1d):
     """1D causal transpose convolution (conv_layer.py:153-191): replicate-pad 1,
-    ConvTranspose1d(k=2s, s), crop [s:-s]; lowered to a 2-tap conv producing
-    s output phases per input step."""
+    ConvTranspose1d(k, s), crop [s:-s].  k = 2s (every shipped config) is a
+    2-tap conv producing s output phases per input step with the replicate pad
+    in the kernel; other k go through sel.genconv."""
 
     def __init__(self, in_channels, out_channels, kernel_size, stride, bias=True, pad_buffer=None):
         super().__init__(in_channels=in_channels, out_channels=out_channels, kernel_size=kernel_size,
                          stride=stride, padding=0, output_padding=0, bias=bias)
-        if kernel_size != 2 * stride:
-            raise NotImplementedError("sel: CausalConvTranspose1d is lowered for kernel_size == 2*stride")
         self.stride = stride
+        self.kernel_size = kernel_size
         self.pad_length = 1
         if pad_buffer is None:
             pad_buffer = torch.zeros(1, in_channels, self.pad_length)
         self.register_buffer("pad_buffer", pad_buffer)
 
+    def _deconv_cropped(self, x):
+        """deconv(x)[:, :, s:-s] through sel.genconv (any kernel size)."""
+        d, s = self.deconv, self.stride
+        L = (x.shape[-1] - 1) * s + self.kernel_size - 2 * s
+        return _general(x, lambda xc: GC.conv_transpose1d(xc, d.weight, d.bias, s, s, 0, 1, L))
+
     def forward(self, x):
-        return _run_layer(x, self.deconv.weight, self.deconv.bias, CO.PACK_CONVT, self.stride, 1)
+        if self.kernel_size == 2 * self.stride:
+            return _run_layer(x, self.deconv.weight, self.deconv.bias, CO.PACK_CONVT, self.stride, 1)
+        return self._deconv_cropped(torch.cat((x[:, :, :1], x), -1))
 
     @torch.no_grad()
     def inference(self, x):
@@ -188,6 +189,8 @@ class CausalConvTranspose1d(NonCausalConvTranspose1d):
         sample only reaches the s outputs that are dropped)."""
         xb = torch.cat((self.pad_buffer.to(x.dtype).expand(x.shape[0], -1, -1), x), -1)
         self.pad_buffer = xb[:, :, -self.pad_length:].contiguous()
+        if self.kernel_size != 2 * self.stride:
+            return self._deconv_cropped(xb)
         return self.forward(xb)[:, :, self.stride:]
 
     def reset_buffer(self):

@@ -23,8 +23,20 @@ class NonCausalResidualUnit(nn.Module):
         self.conv2 = Conv1d1x1(out_channels, out_channels, bias)
 
     def forward(self, x):
-        y = self.conv1(self.activation(x))
-        return x + self.conv2(self.activation(y))
+        """x + conv2(ELU(conv1(ELU(x)))) (:43-46) with conv1's symmetric pad
+        (k-1)//2*d: the same fused op as the causal unit, whose descriptor takes
+        the pad (the ELUs in the conv prologues, the residual in the 1x1's epilogue)."""
+        return _fused(self, x, self.conv1.conv.padding[0])
+
+
+def _fused(ru, x, pad):
+    xc = CO.to_cl(x)
+    dt = CO.compute_dtype()
+    if xc.dtype != dt:
+        xc = CO.cast(xc, dt)
+    c1, c2 = ru.conv1.conv, ru.conv2
+    y = CO.ResidualUnitFn.apply(xc, c1.weight, c1.bias, c2.weight, c2.bias, c1.dilation[0], pad)
+    return y.transpose(1, 2)
 
 
 class CausalResidualUnit(NonCausalResidualUnit):
@@ -37,13 +49,7 @@ class CausalResidualUnit(NonCausalResidualUnit):
                                   kernel_size=kernel_size, stride=1, dilation=dilation, bias=bias)
 
     def forward(self, x):
-        xc = CO.to_cl(x)
-        dt = CO.compute_dtype()
-        if xc.dtype != dt:
-            xc = CO.cast(xc, dt)
-        c1, c2 = self.conv1.conv, self.conv2
-        y = CO.ResidualUnitFn.apply(xc, c1.weight, c1.bias, c2.weight, c2.bias, c1.dilation[0])
-        return y.transpose(1, 2)
+        return _fused(self, x, self.conv1.pad_length)
 
     @torch.no_grad()
     def inference(self, x):

@@ -20,6 +20,7 @@ import logging
 
 import torch
 import torch.nn as nn
+from torch.nn.utils.spectral_norm import SpectralNorm
 
 from sel import convops as CO
 from sel import dconvops as DC
@@ -79,24 +80,31 @@ class HiFiGANPeriodDiscriminator(nn.Module):
         self._specs.append((out_chs, out_channels, kernel_sizes[1] - 1, 1, (kernel_sizes[1] - 1) // 2, 1, False))
         if use_weight_norm and use_spectral_norm:
             raise ValueError("Either use use_weight_norm or use_spectral_norm.")
-        if use_spectral_norm:
-            raise NotImplementedError("spectral norm on the period discriminator is not lowered to the HIP path "
-                                      "(no shipped config uses it)")
         self.use_weight_norm = use_weight_norm
         if use_weight_norm:
             self.apply_weight_norm()
+        if use_spectral_norm:
+            self.apply_spectral_norm()
         self._plan = None
 
     def _convs(self):
         return [seq[0] for seq in self.convs] + [self.output_conv]
 
-    def _params(self):
+    def _params(self, power=None):
+        """The chain's parameter list.  Spectral-normalised convs contribute
+        weight_orig / sigma (torch.nn.utils.spectral_norm's own compute_weight,
+        i.e. what the reference's module pre-hook sets before each call, with
+        its power iteration when the module is training; power=False: reuse
+        the current u, v — the second half of a stashed forward)."""
         out = []
         for m in self._convs():
             if self.use_weight_norm:
                 out += [m.weight_v, m.weight_g, m.bias]
             else:
-                out += [m.weight, m.bias]
+                sn = _spectral_norm_hook(m)
+                w = m.weight if sn is None else sn.compute_weight(
+                    m, do_power_iteration=m.training if power is None else power)
+                out += [w, m.bias]
         return out
 
     def plan(self):
@@ -144,9 +152,10 @@ class HiFiGANPeriodDiscriminator(nn.Module):
         """forward(cat[stashed clips, x]) with the stashed half not recomputed."""
         x0, bufs, n, Lv = _take_stash(self)
         x0[n:] = self._x0(x)[0].detach()
+        # (spectral norm: stash_first_half ran this call's power iteration)
         return self._outs(DC.ChainFn.apply(x0, Lv, self.plan(), self.slope, self.use_weight_norm, "period",
                                            2 * x.shape[0], self.period, getattr(self, "_frozen", False),
-                                           (n, bufs), *self._params()))
+                                           (n, bufs), *self._params(power=False)))
 
     def apply_weight_norm(self):
         def _apply_weight_norm(m):
@@ -156,7 +165,20 @@ class HiFiGANPeriodDiscriminator(nn.Module):
         self.apply(_apply_weight_norm)
 
     def apply_spectral_norm(self):
-        raise NotImplementedError("spectral norm is not lowered to the HIP path")
+        """discriminator.py:150-157: torch.nn.utils.spectral_norm on every Conv2d
+        (weight_orig / weight_u / weight_v, as in the reference's state_dict)."""
+        def _apply_spectral_norm(m):
+            if isinstance(m, nn.Conv2d):
+                nn.utils.spectral_norm(m)
+                logging.debug(f"Spectral norm is applied to {m}.")
+        self.apply(_apply_spectral_norm)
+
+
+def _spectral_norm_hook(m):
+    for h in m._forward_pre_hooks.values():
+        if isinstance(h, SpectralNorm):
+            return h
+    return None
 
 
 def _take_stash(f):

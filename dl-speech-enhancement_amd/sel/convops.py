@@ -809,15 +809,18 @@ def _ru_meta(d1, xf, wp1, wp2):
 
 class ResidualUnitFn(torch.autograd.Function):
     """x + conv1x1(ELU(causal_conv_k(ELU(x)))) fused into two primitive calls
-    forward and four backward (residual_unit.py:43-46)."""
+    forward and four backward (residual_unit.py:43-46).  `pad` (optional): the
+    conv's left zero pad, (k-1)*dil causal by default; the noncausal unit
+    (residual_unit.py:20-46) passes (k-1)//2*dil and runs the unfused kernels."""
 
     @staticmethod
-    def forward(ctx, x, w1, b1, w2, b2, dil):
+    def forward(ctx, x, w1, b1, w2, b2, dil, pad=None):
         L.need_device(x, w1, w2)
         B, T, C = x.shape
         k = w1.shape[2]
         cm = w1.shape[0]
-        d1 = ConvDesc(B * T, T, C, cm, k, dil, (k - 1) * dil, PAD_ZERO, 1, cm if b1 is not None else 0)
+        pad = (k - 1) * dil if pad is None else pad
+        d1 = ConvDesc(B * T, T, C, cm, k, dil, pad, PAD_ZERO, 1, cm if b1 is not None else 0)
         d2 = ConvDesc(B * T, T, cm, w2.shape[0], 1, 1, 0, PAD_ZERO, 1, w2.shape[0] if b2 is not None else 0)
         if w2.shape[0] != C:
             raise L.SelError("residual unit needs out_channels == in_channels")
@@ -858,7 +861,7 @@ class ResidualUnitFn(torch.autograd.Function):
             p2 = _live(pr[2], pr[3] if want_b2 else None) if ctx.needs_input_grad[3] else None
             gx, gw1, gb1, gw2, gb2 = resunit_bwd_wgrad(d1, gf, h, xf, wd1, wd2, s1, s2, want_b1, want_b2, p1, p2)
             return (gx.view(B, T, C), gw1 if ctx.needs_input_grad[1] else None, gb1,
-                    gw2 if ctx.needs_input_grad[3] else None, gb2, None)
+                    gw2 if ctx.needs_input_grad[3] else None, gb2, None, None)
         if ctx.needs_input_grad[0] and ru_bwd_fused_ok(d1, x.dtype):
             # one launch: gh = (W2^T g) * ELU'(h) and gx = g + conv_adjoint(gh) * ELU'(x)
             gx, gh = resunit_bwd(d1, gf, h, xf, wd1, wd2, need_w1)
@@ -880,4 +883,4 @@ class ResidualUnitFn(torch.autograd.Function):
             params = _live(pr[0], pr[1] if want_b else None) if ctx.needs_input_grad[1] else None
             gw1, gb1 = wgrad_torch(d1, gh, xf, PACK_FWD, s1, 1, want_b, params)
             gw1 = gw1 if ctx.needs_input_grad[1] else None
-        return gx, gw1, gb1, gw2, gb2, None
+        return gx, gw1, gb1, gw2, gb2, None, None

@@ -153,14 +153,42 @@ def causal_conv_transpose1d(x, w, b=None, stride=1):
     return y[:, :, stride:-stride]
 
 
+def noncausal_conv1d(x, w, b=None, stride=1, padding=-1, dilation=1, groups=1):
+    """layers/conv_layer.py:26-65 — nn.Conv1d with padding (k-1)//2*d by default."""
+    if padding < 0:
+        padding = (w.shape[-1] - 1) // 2 * dilation
+    return F.conv1d(x, w, b, stride=stride, padding=padding, dilation=dilation, groups=groups)
+
+
+def noncausal_conv_transpose1d(x, w, b=None, stride=1, padding=-1, output_padding=-1, groups=1):
+    """layers/conv_layer.py:68-106 — nn.ConvTranspose1d, padding (s+1)//2 and
+    output_padding s % 2 by default."""
+    if padding < 0:
+        padding = (stride + 1) // 2
+    if output_padding < 0:
+        output_padding = 1 if stride % 2 else 0
+    return F.conv_transpose1d(x, w, b, stride=stride, padding=padding, output_padding=output_padding,
+                              groups=groups)
+
+
+def grouped_causal_conv1d(x, w, b=None, stride=1, dilation=1, groups=1):
+    """layers/conv_layer.py:109-142 with groups: left zero pad (k-1)*d, conv."""
+    k = w.shape[-1]
+    return F.conv1d(F.pad(x, ((k - 1) * dilation, 0)), w, b, stride=stride, dilation=dilation, groups=groups)
+
+
 def elu(x):
     """nn.ELU(alpha=1): models/autoencoder/modules/residual_unit.py:32."""
     return F.elu(x)
 
 
-def residual_unit(x, w1, w2, dilation):
-    """residual_unit.py:43-46 — x + conv1x1(ELU(causal_conv_k7_d(ELU(x))))."""
-    y = causal_conv1d(elu(x), w1, None, 1, dilation)
+def residual_unit(x, w1, w2, dilation, mode="causal"):
+    """residual_unit.py:43-46 — x + conv1x1(ELU(conv_k7_d(ELU(x)))), conv1
+    causal (:49-76) or noncausal with 'same' padding (:20-41)."""
+    if mode == "causal":
+        y = causal_conv1d(elu(x), w1, None, 1, dilation)
+    else:
+        y = noncausal_conv1d(elu(x), w1, None, 1, -1, dilation)
     y = F.conv1d(elu(y), w2)
     return x + y
 
@@ -231,42 +259,52 @@ def generator_geometry(encode_channels=32, decode_channels=32, enc_ratios=(2, 4,
     return enc, dec
 
 
-def encoder_forward(P, x, geo, dilations=(1, 3, 9)):
-    """encoder.py:112-116 / EncoderBlock :61-65."""
+def _conv(mode):
+    """The mode's Conv1d (encoder.py:38-45, decoder.py:38-45, projector.py:31-37)."""
+    if mode == "causal":
+        return causal_conv1d
+    return lambda x, w, b=None, stride=1, dilation=1: noncausal_conv1d(x, w, b, stride, -1, dilation)
+
+
+def encoder_forward(P, x, geo, dilations=(1, 3, 9), mode="causal"):
+    """encoder.py:112-116 / EncoderBlock :61-65 (mode 'causal' or 'noncausal')."""
     enc, _ = geo
-    h = causal_conv1d(x, P["encoder.conv.conv.weight"])
+    conv = _conv(mode)
+    h = conv(x, P["encoder.conv.conv.weight"])
     for i, (ci, co, s) in enumerate(enc):
         pre = f"encoder.conv_blocks.{i}"
         for j, d in enumerate(dilations):
             ru = f"{pre}.res_units.{j}"
-            h = residual_unit(h, P[f"{ru}.conv1.conv.weight"], P[f"{ru}.conv2.weight"], d)
-        h = causal_conv1d(h, P[f"{pre}.conv.conv.weight"], P.get(f"{pre}.conv.conv.bias"), stride=s)
+            h = residual_unit(h, P[f"{ru}.conv1.conv.weight"], P[f"{ru}.conv2.weight"], d, mode)
+        h = conv(h, P[f"{pre}.conv.conv.weight"], P.get(f"{pre}.conv.conv.bias"), stride=s)
     return h
 
 
-def decoder_forward(P, z, geo, pqc=True, dilations=(1, 3, 9)):
+def decoder_forward(P, z, geo, pqc=True, dilations=(1, 3, 9), mode="causal"):
     """decoder.py:116-121 (PQC) / without_PQC decoder.py:116-123 (conv1 skipped)."""
     _, dec = geo
-    h = causal_conv1d(z, P["decoder.conv1.conv.weight"]) if pqc else z
+    conv = _conv(mode)
+    convt = causal_conv_transpose1d if mode == "causal" else noncausal_conv_transpose1d
+    h = conv(z, P["decoder.conv1.conv.weight"]) if pqc else z
     for i, (ci, co, s) in enumerate(dec):
         pre = f"decoder.conv_blocks.{i}"
-        h = causal_conv_transpose1d(h, P[f"{pre}.conv.deconv.weight"], P.get(f"{pre}.conv.deconv.bias"), s)
+        h = convt(h, P[f"{pre}.conv.deconv.weight"], P.get(f"{pre}.conv.deconv.bias"), s)
         for j, d in enumerate(dilations):
             ru = f"{pre}.res_units.{j}"
-            h = residual_unit(h, P[f"{ru}.conv1.conv.weight"], P[f"{ru}.conv2.weight"], d)
-    return causal_conv1d(h, P["decoder.conv2.conv.weight"])
+            h = residual_unit(h, P[f"{ru}.conv1.conv.weight"], P[f"{ru}.conv2.weight"], d, mode)
+    return conv(h, P["decoder.conv2.conv.weight"])
 
 
-def generator_forward(P, x, geo, pqc=True, codebook_num=8):
+def generator_forward(P, x, geo, pqc=True, codebook_num=8, mode="causal"):
     """AudioDec.py:95-103 (PQC) or autoencoder_without_PQC/AudioDec.py:94-100."""
-    h = encoder_forward(P, x, geo)
+    h = encoder_forward(P, x, geo, mode=mode)
     if not pqc:
-        return decoder_forward(P, h, geo, pqc=False)
-    z = causal_conv1d(h, P["projector.project.conv.weight"])
+        return decoder_forward(P, h, geo, pqc=False, mode=mode)
+    z = _conv(mode)(h, P["projector.project.conv.weight"])
     embeds = [P[f"quantizer.codebook.layers.{i}.embed"] for i in range(codebook_num)]
     zq, vql, ppl, _ = rvq_forward(z.transpose(2, 1), embeds)
     zq = zq.transpose(2, 1)
-    y = decoder_forward(P, zq, geo, pqc=True)
+    y = decoder_forward(P, zq, geo, pqc=True, mode=mode)
     return y, zq, z, vql, ppl
 
 
@@ -274,13 +312,13 @@ def generator_forward(P, x, geo, pqc=True, codebook_num=8):
 # streaming  (layers/conv_layer.py:144-191, models/autoencoder/AudioDec.py:106-191)
 # --------------------------------------------------------------------------
 
-def stream_causal_conv1d(S, key, x, w, b=None, stride=1, dilation=1):
+def stream_causal_conv1d(S, key, x, w, b=None, stride=1, dilation=1, groups=1):
     """conv_layer.py:144-147 — conv over cat(pad_buffer, x); keep the last (k-1)d."""
     pad = (w.shape[-1] - 1) * dilation
     buf = S.get(key, torch.zeros(x.shape[0], x.shape[1], pad, dtype=x.dtype))
     xb = torch.cat([buf, x], -1)
     S[key] = xb[:, :, -pad:]
-    return F.conv1d(xb, w, b, stride=stride, dilation=dilation)
+    return F.conv1d(xb, w, b, stride=stride, dilation=dilation, groups=groups)
 
 
 def stream_conv_transpose1d(S, key, x, w, b=None, stride=1):
@@ -421,10 +459,27 @@ def snr_db(preds, target):
 # (losses/adversarial_loss.py:13-124, losses/feat_match_loss.py:13-55)
 # --------------------------------------------------------------------------
 
+def spectral_norm_weight(w_orig, u, v, training=True, eps=1e-12):
+    """torch.nn.utils.spectral_norm(n_power_iterations=1, dim=0) as applied by
+    discriminator.py:150-157, restated: in training one power iteration
+    v = normalize(W^T u), u = normalize(W v) on W = w_orig.flatten(1), then
+    w = w_orig / (u . W v).  Returns (w, u', v')."""
+    W = w_orig.flatten(1)
+    if training:
+        with torch.no_grad():   # u, v are constants of the backward (torch clones them)
+            v = F.normalize(torch.mv(W.t(), u), dim=0, eps=eps)
+            u = F.normalize(torch.mv(W, v), dim=0, eps=eps)
+    sigma = torch.dot(u, torch.mv(W, v))
+    return w_orig / sigma, u, v
+
+
 def _wn(P, key):
-    """torch.nn.utils.weight_norm(dim=0): w = g * v / ||v|| (norm over all dims but 0)."""
+    """torch.nn.utils.weight_norm(dim=0): w = g * v / ||v|| (norm over all dims but 0);
+    spectral-norm keys (weight_orig / weight_u / weight_v): one training-mode step."""
     if key + ".weight" in P:
         return P[key + ".weight"]
+    if key + ".weight_orig" in P:
+        return spectral_norm_weight(P[key + ".weight_orig"], P[key + ".weight_u"], P[key + ".weight_v"])[0]
     g, v = P[key + ".weight_g"], P[key + ".weight_v"]
     return g * v / v.flatten(1).norm(dim=1).view(-1, *([1] * (v.dim() - 1)))
 

@@ -325,6 +325,111 @@ def make_trainer(ref, clean, noise, out):
     np.savez_compressed(os.path.join(out, "trainer_step.npz"), **d)
 
 
+# (name, Cin, Cout, k, stride, padding, dilation, groups, bias, T) of NonCausalConv1d
+GENERAL_CONV = [
+    ("nc_same", 8, 8, 7, 1, -1, 3, 1, False, 100),
+    ("nc_down3", 8, 16, 6, 3, -1, 1, 1, True, 240),     # noncausal EncoderBlock conv (encoder.py:50-57)
+    ("nc_s2_p0", 6, 10, 5, 2, 0, 1, 1, True, 101),
+    ("nc_grp", 8, 12, 5, 1, 2, 2, 4, True, 90),
+    ("nc_grp_s4", 16, 16, 41, 4, 20, 1, 4, True, 200),  # the MSD's grouped k41 layer shape, 41 taps
+    ("nc_bigpad", 4, 6, 3, 1, 5, 1, 1, True, 50),
+]
+# (name, Cin, Cout, k, stride, padding, output_padding, groups, bias, T) of NonCausalConvTranspose1d
+GENERAL_CONVT = [
+    ("nct_up5", 16, 8, 10, 5, -1, -1, 1, True, 20),    # noncausal DecoderBlock deconv (decoder.py:47-54)
+    ("nct_up4", 12, 8, 8, 4, -1, -1, 1, True, 25),
+    ("nct_grp", 8, 12, 5, 3, 1, 2, 4, True, 30),
+    ("nct_k3s1", 6, 4, 3, 1, 0, 0, 1, False, 40),
+]
+# grouped / odd-stride CausalConv1d: (name, Cin, Cout, k, stride, dilation, groups, bias, T)
+GENERAL_CAUSAL = [
+    ("c_grp", 8, 8, 7, 1, 2, 2, True, 100),
+    ("c_s3k4", 6, 8, 4, 3, 1, 1, True, 100),
+]
+# CausalConvTranspose1d with k != 2s: (name, Cin, Cout, k, stride, T)
+GENERAL_CAUSALT = [("ct_k3s2", 8, 4, 3, 2, 30), ("ct_k7s3", 6, 6, 7, 3, 20)]
+
+
+def _record(d, name, m, conv, xin, cfg):
+    yo = m(xin)
+    gy = torch.randn_like(yo)
+    yo.backward(gy)
+    d[f"{name}.cfg"] = np.array(cfg)
+    d[f"{name}.x"], d[f"{name}.w"] = _np(xin), _np(conv.weight)
+    d[f"{name}.y"], d[f"{name}.gy"] = _np(yo), _np(gy)
+    d[f"{name}.gx"], d[f"{name}.gw"] = _np(xin.grad), _np(conv.weight.grad)
+    if conv.bias is not None:
+        d[f"{name}.b"], d[f"{name}.gb"] = _np(conv.bias), _np(conv.bias.grad)
+
+
+def make_general(ref, clean, noise, out):
+    """Layer forms outside the shipped causal configs (layers/conv_layer.py:26-191
+    with any stride / padding / dilation / groups), the noncausal AudioDec
+    generators (mode='noncausal', encoder.py:38-57, decoder.py:38-57) and a
+    spectral-normalised period discriminator (discriminator.py:99-157)."""
+    conv_mod = importlib.import_module("layers.conv_layer")
+    torch.manual_seed(7)
+    d = {}
+    for name, ci, co, k, s, p, dl, g, b, t in GENERAL_CONV:
+        m = conv_mod.NonCausalConv1d(ci, co, k, stride=s, padding=p, dilation=dl, groups=g, bias=b)
+        _record(d, name, m, m.conv, torch.randn(2, ci, t, requires_grad=True), [ci, co, k, s, p, dl, g, int(b), t])
+    for name, ci, co, k, s, p, op, g, b, t in GENERAL_CONVT:
+        m = conv_mod.NonCausalConvTranspose1d(ci, co, k, s, padding=p, output_padding=op, groups=g, bias=b)
+        _record(d, name, m, m.deconv, torch.randn(2, ci, t, requires_grad=True), [ci, co, k, s, p, op, g, int(b), t])
+    for name, ci, co, k, s, dl, g, b, t in GENERAL_CAUSAL:
+        m = conv_mod.CausalConv1d(ci, co, k, stride=s, dilation=dl, groups=g, bias=b)
+        _record(d, name, m, m.conv, torch.randn(2, ci, t, requires_grad=True), [ci, co, k, s, dl, g, int(b), t])
+    for name, ci, co, k, s, t in GENERAL_CAUSALT:
+        m = conv_mod.CausalConvTranspose1d(ci, co, k, s)
+        _record(d, name, m, m.deconv, torch.randn(2, ci, t, requires_grad=True), [ci, co, k, s, t])
+    np.savez_compressed(os.path.join(out, "general_conv.npz"), **d)
+
+    # noncausal generators (reduced width), as the causal generator_{pqc,nopqc} fixtures
+    mel_mod = _load("ref_mel_loss", os.path.join(ref, "losses", "mel_loss.py"))
+    mel = mel_mod.MultiMelSpectrogramLoss(fs=24000, fft_sizes=[2048], hop_sizes=[300], win_lengths=[None],
+                                          window="hann_window", num_mels=80, fmin=0, fmax=24000, log_base=None)
+    gp = dict(encode_channels=4, decode_channels=4, code_dim=64, codebook_num=2, codebook_size=64)
+    T = 2400
+    xn = torch.from_numpy(np.stack([clean[0][:T] + 0.1 * noise[0][:T],
+                                    clean[1][:T] + 0.1 * noise[1][:T]]).astype(np.float32)).unsqueeze(1)
+    xc = torch.from_numpy(np.stack([clean[0][:T], clean[1][:T]])).unsqueeze(1)
+    for tag, mod in (("pqc", "models.autoencoder.AudioDec"), ("nopqc", "models.autoencoder_without_PQC.AudioDec")):
+        torch.manual_seed(93)
+        G = importlib.import_module(mod).Generator(mode="noncausal", **gp)
+        d = {"x_noisy": _np(xn), "x_clean": _np(xc)}
+        d.update(_sd(G))
+        if tag == "pqc":
+            G.quantizer.codebook.eval()
+            y, zq, z, vql, ppl = G(xn)
+            loss = 45.0 * mel(y, xc) + vql.sum()
+            d.update({"y": _np(y), "zq": _np(zq), "z": _np(z), "vqloss": _np(vql), "ppl": _np(ppl)})
+        else:
+            y = G(xn)
+            loss = 45.0 * mel(y, xc)
+            d["y"] = _np(y)
+        loss.backward()
+        d["loss"] = _np(loss)
+        d.update(_grads(G))
+        np.savez_compressed(os.path.join(out, f"generator_noncausal_{tag}.npz"), **d)
+
+    # spectral-normalised period discriminator, training mode (one power iteration per call)
+    _install_trainer_stubs()
+    disc = importlib.import_module("models.vocoder.modules.discriminator")
+    torch.manual_seed(11)
+    D = disc.HiFiGANPeriodDiscriminator(period=3, channels=4, max_downsample_channels=32,
+                                        use_weight_norm=False, use_spectral_norm=True)
+    d = _sd(D, "sd0.")
+    x = torch.from_numpy(np.stack([clean[0][:600], clean[1][:600]])).unsqueeze(1).requires_grad_(True)
+    d["x"] = _np(x)
+    outs = D(x)
+    d.update({f"out.{j}": _np(t) for j, t in enumerate(outs)})
+    sum((t * gan_cotangent(t.shape, 0, j)).sum() for j, t in enumerate(outs)).backward()
+    d["grad_x"] = _np(x.grad)
+    d.update(_grads(D))
+    d.update(_sd(D, "sd1."))
+    np.savez_compressed(os.path.join(out, "spectral_norm.npz"), **d)
+
+
 def make(ref, out, only=None):
     du = _install_stubs(ref)
     stft_mod = _load("ref_stft_loss", os.path.join(ref, "losses", "stft_loss.py"))
@@ -343,6 +448,8 @@ def make(ref, out, only=None):
         return make_waveform(ref, clean, noise, out)
     if only == "gan":
         return make_gan(ref, clean, noise, out)
+    if only == "general":
+        return make_general(ref, clean, noise, out)
     if only == "trainer":
         return make_trainer(ref, clean, noise, out)
     torch.manual_seed(93)

@@ -366,3 +366,93 @@ def test_denoise_trainer_step():
             close(ppl[i], g[f"rec.{s}.train/train/ppl_{i}"], rtol=1e-5)
         for k in train:
             close(P[k], g[f"sd{s + 1}.{k}"], rtol=1e-5, atol=1e-7)
+
+
+# ---- layer forms outside the shipped causal configs (tests/golden/general_conv.npz) ----
+
+def _general_case(g, name, fn):
+    x = T(g[f"{name}.x"]).requires_grad_(True)
+    w = T(g[f"{name}.w"]).requires_grad_(True)
+    b = T(g[f"{name}.b"]).requires_grad_(True) if f"{name}.b" in g else None
+    y = fn(x, w, b)
+    close(y, g[f"{name}.y"], rtol=1e-5, atol=1e-5)
+    y.backward(T(g[f"{name}.gy"]))
+    close(x.grad, g[f"{name}.gx"], rtol=1e-5, atol=1e-5)
+    close(w.grad, g[f"{name}.gw"], rtol=1e-5, atol=1e-4)
+    if b is not None:
+        close(b.grad, g[f"{name}.gb"], rtol=1e-5, atol=1e-4)
+
+
+def test_general_conv_layers():
+    """NonCausalConv1d / NonCausalConvTranspose1d with any stride, padding,
+    dilation, groups; grouped and odd-stride CausalConv1d; CausalConvTranspose1d
+    with k != 2s (layers/conv_layer.py:26-191) against the reference's own layers."""
+    from golden.make_goldens import GENERAL_CAUSAL, GENERAL_CAUSALT, GENERAL_CONV, GENERAL_CONVT
+    g = golden("general_conv")
+    for name, ci, co, k, s, p, dl, gr, b, t in GENERAL_CONV:
+        _general_case(g, name, lambda x, w, bb: R.noncausal_conv1d(x, w, bb, s, p, dl, gr))
+    for name, ci, co, k, s, p, op, gr, b, t in GENERAL_CONVT:
+        _general_case(g, name, lambda x, w, bb: R.noncausal_conv_transpose1d(x, w, bb, s, p, op, gr))
+    for name, ci, co, k, s, dl, gr, b, t in GENERAL_CAUSAL:
+        _general_case(g, name, lambda x, w, bb: R.grouped_causal_conv1d(x, w, bb, s, dl, gr))
+    for name, ci, co, k, s, t in GENERAL_CAUSALT:
+        _general_case(g, name, lambda x, w, bb: R.causal_conv_transpose1d(x, w, bb, s))
+
+
+@pytest.mark.parametrize("tag", ["pqc", "nopqc"])
+def test_noncausal_generator(tag):
+    """Generator(mode='noncausal') (encoder.py:38-57, decoder.py:38-57, residual_unit.py:20-46)."""
+    g = golden(f"generator_noncausal_{tag}")
+    gm = golden("melmat")
+    P = {k[3:]: T(v) for k, v in g.items() if k.startswith("sd.")}
+    for k, v in P.items():
+        if v.dtype == torch.float32 and not k.endswith(("pad_buffer", "embed", "cluster_size", "embed_avg")):
+            v.requires_grad_(True)
+    geo = R.generator_geometry(encode_channels=4, decode_channels=4)
+    xn, xc = T(g["x_noisy"]), T(g["x_clean"])
+    mm = T(gm["melmat.24k_fmax24000"])
+    mel = lambda a, b: R.multi_mel_loss(a, b, [(2048, 300, 2048)], [R.hann(2048)], [mm], 1e-10, None)
+    if tag == "pqc":
+        y, zq, z, vql, ppl = R.generator_forward(P, xn, geo, pqc=True, codebook_num=2, mode="noncausal")
+        close(z, g["z"], rtol=1e-5, atol=1e-6)
+        close(zq, g["zq"], rtol=1e-5, atol=1e-6)
+        close(vql, g["vqloss"], rtol=1e-5, atol=1e-7)
+        loss = 45.0 * mel(y, xc) + vql.sum()
+    else:
+        y = R.generator_forward(P, xn, geo, pqc=False, mode="noncausal")
+        loss = 45.0 * mel(y, xc)
+    close(y, g["y"], rtol=1e-5, atol=1e-6)
+    close(loss, g["loss"], rtol=1e-5)
+    loss.backward()
+    for k, v in g.items():
+        if k.startswith("g."):
+            close(P[k[2:]].grad, v, rtol=1e-4, atol=1e-6)
+
+
+def test_spectral_norm_period_discriminator():
+    """discriminator.py:99-157 with use_spectral_norm: one training-mode power
+    iteration per call (torch.nn.utils.spectral_norm), outputs, input and
+    weight_orig gradients, and the updated u / v buffers."""
+    g = golden("spectral_norm")
+    sd0 = {k[4:]: T(v) for k, v in g.items() if k.startswith("sd0.")}
+    P = {f"d.{k}": v.clone().requires_grad_(k.endswith(("weight_orig", "bias"))) for k, v in sd0.items()}
+    plan = R.period_discriminator_plan(channels=4, max_downsample_channels=32)
+    for key in [k for k in sd0 if k.endswith("weight_orig")]:
+        m = key[:-len(".weight_orig")]
+        _, u, v = R.spectral_norm_weight(sd0[key], sd0[m + ".weight_u"], sd0[m + ".weight_v"])
+        close(u, g[f"sd1.{m}.weight_u"], rtol=1e-5, atol=1e-7)
+        close(v, g[f"sd1.{m}.weight_v"], rtol=1e-5, atol=1e-7)
+    x = T(g["x"]).requires_grad_(True)
+    outs = R.period_discriminator(P, "d", x, 3, plan)
+    for j, o in enumerate(outs):
+        close(o, g[f"out.{j}"], rtol=1e-5, atol=1e-6)
+    sum((o * R_cot(o.shape, j)).sum() for j, o in enumerate(outs)).backward()
+    close(x.grad, g["grad_x"], rtol=1e-4, atol=1e-6)
+    for k, v in g.items():
+        if k.startswith("g."):
+            close(P["d." + k[2:]].grad, v, rtol=1e-4, atol=1e-6)
+
+
+def R_cot(shape, j):
+    """tests/golden/make_goldens.gan_cotangent(shape, 0, j)."""
+    return torch.randn(shape, generator=torch.Generator().manual_seed(j))
