@@ -334,3 +334,204 @@ int sel_adam_step_many_dev(const sel_adam_tensor* ts, int nt, double beta1, doub
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// BatchNorm1d over channels-last rows (models/autoencoder/modules/projector.py
+// :40-44, model='conv1d_bn': Conv1d then torch.nn.BatchNorm1d(code_dim)).
+// x is (rows, C) fp32 with rows = B*T (the (B, C, T) tensor stored as (B, T, C)).
+// Per-channel statistics: row chunks of kBnRows rows x 64-channel groups, each
+// thread one channel of one row lane, fp64 sums; the chunk partials are summed
+// in chunk order by one thread per channel (deterministic, no atomics).
+// ---------------------------------------------------------------------------
+namespace sel {
+namespace glue {
+
+constexpr int kBnRows = 256;   // rows per statistics chunk
+constexpr int kBnLanes = 4;    // row lanes per 64-channel group (256 threads)
+
+// mode 0: (sum x, sum x^2); mode 1: (sum gy, sum gy * (x - mean))
+__global__ __launch_bounds__(256) void k_bn_partials(const float* __restrict__ x, const float* __restrict__ gy,
+                                                     int64_t rows, int C, const float* __restrict__ mean, int mode,
+                                                     double* __restrict__ part) {
+  __shared__ double red[2][kBnLanes][64];
+  const int cl = threadIdx.x & 63, lane = threadIdx.x >> 6;
+  const int c = blockIdx.y * 64 + cl;
+  const int64_t r0 = int64_t(blockIdx.x) * kBnRows;
+  const int64_t r1 = r0 + kBnRows < rows ? r0 + kBnRows : rows;
+  double a = 0.0, b = 0.0;
+  if (c < C) {
+    const float mu = mode ? mean[c] : 0.f;
+    for (int64_t r = r0 + lane; r < r1; r += kBnLanes) {
+      const float v = x[r * C + c];
+      if (mode == 0) {
+        a += double(v);
+        b += double(v) * v;
+      } else {
+        const float g = gy[r * C + c];
+        a += double(g);
+        b += double(g) * double(v - mu);
+      }
+    }
+  }
+  red[0][lane][cl] = a;
+  red[1][lane][cl] = b;
+  __syncthreads();
+  if (lane == 0 && c < C) {
+    for (int l = 1; l < kBnLanes; ++l) {
+      a += red[0][l][cl];
+      b += red[1][l][cl];
+    }
+    part[(int64_t(blockIdx.x) * C + c) * 2] = a;
+    part[(int64_t(blockIdx.x) * C + c) * 2 + 1] = b;
+  }
+}
+
+// training statistics: mean, biased var -> invstd; running stats (torch's
+// momentum update with the unbiased variance, batch_norm.cpp)
+__global__ __launch_bounds__(256) void k_bn_stats(const double* __restrict__ part, int nchunk, int64_t rows, int C,
+                                                  float eps, float momentum, float* __restrict__ running_mean,
+                                                  float* __restrict__ running_var, float* __restrict__ save_mean,
+                                                  float* __restrict__ save_invstd) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0, ss = 0.0;
+  for (int k = 0; k < nchunk; ++k) {
+    s += part[(int64_t(k) * C + c) * 2];
+    ss += part[(int64_t(k) * C + c) * 2 + 1];
+  }
+  const double m = s / double(rows);
+  double var = ss / double(rows) - m * m;
+  var = var > 0.0 ? var : 0.0;
+  save_mean[c] = float(m);
+  save_invstd[c] = float(1.0 / sqrt(var + double(eps)));
+  if (running_mean) {
+    const double unb = rows > 1 ? var * double(rows) / double(rows - 1) : var;
+    running_mean[c] = float((1.0 - momentum) * double(running_mean[c]) + momentum * m);
+    running_var[c] = float((1.0 - momentum) * double(running_var[c]) + momentum * unb);
+  }
+}
+
+// evaluation statistics from the running buffers
+__global__ __launch_bounds__(256) void k_bn_eval_stats(const float* __restrict__ running_mean,
+                                                       const float* __restrict__ running_var, int C, float eps,
+                                                       float* __restrict__ save_mean, float* __restrict__ save_invstd) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  save_mean[c] = running_mean[c];
+  save_invstd[c] = float(1.0 / sqrt(double(running_var[c]) + double(eps)));
+}
+
+// y = (x - mean) * invstd * gamma + beta
+__global__ __launch_bounds__(256) void k_bn_apply(const float* __restrict__ x, int64_t n, int C,
+                                                  const float* __restrict__ mean, const float* __restrict__ invstd,
+                                                  const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                  float* __restrict__ y) {
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    const int c = int(i % C);
+    const float v = (x[i] - mean[c]) * invstd[c];
+    y[i] = gamma ? fmaf(v, gamma[c], beta ? beta[c] : 0.f) : v;
+  }
+}
+
+// gx = gamma invstd (gy - sum_gy / M - xhat sum(gy xhat) / M) (training), or
+// gamma invstd gy (evaluation); also d gamma = sum(gy xhat), d beta = sum(gy)
+__global__ __launch_bounds__(256) void k_bn_bwd(const float* __restrict__ x, const float* __restrict__ gy, int64_t n,
+                                                int C, int64_t rows, const float* __restrict__ mean,
+                                                const float* __restrict__ invstd, const float* __restrict__ gamma,
+                                                const double* __restrict__ part, int nchunk, int training,
+                                                float* __restrict__ gx) {
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    const int c = int(i % C);
+    const float is = invstd[c];
+    const float w = gamma ? gamma[c] : 1.f;
+    if (!training) {
+      gx[i] = gy[i] * is * w;
+      continue;
+    }
+    // the chunk sums were folded into part[0 .. 2C) by k_bn_gsum
+    const float sg = float(part[2 * c] / double(rows));
+    const float sgx = float(part[2 * c + 1] / double(rows)) * is * is;   // sum(gy (x - mu)) / M * invstd^2
+    gx[i] = w * is * (gy[i] - sg - (x[i] - mean[c]) * sgx);
+  }
+}
+
+// chunk partials -> per-channel totals (in place into chunk 0) and the affine gradients
+__global__ __launch_bounds__(256) void k_bn_gsum(double* __restrict__ part, int nchunk, int C,
+                                                 const float* __restrict__ invstd, float* __restrict__ ggamma,
+                                                 float* __restrict__ gbeta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0, sx = 0.0;
+  for (int k = 0; k < nchunk; ++k) {
+    s += part[(int64_t(k) * C + c) * 2];
+    sx += part[(int64_t(k) * C + c) * 2 + 1];
+  }
+  part[2 * c] = s;
+  part[2 * c + 1] = sx;
+  if (ggamma) ggamma[c] = float(sx * double(invstd[c]));
+  if (gbeta) gbeta[c] = float(s);
+}
+
+inline int bn_chunks(int64_t rows) { return int((rows + kBnRows - 1) / kBnRows); }
+inline int bn_grid(int64_t n) { return int(std::min<int64_t>(4096, (n + 255) / 256)); }
+
+}  // namespace glue
+}  // namespace sel
+
+extern "C" {
+
+size_t sel_batchnorm_workspace(int64_t rows, int C) {
+  return size_t(sel::glue::bn_chunks(rows)) * size_t(C) * 2 * sizeof(double);
+}
+
+int sel_batchnorm_fwd(const float* x, int64_t rows, int C, const float* gamma, const float* beta, int training,
+                      float eps, float momentum, float* running_mean, float* running_var, float* save_mean,
+                      float* save_invstd, float* y, void* ws, size_t ws_bytes, sel_stream_t stream) {
+  using namespace sel::glue;
+  SEL_REQUIRE(rows > 0 && C > 0 && x && y && save_mean && save_invstd, SEL_ERR_ARG, "bad batch-norm arguments");
+  SEL_REQUIRE(training || (running_mean && running_var), SEL_ERR_ARG, "evaluation needs the running statistics");
+  SEL_REQUIRE(!training || ws_bytes >= sel_batchnorm_workspace(rows, C), SEL_ERR_WORKSPACE, "workspace too small");
+  SEL_REQUIRE(bn_chunks(rows) < 65536 * 16, SEL_ERR_ARG, "batch too large");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int cb = (C + 255) / 256;
+  if (training) {
+    double* part = static_cast<double*>(ws);
+    hipLaunchKernelGGL(k_bn_partials, dim3(bn_chunks(rows), (C + 63) / 64), dim3(256), 0, s, x, nullptr, rows, C,
+                       nullptr, 0, part);
+    SEL_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_bn_stats, dim3(cb), dim3(256), 0, s, part, bn_chunks(rows), rows, C, eps, momentum,
+                       running_mean, running_var, save_mean, save_invstd);
+  } else {
+    hipLaunchKernelGGL(k_bn_eval_stats, dim3(cb), dim3(256), 0, s, running_mean, running_var, C, eps, save_mean,
+                       save_invstd);
+  }
+  SEL_LAUNCH_CHECK();
+  const int64_t n = rows * C;
+  hipLaunchKernelGGL(k_bn_apply, dim3(bn_grid(n)), dim3(256), 0, s, x, n, C, save_mean, save_invstd, gamma, beta, y);
+  SEL_LAUNCH_CHECK();
+  return SEL_OK;
+}
+
+int sel_batchnorm_bwd(const float* x, const float* gy, int64_t rows, int C, const float* gamma,
+                      const float* save_mean, const float* save_invstd, int training, float* gx, float* ggamma,
+                      float* gbeta, void* ws, size_t ws_bytes, sel_stream_t stream) {
+  using namespace sel::glue;
+  SEL_REQUIRE(rows > 0 && C > 0 && x && gy && save_mean && save_invstd, SEL_ERR_ARG, "bad batch-norm arguments");
+  SEL_REQUIRE(ws_bytes >= sel_batchnorm_workspace(rows, C), SEL_ERR_WORKSPACE, "workspace too small");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  double* part = static_cast<double*>(ws);
+  const int nc = bn_chunks(rows);
+  hipLaunchKernelGGL(k_bn_partials, dim3(nc, (C + 63) / 64), dim3(256), 0, s, x, gy, rows, C, save_mean, 1, part);
+  SEL_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_bn_gsum, dim3((C + 255) / 256), dim3(256), 0, s, part, nc, C, save_invstd, ggamma, gbeta);
+  SEL_LAUNCH_CHECK();
+  if (gx) {
+    const int64_t n = rows * C;
+    hipLaunchKernelGGL(k_bn_bwd, dim3(bn_grid(n)), dim3(256), 0, s, x, gy, n, C, rows, save_mean, save_invstd, gamma,
+                       part, nc, training, gx);
+    SEL_LAUNCH_CHECK();
+  }
+  return SEL_OK;
+}
+
+}  // extern "C"

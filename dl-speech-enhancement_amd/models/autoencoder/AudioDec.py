@@ -33,8 +33,10 @@ class Generator(torch.nn.Module):
                                    model=quantier)
         # the quantizer works in fp32 (ResidualVQFn): the projector's conv writes
         # z as fp32 from its epilogue instead of bf16 + a cast launch each way
-        if hasattr(self.projector.project, "out_float"):
-            self.projector.project.out_float = True
+        conv = self.projector.project
+        conv = conv[0] if isinstance(conv, torch.nn.Sequential) else conv   # 'conv1d_bn': the BN reads fp32
+        if hasattr(conv, "out_float"):
+            conv.out_float = True
 
     def _flatten_channels(self, x):
         B, C, T = x.size()

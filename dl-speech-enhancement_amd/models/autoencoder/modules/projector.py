@@ -2,6 +2,7 @@
 import torch
 
 from layers.conv_layer import CausalConv1d, NonCausalConv1d
+from sel.bnops import BatchNorm1d
 
 
 class Projector(torch.nn.Module):
@@ -12,9 +13,14 @@ class Projector(torch.nn.Module):
         Conv = {"causal": CausalConv1d, "noncausal": NonCausalConv1d}.get(mode)
         if Conv is None:
             raise NotImplementedError(f"Mode ({mode}) is not supported!")
-        if model != "conv1d":
+        if model == "conv1d":
+            self.project = Conv(input_channels, code_dim, kernel_size=kernel_size, stride=stride, bias=bias)
+        elif model == "conv1d_bn":   # (:40-44) the conv, then BatchNorm1d on the HIP kernels (sel.bnops)
+            self.project = torch.nn.Sequential(
+                Conv(input_channels, code_dim, kernel_size=kernel_size, stride=stride, bias=bias),
+                BatchNorm1d(code_dim))
+        else:
             raise NotImplementedError(f"Model ({model}) is not supported!")
-        self.project = Conv(input_channels, code_dim, kernel_size=kernel_size, stride=stride, bias=bias)
 
     def forward(self, x):
         return self.project(x)

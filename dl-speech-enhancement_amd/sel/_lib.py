@@ -77,6 +77,9 @@ SIGNATURES = {
     "sel_mix_noise": (I32, [P, P, I64, P, F32, P, P]),
     "sel_snr_fwd": (I32, [P, P, I64, I64, P, P, P]),
     "sel_snr_bwd": (I32, [P, P, I64, I64, P, P, P, P]),
+    "sel_batchnorm_workspace": (SZ, [I64, I32]),
+    "sel_batchnorm_fwd": (I32, [P, I64, I32, P, P, I32, F32, F32, P, P, P, P, P, P, SZ, P]),
+    "sel_batchnorm_bwd": (I32, [P, P, I64, I32, P, P, P, I32, P, P, P, P, SZ, P]),
     "sel_resample_plan": (I32, [I32, I32, I32, F32, P, P]),
     "sel_resample_out_len": (I64, [I64, I32, I32]),
     "sel_resample_kernel": (I32, [I32, I32, I32, F32, P]),

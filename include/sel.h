@@ -310,6 +310,23 @@ int sel_sumsq2(const float* speech, const float* noise, int64_t n, double* sums2
 int sel_mix_noise(const float* speech, const float* noise, int64_t n, const double* sums2, float snr,
                   float* out, sel_stream_t stream);
 
+/* ---- BatchNorm1d (models/autoencoder/modules/projector.py:40-44, model='conv1d_bn';
+ * replaces torch.nn.BatchNorm1d.forward / its autograd backward) -------------
+ * x, y, gy, gx: (rows, C) fp32 channels-last (rows = B*T).  training: batch
+ * statistics (biased variance for the normalisation; running_mean / running_var,
+ * when given, updated with `momentum` and the unbiased variance, as torch);
+ * otherwise the running statistics.  save_mean / save_invstd (C floats) are
+ * written by the forward and read by the backward.  gamma / beta may be null
+ * (affine=False); ggamma / gbeta / gx may be null (not wanted).  ws: at least
+ * sel_batchnorm_workspace(rows, C) bytes. */
+size_t sel_batchnorm_workspace(int64_t rows, int C);
+int sel_batchnorm_fwd(const float* x, int64_t rows, int C, const float* gamma, const float* beta, int training,
+                      float eps, float momentum, float* running_mean, float* running_var, float* save_mean,
+                      float* save_invstd, float* y, void* ws, size_t ws_bytes, sel_stream_t stream);
+int sel_batchnorm_bwd(const float* x, const float* gy, int64_t rows, int C, const float* gamma,
+                      const float* save_mean, const float* save_invstd, int training, float* gx, float* ggamma,
+                      float* gbeta, void* ws, size_t ws_bytes, sel_stream_t stream);
+
 /* ---- optimizer step (trainer/trainerGAN.py:271-281 optimizer.step()) ---- */
 /* Adam update (torch.optim.Adam semantics: L2 weight decay, no amsgrad /
  * maximize) of nt fp32 tensors in one launch: per element, g += wd p;

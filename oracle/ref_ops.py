@@ -295,12 +295,38 @@ def decoder_forward(P, z, geo, pqc=True, dilations=(1, 3, 9), mode="causal"):
     return conv(h, P["decoder.conv2.conv.weight"])
 
 
-def generator_forward(P, x, geo, pqc=True, codebook_num=8, mode="causal"):
-    """AudioDec.py:95-103 (PQC) or autoencoder_without_PQC/AudioDec.py:94-100."""
+def batch_norm1d(x, w, b, running_mean, running_var, training=True, momentum=0.1, eps=1e-5):
+    """torch.nn.BatchNorm1d on (B, C, T) (projector.py:40-44, model='conv1d_bn'),
+    restated: training normalises with the batch mean and biased variance and
+    returns the momentum-updated running statistics (unbiased variance);
+    evaluation uses the running statistics.  Returns (y, running_mean', running_var')."""
+    if training:
+        n = x.shape[0] * x.shape[2]
+        mean = x.mean((0, 2))
+        var = ((x - mean.view(1, -1, 1)) ** 2).mean((0, 2))
+        with torch.no_grad():
+            rm = (1 - momentum) * running_mean + momentum * mean
+            rv = (1 - momentum) * running_var + momentum * var * n / (n - 1)
+    else:
+        mean, var, rm, rv = running_mean, running_var, running_mean, running_var
+    y = (x - mean.view(1, -1, 1)) / torch.sqrt(var.view(1, -1, 1) + eps)
+    return y * w.view(1, -1, 1) + b.view(1, -1, 1), rm, rv
+
+
+def generator_forward(P, x, geo, pqc=True, codebook_num=8, mode="causal", training=True):
+    """AudioDec.py:95-103 (PQC) or autoencoder_without_PQC/AudioDec.py:94-100.
+    A 'conv1d_bn' projector (projector.project.1.* keys) runs its BatchNorm1d in
+    `training` mode; the updated running statistics are written back into P."""
     h = encoder_forward(P, x, geo, mode=mode)
     if not pqc:
         return decoder_forward(P, h, geo, pqc=False, mode=mode)
-    z = _conv(mode)(h, P["projector.project.conv.weight"])
+    if "projector.project.1.weight" in P:
+        z = _conv(mode)(h, P["projector.project.0.conv.weight"])
+        pre = "projector.project.1"
+        z, P[pre + ".running_mean"], P[pre + ".running_var"] = batch_norm1d(
+            z, P[pre + ".weight"], P[pre + ".bias"], P[pre + ".running_mean"], P[pre + ".running_var"], training)
+    else:
+        z = _conv(mode)(h, P["projector.project.conv.weight"])
     embeds = [P[f"quantizer.codebook.layers.{i}.embed"] for i in range(codebook_num)]
     zq, vql, ppl, _ = rvq_forward(z.transpose(2, 1), embeds)
     zq = zq.transpose(2, 1)

@@ -412,6 +412,24 @@ def make_general(ref, clean, noise, out):
         d.update(_grads(G))
         np.savez_compressed(os.path.join(out, f"generator_noncausal_{tag}.npz"), **d)
 
+    # projector model='conv1d_bn' (projector.py:40-44): BatchNorm1d in training mode, then evaluation
+    torch.manual_seed(93)
+    G = importlib.import_module("models.autoencoder.AudioDec").Generator(projector="conv1d_bn", **gp)
+    G.quantizer.codebook.eval()
+    d = {"x_noisy": _np(xn), "x_clean": _np(xc)}
+    d.update(_sd(G))
+    y, zq, z, vql, ppl = G(xn)
+    loss = 45.0 * mel(y, xc) + vql.sum()
+    d.update({"y": _np(y), "zq": _np(zq), "z": _np(z), "vqloss": _np(vql), "loss": _np(loss)})
+    loss.backward()
+    d.update(_grads(G))
+    d.update(_sd(G, "sd1."))
+    G.eval()
+    with torch.no_grad():
+        y, zq, z, vql, ppl = G(xn)
+    d.update({"eval.y": _np(y), "eval.z": _np(z)})
+    np.savez_compressed(os.path.join(out, "generator_bn.npz"), **d)
+
     # spectral-normalised period discriminator, training mode (one power iteration per call)
     _install_trainer_stubs()
     disc = importlib.import_module("models.vocoder.modules.discriminator")

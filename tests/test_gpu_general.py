@@ -192,3 +192,79 @@ def test_grouped_causal_conv_streaming_vs_oracle(gpu):
             else:
                 yr = R.stream_conv_transpose1d(S, "k", xc, w, b, **kw)
             nclose(y, yr, 1e-5, f"{kind}{kw}.{c}")
+
+
+def test_conv1d_bn_projector_generator_matches_reference_golden(gpu):
+    """Generator(projector='conv1d_bn'): the projector's BatchNorm1d on the HIP
+    kernels (sel_batchnorm_fwd / _bwd) in training mode — outputs, gradients,
+    running statistics, num_batches_tracked — then in evaluation."""
+    from losses import MultiMelSpectrogramLoss
+    from models.autoencoder.AudioDec import Generator
+    g = golden("generator_bn")
+    G = Generator(projector="conv1d_bn", encode_channels=4, decode_channels=4, code_dim=64, codebook_num=2,
+                  codebook_size=64)
+    sd = {k[3:]: torch.from_numpy(v) for k, v in g.items() if k.startswith("sd.")}
+    assert set(sd) == set(G.state_dict()), set(sd) ^ set(G.state_dict())
+    G.load_state_dict(sd)
+    G = G.to(gpu)
+    G.quantizer.codebook.eval()
+    mel = MultiMelSpectrogramLoss(fs=24000, fft_sizes=[2048], hop_sizes=[300], win_lengths=[None],
+                                  num_mels=80, fmin=0, fmax=24000, log_base=None).to(gpu)
+    xn = torch.from_numpy(g["x_noisy"]).to(gpu)
+    xc = torch.from_numpy(g["x_clean"]).to(gpu)
+    y, zq, z, vql, ppl = G(xn)
+    nclose(z, g["z"], 1e-5, "z")
+    nclose(y, g["y"], 1e-5, "y")
+    loss = 45.0 * mel(y, xc) + vql.sum()
+    nclose(loss, g["loss"], 1e-4, "loss")
+    loss.backward()
+    for name, p in G.named_parameters():
+        if "g." + name in g:
+            nclose(p.grad, g["g." + name], 5e-3, name)
+    for k, v in G.state_dict().items():
+        if "project.1." in k:
+            nclose(v, g["sd1." + k], 1e-6, k)
+    G.eval()
+    with torch.no_grad():
+        y, zq, z, vql, ppl = G(xn)
+    nclose(z, g["eval.z"], 1e-5, "eval.z")
+    nclose(y, g["eval.y"], 1e-5, "eval.y")
+
+
+@pytest.mark.parametrize("shape", [(4, 64, 80), (3, 5, 1), (2, 130, 333)])
+def test_batchnorm_vs_torch(gpu, shape):
+    """sel BatchNorm1d against torch.nn.BatchNorm1d (fp32, the module the
+    reference uses) in both modes, with ragged channel counts and T = 1."""
+    from sel.bnops import BatchNorm1d
+    B, C, T = shape
+    torch.manual_seed(5)
+    ref = torch.nn.BatchNorm1d(C).to(gpu)
+    with torch.no_grad():
+        ref.weight.uniform_(0.5, 1.5)
+        ref.bias.uniform_(-0.5, 0.5)
+    m = BatchNorm1d(C).to(gpu)
+    m.load_state_dict(ref.state_dict())
+    for step in range(2):
+        x = (3.0 * torch.randn(B, C, T, device=gpu) + 1.0)
+        xa, xb = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
+        ya, yb = m(xa), ref(xb)
+        nclose(ya, yb, 1e-5, f"y{step}")
+        r = torch.randn_like(yb)
+        (ya * r).sum().backward()
+        (yb * r).sum().backward()
+        nclose(xa.grad, xb.grad, 1e-5, f"gx{step}")
+        nclose(m.weight.grad, ref.weight.grad, 1e-5, "gw")
+        nclose(m.bias.grad, ref.bias.grad, 1e-5, "gb")
+        m.zero_grad()
+        ref.zero_grad()
+    for k, v in ref.state_dict().items():
+        nclose(m.state_dict()[k], v, 1e-6, k)
+    m.eval()
+    ref.eval()
+    x = torch.randn(B, C, T, device=gpu, requires_grad=True)
+    x2 = x.detach().clone().requires_grad_(True)
+    ya, yb = m(x), ref(x2)
+    nclose(ya, yb, 1e-6, "eval.y")
+    ya.sum().backward()
+    yb.sum().backward()
+    nclose(x.grad, x2.grad, 1e-6, "eval.gx")

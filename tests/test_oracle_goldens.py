@@ -456,3 +456,33 @@ def test_spectral_norm_period_discriminator():
 def R_cot(shape, j):
     """tests/golden/make_goldens.gan_cotangent(shape, 0, j)."""
     return torch.randn(shape, generator=torch.Generator().manual_seed(j))
+
+
+def test_conv1d_bn_projector_generator():
+    """Generator(projector='conv1d_bn') (projector.py:40-44): BatchNorm1d in
+    training mode (outputs, gradients, running statistics), then evaluation."""
+    g = golden("generator_bn")
+    gm = golden("melmat")
+    P = {k[3:]: T(v) for k, v in g.items() if k.startswith("sd.")}
+    for k, v in P.items():
+        if v.dtype == torch.float32 and not k.endswith(("pad_buffer", "embed", "cluster_size", "embed_avg",
+                                                         "running_mean", "running_var")):
+            v.requires_grad_(True)
+    geo = R.generator_geometry(encode_channels=4, decode_channels=4)
+    xn, xc = T(g["x_noisy"]), T(g["x_clean"])
+    mm = T(gm["melmat.24k_fmax24000"])
+    y, zq, z, vql, ppl = R.generator_forward(P, xn, geo, pqc=True, codebook_num=2)
+    close(z, g["z"], rtol=1e-5, atol=1e-5)
+    close(y, g["y"], rtol=1e-5, atol=1e-5)  # BN divides by the batch std
+    loss = 45.0 * R.multi_mel_loss(y, xc, [(2048, 300, 2048)], [R.hann(2048)], [mm], 1e-10, None) + vql.sum()
+    close(loss, g["loss"], rtol=1e-5)
+    loss.backward()
+    for k, v in g.items():
+        if k.startswith("g."):
+            close(P[k[2:]].grad, v, rtol=1e-4, atol=1e-5)
+    for k in ("running_mean", "running_var"):
+        close(P[f"projector.project.1.{k}"], g[f"sd1.projector.project.1.{k}"], rtol=1e-5, atol=1e-7)
+    with torch.no_grad():
+        y, zq, z, vql, ppl = R.generator_forward(P, xn, geo, pqc=True, codebook_num=2, training=False)
+    close(z, g["eval.z"], rtol=1e-5, atol=1e-5)
+    close(y, g["eval.y"], rtol=1e-5, atol=1e-5)
