@@ -268,3 +268,41 @@ def test_batchnorm_vs_torch(gpu, shape):
     ya.sum().backward()
     yb.sum().backward()
     nclose(x.grad, x2.grad, 1e-6, "eval.gx")
+
+
+def _full_noncausal(dev, B=2, T=2400, seed=93):
+    from models.autoencoder_without_PQC.AudioDec import Generator
+    from oracle import ref_ops as R
+    torch.manual_seed(seed)
+    G = Generator(mode="noncausal")
+    P = {k: v.clone() for k, v in G.state_dict().items()}
+    for k, v in P.items():
+        if k.endswith("weight") or k.endswith("bias"):
+            v.requires_grad_(True)
+    x = 0.1 * torch.randn(B, 1, T)
+    y = R.generator_forward(P, x, R.generator_geometry(), pqc=False, mode="noncausal")
+    r = torch.randn_like(y)
+    (y * r).sum().backward()
+    return G.to(dev), x, r, y, P
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_full_width_noncausal_generator_vs_oracle(gpu, dtype):
+    """The full-width noncausal generator (32 -> 512 channels: the residual units
+    on the unfused primitive with the symmetric pad, the k = 2s stride-s
+    noncausal down convs and transposed up convs through sel.genconv) against
+    the fp32 oracle; bounds as tests/test_gpu_model.py's causal full-width tests."""
+    from sel import convops as CO
+    G, x, r, y_ref, P = _full_noncausal(gpu)
+    prec = torch.float32 if dtype == "fp32" else torch.bfloat16
+    ty, tg = (1e-4, 1e-3) if dtype == "fp32" else (5e-2, 1e-1)
+    with CO.precision(prec):
+        y = G(x.to(gpu))
+        nclose(y, y_ref, ty, "y")
+        (y.float() * r.to(gpu)).sum().backward()
+    n = 0
+    for name, p in G.named_parameters():
+        if P[name].grad is not None:
+            nclose(p.grad, P[name].grad, tg, name)
+            n += 1
+    assert n > 50
