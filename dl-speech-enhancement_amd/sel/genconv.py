@@ -111,6 +111,19 @@ def _rows(x, w, b, dil, pad, T_out):
     return y if y.shape[1] == T_out else y[:, :T_out]
 
 
+_POS = {}
+
+
+def _positions(pos, device):
+    """Device index tensor of the phase-fold tap positions, made once per layer
+    geometry (no host-to-device copy per call: capturable in a HIP graph)."""
+    key = (pos, str(device))
+    t = _POS.get(key)
+    if t is None:
+        t = _POS[key] = torch.tensor(pos, dtype=torch.int64, device=device)
+    return t
+
+
 def _dense(w, groups):
     """Grouped torch weight (N, C/g, K) -> block-diagonal (N, C, K)."""
     if groups == 1:
@@ -138,7 +151,7 @@ def conv1d(x, w, b, stride=1, pad_left=0, dilation=1, groups=1, T_out=None):
     q = [o // s for o in offs]          # row offset (floor) and phase of every tap
     j = [o % s for o in offs]
     qmin, kp = min(q), max(q) - min(q) + 1
-    pos = torch.tensor([(qk - qmin) * s + jk for qk, jk in zip(q, j)], device=w.device)
+    pos = _positions(tuple((qk - qmin) * s + jk for qk, jk in zip(q, j)), w.device)
     wf = wd.new_zeros(N, kp * s, C).index_copy(1, pos, wd.permute(0, 2, 1))
     wf = wf.view(N, kp, s * C).permute(0, 2, 1)            # (N, s*C, kp)
     tf = max(-(-T // s), 1)
