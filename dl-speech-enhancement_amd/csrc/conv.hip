@@ -2160,6 +2160,138 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 128 ? 
   }
 }
 
+// k_ru32_fwd at four blocks per CU (tune key 70 = 1; round 6): the conv1
+// weights live in LDS (one A-fragment ds_read_b128 per MFMA instead of 56
+// VGPRs), ELU(x) rows are 64 B with their 16-B slots XOR-swizzled by
+// (row >> 2) & 3 (the 16 rows of every ds_read_b128 lane group hit 16 distinct
+// bank groups), and the residual rows are re-read from global memory (staged
+// one tile earlier: L2-hot) instead of a raw LDS plane.  35 KB of LDS and at
+// most 128 VGPRs: four blocks per CU instead of three keep a third more tiles'
+// loads in flight.  Same operands, MFMA order and epilogue as k_ru32_fwd:
+// bit-identical.
+constexpr int RU4_WP = RU_K * RU_C + 8;  // bf16 pitch of a W1 row in LDS (464 B: conflict-free A reads)
+__device__ __forceinline__ int ru4_swz(int row) { return (row >> 2) & 3; }
+
+template <int R>
+struct Ru32F4 {
+  static constexpr int SPAN = R + F4_HALOMAX;
+  static constexpr int TM = R / 128;
+  static constexpr size_t LDS = size_t(SPAN) * RU_C * 2 + size_t(RU_C) * RU4_WP * 2;
+};
+
+template <int R>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_ru32_fwd4(
+    Args a, const __bf16* __restrict__ x, const __bf16* __restrict__ w1p, const float* __restrict__ b1,
+    const __bf16* __restrict__ w2p, const float* __restrict__ b2, __bf16* __restrict__ hout,
+    __bf16* __restrict__ out, int tiles_per_block) {
+  using G = Ru32F4<R>;
+  extern __shared__ __align__(16) unsigned char smem[];
+  __bf16* const xs = reinterpret_cast<__bf16*>(smem);  // [SPAN][32]: ELU(x) rows t0 - pad .., swizzled slots
+  __bf16* const wsm = xs + G::SPAN * RU_C;             // [32][RU4_WP]: W1 rows (packed [n][k][c])
+  const int lane = threadIdx.x & 63, hl = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int span = R + a.pad;
+  const int tps = (a.T + R - 1) / R;
+  int64_t tile0, tile_end;
+  if (!ru_tiles((a.rows / a.T) * tps, tiles_per_block, tile0, tile_end)) return;
+
+  for (int i = threadIdx.x; i < RU_C * RU_K * RU_C / 8; i += 256) {
+    const int n = i / (RU_K * RU_C / 8), r = i % (RU_K * RU_C / 8);
+    *reinterpret_cast<uint4*>(wsm + n * RU4_WP + 8 * r) =
+        *reinterpret_cast<const uint4*>(w1p + int64_t(n) * RU_K * RU_C + 8 * r);
+  }
+  bf16x8 w2f[1][2];
+  ru_wfrags<1>(w2p, w2f);
+  ws_wait_vm<0>();  // weights landed: the tile loop's waits then count only its own loads
+
+  __shared__ __align__(16) float bsm[2][RU_C];
+  if (threadIdx.x < 2 * RU_C) {
+    const int i = threadIdx.x;
+    const float* bp = i < RU_C ? b1 : b2;
+    bsm[i / RU_C][i % RU_C] = bp ? bp[i % RU_C] : 0.f;
+  }
+  const __bf16* const wrow = wsm + (lane & 31) * RU4_WP + 8 * hl;
+  Ru32Stage<R> st;
+  st.load(a, x, tile0 / tps, int(tile0 % tps) * R, -a.pad, span);
+  ru_dummy_stores<4 * G::TM>(out);  // the loop's h / out stores after each prefetch
+  for (int64_t tile = tile0; tile < tile_end; ++tile) {
+    const int64_t b = tile / tps;
+    const int t0 = int(tile % tps) * R;
+    const int mrows = a.T - t0 < R ? a.T - t0 : R;
+    __syncthreads();  // every wave is done with the previous tile's rows (and W1 / biases staged)
+#pragma unroll
+    for (int u = 0; u < Ru32<R>::XV; ++u) {
+      const int v = threadIdx.x + u * 256;
+      const int row = v >> 2, slot = v & 3;
+      if (row >= span) continue;
+      const uint4 val = elu8(st.ok[u] ? st.r[u] : make_uint4(0, 0, 0, 0));
+      *reinterpret_cast<uint4*>(xs + row * RU_C + 8 * (slot ^ ru4_swz(row))) = val;
+    }
+    __syncthreads();
+    {  // unconditional (a dead request loads nothing): exact counts
+      const bool live = tile + 1 < tile_end;
+      const int64_t nt = live ? tile + 1 : tile;
+      st.load(a, x, nt / tps, int(nt % tps) * R, -a.pad, span, live);
+    }
+    const __amdgpu_buffer_rsrc_t rh = ru_rsrc(hout + b * a.T * RU_C, int64_t(a.T) * RU_C);
+    const __amdgpu_buffer_rsrc_t ro = ru_rsrc(out + b * a.T * RU_C, int64_t(a.T) * RU_C);
+#pragma unroll
+    for (int i = 0; i < G::TM; ++i) {
+      const int lr = wave * (R / 4) + i * 32 + (lane & 31);  // this lane's row in the tile
+      const bool valid = lr < mrows;
+      const int off = ((t0 + lr) * RU_C + 8 * hl) * 2;
+      // the residual rows (raw x), requested before conv1: branch-free, clamped row
+      const int64_t orow = (b * a.T + t0 + (valid ? lr : 0)) * RU_C;
+      uint2 xres[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) xres[q] = *reinterpret_cast<const uint2*>(x + orow + 8 * q + 4 * hl);
+      floatx16 acc;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+#pragma unroll
+      for (int k = 0; k < RU_K; ++k) {
+        const int row = lr + k * a.dil;
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+          const bf16x8 af = *reinterpret_cast<const bf16x8*>(wrow + k * RU_C + 16 * g);
+          const bf16x8 bf = *reinterpret_cast<const bf16x8*>(xs + row * RU_C + 8 * ((2 * g + hl) ^ ru4_swz(row)));
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf, acc, 0, 0, 0);
+        }
+      }
+      float v[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const floatx4 bq = *reinterpret_cast<const floatx4*>(&bsm[0][8 * q + 4 * hl]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[4 * q + e] = acc[4 * q + e] + bq[e];
+      }
+      bf16x8 hf[2];
+      ru_acc_to_frags(v, hf);
+      ru_bstore<SEL_RU_FWD_HNT>(rh, valid ? off : RU_OOB, hf[0]);
+      ru_bstore<SEL_RU_FWD_HNT>(rh, valid ? off + 32 : RU_OOB, hf[1]);
+      floatx16 acc2;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc2[e] = 0.f;
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        const bf16x8 ef = __builtin_bit_cast(bf16x8, elu8(__builtin_bit_cast(uint4, hf[g])));
+        acc2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w2f[0][g], ef, acc2, 0, 0, 0);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const __bf16* rv = reinterpret_cast<const __bf16*>(&xres[q]);
+        const floatx4 bq = *reinterpret_cast<const floatx4*>(&bsm[1][8 * q + 4 * hl]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[4 * q + e] = acc2[4 * q + e] + bq[e] + float(rv[e]);
+      }
+      bf16x8 of[2];
+      ru_acc_to_frags(v, of);
+      ru_bstore<SEL_RU_FWD_ONT>(ro, valid ? off : RU_OOB, of[0]);
+      ru_bstore<SEL_RU_FWD_ONT>(ro, valid ? off + 32 : RU_OOB, of[1]);
+    }
+  }
+}
+
 // Residual unit at 64 channels, forward in ONE launch (round 3): the 32-channel
 // scheme with the 1x1 still fed from registers, but a wave computes conv1 for
 // one 32-channel output slice only (all 64 x 7 input fragments of its slice in
@@ -5270,6 +5402,29 @@ int launch_ru32_fwd(const Args& a, const void* x, const void* w1p, const float* 
   return SEL_OK;
 }
 
+int launch_ru32_fwd4(const Args& a, const void* x, const void* w1p, const float* b1, const void* w2p,
+                     const float* b2, void* h, void* out, hipStream_t s) {
+  constexpr int R = 256;
+  const int64_t ntiles = (a.rows / a.T) * ((a.T + R - 1) / R);
+  if (ntiles == 0) return SEL_OK;
+  static const int64_t slots = [] {
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_ru32_fwd4<R>, 256, Ru32F4<R>::LDS) != hipSuccess)
+      return int64_t(0);
+    return int64_t(cus) * per_cu / 8 * 8;
+  }();
+  const int64_t target = slots > 0 ? slots : 1024;
+  const int64_t tpb = std::max<int64_t>(1, (ntiles + target - 1) / target);
+  const unsigned nb = unsigned(((ntiles + tpb - 1) / tpb + 7) / 8 * 8);
+  hipLaunchKernelGGL(k_ru32_fwd4<R>, dim3(nb), dim3(256), Ru32F4<R>::LDS, s, a, static_cast<const __bf16*>(x),
+                     static_cast<const __bf16*>(w1p), b1, static_cast<const __bf16*>(w2p), b2,
+                     static_cast<__bf16*>(h), static_cast<__bf16*>(out), int(tpb));
+  SEL_LAUNCH_CHECK();
+  return SEL_OK;
+}
+
 template <int R>
 int launch_ru64_fwd(const Args& a, const void* x, const void* w1p, const float* b1, const void* w2p,
                     const float* b2, void* h, void* out, hipStream_t s) {
@@ -5802,6 +5957,8 @@ int sel_resunit_fwd(const sel_conv_desc* d1, int dtype, const void* x, const voi
   // tune key 56 = 1: 128-row tiles (4 resident workgroups per CU instead of 3):
   // 66-67 -> 58.6-59 us per unit in tools/ru_bench.py, which re-reads the same
   // input, but 69.5 -> 72.6 us inside the profiled C3 step, so off
+  // tune key 70 = 1: k_ru32_fwd4 (W1 in LDS, four blocks per CU; bit-identical)
+  if (a.C == 32 && tune(70) == 1 && tune(56) != 1) return launch_ru32_fwd4(a, x, w1pack, b1, w2pack, b2, h, out, s);
   if (a.C == 32)
     return tune(56) == 1 ? launch_ru32_fwd<128>(a, x, w1pack, b1, w2pack, b2, h, out, s)
                          : launch_ru32_fwd<256>(a, x, w1pack, b1, w2pack, b2, h, out, s);

@@ -538,6 +538,7 @@ def test_thin_kernel_multi_tile_loops(gpu, shape, epi):
 # (C, dil, bias, B, T): the fused residual-unit forward's instances at the
 # AudioDec dilations, ragged tails (T not a multiple of the tile rows) and T < halo
 RU_SHAPES = [(32, 1, 0, 2, 1000), (32, 3, 0, 3, 777), (32, 9, 1, 2, 1000), (32, 9, 0, 2, 40),
+             (32, 9, 1, 64, 24000),   # the C3 size (k_ru32_fwd4 under key 70 too)
              (64, 1, 0, 2, 500), (64, 3, 1, 3, 333), (64, 9, 0, 2, 260), (64, 9, 1, 2, 40),
              (64, 9, 1, 8, 8000),
              # 128 channels: k_conv_wss<7, 16, 128> with the 1x1 in its epilogue (round 6,
@@ -581,6 +582,17 @@ def test_fused_residual_unit_matches_two_calls(gpu, shape, monkeypatch):
     # k_ru32_fwd / k_ru64_fwd / k_conv_wss RU: same MFMA order and rounding points as the two calls
     assert torch.equal(h, h_ref), (h.float() - h_ref.float()).abs().max().item()
     assert torch.equal(out, out_ref), (out.float() - out_ref.float()).abs().max().item()
+    if C == 32:
+        # k_ru32_fwd4 (tune key 70 = 1: W1 in LDS, swizzled ELU(x) rows, residual
+        # re-read from global memory): the same operands and MFMA order, same bits
+        from sel import _lib as Lb
+        p70 = Lb.lib().sel_tune(70, 1)
+        try:
+            h4, out4 = CO.resunit_fwd(d1, x, wp1, b1, wp2, b2)
+        finally:
+            Lb.lib().sel_tune(70, p70)
+        assert torch.equal(h4, h_ref), (h4.float() - h_ref.float()).abs().max().item()
+        assert torch.equal(out4, out_ref), (out4.float() - out_ref.float()).abs().max().item()
     if C == 64:
         # the round-2 LDS-staged instance (tune key 24 = -1): within one bf16 ulp norm-wise
         from sel import _lib as Lb
