@@ -495,9 +495,9 @@ def stft_kernel_roofline(dev, B=2048):
     dst = torch.empty_like(src)
     cus = torch.cuda.get_device_properties(dev).multi_processor_count
 
-    def timed(fn, iters=5):
-        """mean of per-launch event pairs (back-to-back Python launches leave host
-        gaps between short kernels that one pair around a loop would count)"""
+    def launches(fn, iters=15):
+        """per-launch event-pair times in s (back-to-back Python launches leave
+        host gaps between short kernels that one pair around a loop would count)"""
         for _ in range(2):
             fn()
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(iters)]
@@ -506,21 +506,35 @@ def stft_kernel_roofline(dev, B=2048):
             fn()
             e1.record()
         torch.cuda.synchronize()
-        return sum(e0.elapsed_time(e1) for e0, e1 in ev) / iters * 1e-3
+        return [e0.elapsed_time(e1) * 1e-3 for e0, e1 in ev]
+
+    def timed(fn):
+        """median of 15 launches: the sustained rate.  The |X| kernel slows under
+        back-to-back load while the copy probe stays flat (tools/stft_clock_trace.py,
+        profiles/r6_stft_launch_trace.txt: ~256 us for the first launches, up to
+        ~360 around the tenth, ~305-315 after forty; consistent with a power /
+        clock limit on the VALU-heavy FFT), so the round-5 protocol (mean of the
+        first five timed launches) is kept beside it as the burst rate."""
+        ts = launches(fn)
+        return sorted(ts)[len(ts) // 2], sum(ts[:5]) / 5
 
     copy_bytes = 2 * src.numel() * 4
-    t_torch = timed(lambda: dst.copy_(src))
-    t_f4 = timed(lambda: L.call("sel_probe_copy_f4", L.ptr(src), L.ptr(dst), src.numel() // 4, 8 * cus, L.stream()))
+    t_torch = timed(lambda: dst.copy_(src))[0]
+    t_f4 = timed(lambda: L.call("sel_probe_copy_f4", L.ptr(src), L.ptr(dst), src.numel() // 4, 8 * cus, L.stream()))[0]
     torch_gbs, f4_gbs = copy_bytes / t_torch / 1e9, copy_bytes / t_f4 / 1e9
     del src, dst
-    t = timed(lambda: L.call("sel_stft_mag_fwd", L.ptr(x), B, T, n, h, w, L.ptr(win), 1e-7, L.ptr(mag), L.stream()))
+    t, t_burst = timed(lambda: L.call("sel_stft_mag_fwd", L.ptr(x), B, T, n, h, w, L.ptr(win), 1e-7, L.ptr(mag),
+                                      L.stream()))
     nbytes = 4 * B * (T + F * K)
     gbs = nbytes / t / 1e9
     return {"kernel": "k_stft_mag_fwd<10>", "shape": f"B={B} x {T}, n_fft/hop/win {n}/{h}/{w}",
-            "avg_launch_us": round(t * 1e6, 1), "alg_bytes": nbytes, "achieved": round(gbs, 1), "unit": "GB/s",
+            "median_launch_us": round(t * 1e6, 1), "launches": 15, "alg_bytes": nbytes, "achieved": round(gbs, 1),
+            "unit": "GB/s",
             "frac_of_spec": round(gbs / HBM_PEAK_GBS, 4),
             "copy_f4_GBs": round(f4_gbs, 1), "frac_of_copy_f4": round(gbs / f4_gbs, 4),
-            "torch_copy_GBs": round(torch_gbs, 1), "frac_of_torch_copy": round(gbs / torch_gbs, 4)}
+            "torch_copy_GBs": round(torch_gbs, 1), "frac_of_torch_copy": round(gbs / torch_gbs, 4),
+            "burst": {"mean_first5_us": round(t_burst * 1e6, 1),
+                      "frac_of_copy_f4": round(nbytes / t_burst / 1e9 / f4_gbs, 4)}}
 
 
 def launch_cmd(n, port, argv):

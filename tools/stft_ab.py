@@ -23,7 +23,7 @@ def main():
             r = bench.stft_kernel_roofline(dev)
             for k, v in prev:
                 lib.sel_tune(k, v)
-            print(rnd, spec, r["avg_launch_us"], "us", r["achieved"], "GB/s", "frac_of_copy_f4", r["frac_of_copy_f4"],
+            print(rnd, spec, r["median_launch_us"], "us", r["achieved"], "GB/s", "frac_of_copy_f4", r["frac_of_copy_f4"],
                   flush=True)
 
 
