@@ -76,6 +76,10 @@ class GradBuckets:
 
     def _reset(self):
         self.count = [0] * len(self.buckets)
+        # streams each bucket's gradients were produced on (the HiFi-GAN
+        # discriminator's chains run on side streams, sel.streams: a bucket can
+        # hold parameters of several chains)
+        self.streams = [[] for _ in self.buckets]
         self.next = 0        # lowest bucket index not yet all-reduced in this backward
         self.used = set()    # ids of the parameters that took a gradient here
         self.works = []
@@ -113,6 +117,10 @@ class GradBuckets:
             v.copy_(g)
             p.grad = v
             self.stats["copies"] += 1
+        # the stream this gradient was produced on (AccumulateGrad runs on it)
+        st = torch.cuda.current_stream(g.device) if g.is_cuda else None
+        if st is not None and all(st != o for o in self.streams[bi]):
+            self.streams[bi].append(st)
         if id(p) not in self.used:
             self.used.add(id(p))
             self.count[bi] += 1
@@ -132,6 +140,15 @@ class GradBuckets:
                 for i in self.used:
                     f[self.slots[i][4]] = 1.0
                 self.flags.copy_(f, non_blocking=False)
+        # the reductions, the 1/W and the all-reduce go on the current stream:
+        # it first waits for every other stream that wrote gradients of this
+        # bucket (without it a bucket spanning two discriminator chains was
+        # read while the other chain's weight-gradient kernels still ran)
+        if self.flat.is_cuda:
+            cur = torch.cuda.current_stream(self.flat.device)
+            for st in self.streams[bi]:
+                if st != cur:
+                    cur.wait_stream(st)
         ps = [self.slots[i][3]() for i in ids]
         CO.flush_params([p for p in ps if p is not None])
         sl = self.flat[lo:hi]
