@@ -261,3 +261,43 @@ def test_ddp_negative_control_without_averaging(gpu, tmp_path):
     e = _grad_err(ref["grads"], ranks[0]["grads"])["G"]
     assert e > 1e-5, e                       # the check of the main test fails ...
     assert abs(e - 1.0) < 1e-3, e            # ... by exactly the missing factor W = 2
+
+
+def test_bucket_waits_for_every_producing_stream(gpu, monkeypatch):
+    """sel.ddp.GradBuckets on gradients produced on two streams (the HiFi-GAN
+    discriminator's chains run on side streams): one parameter's gradient is
+    written on a side stream behind a long queue of work, the other's on the
+    current stream, both in one bucket.  The bucket's 1/W and all-reduce must
+    wait for the side stream: the side-stream gradient comes out halved too
+    (without the wait the scale ran before that write landed).  The process
+    group is stubbed (W = 2, all-reduce a no-op): only the stream order is
+    under test."""
+    import torch.distributed as dist
+    from sel import ddp
+
+    class _Work:
+        def wait(self):
+            pass
+
+    monkeypatch.setattr(dist, "get_world_size", lambda group=None: 2)
+    monkeypatch.setattr(dist, "all_reduce", lambda t, group=None, async_op=False: _Work())
+    p1 = torch.nn.Parameter(torch.zeros(1 << 20, device=gpu))
+    p2 = torch.nn.Parameter(torch.zeros(1 << 10, device=gpu))
+    gb = ddp.GradBuckets([p1, p2], bucket_cap_mb=64.0)
+    assert len(gb.buckets) == 1
+    side = torch.cuda.Stream(device=gpu)
+    a = torch.randn(2048, 2048, device=gpu)
+    torch.cuda.synchronize()
+    # y1 built last: its backward (on the side stream) runs first, so the
+    # bucket completes with p2, on the current stream
+    y2 = (p2 * 5.0).sum()
+    with torch.cuda.stream(side):
+        y1 = (p1 * 3.0).sum()
+    with torch.cuda.stream(side):
+        for _ in range(40):   # a long queue ahead of the side stream's backward
+            a = torch.tanh(a @ a * 1e-3)
+    (y1 + y2).backward()
+    torch.cuda.synchronize()
+    assert torch.equal(p2.grad, torch.full_like(p2, 2.5))
+    assert torch.equal(p1.grad, torch.full_like(p1, 1.5)), p1.grad.unique()[:4]
+    gb.detach()
