@@ -55,6 +55,7 @@ class GradBuckets:
         # known without a collective of its own (torch DDP's local_used_map)
         self.nparams = len(params)
         self.flat = torch.zeros(total + self.nparams, dtype=torch.float32, device=dev)
+        self.dev_index = dev.index if dev.type == "cuda" else None
         cap = max(1, int(bucket_cap_mb * (1 << 20) / 4))
         self.slots = {}     # id(p) -> (offset, numel, bucket index, weakref(p), flag index)
         self.buckets = []   # [lo, hi, [param ids]]
@@ -117,10 +118,14 @@ class GradBuckets:
             v.copy_(g)
             p.grad = v
             self.stats["copies"] += 1
-        # the stream this gradient was produced on (AccumulateGrad runs on it)
-        st = torch.cuda.current_stream(g.device) if g.is_cuda else None
-        if st is not None and all(st != o for o in self.streams[bi]):
-            self.streams[bi].append(st)
+        # the stream this gradient was produced on (AccumulateGrad runs on it);
+        # the raw (id, device, type) triple: this hook runs once per parameter
+        # per backward, and torch.cuda.current_stream() would build a Stream
+        # object each time on the host's critical path
+        if self.dev_index is not None:
+            st = torch._C._cuda_getCurrentStream(self.dev_index)
+            if st not in self.streams[bi]:
+                self.streams[bi].append(st)
         if id(p) not in self.used:
             self.used.add(id(p))
             self.count[bi] += 1
@@ -144,11 +149,13 @@ class GradBuckets:
         # it first waits for every other stream that wrote gradients of this
         # bucket (without it a bucket spanning two discriminator chains was
         # read while the other chain's weight-gradient kernels still ran)
-        if self.flat.is_cuda:
-            cur = torch.cuda.current_stream(self.flat.device)
-            for st in self.streams[bi]:
-                if st != cur:
-                    cur.wait_stream(st)
+        if self.dev_index is not None:
+            cur = torch._C._cuda_getCurrentStream(self.dev_index)
+            others = [st for st in self.streams[bi] if st != cur]
+            if others:
+                cs = torch.cuda.Stream(stream_id=cur[0], device_index=cur[1], device_type=cur[2])
+                for st in others:
+                    cs.wait_stream(torch.cuda.Stream(stream_id=st[0], device_index=st[1], device_type=st[2]))
         ps = [self.slots[i][3]() for i in ids]
         CO.flush_params([p for p in ps if p is not None])
         sl = self.flat[lo:hi]
