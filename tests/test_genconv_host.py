@@ -64,7 +64,10 @@ def _check(fn, ref, x, w, b):
 CONV = [  # Cin, Cout, k, stride, padding, dilation, groups, T
     (3, 5, 7, 1, 3, 1, 1, 40), (4, 6, 6, 3, 2, 1, 1, 61), (4, 4, 5, 2, 0, 2, 2, 33),
     (8, 8, 41, 4, 20, 1, 4, 90), (2, 3, 3, 1, 6, 1, 1, 20), (6, 6, 4, 5, 7, 3, 3, 50),
-    (3, 4, 12, 1, 2, 1, 1, 30)]
+    (3, 4, 12, 1, 2, 1, 1, 30),
+    # edge cases: one input sample with a stride, a 512-row halo (the primitive's
+    # bound), a 1-tap strided conv
+    (1, 1, 3, 2, 1, 1, 1, 1), (5, 3, 9, 1, 256, 64, 1, 600), (2, 2, 1, 3, 0, 1, 1, 10)]
 
 
 @pytest.mark.parametrize("cfg", CONV)
@@ -87,7 +90,9 @@ def test_causal_conv1d_lowering(emulated):
 
 CONVT = [  # Cin, Cout, k, stride, padding, output_padding, groups, T
     (4, 3, 10, 5, 3, 1, 1, 12), (4, 6, 8, 4, 2, 0, 1, 9), (4, 6, 5, 3, 1, 2, 2, 10),
-    (3, 2, 3, 1, 0, 0, 1, 7), (2, 2, 7, 3, 3, 0, 1, 5), (3, 3, 3, 2, 0, 1, 1, 6)]
+    (3, 2, 3, 1, 0, 0, 1, 7), (2, 2, 7, 3, 3, 0, 1, 5), (3, 3, 3, 2, 0, 1, 1, 6),
+    # edge cases: one input sample, a 1-tap transposed conv with output padding
+    (2, 3, 4, 2, 0, 1, 1, 1), (3, 3, 1, 3, 0, 2, 1, 4)]
 
 
 @pytest.mark.parametrize("cfg", CONVT)

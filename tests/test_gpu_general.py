@@ -306,3 +306,39 @@ def test_full_width_noncausal_generator_vs_oracle(gpu, dtype):
             nclose(p.grad, P[name].grad, tg, name)
             n += 1
     assert n > 50
+
+
+def _cases():
+    from test_genconv_host import CONV, CONVT
+    return [("conv",) + c for c in CONV] + [("convt",) + c for c in CONVT]
+
+
+@pytest.mark.parametrize("case", _cases(), ids=lambda c: "_".join(map(str, c)))
+def test_genconv_forms_on_the_kernels(gpu, case):
+    """sel.genconv through the HIP kernels (fp32) at the host test's shapes,
+    edge cases included (one input sample, a 512-row halo, 1-tap strided and
+    transposed forms), against torch's fp64 conv / transposed conv on the same
+    operands: outputs and all three gradients <= 1e-5 norm-wise."""
+    import torch.nn.functional as F
+    from sel import genconv as GC
+    kind, ci, co, k, s, p, a, g, t = case
+    torch.manual_seed(11)
+    x = torch.randn(2, t, ci, dtype=torch.float64)
+    w = torch.randn((co, ci // g, k) if kind == "conv" else (ci, co // g, k), dtype=torch.float64)
+    b = torch.randn(co, dtype=torch.float64)
+    xs, ws, bs = (v.clone().requires_grad_(True) for v in (x, w, b))
+    if kind == "conv":
+        ref = F.conv1d(xs.transpose(1, 2), ws, bs, s, p, a, g).transpose(1, 2)
+    else:
+        ref = F.conv_transpose1d(xs.transpose(1, 2), ws, bs, s, p, a, g).transpose(1, 2)
+    r = torch.randn_like(ref)
+    (ref * r).sum().backward()
+    xg, wg, bg = (v.float().to(gpu).requires_grad_(True) for v in (x, w, b))
+    if kind == "conv":
+        y = GC.conv1d(xg.contiguous(), wg, bg, s, p, a, g)
+    else:
+        y = GC.conv_transpose1d(xg.contiguous(), wg, bg, s, p, a, g)
+    nclose(y, ref, 1e-5, "y")
+    (y * r.float().to(gpu)).sum().backward()
+    for name, got, want in (("gx", xg.grad, xs.grad), ("gw", wg.grad, ws.grad), ("gb", bg.grad, bs.grad)):
+        nclose(got, want, 1e-5, name)
